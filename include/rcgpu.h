@@ -1,0 +1,160 @@
+/*
+ * rcgpu.h -- C ABI of the MI355X pairwise-distance engine for RNA-clique.
+ *
+ * One engine = one GPU. It replaces, for a whole set of samples at once:
+ *
+ *   BlastDBCache(db).makedb(fasta)                      find_all_pairs.py:120-159
+ *   TabularBlastnSearch(query=t2, subject=t1, evalue=..,
+ *     additional_columns=["gaps","nident","sstrand"])   find_homologs.py:124,209
+ *   HomologFinder(...).get_match_table(t1, t2)          find_homologs.py:215-302
+ *   find_all_pairs(...) over combinations(inputs, 2)    find_all_pairs.py:161-233
+ *   build_graph(tables)                                 build_graph.py:40-68
+ *   SampleSimilarity(graph, tables).valid/.restricted   filtered_distance.py:162-247
+ *   ComparisonSimilarityComputer.get_dissimilarity_*    similarity_computer.py:216-375
+ *
+ * Conventions: every function returns 0 on success or a negative RC_E_* code;
+ * the message of the last failure on the calling thread is rc_last_error().
+ * The engine copies every input (no caller pointer is retained) and writes
+ * outputs only into caller buffers sized by a prior call with buf == NULL.
+ * Samples are numbered in the order they are added; that order plays the role
+ * of the reference's `inputs` order (itertools.combinations(inputs, 2): for a
+ * pair (a, b) with a < b, a is t1 = `ssample`, b is t2 = `qsample`).
+ * An engine is not thread-safe; calls block until the GPU work is done.
+ */
+#ifndef RCGPU_H
+#define RCGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RC_OK 0
+#define RC_E_ARG (-1)        /* bad argument */
+#define RC_E_STATE (-2)      /* call out of order (e.g. rows before rc_run) */
+#define RC_E_HIP (-3)        /* HIP runtime error */
+#define RC_E_NOMEM (-4)      /* device or host allocation failed */
+#define RC_E_NO_IDEAL (-5)   /* a pair has no ideal-component rows:
+                                NoIdealComponentsError, filtered_distance.py:242-247 */
+#define RC_E_CAPACITY (-6)   /* caller buffer too small */
+#define RC_E_LIMIT (-7)      /* input beyond a documented engine limit */
+
+typedef struct rc_engine rc_engine;
+
+/* Run options. Defaults (rc_default_opts) follow config.py:77-81. */
+typedef struct rc_opts {
+    int32_t top_matches;   /* N of highest_bitscores (config.py:77), >= 1 */
+    int32_t keep_all;      /* keep ties (config.py:81); 0 = keep "first" */
+    double evalue;         /* BLAST e-value cutoff (config.py:79) */
+    int32_t word_size;     /* seed length W, 16..64 (megablast default 28) */
+    int32_t xdrop_half;    /* greedy X-drop in half-score units (108 = 100 bits) */
+    int32_t device;        /* HIP device ordinal */
+    int32_t shard_rank;    /* rc_align() processes query genes of this shard */
+    int32_t shard_count;   /* number of shards (1 = everything) */
+} rc_opts;
+
+/* One HSP of a directed search, BLAST tabular semantics (1-based, inclusive;
+ * qstart < qend; sstart > send on the minus strand). q_tx / s_tx are transcript
+ * indices within their samples (input order). */
+typedef struct rc_hsp {
+    uint32_t q_tx, s_tx;
+    int32_t qstart, qend, sstart, send;
+    int32_t length, nident, mismatch, gaps, gapopen;
+    int32_t score_half;    /* raw score x 2 (match 2, mismatch -4, gap -5) */
+    int32_t bits10;        /* bit score as BLAST prints it, in tenths */
+    int32_t strand;        /* 0 plus, 1 minus (sstrand) */
+    double evalue;
+} rc_hsp;
+
+/* One row of a gene matches table (docs/formats.md:231-252) of pair (s1, s2):
+ * qgene/qiso belong to s2 (`qsample`), sgene/siso to s1 (`ssample`). For
+ * reverse rows the coordinates are those of the t1-query search, exactly as the
+ * reference's column rename leaves them (find_homologs.py:248-255). */
+typedef struct rc_row {
+    int32_t qgene, qiso, sgene, siso;
+    uint32_t q_tx, s_tx;   /* transcript indices (qgene's sample / sgene's) */
+    int32_t reverse;
+    int32_t label;         /* pandas index label the reference would keep */
+    rc_hsp hsp;            /* q_tx/s_tx in hsp are those of the search row */
+} rc_row;
+
+typedef struct rc_stats {
+    int64_t nodes;            /* vertices of the gene matches graph */
+    int64_t edges;            /* distinct undirected edges */
+    int64_t components;
+    int64_t ideal_components;
+    int64_t ideal_nodes;
+    int32_t sample_count;     /* distinct samples among vertices (filtered_distance.py:171-182) */
+    int32_t pad;
+    int64_t hsps;             /* HSPs of all directed searches after the e-value cut */
+    int64_t table_rows;       /* rows of all gene matches tables */
+} rc_stats;
+
+typedef struct rc_edge {
+    int32_t sample_a, gene_a, sample_b, gene_b;   /* sample_a < sample_b */
+} rc_edge;
+
+typedef struct rc_timing {
+    double pack_ms, index_ms, align_ms, topn_ms, rbh_ms, graph_ms, reduce_ms, total_ms;
+    double align_kernel_ms;   /* device time of the seed-and-extend kernel */
+} rc_timing;
+
+void rc_default_opts(rc_opts *opts);
+
+int rc_create(const rc_opts *opts, rc_engine **eng);
+int rc_destroy(rc_engine *eng);
+const char *rc_last_error(void);
+
+/* Add one sample: `seq` holds all transcripts concatenated (ASCII; A/C/G/T
+ * any case, anything else is an ambiguous base), tx_offsets[n_tx + 1] their
+ * boundaries; gene / iso the parsed TranscriptID fields (transcripts.py:60-126).
+ * `label` is the sample string used in tables and matrix order. */
+int rc_add_sample(rc_engine *eng, const char *label, const char *seq,
+                  const uint64_t *tx_offsets, const int32_t *gene,
+                  const int32_t *iso, uint32_t n_tx, int32_t *sample_id);
+
+/* External-alignment mode: supply the HSPs of directed search
+ * (query sample q, subject sample s) yourself -- e.g. real blastn output in
+ * BLAST output order -- instead of running the GPU aligner. Either every
+ * ordered pair gets rc_add_hsps (missing ones are empty) or none does. */
+int rc_add_hsps(rc_engine *eng, int32_t q, int32_t s, const rc_hsp *hsps, uint64_t n);
+
+/* Copy inputs to the device (done implicitly by rc_run); after this the inputs
+ * are resident in HBM and rc_run repeats the whole path from them. */
+int rc_upload(rc_engine *eng);
+
+/* Phases. rc_run = rc_align + rc_finish. rc_align runs the seed-and-extend
+ * kernel for the query genes of this engine's shard; rc_finish runs top-N,
+ * reciprocal best hits, the graph, the ideal filter and the pair sums over the
+ * top hits of all shards (see rc_export_tops / rc_import_tops). */
+int rc_run(rc_engine *eng);
+int rc_align(rc_engine *eng);
+int rc_finish(rc_engine *eng);
+
+/* Multi-GPU exchange of per-(query gene, subject sample) top hits. Records are
+ * opaque, fixed-size (rc_top_record_size() bytes). export: the records of this
+ * shard into a caller buffer (host or device pointer, `on_device` says which);
+ * import: replace this engine's top hits by the concatenation of all shards'
+ * records (in shard order). */
+uint64_t rc_top_record_size(void);
+int rc_export_tops(rc_engine *eng, void *buf, uint64_t cap, uint64_t *n, int on_device);
+int rc_import_tops(rc_engine *eng, const void *buf, uint64_t n, int on_device);
+
+/* Results (after rc_run / rc_finish). */
+int rc_hsps(rc_engine *eng, int32_t q, int32_t s, rc_hsp *buf, uint64_t cap, uint64_t *n);
+int rc_pair_rows(rc_engine *eng, int32_t s1, int32_t s2, rc_row *buf, uint64_t cap, uint64_t *n);
+int rc_graph_stats(rc_engine *eng, rc_stats *stats);
+int rc_edges(rc_engine *eng, rc_edge *buf, uint64_t cap, uint64_t *n);
+int rc_ideal_nodes(rc_engine *eng, int32_t *sample, int32_t *gene, uint64_t cap, uint64_t *n);
+/* num/den: n_samples x n_samples row-major (sample ids), 0 on the diagonal. */
+int rc_pair_sums(rc_engine *eng, int64_t *num, int64_t *den);
+/* order[n]: sample ids in output order; out: n x n row-major distances.
+ * Returns RC_E_NO_IDEAL when some pair has no ideal rows. */
+int rc_distance(rc_engine *eng, const int32_t *order, double *out);
+int rc_timings(rc_engine *eng, rc_timing *t);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RCGPU_H */

@@ -1,0 +1,514 @@
+/*
+ * CPU oracle for the alignment stage (the NCBI BLAST+ `blastn` replacement).
+ * TEST INFRASTRUCTURE ONLY: loaded by tests/, by __graft_entry__.smoke() and by
+ * bench.py's cpu_baseline leg, as the checker. The product never links it.
+ *
+ * PARITY STATUS: BLAST+ is absent from this image and simple_blast's flags are
+ * not visible in /root/reference, so this file restates the
+ * *published* megablast algorithm as an exact specification ("RC-megablast v1")
+ * that the HIP kernel must reproduce bit for bit. Against BLAST itself the
+ * alignment stage is "parity unpinned"; see DESIGN.md §Oracle.
+ *
+ * Reference call sites this replaces:
+ *   TabularBlastnSearch(query=path2, subject=path1, evalue, additional_columns=
+ *   ["gaps","nident","sstrand"])                      find_homologs.py:124,209
+ *   BlastDBCache.makedb                              find_all_pairs.py:120-132
+ *
+ * Spec (one directed search: query sample Q against subject sample T):
+ *  1. Words. w = 16 (index word), W = word_size (28 = megablast default),
+ *     stride s = W - w + 1. Query positions p with p % s == 0 on the oriented
+ *     query (plus strand = q, minus strand = revcomp(q)); subject positions at
+ *     every offset. Windows containing a non-ACGT base are skipped.
+ *  2. Seeds. A word hit (p, subject tx t, offset o) lies on a maximal exact run
+ *     [x, e) of its diagonal (non-ACGT never matches). It is canonical iff
+ *     p - x < s; a canonical hit with e - x >= W is a seed (x, y = x + o - p,
+ *     len = e - x). Every exact match of length >= W yields exactly one seed.
+ *  3. Per (query tx, strand, subject tx) seeds are sorted by (x, y). Each seed
+ *     not contained in an HSP found so far (box containment) is extended left
+ *     and right with the greedy X-drop algorithm below (at most 8 HSPs).
+ *  4. Greedy X-drop (Zhang et al. 2000, non-affine, megablast reward 1 /
+ *     penalty -2 / linear gap 2.5): in half-score units match +2, mismatch -4,
+ *     gap -5, so score(i, j, d) = i + j - 6d. Band of 64 diagonals around the
+ *     seed diagonal, X = xdrop_half (108 = 100 bits, BLAST's final x-dropoff).
+ *  5. Purge HSPs sharing a start or end point (keep higher score, then earlier),
+ *     keep HSPs whose e-value <= evalue (Karlin-Altschul, lambda 1.28, K 0.46,
+ *     H 0.85, alpha 1.5, beta -2 for 1/-2 linear; BLAST length adjustment).
+ *  6. Bitscore as BLAST prints it (integer-truncated above 99.9) in tenths.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define W16 16
+#define BAND 64
+#define BAND_LO (-32)
+#define MAX_HSP 8
+#define DMAX 4096
+
+typedef struct {
+    uint32_t q_tx, s_tx;
+    int32_t qstart, qend, sstart, send;
+    int32_t length, nident, mismatch, gaps, gapopen, score_half, bits10, strand;
+    double evalue;
+} orc_hsp;
+
+typedef struct {
+    int32_t word_size;
+    int32_t xdrop_half;
+    double evalue;
+} orc_params;
+
+/* Karlin-Altschul parameters for reward 1 / penalty -2, linear gaps
+ * (BLAST's blastn table entry {0,0,1.28,0.46,0.85,1.5,-2,0.45}). */
+static const double KA_LAMBDA = 1.28, KA_K = 0.46, KA_ALPHA = 1.5, KA_BETA = -2.0;
+
+static uint8_t code_of(char c)
+{
+    switch (c) {
+    case 'A': case 'a': return 0;
+    case 'C': case 'c': return 1;
+    case 'G': case 'g': return 2;
+    case 'T': case 't': return 3;
+    default: return 4;
+    }
+}
+
+/* ---------------- statistics (host-side in the product too) ---------------- */
+
+/* BLAST_ComputeLengthAdjustment (restated from the published BLAST+ algorithm). */
+static int32_t length_adjustment(double m, double n, double N)
+{
+    const double logK = log(KA_K), adl = KA_ALPHA / KA_LAMBDA, beta = KA_BETA;
+    double ell = 0, ss, ell_min = 0, ell_max, ell_next = 0;
+    int converged = 0, i;
+    {
+        double a = N, mb = m * N + n, c = n * m - (m > n ? m : n) / KA_K;
+        if (c < 0) return 0;
+        ell_max = 2 * c / (mb + sqrt(mb * mb - 4 * a * c));
+    }
+    for (i = 1; i <= 20; i++) {
+        double ell_bar;
+        ell = ell_next;
+        ss = (m - ell) * (n - N * ell);
+        ell_bar = adl * (logK + log(ss)) + beta;
+        if (ell_bar >= ell) {
+            ell_min = ell;
+            if (ell_bar - ell_min <= 1.0) { converged = 1; break; }
+            if (ell_min == ell_max) break;
+        } else {
+            ell_max = ell;
+        }
+        if (ell_min <= ell_bar && ell_bar <= ell_max) ell_next = ell_bar;
+        else ell_next = (i == 1) ? ell_max : (ell_min + ell_max) / 2;
+    }
+    if (converged) {
+        int32_t adj = (int32_t)ell_min;
+        ell = ceil(ell_min);
+        if (ell <= ell_max) {
+            ss = (m - ell) * (n - N * ell);
+            if (adl * (logK + log(ss)) + beta >= ell) adj = (int32_t)ell;
+        }
+        return adj;
+    }
+    return (int32_t)ell_min;
+}
+
+static double search_space(int64_t qlen, int64_t dblen, int64_t dbn)
+{
+    int32_t ell = length_adjustment((double)qlen, (double)dblen, (double)dbn);
+    double mq = (double)(qlen - ell), nd = (double)(dblen - dbn * (int64_t)ell);
+    if (mq < 1) mq = 1;
+    if (nd < 1) nd = 1;
+    return mq * nd;
+}
+
+static double evalue_of(double ss, int32_t score_half)
+{
+    return ss * KA_K * exp(-KA_LAMBDA * (score_half / 2.0));
+}
+
+/* smallest half-unit score whose e-value passes the cutoff */
+static int32_t score_threshold(double ss, double cutoff)
+{
+    int32_t lo = 0, hi = 1 << 26;
+    if (evalue_of(ss, hi) > cutoff) return hi;
+    while (lo < hi) {
+        int32_t mid = lo + (hi - lo) / 2;
+        if (evalue_of(ss, mid) <= cutoff) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+}
+
+/* CAlignFormatUtil::GetScoreString bit-score formatting, in tenths */
+static int32_t bits10_of(int32_t score_half)
+{
+    double bits = (KA_LAMBDA * (score_half / 2.0) - log(KA_K)) / log(2.0);
+    char buf[64];
+    if (bits > 99999) {
+        snprintf(buf, sizeof buf, "%5.3le", bits);
+        return (int32_t)llround(strtod(buf, NULL) * 10.0);
+    } else if (bits > 99.9) {
+        return (int32_t)((long)bits) * 10;
+    }
+    snprintf(buf, sizeof buf, "%4.1lf", bits);
+    return (int32_t)llround(strtod(buf, NULL) * 10.0);
+}
+
+/* ---------------- sequences ---------------- */
+
+typedef struct {
+    const uint8_t *c;   /* codes 0..4 of the whole concatenation */
+    const uint64_t *tx_start;
+    const int32_t *tx_sample;
+    uint32_t n_tx;
+} seqdb;
+
+static inline uint8_t qbase(const uint8_t *codes, uint64_t start, int32_t len, int strand, int32_t u)
+{
+    if (!strand) return codes[start + u];
+    uint8_t b = codes[start + (uint64_t)(len - 1 - u)];
+    return b < 4 ? (uint8_t)(3 - b) : 4;
+}
+
+/* ---------------- index of one subject sample ---------------- */
+
+typedef struct { uint32_t key, tx, off; } ientry;
+
+typedef struct { ientry *e; uint64_t n; } sindex;
+
+static void build_index(const seqdb *db, int32_t sample, sindex *ix)
+{
+    uint64_t cap = 0, n = 0;
+    uint32_t t;
+    for (t = 0; t < db->n_tx; t++)
+        if (db->tx_sample[t] == sample) {
+            int64_t L = (int64_t)(db->tx_start[t + 1] - db->tx_start[t]);
+            if (L >= W16) cap += (uint64_t)(L - W16 + 1);
+        }
+    ientry *a = (ientry *)malloc((cap ? cap : 1) * sizeof(ientry));
+    ientry *b = (ientry *)malloc((cap ? cap : 1) * sizeof(ientry));
+    for (t = 0; t < db->n_tx; t++) {
+        if (db->tx_sample[t] != sample) continue;
+        uint64_t s0 = db->tx_start[t];
+        int64_t L = (int64_t)(db->tx_start[t + 1] - s0);
+        for (int64_t o = 0; o + W16 <= L; o++) {
+            uint32_t key = 0;
+            int ok = 1;
+            for (int k = 0; k < W16; k++) {
+                uint8_t c = db->c[s0 + o + k];
+                if (c > 3) { ok = 0; break; }
+                key |= (uint32_t)c << (2 * k);
+            }
+            if (!ok) continue;
+            a[n].key = key; a[n].tx = t; a[n].off = (uint32_t)o; n++;
+        }
+    }
+    /* stable LSD radix sort on key: entries stay in (tx, off) order per key */
+    for (int pass = 0; pass < 4; pass++) {
+        uint64_t cnt[257];
+        memset(cnt, 0, sizeof cnt);
+        for (uint64_t i = 0; i < n; i++) cnt[((a[i].key >> (8 * pass)) & 255) + 1]++;
+        for (int k = 0; k < 256; k++) cnt[k + 1] += cnt[k];
+        for (uint64_t i = 0; i < n; i++) b[cnt[(a[i].key >> (8 * pass)) & 255]++] = a[i];
+        ientry *tmp = a; a = b; b = tmp;
+    }
+    free(b);
+    ix->e = a;
+    ix->n = n;
+}
+
+static uint64_t lower_key(const sindex *ix, uint32_t key)
+{
+    uint64_t lo = 0, hi = ix->n;
+    while (lo < hi) {
+        uint64_t mid = (lo + hi) / 2;
+        if (ix->e[mid].key < key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+/* ---------------- greedy X-drop extension ---------------- */
+
+typedef struct { int32_t score, i, j, d, g, o; } ext_result;
+
+/* A(u) / B(u): base u of the two extension sequences (u < alen / blen). */
+typedef struct {
+    const uint8_t *codes;
+    uint64_t start;
+    int32_t len;
+    int strand;    /* oriented transcript: 0 = forward, 1 = revcomp */
+    int reverse;   /* walk backwards from `from` */
+    int32_t from;  /* first oriented position walked */
+} walker;
+
+static inline uint8_t wbase(const walker *w, int32_t u)
+{
+    int32_t pos = w->reverse ? (w->from - u) : (w->from + u);
+    return qbase(w->codes, w->start, w->len, w->strand, pos);
+}
+
+static int32_t slide(const walker *A, int32_t ia, const walker *B, int32_t ib, int32_t maxn)
+{
+    int32_t n = 0;
+    while (n < maxn) {
+        uint8_t a = wbase(A, ia + n), b = wbase(B, ib + n);
+        if (a > 3 || b > 3 || a != b) break;
+        n++;
+    }
+    return n;
+}
+
+static ext_result greedy_ext(const walker *A, int32_t alen, const walker *B, int32_t blen, int32_t X)
+{
+    int32_t R[BAND], G[BAND], O[BAND], E[BAND];
+    int32_t Rn[BAND], Gn[BAND], On[BAND], En[BAND];
+    int32_t sc[BAND];
+    ext_result best;
+    int32_t k0 = -BAND_LO;  /* lane of diagonal 0 */
+    for (int l = 0; l < BAND; l++) R[l] = -1, G[l] = O[l] = E[l] = 0;
+    {
+        int32_t m = alen < blen ? alen : blen;
+        R[k0] = slide(A, 0, B, 0, m);
+    }
+    best.score = 2 * R[k0]; best.i = best.j = R[k0]; best.d = best.g = best.o = 0;
+    for (int32_t d = 1; d <= DMAX; d++) {
+        int any = 0;
+        for (int l = 0; l < BAND; l++) {
+            int32_t k = l + BAND_LO;
+            int32_t ni = -1, ng = 0, no = 0, ne = 0;
+            /* mismatch from k */
+            if (R[l] >= 0 && R[l] < alen && R[l] - k < blen) {
+                ni = R[l] + 1; ng = G[l]; no = O[l]; ne = 0;
+            }
+            /* insertion (A advances) from k-1 */
+            if (l > 0 && R[l - 1] >= 0 && R[l - 1] < alen) {
+                int32_t c = R[l - 1] + 1;
+                if (c > ni) { ni = c; ng = G[l - 1] + 1; no = O[l - 1] + (E[l - 1] == 1 ? 0 : 1); ne = 1; }
+            }
+            /* deletion (B advances) from k+1 */
+            if (l < BAND - 1 && R[l + 1] >= 0 && R[l + 1] - (k + 1) < blen) {
+                int32_t c = R[l + 1];
+                if (c > ni) { ni = c; ng = G[l + 1] + 1; no = O[l + 1] + (E[l + 1] == 2 ? 0 : 1); ne = 2; }
+            }
+            if (ni >= 0 && ni - k >= 0) {
+                int32_t ja = ni - k;
+                int32_t m = alen - ni < blen - ja ? alen - ni : blen - ja;
+                int32_t s = slide(A, ni, B, ja, m);
+                if (s > 0) { ni += s; ne = 0; }
+                int32_t score = 2 * ni - k - 6 * d;
+                if (score < best.score - X) ni = -1;
+                sc[l] = score;
+            } else {
+                ni = -1;
+            }
+            Rn[l] = ni; Gn[l] = ng; On[l] = no; En[l] = ne;
+            if (ni >= 0) any = 1;
+        }
+        /* best update uses this step's live diagonals; ties -> smallest k */
+        {
+            int bl = -1;
+            for (int l = 0; l < BAND; l++)
+                if (Rn[l] >= 0 && (bl < 0 || sc[l] > sc[bl])) bl = l;
+            if (bl >= 0 && sc[bl] > best.score) {
+                int32_t k = bl + BAND_LO;
+                best.score = sc[bl]; best.i = Rn[bl]; best.j = Rn[bl] - k;
+                best.d = d; best.g = Gn[bl]; best.o = On[bl];
+            }
+        }
+        memcpy(R, Rn, sizeof R); memcpy(G, Gn, sizeof G); memcpy(O, On, sizeof O); memcpy(E, En, sizeof E);
+        if (!any) break;
+    }
+    return best;
+}
+
+/* ---------------- one directed search ---------------- */
+
+typedef struct { uint32_t tx; int32_t x, y, len; } seed;
+
+typedef struct { int32_t qa, qb, sa, sb, score, d, g, o, nident; } hsp_box;
+
+static int seed_cmp(const void *pa, const void *pb)
+{
+    const seed *a = (const seed *)pa, *b = (const seed *)pb;
+    if (a->tx != b->tx) return a->tx < b->tx ? -1 : 1;
+    if (a->x != b->x) return a->x < b->x ? -1 : 1;
+    if (a->y != b->y) return a->y < b->y ? -1 : 1;
+    return 0;
+}
+
+typedef struct { orc_hsp *v; uint64_t n, cap; } hsp_vec;
+
+static void push_hsp(hsp_vec *hv, const orc_hsp *h)
+{
+    if (hv->n == hv->cap) {
+        hv->cap = hv->cap ? 2 * hv->cap : 1024;
+        hv->v = (orc_hsp *)realloc(hv->v, hv->cap * sizeof(orc_hsp));
+    }
+    hv->v[hv->n++] = *h;
+}
+
+static void process_candidate(const seqdb *db, uint32_t qtx, int strand, uint32_t stx,
+                              const seed *sd, int ns, int32_t X, int32_t thr,
+                              double ss, hsp_vec *out)
+{
+    hsp_box H[MAX_HSP];
+    int nh = 0;
+    uint64_t qs = db->tx_start[qtx], ts = db->tx_start[stx];
+    int32_t Lq = (int32_t)(db->tx_start[qtx + 1] - qs), Lt = (int32_t)(db->tx_start[stx + 1] - ts);
+    for (int i = 0; i < ns && nh < MAX_HSP; i++) {
+        int32_t x = sd[i].x, y = sd[i].y, len = sd[i].len, c = 0;
+        for (int h = 0; h < nh; h++)
+            if (H[h].qa <= x && x + len <= H[h].qb && H[h].sa <= y && y + len <= H[h].sb) { c = 1; break; }
+        if (c) continue;
+        walker qa = {db->c, qs, Lq, strand, 0, x + len};
+        walker ta = {db->c, ts, Lt, 0, 0, y + len};
+        ext_result r = greedy_ext(&qa, Lq - (x + len), &ta, Lt - (y + len), X);
+        walker qb = {db->c, qs, Lq, strand, 1, x - 1};
+        walker tb = {db->c, ts, Lt, 0, 1, y - 1};
+        ext_result l = greedy_ext(&qb, x, &tb, y, X);
+        hsp_box b;
+        b.qa = x - l.i; b.qb = x + len + r.i; b.sa = y - l.j; b.sb = y + len + r.j;
+        b.score = l.score + 2 * len + r.score;
+        b.d = l.d + r.d; b.g = l.g + r.g; b.o = l.o + r.o;
+        b.nident = len + (l.i + l.j - 2 * l.d + l.g) / 2 + (r.i + r.j - 2 * r.d + r.g) / 2;
+        H[nh++] = b;
+    }
+    /* purge common endpoints: by (score desc, index asc), keep unless it shares
+     * a start or end point with an already kept HSP */
+    int order[MAX_HSP], keep[MAX_HSP];
+    for (int i = 0; i < nh; i++) order[i] = i, keep[i] = 0;
+    for (int i = 1; i < nh; i++)
+        for (int j = i; j > 0; j--) {
+            int a = order[j - 1], b = order[j];
+            if (H[b].score > H[a].score) { order[j - 1] = b; order[j] = a; } else break;
+        }
+    for (int ii = 0; ii < nh; ii++) {
+        int i = order[ii], ok = 1;
+        for (int jj = 0; jj < ii; jj++) {
+            int j = order[jj];
+            if (!keep[j]) continue;
+            if ((H[i].qa == H[j].qa && H[i].sa == H[j].sa) || (H[i].qb == H[j].qb && H[i].sb == H[j].sb)) { ok = 0; break; }
+        }
+        keep[i] = ok;
+    }
+    for (int i = 0; i < nh; i++) {
+        if (!keep[i] || H[i].score < thr) continue;
+        const hsp_box *b = &H[i];
+        orc_hsp o;
+        memset(&o, 0, sizeof o);
+        o.q_tx = qtx; o.s_tx = stx; o.strand = strand;
+        if (!strand) {
+            o.qstart = b->qa + 1; o.qend = b->qb; o.sstart = b->sa + 1; o.send = b->sb;
+        } else {
+            o.qstart = Lq - b->qb + 1; o.qend = Lq - b->qa; o.sstart = b->sb; o.send = b->sa + 1;
+        }
+        o.gaps = b->g; o.gapopen = b->o; o.mismatch = b->d - b->g; o.nident = b->nident;
+        o.length = o.nident + o.mismatch + o.gaps;
+        o.score_half = b->score;
+        o.bits10 = bits10_of(b->score);
+        o.evalue = evalue_of(ss, b->score);
+        push_hsp(out, &o);
+    }
+}
+
+/* Directed search: every gene of query sample Q (genes in ascending global gene
+ * order, isoforms in input order) against subject sample T. Output order:
+ * (gene, isoform, strand, subject tx, HSP). gene_tx: CSR over transcripts. */
+int orc_align(const char *seq, uint64_t total_len, const uint64_t *tx_start,
+              const int32_t *tx_sample, uint32_t n_tx,
+              const uint32_t *gene_tx_off, const uint32_t *gene_tx, uint32_t n_genes,
+              const int32_t *gene_sample, int32_t qsample, int32_t tsample,
+              const orc_params *P, orc_hsp **out, uint64_t *n_out)
+{
+    if (P->word_size < W16 || P->word_size > 64) return -1;
+    uint8_t *codes = (uint8_t *)malloc(total_len ? total_len : 1);
+    for (uint64_t i = 0; i < total_len; i++) codes[i] = code_of(seq[i]);
+    seqdb db = {codes, tx_start, tx_sample, n_tx};
+    sindex ix;
+    build_index(&db, tsample, &ix);
+    int64_t dblen = 0, dbn = 0;
+    for (uint32_t t = 0; t < n_tx; t++)
+        if (tx_sample[t] == tsample) { dblen += (int64_t)(tx_start[t + 1] - tx_start[t]); dbn++; }
+    const int32_t s = P->word_size - W16 + 1;
+    hsp_vec hv = {0, 0, 0};
+    seed *sd = NULL;
+    uint64_t sdcap = 0;
+    for (uint32_t g = 0; g < n_genes; g++) {
+        if (gene_sample[g] != qsample) continue;
+        for (uint32_t ii = gene_tx_off[g]; ii < gene_tx_off[g + 1]; ii++) {
+            uint32_t q = gene_tx[ii];
+            uint64_t qs = tx_start[q];
+            int32_t Lq = (int32_t)(tx_start[q + 1] - qs);
+            double ss = search_space(Lq, dblen, dbn);
+            int32_t thr = score_threshold(ss, P->evalue);
+            for (int strand = 0; strand < 2; strand++) {
+                uint64_t nsd = 0;
+                for (int32_t p = 0; p + W16 <= Lq; p += s) {
+                    uint32_t key = 0;
+                    int ok = 1;
+                    for (int k = 0; k < W16; k++) {
+                        uint8_t c = qbase(codes, qs, Lq, strand, p + k);
+                        if (c > 3) { ok = 0; break; }
+                        key |= (uint32_t)c << (2 * k);
+                    }
+                    if (!ok) continue;
+                    for (uint64_t e = lower_key(&ix, key); e < ix.n && ix.e[e].key == key; e++) {
+                        uint32_t t = ix.e[e].tx;
+                        int32_t o = (int32_t)ix.e[e].off;
+                        uint64_t ts = tx_start[t];
+                        int32_t Lt = (int32_t)(tx_start[t + 1] - ts);
+                        int32_t x = p, y = o;
+                        while (x > 0 && y > 0) {
+                            uint8_t a = qbase(codes, qs, Lq, strand, x - 1), b = codes[ts + y - 1];
+                            if (a > 3 || b > 3 || a != b) break;
+                            x--, y--;
+                        }
+                        if (p - x >= s) continue;  /* not canonical */
+                        int32_t e2 = p + W16, f2 = o + W16;
+                        while (e2 < Lq && f2 < Lt) {
+                            uint8_t a = qbase(codes, qs, Lq, strand, e2), b = codes[ts + f2];
+                            if (a > 3 || b > 3 || a != b) break;
+                            e2++, f2++;
+                        }
+                        if (e2 - x < P->word_size) continue;
+                        if (nsd == sdcap) {
+                            sdcap = sdcap ? 2 * sdcap : 256;
+                            sd = (seed *)realloc(sd, sdcap * sizeof(seed));
+                        }
+                        sd[nsd].tx = t; sd[nsd].x = x; sd[nsd].y = y; sd[nsd].len = e2 - x;
+                        nsd++;
+                    }
+                }
+                qsort(sd, nsd, sizeof(seed), seed_cmp);
+                for (uint64_t i = 0; i < nsd;) {
+                    uint64_t j = i;
+                    while (j < nsd && sd[j].tx == sd[i].tx) j++;
+                    process_candidate(&db, q, strand, sd[i].tx, sd + i, (int)(j - i),
+                                      P->xdrop_half, thr, ss, &hv);
+                    i = j;
+                }
+            }
+        }
+    }
+    free(sd);
+    free(ix.e);
+    free(codes);
+    *out = hv.v;
+    *n_out = hv.n;
+    return 0;
+}
+
+void orc_free(void *p) { free(p); }
+
+/* exported helpers so tests can check the statistics tables directly */
+int32_t orc_bits10(int32_t score_half) { return bits10_of(score_half); }
+int32_t orc_threshold(int64_t qlen, int64_t dblen, int64_t dbn, double cutoff)
+{
+    return score_threshold(search_space(qlen, dblen, dbn), cutoff);
+}
+double orc_evalue(int64_t qlen, int64_t dblen, int64_t dbn, int32_t score_half)
+{
+    return evalue_of(search_space(qlen, dblen, dbn), score_half);
+}

@@ -1,0 +1,152 @@
+"""Parity checks between the native engine and the CPU oracles.
+
+TEST INFRASTRUCTURE ONLY (tests/, __graft_entry__.smoke(), bench.py).
+The engine is the thing checked; the oracles (align_oracle.c for the
+alignment restatement, post_oracle.py pinned to the reference for the rest)
+are the checkers.
+"""
+from __future__ import annotations
+
+import itertools
+
+import numpy as np
+
+from . import post_oracle
+from .align import OracleDB
+
+INT_FIELDS = ["qstart", "qend", "sstart", "send", "length", "nident",
+              "mismatch", "gaps", "gapopen", "score_half", "bits10", "strand"]
+ROW_COMPARE = ["label", "qgene", "qiso", "sgene", "siso", "reverse", "bitscore",
+               "nident", "length", "gaps", "mismatch", "gapopen", "qstart",
+               "qend", "sstart", "send", "sstrand"]
+
+
+def oracle_all_hsps(db: OracleDB, n_samples, word_size=28, xdrop_half=108,
+                    evalue=1e-99):
+    """Every directed search (q, s), q != s, with the C oracle."""
+    return {(q, s): db.align(q, s, word_size, xdrop_half, evalue)
+            for q, s in itertools.permutations(range(n_samples), 2)}
+
+
+def diff_hsps(eng, ora, db: OracleDB, q, s):
+    """Engine HSPs of search (q, s) (transcript indices local to the samples)
+    vs oracle HSPs (global transcript indices). Returns a list of messages."""
+    msgs = []
+    qb, sb = db.tx_base[q], db.tx_base[s]
+    if len(eng) != len(ora):
+        msgs.append(f"search {q}->{s}: {len(eng)} HSPs on GPU vs {len(ora)} in oracle")
+    for i, (a, b) in enumerate(zip(eng, ora)):
+        ea = [int(a["q_tx"]) + qb, int(a["s_tx"]) + sb] + [int(a[f]) for f in INT_FIELDS]
+        eb = [int(b["q_tx"]), int(b["s_tx"])] + [int(b[f]) for f in INT_FIELDS]
+        if ea != eb:
+            msgs.append(f"search {q}->{s} HSP {i}: GPU {ea} vs oracle {eb}")
+            break
+    return msgs
+
+
+def hits_for_post(samples, db: OracleDB, hsps_by_search):
+    """Oracle HSP arrays -> BLAST-tabular dicts keyed by sample labels."""
+    ids = [s.ids() for s in samples]
+    out = {}
+    for (q, s), arr in hsps_by_search.items():
+        rows = []
+        for h in arr:
+            qt = int(h["q_tx"]) - db.tx_base[q]
+            st = int(h["s_tx"]) - db.tx_base[s]
+            rows.append({
+                "qseqid": ids[q][qt], "sseqid": ids[s][st],
+                "pident": 0.0, "length": int(h["length"]),
+                "mismatch": int(h["mismatch"]), "gapopen": int(h["gapopen"]),
+                "qstart": int(h["qstart"]), "qend": int(h["qend"]),
+                "sstart": int(h["sstart"]), "send": int(h["send"]),
+                "evalue": float(h["evalue"]), "bitscore": int(h["bits10"]) / 10.0,
+                "gaps": int(h["gaps"]), "nident": int(h["nident"]),
+                "sstrand": "minus" if int(h["strand"]) else "plus"})
+        out[(samples[q].name, samples[s].name)] = rows
+    return out
+
+
+def engine_rows_as_dicts(rows):
+    out = []
+    for r in rows:
+        h = r["hsp"]
+        out.append({
+            "label": int(r["label"]), "qgene": int(r["qgene"]), "qiso": int(r["qiso"]),
+            "sgene": int(r["sgene"]), "siso": int(r["siso"]),
+            "reverse": bool(r["reverse"]), "bitscore": int(h["bits10"]) / 10.0,
+            "nident": int(h["nident"]), "length": int(h["length"]),
+            "gaps": int(h["gaps"]), "mismatch": int(h["mismatch"]),
+            "gapopen": int(h["gapopen"]), "qstart": int(h["qstart"]),
+            "qend": int(h["qend"]), "sstart": int(h["sstart"]), "send": int(h["send"]),
+            "sstrand": "minus" if int(h["strand"]) else "plus"})
+    return out
+
+
+def diff_rows(eng_rows, ora_rows, tag=""):
+    a = [[r[k] for k in ROW_COMPARE] for r in engine_rows_as_dicts(eng_rows)]
+    b = [[r[k] for k in ROW_COMPARE] for r in ora_rows]
+    if a == b:
+        return []
+    msgs = [f"{tag}: {len(a)} rows on GPU vs {len(b)} in oracle"]
+    for x, y in zip(a, b):
+        if x != y:
+            msgs.append(f"{tag}: first differing row GPU {x} vs oracle {y}")
+            break
+    return msgs
+
+
+def full_check(engine, samples, word_size=28, xdrop_half=108, evalue=1e-99,
+               top_matches=1, keep_all=True, check_hsps=True):
+    """Engine (already run) vs oracles on the same samples. Returns messages
+    (empty = bit-exact parity) and a small summary dict."""
+    db = OracleDB(samples)
+    N = len(samples)
+    ora = oracle_all_hsps(db, N, word_size, xdrop_half, evalue)
+    msgs = []
+    if check_hsps:
+        for (q, s), arr in ora.items():
+            msgs += diff_hsps(engine.hsps(q, s), arr, db, q, s)
+    names = [s.name for s in samples]
+    hits = hits_for_post(samples, db, ora)
+    res = post_oracle.run_pipeline(names, hits, post_oracle.default_parse_id,
+                                   top_matches, keep_all)
+    for a in range(N):
+        for b in range(a + 1, N):
+            msgs += diff_rows(engine.pair_rows(a, b), res["tables"][(names[a], names[b])],
+                              f"pair {a},{b}")
+    e_edges = engine.edges()
+    eng_edges = sorted(tuple(sorted(((names[e["sample_a"]], int(e["gene_a"])),
+                                     (names[e["sample_b"]], int(e["gene_b"])))))
+                       for e in e_edges)
+    ora_edges = sorted(res["edges"])
+    if eng_edges != ora_edges:
+        msgs.append(f"edges: {len(eng_edges)} on GPU vs {len(ora_edges)} in oracle")
+    s_, g_ = engine.ideal_nodes()
+    eng_valid = sorted((names[a], int(b)) for a, b in zip(s_, g_))
+    if eng_valid != sorted(res["valid"]):
+        msgs.append(f"ideal nodes: {len(eng_valid)} on GPU vs {len(res['valid'])} in oracle")
+    st = engine.stats()
+    if st["sample_count"] != res["sample_count"]:
+        msgs.append(f"sample_count {st['sample_count']} vs {res['sample_count']}")
+    num, den = engine.pair_sums()
+    for (ta, tb), (n_, d_) in res["sums"].items():
+        a, b = names.index(ta), names.index(tb)
+        if (int(num[a, b]), int(den[a, b])) != (n_, d_):
+            msgs.append(f"sums {ta},{tb}: GPU {(int(num[a, b]), int(den[a, b]))} vs {(n_, d_)}")
+    ok_matrix = None
+    try:
+        labels_o, mat_o = post_oracle.distance_matrix(names, res["sums"])
+        labels_e, mat_e = engine.distance()
+        if labels_e != labels_o or not np.array_equal(mat_e, np.array(mat_o)):
+            msgs.append("distance matrix differs")
+        ok_matrix = mat_e
+    except post_oracle.NoIdealComponentsError:
+        try:
+            engine.distance()
+            msgs.append("engine produced a matrix where the reference raises NoIdealComponentsError")
+        except Exception:
+            pass
+    summary = {"hsps": int(sum(len(v) for v in ora.values())),
+               "edges": len(ora_edges), "ideal_nodes": len(res["valid"]),
+               "stats": st, "matrix": ok_matrix}
+    return msgs, summary

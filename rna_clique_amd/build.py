@@ -1,0 +1,36 @@
+"""Build librcgpu.so in-tree with hipcc for gfx950 (no JIT cache, no pip)."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "librcgpu.so")
+SOURCES = ["kernels.hip", "engine.hip"]
+HEADERS = ["device.h", os.path.join("..", "..", "include", "rcgpu.h")]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+         "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
+
+
+def _stale():
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build_native(force=False, verbose=False):
+    """Compile the HIP engine into rna_clique_amd/librcgpu.so."""
+    if not force and not _stale():
+        return OUT
+    cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", *SOURCES]
+    res = subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"hipcc failed:\n{' '.join(cmd)}\n{res.stderr[-8000:]}")
+    if verbose and res.stderr:
+        print(res.stderr)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT

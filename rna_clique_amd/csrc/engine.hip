@@ -1,0 +1,1115 @@
+// Host side of the MI355X RNA-clique engine: the C ABI of include/rcgpu.h.
+//
+// Owns the device buffers, drives the kernels of kernels.hip on one HIP
+// stream, and converts results back to reference semantics (1-based BLAST
+// coordinates, pandas index labels, sorted-label matrix order).
+#include "../../include/rcgpu.h"
+#include "device.h"
+
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <numeric>
+#include <string>
+#include <vector>
+
+namespace rcg {
+void launch_pack(const uint8_t *, uint64_t, uint64_t, uint64_t *, uint64_t *, uint64_t *, uint64_t *, hipStream_t);
+void launch_kmer_count(const TxInfo *, uint32_t, const uint64_t *, uint64_t *, hipStream_t);
+void launch_kmer_fill(bool, const TxInfo *, uint32_t, const uint64_t *, const uint64_t *, const uint64_t *,
+                      uint32_t *, uint64_t *, hipStream_t);
+void launch_bucket_fill(const uint32_t *, uint64_t, int, uint32_t *, hipStream_t);
+void launch_align(bool, const Db &, const Index &, const AlignParams &, hipStream_t);
+
+void launch_rbh(const RbhParams &, int, hipStream_t);
+void launch_cc(const DEdge *, uint64_t, uint32_t, const int32_t *, int, uint32_t *, uint32_t *, uint32_t *,
+               uint32_t *, uint32_t *, uint8_t *, unsigned long long *, hipStream_t);
+void launch_pair_sums(const DEdge *, uint64_t, const uint32_t *, const uint8_t *, unsigned long long *,
+                      unsigned long long *, hipStream_t);
+void launch_distance(const unsigned long long *, const unsigned long long *, const int32_t *, const int32_t *,
+                     int, double *, unsigned int *, hipStream_t);
+}  // namespace rcg
+
+using namespace rcg;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string &msg)
+{
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(x)                                                                                    \
+    do {                                                                                             \
+        hipError_t e_ = (x);                                                                         \
+        if (e_ != hipSuccess) return fail(RC_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define CHK(x)                  \
+    do {                        \
+        int r_ = (x);           \
+        if (r_ != RC_OK) return r_; \
+    } while (0)
+
+// Device buffer that only grows (no allocation once sized: reruns are alloc-free).
+template <class T>
+struct DBuf {
+    T *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n)
+    {
+        if (n <= cap && p) return RC_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+        if (hipMalloc((void **)&p, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(RC_E_NOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
+        }
+        cap = std::max<size_t>(n, 1);
+        return RC_OK;
+    }
+    ~DBuf() { release(); }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+// ------------------------------------------------------------------------
+// Karlin-Altschul statistics (BLAST restated; same spec as the oracle)
+// ------------------------------------------------------------------------
+namespace stats {
+const double LAMBDA = 1.28, K = 0.46, ALPHA = 1.5, BETA = -2.0;
+
+// BLAST_ComputeLengthAdjustment
+int32_t length_adjustment(double m, double n, double N)
+{
+    const double logK = std::log(K), adl = ALPHA / LAMBDA;
+    double ell = 0, ss, ell_min = 0, ell_max, ell_next = 0;
+    bool converged = false;
+    {
+        const double a = N, mb = m * N + n, c = n * m - std::max(m, n) / K;
+        if (c < 0) return 0;
+        ell_max = 2 * c / (mb + std::sqrt(mb * mb - 4 * a * c));
+    }
+    for (int i = 1; i <= 20; i++) {
+        ell = ell_next;
+        ss = (m - ell) * (n - N * ell);
+        const double ell_bar = adl * (logK + std::log(ss)) + BETA;
+        if (ell_bar >= ell) {
+            ell_min = ell;
+            if (ell_bar - ell_min <= 1.0) {
+                converged = true;
+                break;
+            }
+            if (ell_min == ell_max) break;
+        } else {
+            ell_max = ell;
+        }
+        if (ell_min <= ell_bar && ell_bar <= ell_max)
+            ell_next = ell_bar;
+        else
+            ell_next = (i == 1) ? ell_max : (ell_min + ell_max) / 2;
+    }
+    if (!converged) return (int32_t)ell_min;
+    int32_t adj = (int32_t)ell_min;
+    ell = std::ceil(ell_min);
+    if (ell <= ell_max) {
+        ss = (m - ell) * (n - N * ell);
+        if (adl * (logK + std::log(ss)) + BETA >= ell) adj = (int32_t)ell;
+    }
+    return adj;
+}
+
+double search_space(int64_t qlen, int64_t dblen, int64_t dbn)
+{
+    const int32_t ell = length_adjustment((double)qlen, (double)dblen, (double)dbn);
+    double mq = (double)(qlen - ell), nd = (double)(dblen - dbn * (int64_t)ell);
+    if (mq < 1) mq = 1;
+    if (nd < 1) nd = 1;
+    return mq * nd;
+}
+
+double evalue(double ss, int32_t score_half) { return ss * K * std::exp(-LAMBDA * (score_half / 2.0)); }
+
+int32_t threshold(double ss, double cutoff)
+{
+    int32_t lo = 0, hi = 1 << 26;
+    if (evalue(ss, hi) > cutoff) return hi;
+    while (lo < hi) {
+        const int32_t mid = lo + (hi - lo) / 2;
+        if (evalue(ss, mid) <= cutoff) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+}
+
+// CAlignFormatUtil::GetScoreString formatting of the bit score, in tenths
+int32_t bits10(int32_t score_half)
+{
+    const double bits = (LAMBDA * (score_half / 2.0) - std::log(K)) / std::log(2.0);
+    char buf[64];
+    if (bits > 99999) {
+        std::snprintf(buf, sizeof buf, "%5.3le", bits);
+        return (int32_t)std::llround(std::strtod(buf, nullptr) * 10.0);
+    }
+    if (bits > 99.9) return (int32_t)((long)bits) * 10;
+    std::snprintf(buf, sizeof buf, "%4.1lf", bits);
+    return (int32_t)std::llround(std::strtod(buf, nullptr) * 10.0);
+}
+}  // namespace stats
+
+// ------------------------------------------------------------------------
+// engine
+// ------------------------------------------------------------------------
+
+struct SampleRec {
+    std::string label;
+    uint64_t base = 0, nbases = 0;
+    uint32_t tx_begin = 0, n_tx = 0;
+    uint32_t gene_begin = 0, n_genes = 0;
+};
+
+struct rc_engine {
+    rc_opts o{};
+    hipStream_t st = nullptr;
+    std::vector<SampleRec> samples;
+    std::vector<char> seq;
+    std::vector<uint64_t> tx_start{0};
+    std::vector<int32_t> tx_sample, tx_gene_id, tx_iso;
+    bool has_amb = false;
+
+    // derived on upload
+    std::vector<uint32_t> tx_gene, gene_tx_off, gene_tx, sample_gene_begin, sample_tx_begin;
+    std::vector<int32_t> gene_sample, gene_id;
+    std::vector<int64_t> db_len, db_n;
+    std::vector<int32_t> pair_a, pair_b, pair_index;
+    std::vector<uint32_t> pair_item_begin;
+    int32_t max_len = 0;
+    uint64_t n_items = 0;
+    int index_bits = 16;
+    uint64_t n_kpos = 0;
+
+    // external HSPs
+    bool external = false;
+    std::map<std::pair<int, int>, std::vector<rc_hsp>> ext;
+
+    // state
+    bool uploaded = false, aligned = false, finished = false;
+
+    // device buffers
+    DBuf<uint8_t> d_ascii;
+    DBuf<uint64_t> d_F, d_RC, d_AF, d_ARC;
+    DBuf<TxInfo> d_tx;
+    DBuf<uint32_t> d_tx_gene, d_gene_tx_off, d_gene_tx, d_sample_gene_begin, d_sample_tx_begin;
+    DBuf<int32_t> d_gene_sample;
+    DBuf<uint64_t> d_kpos_off, d_kcnt;
+    DBuf<uint32_t> d_keys, d_keys2, d_bucket;
+    DBuf<uint64_t> d_vals, d_vals2;
+    DBuf<uint8_t> d_tmp;
+    DBuf<int32_t> d_thr, d_bits10;
+    DBuf<DHsp> d_hsp;
+    uint64_t hsp_cap_hint = 0;
+    DBuf<uint32_t> d_grp_off, d_grp_cnt;
+    DBuf<unsigned long long> d_count;
+    DBuf<unsigned int> d_status;
+    DBuf<uint32_t> d_pair_item_begin;
+    DBuf<int32_t> d_pair_a, d_pair_b, d_pair_index;
+    DBuf<uint32_t> d_cnt4;   // 4 * (n_items + 1)
+    DBuf<uint64_t> d_off4;   // 4 * (n_items + 1)
+    DBuf<DRow> d_rows;
+    DBuf<DEdge> d_edges;
+    uint64_t n_rows = 0, n_edges = 0, n_hsps = 0;
+    DBuf<uint32_t> d_parent, d_present, d_cnodes, d_cedges, d_sample_present;
+    DBuf<uint8_t> d_ideal;
+    DBuf<unsigned long long> d_stats, d_num, d_den;
+    DBuf<int32_t> d_order;
+    DBuf<double> d_dist;
+
+    // host results
+    std::vector<unsigned long long> h_num, h_den, h_stats;
+    rc_timing tm{};
+    hipEvent_t ev[12] = {};
+
+    ~rc_engine()
+    {
+        for (auto &e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (st) (void)hipStreamDestroy(st);
+    }
+};
+
+static int set_device(rc_engine *e) { HIPCHK(hipSetDevice(e->o.device)); return RC_OK; }
+
+extern "C" {
+
+void rc_default_opts(rc_opts *o)
+{
+    o->top_matches = 1;
+    o->keep_all = 1;
+    o->evalue = 1e-99;
+    o->word_size = 28;
+    o->xdrop_half = 108;
+    o->device = 0;
+    o->shard_rank = 0;
+    o->shard_count = 1;
+}
+
+const char *rc_last_error(void) { return g_err.c_str(); }
+
+uint64_t rc_top_record_size(void) { return sizeof(DHsp); }
+
+int rc_create(const rc_opts *opts, rc_engine **out)
+{
+    if (!opts || !out) return fail(RC_E_ARG, "null argument");
+    if (opts->top_matches < 1) return fail(RC_E_ARG, "top_matches must be >= 1");
+    if (opts->word_size < W16 || opts->word_size > 64) return fail(RC_E_ARG, "word_size must be in [16, 64]");
+    if (opts->xdrop_half < 0) return fail(RC_E_ARG, "xdrop_half must be >= 0");
+    if (opts->shard_count < 1 || opts->shard_rank < 0 || opts->shard_rank >= opts->shard_count)
+        return fail(RC_E_ARG, "bad shard");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        (void)hipGetLastError();
+        return fail(RC_E_HIP, "no HIP device available");
+    }
+    if (opts->device < 0 || opts->device >= ndev) return fail(RC_E_ARG, "bad device ordinal");
+    rc_engine *e = new rc_engine();
+    e->o = *opts;
+    if (hipSetDevice(e->o.device) != hipSuccess || hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking) != hipSuccess) {
+        delete e;
+        return fail(RC_E_HIP, "stream creation failed");
+    }
+    for (auto &ev : e->ev)
+        if (hipEventCreate(&ev) != hipSuccess) {
+            delete e;
+            return fail(RC_E_HIP, "event creation failed");
+        }
+    *out = e;
+    return RC_OK;
+}
+
+int rc_destroy(rc_engine *e)
+{
+    if (!e) return RC_OK;
+    (void)hipSetDevice(e->o.device);
+    delete e;  // DBuf destructors free the device buffers
+    return RC_OK;
+}
+
+int rc_add_sample(rc_engine *e, const char *label, const char *seq, const uint64_t *tx_offsets,
+                  const int32_t *gene, const int32_t *iso, uint32_t n_tx, int32_t *sample_id)
+{
+    if (!e || !label || !tx_offsets || (n_tx && (!gene || !iso))) return fail(RC_E_ARG, "null argument");
+    if (e->uploaded) return fail(RC_E_STATE, "samples must be added before rc_run");
+    if (e->samples.size() >= 256) return fail(RC_E_LIMIT, "at most 256 samples per engine");
+    if (tx_offsets[0] != 0) return fail(RC_E_ARG, "tx_offsets[0] must be 0");
+    for (uint32_t t = 0; t < n_tx; t++) {
+        if (tx_offsets[t + 1] < tx_offsets[t]) return fail(RC_E_ARG, "tx_offsets must be non-decreasing");
+        if (tx_offsets[t + 1] - tx_offsets[t] > (1u << 24) - 64)
+            return fail(RC_E_LIMIT, "transcripts longer than 16 Mbp are not supported");
+    }
+    const uint64_t nb = tx_offsets[n_tx];
+    if (nb && !seq) return fail(RC_E_ARG, "null sequence");
+    SampleRec s;
+    s.label = label;
+    s.base = e->seq.size();
+    s.nbases = nb;
+    s.tx_begin = (uint32_t)e->tx_sample.size();
+    s.n_tx = n_tx;
+    e->seq.insert(e->seq.end(), seq, seq + nb);
+    if (!e->has_amb) {
+        for (uint64_t i = 0; i < nb; i++) {
+            const char c = (char)(seq[i] | 0x20);
+            if (c != 'a' && c != 'c' && c != 'g' && c != 't') {
+                e->has_amb = true;
+                break;
+            }
+        }
+    }
+    const int32_t sid = (int32_t)e->samples.size();
+    for (uint32_t t = 0; t < n_tx; t++) {
+        e->tx_start.push_back(s.base + tx_offsets[t + 1]);
+        e->tx_sample.push_back(sid);
+        e->tx_gene_id.push_back(gene[t]);
+        e->tx_iso.push_back(iso[t]);
+    }
+    e->samples.push_back(s);
+    if (sample_id) *sample_id = sid;
+    return RC_OK;
+}
+
+int rc_add_hsps(rc_engine *e, int32_t q, int32_t s, const rc_hsp *h, uint64_t n)
+{
+    if (!e || (n && !h)) return fail(RC_E_ARG, "null argument");
+    if (e->uploaded) return fail(RC_E_STATE, "HSPs must be added before rc_run");
+    const int N = (int)e->samples.size();
+    if (q < 0 || q >= N || s < 0 || s >= N || q == s) return fail(RC_E_ARG, "bad sample pair");
+    for (uint64_t i = 0; i < n; i++)
+        if (h[i].q_tx >= e->samples[q].n_tx || h[i].s_tx >= e->samples[s].n_tx)
+            return fail(RC_E_ARG, "HSP transcript index out of range");
+    e->external = true;
+    auto &v = e->ext[{q, s}];
+    v.insert(v.end(), h, h + n);
+    return RC_OK;
+}
+
+}  // extern "C"
+
+// Build gene numbering, tables and upload everything that does not change
+// between runs. Inputs are then resident in HBM; rc_run repacks from them.
+static int upload(rc_engine *e)
+{
+    if (e->uploaded) return RC_OK;
+    CHK(set_device(e));
+    const int N = (int)e->samples.size();
+    if (N < 2) return fail(RC_E_ARG, "need at least two samples");
+    const uint32_t n_tx = (uint32_t)e->tx_sample.size();
+    // genes: per sample distinct gene ids ascending; a gene's transcripts in input order
+    e->tx_gene.assign(n_tx, 0);
+    e->gene_tx_off.assign(1, 0);
+    e->gene_tx.clear();
+    e->gene_sample.clear();
+    e->gene_id.clear();
+    e->sample_gene_begin.assign(N + 1, 0);
+    e->sample_tx_begin.assign(N + 1, 0);
+    e->db_len.assign(N, 0);
+    e->db_n.assign(N, 0);
+    e->max_len = 0;
+    for (int si = 0; si < N; si++) {
+        SampleRec &s = e->samples[si];
+        e->sample_tx_begin[si] = s.tx_begin;
+        s.gene_begin = (uint32_t)e->gene_sample.size();
+        e->sample_gene_begin[si] = s.gene_begin;
+        std::vector<std::pair<int32_t, uint32_t>> byg;
+        for (uint32_t t = 0; t < s.n_tx; t++) byg.push_back({e->tx_gene_id[s.tx_begin + t], s.tx_begin + t});
+        std::stable_sort(byg.begin(), byg.end(),
+                         [](const std::pair<int32_t, uint32_t> &a, const std::pair<int32_t, uint32_t> &b) {
+                             return a.first < b.first;
+                         });
+        for (size_t i = 0; i < byg.size(); i++) {
+            if (i == 0 || byg[i].first != byg[i - 1].first) {
+                if (i) e->gene_tx_off.push_back((uint32_t)e->gene_tx.size());
+                e->gene_sample.push_back(si);
+                e->gene_id.push_back(byg[i].first);
+            }
+            e->tx_gene[byg[i].second] = (uint32_t)(e->gene_sample.size() - 1);
+            e->gene_tx.push_back(byg[i].second);
+        }
+        if (!byg.empty()) e->gene_tx_off.push_back((uint32_t)e->gene_tx.size());
+        s.n_genes = (uint32_t)e->gene_sample.size() - s.gene_begin;
+        for (uint32_t t = 0; t < s.n_tx; t++) {
+            const uint64_t L = e->tx_start[s.tx_begin + t + 1] - e->tx_start[s.tx_begin + t];
+            e->db_len[si] += (int64_t)L;
+            e->max_len = std::max<int32_t>(e->max_len, (int32_t)L);
+        }
+        e->db_n[si] = s.n_tx;
+    }
+    e->sample_tx_begin[N] = n_tx;
+    e->sample_gene_begin[N] = (uint32_t)e->gene_sample.size();
+    const uint32_t n_genes = (uint32_t)e->gene_sample.size();
+    for (uint32_t g = 0; g < n_genes; g++)
+        if (e->gene_tx_off[g + 1] - e->gene_tx_off[g] > (uint32_t)MAX_ISO)
+            return fail(RC_E_LIMIT, "gene " + std::to_string(e->gene_id[g]) + " has more than 127 transcripts");
+    // pairs in itertools.combinations order; items = (pair, gene of the second sample)
+    e->pair_a.clear();
+    e->pair_b.clear();
+    e->pair_item_begin.assign(1, 0);
+    e->pair_index.assign((size_t)N * N, -1);
+    uint64_t items = 0;
+    for (int a = 0; a < N; a++)
+        for (int b = a + 1; b < N; b++) {
+            e->pair_index[a * N + b] = e->pair_index[b * N + a] = (int32_t)e->pair_a.size();
+            e->pair_a.push_back(a);
+            e->pair_b.push_back(b);
+            items += e->samples[b].n_genes;
+            if (items > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "too many (pair, gene) items");
+            e->pair_item_begin.push_back((uint32_t)items);
+        }
+    e->n_items = items;
+
+    // device copies
+    const uint64_t total = e->seq.size();
+    const uint64_t nwords = (total + 31) / 32 + 2;
+    CHK(e->d_ascii.ensure(total + 64));
+    HIPCHK(hipMemcpyAsync(e->d_ascii.p, e->seq.data(), total, hipMemcpyHostToDevice, e->st));
+    CHK(e->d_F.ensure(nwords));
+    CHK(e->d_RC.ensure(nwords));
+    if (e->has_amb) {
+        CHK(e->d_AF.ensure(nwords));
+        CHK(e->d_ARC.ensure(nwords));
+    }
+    std::vector<TxInfo> txi(n_tx);
+    for (uint32_t t = 0; t < n_tx; t++) {
+        txi[t].start = e->tx_start[t];
+        txi[t].len = (uint32_t)(e->tx_start[t + 1] - e->tx_start[t]);
+        txi[t].sample = e->tx_sample[t];
+    }
+    auto up = [&](auto &buf, const auto &vec) -> int {
+        using T = typename std::remove_reference<decltype(vec)>::type::value_type;
+        CHK(buf.ensure(vec.size()));
+        if (!vec.empty())
+            HIPCHK(hipMemcpyAsync(buf.p, vec.data(), vec.size() * sizeof(T), hipMemcpyHostToDevice, e->st));
+        return RC_OK;
+    };
+    CHK(up(e->d_tx, txi));
+    CHK(up(e->d_tx_gene, e->tx_gene));
+    CHK(up(e->d_gene_tx_off, e->gene_tx_off));
+    CHK(up(e->d_gene_tx, e->gene_tx));
+    CHK(up(e->d_gene_sample, e->gene_sample));
+    CHK(up(e->d_sample_gene_begin, e->sample_gene_begin));
+    CHK(up(e->d_sample_tx_begin, e->sample_tx_begin));
+    CHK(up(e->d_pair_item_begin, e->pair_item_begin));
+    CHK(up(e->d_pair_a, e->pair_a));
+    CHK(up(e->d_pair_b, e->pair_b));
+    CHK(up(e->d_pair_index, e->pair_index));
+    // k-mer positions per transcript (closed form when there are no ambiguous bases)
+    std::vector<uint64_t> koff(n_tx + 1, 0);
+    for (uint32_t t = 0; t < n_tx; t++) {
+        const int64_t L = (int64_t)txi[t].len;
+        koff[t + 1] = koff[t] + (uint64_t)(L >= W16 ? L - W16 + 1 : 0);
+    }
+    CHK(up(e->d_kpos_off, koff));
+    e->n_kpos = koff[n_tx];   // upper bound; exact count for the no-ambiguity case
+    if (e->n_kpos > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "more than 2^32 seed positions on one GPU");
+    // statistics tables
+    std::vector<int32_t> thr((size_t)N * (e->max_len + 1));
+    for (int T = 0; T < N; T++)
+        for (int32_t L = 0; L <= e->max_len; L++)
+            thr[(size_t)T * (e->max_len + 1) + L] =
+                L ? stats::threshold(stats::search_space(L, e->db_len[T], e->db_n[T]), e->o.evalue) : (1 << 26);
+    std::vector<int32_t> b10((size_t)2 * e->max_len + 2);
+    for (size_t sc = 0; sc < b10.size(); sc++) b10[sc] = stats::bits10((int32_t)sc);
+    CHK(up(e->d_thr, thr));
+    CHK(up(e->d_bits10, b10));
+    CHK(e->d_status.ensure(4));
+    CHK(e->d_count.ensure(4));
+    HIPCHK(hipStreamSynchronize(e->st));
+    int bits = 16;
+    while (bits < 30 && (1ull << bits) < e->n_kpos) bits++;
+    e->index_bits = bits;
+    e->uploaded = true;
+    return RC_OK;
+}
+
+static double ev_ms(rc_engine *e, int a, int b)
+{
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, e->ev[a], e->ev[b]) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return ms;
+}
+
+static int build_index(rc_engine *e)
+{
+    const uint32_t n_tx = (uint32_t)e->tx_sample.size();
+    const bool amb = e->has_amb;
+    uint64_t npos = e->n_kpos;
+    if (amb) {
+        CHK(e->d_kcnt.ensure(n_tx + 1));
+        HIPCHK(hipMemsetAsync(e->d_kcnt.p, 0, (n_tx + 1) * sizeof(uint64_t), e->st));
+        if (n_tx) launch_kmer_count(e->d_tx.p, n_tx, e->d_AF.p, e->d_kcnt.p, e->st);
+        size_t tmp = 0;
+        HIPCHK(rocprim::exclusive_scan(nullptr, tmp, e->d_kcnt.p, e->d_kpos_off.p, (uint64_t)0, (size_t)n_tx + 1,
+                                       rocprim::plus<uint64_t>(), e->st));
+        CHK(e->d_tmp.ensure(tmp));
+        HIPCHK(rocprim::exclusive_scan(e->d_tmp.p, tmp, e->d_kcnt.p, e->d_kpos_off.p, (uint64_t)0,
+                                       (size_t)n_tx + 1, rocprim::plus<uint64_t>(), e->st));
+        HIPCHK(hipMemcpyAsync(&npos, e->d_kpos_off.p + n_tx, sizeof(uint64_t), hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipStreamSynchronize(e->st));
+    }
+    CHK(e->d_keys.ensure(npos));
+    CHK(e->d_keys2.ensure(npos));
+    CHK(e->d_vals.ensure(npos));
+    CHK(e->d_vals2.ensure(npos));
+    if (n_tx) launch_kmer_fill(amb, e->d_tx.p, n_tx, e->d_F.p, e->d_AF.p, e->d_kpos_off.p, e->d_keys.p, e->d_vals.p,
+                               e->st);
+    size_t tmp = 0;
+    HIPCHK(rocprim::radix_sort_pairs(nullptr, tmp, e->d_keys.p, e->d_keys2.p, e->d_vals.p, e->d_vals2.p, (size_t)npos,
+                                     0, 32, e->st));
+    CHK(e->d_tmp.ensure(tmp));
+    HIPCHK(rocprim::radix_sort_pairs(e->d_tmp.p, tmp, e->d_keys.p, e->d_keys2.p, e->d_vals.p, e->d_vals2.p,
+                                     (size_t)npos, 0, 32, e->st));
+    CHK(e->d_bucket.ensure((1ull << e->index_bits) + 1));
+    launch_bucket_fill(e->d_keys2.p, npos, e->index_bits, e->d_bucket.p, e->st);
+    e->n_kpos = npos;
+    return RC_OK;
+}
+
+static Db make_db(rc_engine *e)
+{
+    Db db;
+    db.F = e->d_F.p;
+    db.RC = e->d_RC.p;
+    db.AF = e->has_amb ? e->d_AF.p : nullptr;
+    db.ARC = e->has_amb ? e->d_ARC.p : nullptr;
+    db.total = e->seq.size();
+    db.tx = e->d_tx.p;
+    db.tx_gene = e->d_tx_gene.p;
+    db.gene_tx_off = e->d_gene_tx_off.p;
+    db.gene_tx = e->d_gene_tx.p;
+    db.gene_sample = e->d_gene_sample.p;
+    db.sample_gene_begin = e->d_sample_gene_begin.p;
+    db.sample_tx_begin = e->d_sample_tx_begin.p;
+    db.n_samples = (int32_t)e->samples.size();
+    return db;
+}
+
+static void shard_range(rc_engine *e, uint32_t &g0, uint32_t &g1)
+{
+    // contiguous gene ranges of roughly equal sequence length
+    const uint32_t n_genes = (uint32_t)e->gene_sample.size();
+    if (e->o.shard_count == 1) {
+        g0 = 0;
+        g1 = n_genes;
+        return;
+    }
+    const uint64_t total = e->seq.size();
+    auto cut = [&](int r) -> uint32_t {
+        if (r <= 0) return 0;
+        if (r >= e->o.shard_count) return n_genes;
+        const uint64_t target = total * (uint64_t)r / (uint64_t)e->o.shard_count;
+        uint64_t acc = 0;
+        for (uint32_t g = 0; g < n_genes; g++) {
+            if (acc >= target) return g;
+            for (uint32_t i = e->gene_tx_off[g]; i < e->gene_tx_off[g + 1]; i++) {
+                const uint32_t t = e->gene_tx[i];
+                acc += e->tx_start[t + 1] - e->tx_start[t];
+            }
+        }
+        return n_genes;
+    };
+    g0 = cut(e->o.shard_rank);
+    g1 = cut(e->o.shard_rank + 1);
+}
+
+// External HSPs -> device groups in canonical (query gene, subject sample) order.
+static int load_external(rc_engine *e)
+{
+    const int N = (int)e->samples.size();
+    const uint32_t n_genes = (uint32_t)e->gene_sample.size();
+    std::vector<std::vector<DHsp>> grp((size_t)n_genes * N);
+    for (auto &kv : e->ext) {
+        const int q = kv.first.first, s = kv.first.second;
+        for (const rc_hsp &h : kv.second) {
+            DHsp d;
+            d.q_tx = e->samples[q].tx_begin + h.q_tx;
+            d.s_tx = e->samples[s].tx_begin + h.s_tx;
+            d.qstart = h.qstart; d.qend = h.qend; d.sstart = h.sstart; d.send = h.send;
+            d.length = h.length; d.nident = h.nident; d.mismatch = h.mismatch; d.gaps = h.gaps;
+            d.gapopen = h.gapopen; d.score_half = h.score_half; d.bits10 = h.bits10; d.strand = h.strand;
+            grp[(size_t)e->tx_gene[d.q_tx] * N + s].push_back(d);
+        }
+    }
+    std::vector<DHsp> all;
+    std::vector<uint32_t> off(grp.size()), cnt(grp.size());
+    for (size_t i = 0; i < grp.size(); i++) {
+        off[i] = (uint32_t)all.size();
+        cnt[i] = (uint32_t)grp[i].size();
+        all.insert(all.end(), grp[i].begin(), grp[i].end());
+    }
+    CHK(e->d_hsp.ensure(all.size()));
+    CHK(e->d_grp_off.ensure(off.size()));
+    CHK(e->d_grp_cnt.ensure(cnt.size()));
+    if (!all.empty()) HIPCHK(hipMemcpyAsync(e->d_hsp.p, all.data(), all.size() * sizeof(DHsp), hipMemcpyHostToDevice, e->st));
+    HIPCHK(hipMemcpyAsync(e->d_grp_off.p, off.data(), off.size() * 4, hipMemcpyHostToDevice, e->st));
+    HIPCHK(hipMemcpyAsync(e->d_grp_cnt.p, cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    e->n_hsps = all.size();
+    return RC_OK;
+}
+
+static int do_align(rc_engine *e)
+{
+    CHK(upload(e));
+    CHK(set_device(e));
+    e->aligned = e->finished = false;
+    e->tm = rc_timing{};
+    if (e->external) {
+        HIPCHK(hipEventRecord(e->ev[0], e->st));
+        CHK(load_external(e));
+        HIPCHK(hipEventRecord(e->ev[1], e->st));
+        HIPCHK(hipEventSynchronize(e->ev[1]));
+        e->tm.align_ms = ev_ms(e, 0, 1);
+        e->aligned = true;
+        return RC_OK;
+    }
+    const uint64_t total = e->seq.size();
+    const uint64_t nwords = (total + 31) / 32 + 2;
+    HIPCHK(hipEventRecord(e->ev[0], e->st));
+    launch_pack(e->d_ascii.p, total, nwords, e->d_F.p, e->d_RC.p, e->has_amb ? e->d_AF.p : nullptr,
+                e->has_amb ? e->d_ARC.p : nullptr, e->st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(e->ev[1], e->st));
+    CHK(build_index(e));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(e->ev[2], e->st));
+
+    const int N = (int)e->samples.size();
+    uint32_t g0, g1;
+    shard_range(e, g0, g1);
+    const uint32_t n_genes = (uint32_t)e->gene_sample.size();
+    const size_t ngrp = (size_t)n_genes * N;
+    CHK(e->d_grp_off.ensure(ngrp));
+    CHK(e->d_grp_cnt.ensure(ngrp));
+    if (e->hsp_cap_hint == 0) e->hsp_cap_hint = (uint64_t)(g1 - g0) * (uint64_t)std::max(N - 1, 1) * 2 + 1024;
+    Index ix;
+    for (int attempt = 0; attempt < 3; attempt++) {
+        CHK(e->d_hsp.ensure(e->hsp_cap_hint));
+        HIPCHK(hipMemsetAsync(e->d_grp_cnt.p, 0, ngrp * 4, e->st));
+        HIPCHK(hipMemsetAsync(e->d_grp_off.p, 0, ngrp * 4, e->st));
+        HIPCHK(hipMemsetAsync(e->d_count.p, 0, 4 * sizeof(unsigned long long), e->st));
+        HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
+        Db db = make_db(e);
+        ix.keys = e->d_keys2.p;
+        ix.ent = reinterpret_cast<const uint2 *>(e->d_vals2.p);
+        ix.bucket = e->d_bucket.p;
+        ix.bits = e->index_bits;
+        AlignParams P;
+        P.word = e->o.word_size;
+        P.stride = e->o.word_size - W16 + 1;
+        P.xdrop = e->o.xdrop_half;
+        P.max_len = e->max_len;
+        P.thr = e->d_thr.p;
+        P.bits10 = e->d_bits10.p;
+        P.gene_begin = g0;
+        P.gene_end = g1;
+        P.out = e->d_hsp.p;
+        P.out_cap = e->d_hsp.cap;
+        P.out_count = e->d_count.p;
+        // groups are indexed by global gene so that rc_finish sees one table
+        P.grp_off = e->d_grp_off.p + (size_t)g0 * N;
+        P.grp_cnt = e->d_grp_cnt.p + (size_t)g0 * N;
+        P.status = e->d_status.p;
+        HIPCHK(hipEventRecord(e->ev[3], e->st));
+        launch_align(e->has_amb, db, ix, P, e->st);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(e->ev[4], e->st));
+        unsigned long long cnt = 0;
+        unsigned int status = 0;
+        HIPCHK(hipMemcpyAsync(&cnt, e->d_count.p, sizeof cnt, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipStreamSynchronize(e->st));
+        if (status & 2u)
+            return fail(RC_E_LIMIT, "a query gene exceeds the per-gene seed/HSP capacity against a single sample");
+        if (status & 1u) {
+            e->hsp_cap_hint = (uint64_t)(cnt * 1.25) + 1024;
+            continue;
+        }
+        e->n_hsps = cnt;
+        e->tm.pack_ms = ev_ms(e, 0, 1);
+        e->tm.index_ms = ev_ms(e, 1, 2);
+        e->tm.align_ms = ev_ms(e, 2, 4);
+        e->tm.align_kernel_ms = ev_ms(e, 3, 4);
+        e->aligned = true;
+        return RC_OK;
+    }
+    return fail(RC_E_NOMEM, "HSP scratch kept overflowing");
+}
+
+static int do_finish(rc_engine *e)
+{
+    if (!e->aligned) return fail(RC_E_STATE, "rc_finish before rc_align");
+    CHK(set_device(e));
+    const int N = (int)e->samples.size();
+    const uint32_t n_genes = (uint32_t)e->gene_sample.size();
+    const uint64_t ni = e->n_items;
+    const size_t np = e->pair_a.size();
+    HIPCHK(hipEventRecord(e->ev[5], e->st));
+    CHK(e->d_cnt4.ensure(4 * (ni + 1)));
+    CHK(e->d_off4.ensure(4 * (ni + 1)));
+    HIPCHK(hipMemsetAsync(e->d_cnt4.p, 0, 4 * (ni + 1) * 4, e->st));
+    RbhParams R{};
+    R.hsp = e->d_hsp.p;
+    R.grp_off = e->d_grp_off.p;
+    R.grp_cnt = e->d_grp_cnt.p;
+    R.tx_gene = e->d_tx_gene.p;
+    R.tx = e->d_tx.p;
+    R.sample_gene_begin = e->d_sample_gene_begin.p;
+    R.pair_item_begin = e->d_pair_item_begin.p;
+    R.pair_a = e->d_pair_a.p;
+    R.pair_b = e->d_pair_b.p;
+    R.n_pairs = (int32_t)np;
+    R.N = N;
+    R.top_n = e->o.top_matches;
+    R.keep_all = e->o.keep_all;
+    R.n_items = ni;
+    R.n_rows = e->d_cnt4.p;
+    R.n_fsel = e->d_cnt4.p + (ni + 1);
+    R.n_rsel = e->d_cnt4.p + 2 * (ni + 1);
+    R.n_edges = e->d_cnt4.p + 3 * (ni + 1);
+    launch_rbh(R, 0, e->st);
+    HIPCHK(hipGetLastError());
+    for (int k = 0; k < 4; k++) {
+        size_t tmp = 0;
+        const uint32_t *in = e->d_cnt4.p + k * (ni + 1);
+        uint64_t *out = e->d_off4.p + k * (ni + 1);
+        HIPCHK(rocprim::exclusive_scan(nullptr, tmp, in, out, (uint64_t)0, (size_t)ni + 1, rocprim::plus<uint64_t>(),
+                                       e->st));
+        CHK(e->d_tmp.ensure(tmp));
+        HIPCHK(rocprim::exclusive_scan(e->d_tmp.p, tmp, in, out, (uint64_t)0, (size_t)ni + 1,
+                                       rocprim::plus<uint64_t>(), e->st));
+    }
+    uint64_t tot[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 4; k++)
+        HIPCHK(hipMemcpyAsync(&tot[k], e->d_off4.p + k * (ni + 1) + ni, 8, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    e->n_rows = tot[0];
+    e->n_edges = tot[3];
+    CHK(e->d_rows.ensure(e->n_rows));
+    CHK(e->d_edges.ensure(e->n_edges));
+    R.row_off = e->d_off4.p;
+    R.fsel_off = e->d_off4.p + (ni + 1);
+    R.rsel_off = e->d_off4.p + 2 * (ni + 1);
+    R.edge_off = e->d_off4.p + 3 * (ni + 1);
+    R.rows = e->d_rows.p;
+    R.edges = e->d_edges.p;
+    launch_rbh(R, 1, e->st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(e->ev[6], e->st));
+    // graph
+    CHK(e->d_parent.ensure(n_genes));
+    CHK(e->d_present.ensure(n_genes));
+    CHK(e->d_cnodes.ensure(n_genes));
+    CHK(e->d_cedges.ensure(n_genes));
+    CHK(e->d_ideal.ensure(n_genes));
+    CHK(e->d_sample_present.ensure(N));
+    CHK(e->d_stats.ensure(8));
+    HIPCHK(hipMemsetAsync(e->d_sample_present.p, 0, N * 4, e->st));
+    HIPCHK(hipMemsetAsync(e->d_stats.p, 0, 8 * 8, e->st));
+    launch_cc(e->d_edges.p, e->n_edges, n_genes, e->d_gene_sample.p, N, e->d_parent.p, e->d_present.p, e->d_cnodes.p,
+              e->d_cedges.p, e->d_sample_present.p, e->d_ideal.p, e->d_stats.p, e->st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(e->ev[7], e->st));
+    CHK(e->d_num.ensure(np));
+    CHK(e->d_den.ensure(np));
+    HIPCHK(hipMemsetAsync(e->d_num.p, 0, np * 8, e->st));
+    HIPCHK(hipMemsetAsync(e->d_den.p, 0, np * 8, e->st));
+    launch_pair_sums(e->d_edges.p, e->n_edges, e->d_parent.p, e->d_ideal.p, e->d_num.p, e->d_den.p, e->st);
+    HIPCHK(hipGetLastError());
+    e->h_num.assign(np, 0);
+    e->h_den.assign(np, 0);
+    e->h_stats.assign(8, 0);
+    if (np) {
+        HIPCHK(hipMemcpyAsync(e->h_num.data(), e->d_num.p, np * 8, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipMemcpyAsync(e->h_den.data(), e->d_den.p, np * 8, hipMemcpyDeviceToHost, e->st));
+    }
+    HIPCHK(hipMemcpyAsync(e->h_stats.data(), e->d_stats.p, 8 * 8, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipEventRecord(e->ev[8], e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    e->tm.rbh_ms = ev_ms(e, 5, 6);
+    e->tm.graph_ms = ev_ms(e, 6, 7);
+    e->tm.reduce_ms = ev_ms(e, 7, 8);
+    e->tm.total_ms = e->tm.pack_ms + e->tm.index_ms + e->tm.align_ms + e->tm.rbh_ms + e->tm.graph_ms + e->tm.reduce_ms;
+    e->finished = true;
+    return RC_OK;
+}
+
+// ------------------------------------------------------------------------
+// results
+// ------------------------------------------------------------------------
+
+static rc_hsp to_rc_hsp(rc_engine *e, const DHsp &d, int qs_, int ss_)
+{
+    rc_hsp h;
+    h.q_tx = d.q_tx - e->samples[qs_].tx_begin;
+    h.s_tx = d.s_tx - e->samples[ss_].tx_begin;
+    h.qstart = d.qstart; h.qend = d.qend; h.sstart = d.sstart; h.send = d.send;
+    h.length = d.length; h.nident = d.nident; h.mismatch = d.mismatch; h.gaps = d.gaps;
+    h.gapopen = d.gapopen; h.score_half = d.score_half; h.bits10 = d.bits10; h.strand = d.strand;
+    const int64_t qlen = (int64_t)(e->tx_start[d.q_tx + 1] - e->tx_start[d.q_tx]);
+    h.evalue = stats::evalue(stats::search_space(qlen, e->db_len[ss_], e->db_n[ss_]), d.score_half);
+    return h;
+}
+
+static int copy_groups(rc_engine *e, std::vector<uint32_t> &off, std::vector<uint32_t> &cnt)
+{
+    const size_t n = (size_t)e->gene_sample.size() * e->samples.size();
+    off.resize(n);
+    cnt.resize(n);
+    if (!n) return RC_OK;
+    HIPCHK(hipMemcpy(off.data(), e->d_grp_off.p, n * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(cnt.data(), e->d_grp_cnt.p, n * 4, hipMemcpyDeviceToHost));
+    return RC_OK;
+}
+
+extern "C" {
+
+int rc_upload(rc_engine *e)
+{
+    if (!e) return fail(RC_E_ARG, "null engine");
+    return upload(e);
+}
+
+int rc_align(rc_engine *e)
+{
+    if (!e) return fail(RC_E_ARG, "null engine");
+    return do_align(e);
+}
+
+int rc_finish(rc_engine *e)
+{
+    if (!e) return fail(RC_E_ARG, "null engine");
+    return do_finish(e);
+}
+
+int rc_run(rc_engine *e)
+{
+    if (!e) return fail(RC_E_ARG, "null engine");
+    if (e->o.shard_count != 1) return fail(RC_E_STATE, "sharded engines use rc_align / rc_import_tops / rc_finish");
+    CHK(do_align(e));
+    return do_finish(e);
+}
+
+int rc_hsps(rc_engine *e, int32_t q, int32_t s, rc_hsp *buf, uint64_t cap, uint64_t *n)
+{
+    if (!e || !n) return fail(RC_E_ARG, "null argument");
+    if (!e->aligned) return fail(RC_E_STATE, "no alignment yet");
+    const int N = (int)e->samples.size();
+    if (q < 0 || q >= N || s < 0 || s >= N) return fail(RC_E_ARG, "bad sample");
+    CHK(set_device(e));
+    std::vector<uint32_t> off, cnt;
+    CHK(copy_groups(e, off, cnt));
+    const SampleRec &Q = e->samples[q];
+    uint64_t tot = 0;
+    for (uint32_t g = Q.gene_begin; g < Q.gene_begin + Q.n_genes; g++) tot += cnt[(size_t)g * N + s];
+    *n = tot;
+    if (!buf) return RC_OK;
+    if (cap < tot) return fail(RC_E_CAPACITY, "buffer too small");
+    uint64_t w = 0;
+    std::vector<DHsp> tmp;
+    for (uint32_t g = Q.gene_begin; g < Q.gene_begin + Q.n_genes; g++) {
+        const uint32_t c = cnt[(size_t)g * N + s];
+        if (!c) continue;
+        tmp.resize(c);
+        HIPCHK(hipMemcpy(tmp.data(), e->d_hsp.p + off[(size_t)g * N + s], c * sizeof(DHsp), hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < c; i++) buf[w++] = to_rc_hsp(e, tmp[i], q, s);
+    }
+    return RC_OK;
+}
+
+int rc_pair_rows(rc_engine *e, int32_t s1, int32_t s2, rc_row *buf, uint64_t cap, uint64_t *n)
+{
+    if (!e || !n) return fail(RC_E_ARG, "null argument");
+    if (!e->finished) return fail(RC_E_STATE, "no results yet");
+    const int N = (int)e->samples.size();
+    if (s1 < 0 || s1 >= N || s2 < 0 || s2 >= N || s1 >= s2) return fail(RC_E_ARG, "need s1 < s2 (input order)");
+    CHK(set_device(e));
+    const int p = e->pair_index[s1 * N + s2];
+    const uint64_t ib = e->pair_item_begin[p], ie = e->pair_item_begin[p + 1];
+    uint64_t r0 = 0, r1 = 0;
+    HIPCHK(hipMemcpy(&r0, e->d_off4.p + ib, 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&r1, e->d_off4.p + ie, 8, hipMemcpyDeviceToHost));
+    *n = r1 - r0;
+    if (!buf) return RC_OK;
+    if (cap < r1 - r0) return fail(RC_E_CAPACITY, "buffer too small");
+    std::vector<DRow> rows(r1 - r0);
+    if (!rows.empty()) HIPCHK(hipMemcpy(rows.data(), e->d_rows.p + r0, rows.size() * sizeof(DRow), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < rows.size(); i++) {
+        DHsp d;
+        HIPCHK(hipMemcpy(&d, e->d_hsp.p + rows[i].hsp, sizeof(DHsp), hipMemcpyDeviceToHost));
+        rc_row &r = buf[i];
+        const bool rev = rows[i].reverse != 0;
+        // forward rows: query in s2, subject in s1; reverse rows the other way round
+        const int qs_ = rev ? s1 : s2, ss_ = rev ? s2 : s1;
+        r.hsp = to_rc_hsp(e, d, qs_, ss_);
+        const uint32_t tq = rev ? d.s_tx : d.q_tx;   // transcript of s2 (qgene side)
+        const uint32_t ts = rev ? d.q_tx : d.s_tx;   // transcript of s1 (sgene side)
+        r.qgene = e->tx_gene_id[tq];
+        r.qiso = e->tx_iso[tq];
+        r.sgene = e->tx_gene_id[ts];
+        r.siso = e->tx_iso[ts];
+        r.q_tx = tq - e->samples[s2].tx_begin;
+        r.s_tx = ts - e->samples[s1].tx_begin;
+        r.reverse = rev ? 1 : 0;
+        r.label = rows[i].label;
+    }
+    return RC_OK;
+}
+
+int rc_graph_stats(rc_engine *e, rc_stats *s)
+{
+    if (!e || !s) return fail(RC_E_ARG, "null argument");
+    if (!e->finished) return fail(RC_E_STATE, "no results yet");
+    s->components = (int64_t)e->h_stats[0];
+    s->ideal_components = (int64_t)e->h_stats[1];
+    s->ideal_nodes = (int64_t)e->h_stats[2];
+    s->nodes = (int64_t)e->h_stats[3];
+    s->sample_count = (int32_t)e->h_stats[4];
+    s->pad = 0;
+    s->edges = (int64_t)e->n_edges;
+    s->hsps = (int64_t)e->n_hsps;
+    s->table_rows = (int64_t)e->n_rows;
+    return RC_OK;
+}
+
+int rc_edges(rc_engine *e, rc_edge *buf, uint64_t cap, uint64_t *n)
+{
+    if (!e || !n) return fail(RC_E_ARG, "null argument");
+    if (!e->finished) return fail(RC_E_STATE, "no results yet");
+    *n = e->n_edges;
+    if (!buf) return RC_OK;
+    if (cap < e->n_edges) return fail(RC_E_CAPACITY, "buffer too small");
+    CHK(set_device(e));
+    std::vector<DEdge> ed(e->n_edges);
+    if (!ed.empty()) HIPCHK(hipMemcpy(ed.data(), e->d_edges.p, ed.size() * sizeof(DEdge), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < ed.size(); i++) {
+        buf[i].sample_a = e->gene_sample[ed[i].a];
+        buf[i].gene_a = e->gene_id[ed[i].a];
+        buf[i].sample_b = e->gene_sample[ed[i].b];
+        buf[i].gene_b = e->gene_id[ed[i].b];
+    }
+    return RC_OK;
+}
+
+int rc_ideal_nodes(rc_engine *e, int32_t *sample, int32_t *gene, uint64_t cap, uint64_t *n)
+{
+    if (!e || !n) return fail(RC_E_ARG, "null argument");
+    if (!e->finished) return fail(RC_E_STATE, "no results yet");
+    CHK(set_device(e));
+    const uint32_t ng = (uint32_t)e->gene_sample.size();
+    std::vector<uint32_t> parent(ng), present(ng);
+    std::vector<uint8_t> ideal(ng);
+    if (ng) {
+        HIPCHK(hipMemcpy(parent.data(), e->d_parent.p, ng * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(present.data(), e->d_present.p, ng * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(ideal.data(), e->d_ideal.p, ng, hipMemcpyDeviceToHost));
+    }
+    uint64_t c = 0;
+    for (uint32_t v = 0; v < ng; v++)
+        if (present[v] && ideal[parent[v]]) {
+            if (sample && gene) {
+                if (c >= cap) return fail(RC_E_CAPACITY, "buffer too small");
+                sample[c] = e->gene_sample[v];
+                gene[c] = e->gene_id[v];
+            }
+            c++;
+        }
+    *n = c;
+    return RC_OK;
+}
+
+int rc_pair_sums(rc_engine *e, int64_t *num, int64_t *den)
+{
+    if (!e || !num || !den) return fail(RC_E_ARG, "null argument");
+    if (!e->finished) return fail(RC_E_STATE, "no results yet");
+    const int N = (int)e->samples.size();
+    for (int a = 0; a < N; a++)
+        for (int b = 0; b < N; b++) {
+            if (a == b) {
+                num[a * N + b] = den[a * N + b] = 0;
+                continue;
+            }
+            const int p = e->pair_index[a * N + b];
+            num[a * N + b] = (int64_t)e->h_num[p];
+            den[a * N + b] = (int64_t)e->h_den[p];
+        }
+    return RC_OK;
+}
+
+int rc_distance(rc_engine *e, const int32_t *order, double *out)
+{
+    if (!e || !order || !out) return fail(RC_E_ARG, "null argument");
+    if (!e->finished) return fail(RC_E_STATE, "no results yet");
+    const int N = (int)e->samples.size();
+    std::vector<int> seen(N, 0);
+    for (int i = 0; i < N; i++) {
+        if (order[i] < 0 || order[i] >= N || seen[order[i]]) return fail(RC_E_ARG, "order must be a permutation");
+        seen[order[i]] = 1;
+    }
+    CHK(set_device(e));
+    CHK(e->d_order.ensure(N));
+    CHK(e->d_dist.ensure((size_t)N * N));
+    HIPCHK(hipMemcpyAsync(e->d_order.p, order, N * 4, hipMemcpyHostToDevice, e->st));
+    HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
+    launch_distance(e->d_num.p, e->d_den.p, e->d_pair_index.p, e->d_order.p, N, e->d_dist.p, e->d_status.p, e->st);
+    HIPCHK(hipGetLastError());
+    unsigned int status = 0;
+    HIPCHK(hipMemcpyAsync(out, e->d_dist.p, (size_t)N * N * 8, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipMemcpyAsync(&status, e->d_status.p, 4, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    if (status & 4u) return fail(RC_E_NO_IDEAL, "No ideal components found. Cannot report distances!");
+    return RC_OK;
+}
+
+int rc_timings(rc_engine *e, rc_timing *t)
+{
+    if (!e || !t) return fail(RC_E_ARG, "null argument");
+    *t = e->tm;
+    return RC_OK;
+}
+
+int rc_export_tops(rc_engine *e, void *buf, uint64_t cap, uint64_t *n, int on_device)
+{
+    if (!e || !n) return fail(RC_E_ARG, "null argument");
+    if (!e->aligned) return fail(RC_E_STATE, "rc_export_tops before rc_align");
+    CHK(set_device(e));
+    const int N = (int)e->samples.size();
+    uint32_t g0, g1;
+    shard_range(e, g0, g1);
+    std::vector<uint32_t> off, cnt;
+    CHK(copy_groups(e, off, cnt));
+    uint64_t tot = 0;
+    for (size_t i = (size_t)g0 * N; i < (size_t)g1 * N; i++) tot += cnt[i];
+    *n = tot;
+    if (!buf) return RC_OK;
+    if (cap < tot) return fail(RC_E_CAPACITY, "buffer too small");
+    uint64_t w = 0;
+    for (size_t i = (size_t)g0 * N; i < (size_t)g1 * N; i++) {
+        if (!cnt[i]) continue;
+        DHsp *dst = reinterpret_cast<DHsp *>(buf) + w;
+        HIPCHK(hipMemcpy(dst, e->d_hsp.p + off[i], cnt[i] * sizeof(DHsp),
+                         on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost));
+        w += cnt[i];
+    }
+    return RC_OK;
+}
+
+int rc_import_tops(rc_engine *e, const void *buf, uint64_t n, int on_device)
+{
+    if (!e || (n && !buf)) return fail(RC_E_ARG, "null argument");
+    CHK(upload(e));
+    CHK(set_device(e));
+    const int N = (int)e->samples.size();
+    std::vector<DHsp> all(n);
+    if (n)
+        HIPCHK(hipMemcpy(all.data(), buf, n * sizeof(DHsp), on_device ? hipMemcpyDeviceToHost : hipMemcpyHostToHost));
+    const size_t ngrp = (size_t)e->gene_sample.size() * N;
+    std::vector<uint32_t> off(ngrp, 0), cnt(ngrp, 0);
+    size_t prev = (size_t)-1;
+    for (uint64_t i = 0; i < n; i++) {
+        if (all[i].q_tx >= e->tx_gene.size() || all[i].s_tx >= e->tx_sample.size())
+            return fail(RC_E_ARG, "record out of range");
+        const size_t gi = (size_t)e->tx_gene[all[i].q_tx] * N + e->tx_sample[all[i].s_tx];
+        if (gi != prev) {
+            if (cnt[gi]) return fail(RC_E_ARG, "records are not grouped by (gene, sample)");
+            off[gi] = (uint32_t)i;
+        }
+        cnt[gi]++;
+        prev = gi;
+    }
+    CHK(e->d_hsp.ensure(n));
+    CHK(e->d_grp_off.ensure(ngrp));
+    CHK(e->d_grp_cnt.ensure(ngrp));
+    if (n) HIPCHK(hipMemcpy(e->d_hsp.p, all.data(), n * sizeof(DHsp), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->d_grp_off.p, off.data(), ngrp * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->d_grp_cnt.p, cnt.data(), ngrp * 4, hipMemcpyHostToDevice));
+    e->n_hsps = n;
+    e->aligned = true;
+    e->finished = false;
+    return RC_OK;
+}
+
+}  // extern "C"

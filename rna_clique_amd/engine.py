@@ -1,0 +1,169 @@
+"""Python handle over one native engine (one GPU).
+
+Thin wrapper: inputs are copied into the engine, all compute runs in
+librcgpu.so (hand-written HIP for gfx950), results come back as numpy arrays.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native as nat
+
+
+class Engine:
+    """One engine = one device. Samples are numbered in the order they are
+    added (the reference's `inputs` order)."""
+
+    def __init__(self, top_matches=1, keep_all=True, evalue=1e-99, word_size=28,
+                 xdrop_half=108, device=0, shard_rank=0, shard_count=1):
+        L = nat.lib()
+        o = nat.RcOpts()
+        L.rc_default_opts(ctypes.byref(o))
+        o.top_matches = int(top_matches)
+        o.keep_all = 1 if keep_all else 0
+        o.evalue = float(evalue)
+        o.word_size = int(word_size)
+        o.xdrop_half = int(xdrop_half)
+        o.device = int(device)
+        o.shard_rank = int(shard_rank)
+        o.shard_count = int(shard_count)
+        h = ctypes.c_void_p()
+        nat.check(L.rc_create(ctypes.byref(o), ctypes.byref(h)))
+        self._h = h
+        self.labels = []
+        self.n_tx = []
+
+    def close(self):
+        if getattr(self, "_h", None):
+            nat.lib().rc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ------------------------------------------------------------- inputs
+    def add_sample(self, label, seq, tx_offsets, gene, iso):
+        seq = np.ascontiguousarray(seq, dtype=np.uint8)
+        offs = np.ascontiguousarray(tx_offsets, dtype=np.uint64)
+        gene = np.ascontiguousarray(gene, dtype=np.int32)
+        iso = np.ascontiguousarray(iso, dtype=np.int32)
+        n_tx = len(gene)
+        if len(offs) != n_tx + 1 or len(iso) != n_tx:
+            raise ValueError("tx_offsets must have n_tx + 1 entries, iso n_tx")
+        sid = ctypes.c_int32()
+        P = ctypes.POINTER
+        nat.check(nat.lib().rc_add_sample(
+            self._h, str(label).encode(), seq.ctypes.data_as(ctypes.c_char_p),
+            offs.ctypes.data_as(P(ctypes.c_uint64)), gene.ctypes.data_as(P(ctypes.c_int32)),
+            iso.ctypes.data_as(P(ctypes.c_int32)), n_tx, ctypes.byref(sid)))
+        self.labels.append(str(label))
+        self.n_tx.append(n_tx)
+        return sid.value
+
+    def add_hsps(self, q, s, hsps):
+        arr = np.ascontiguousarray(hsps, dtype=nat.HSP_DTYPE)
+        nat.check(nat.lib().rc_add_hsps(self._h, int(q), int(s),
+                                        arr.ctypes.data_as(ctypes.c_void_p), len(arr)))
+
+    # ------------------------------------------------------------- phases
+    def upload(self):
+        nat.check(nat.lib().rc_upload(self._h))
+
+    def run(self):
+        nat.check(nat.lib().rc_run(self._h))
+
+    def align(self):
+        nat.check(nat.lib().rc_align(self._h))
+
+    def finish(self):
+        nat.check(nat.lib().rc_finish(self._h))
+
+    def export_tops(self):
+        L = nat.lib()
+        n = ctypes.c_uint64()
+        nat.check(L.rc_export_tops(self._h, None, 0, ctypes.byref(n), 0))
+        rs = L.rc_top_record_size()
+        buf = np.zeros(n.value * rs, dtype=np.uint8)
+        nat.check(L.rc_export_tops(self._h, buf.ctypes.data_as(ctypes.c_void_p),
+                                   n.value, ctypes.byref(n), 0))
+        return buf
+
+    def import_tops(self, buf):
+        L = nat.lib()
+        rs = L.rc_top_record_size()
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        if len(buf) % rs:
+            raise ValueError("record buffer size is not a multiple of the record size")
+        nat.check(L.rc_import_tops(self._h, buf.ctypes.data_as(ctypes.c_void_p),
+                                   len(buf) // rs, 0))
+
+    # ------------------------------------------------------------- results
+    def _sized(self, fn, dtype, *args):
+        n = ctypes.c_uint64()
+        nat.check(fn(self._h, *args, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, dtype=dtype)
+        if n.value:
+            nat.check(fn(self._h, *args, out.ctypes.data_as(ctypes.c_void_p), n.value,
+                         ctypes.byref(n)))
+        return out
+
+    def hsps(self, q, s):
+        return self._sized(nat.lib().rc_hsps, nat.HSP_DTYPE, int(q), int(s))
+
+    def pair_rows(self, s1, s2):
+        return self._sized(nat.lib().rc_pair_rows, nat.ROW_DTYPE, int(s1), int(s2))
+
+    def edges(self):
+        return self._sized(nat.lib().rc_edges, nat.EDGE_DTYPE)
+
+    def ideal_nodes(self):
+        L = nat.lib()
+        n = ctypes.c_uint64()
+        nat.check(L.rc_ideal_nodes(self._h, None, None, 0, ctypes.byref(n)))
+        s = np.zeros(n.value, dtype=np.int32)
+        g = np.zeros(n.value, dtype=np.int32)
+        nat.check(L.rc_ideal_nodes(self._h, s.ctypes.data_as(ctypes.c_void_p),
+                                   g.ctypes.data_as(ctypes.c_void_p), n.value, ctypes.byref(n)))
+        return s, g
+
+    def stats(self):
+        st = nat.RcStats()
+        nat.check(nat.lib().rc_graph_stats(self._h, ctypes.byref(st)))
+        return {k: getattr(st, k) for k, _ in nat.RcStats._fields_ if k != "pad"}
+
+    def pair_sums(self):
+        n = len(self.labels)
+        num = np.zeros((n, n), dtype=np.int64)
+        den = np.zeros((n, n), dtype=np.int64)
+        nat.check(nat.lib().rc_pair_sums(self._h, num.ctypes.data_as(ctypes.c_void_p),
+                                         den.ctypes.data_as(ctypes.c_void_p)))
+        return num, den
+
+    def distance(self, order=None):
+        """N x N distances with rows/columns in `order` (default: sorted labels,
+        similarity_computer.py:220). Raises NativeError(RC_E_NO_IDEAL) when a
+        pair has no ideal rows."""
+        n = len(self.labels)
+        if order is None:
+            order = sorted(range(n), key=lambda i: self.labels[i])
+        order = np.ascontiguousarray(order, dtype=np.int32)
+        out = np.zeros((n, n), dtype=np.float64)
+        nat.check(nat.lib().rc_distance(self._h, order.ctypes.data_as(ctypes.c_void_p),
+                                        out.ctypes.data_as(ctypes.c_void_p)))
+        return [self.labels[i] for i in order], out
+
+    def timings(self):
+        t = nat.RcTiming()
+        nat.check(nat.lib().rc_timings(self._h, ctypes.byref(t)))
+        return {k: getattr(t, k) for k, _ in nat.RcTiming._fields_}

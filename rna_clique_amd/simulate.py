@@ -1,0 +1,206 @@
+"""Synthetic transcriptomes for tests and benchmarks.
+
+The reference's own test data come from its `distance_sequence_simulator`
+submodule, which is empty in this checkout (.gitmodules:1-3). This generator
+follows the configuration the reference's install test feeds it
+(tests/verify_install/minimal_config.yaml:1-39):
+
+* a birth-death tree (birth 1.0, death 0.5) grown until `taxa` lineages exist;
+* transcript lengths `loc + Binomial(n, p)` (1950 + B(1000, 0.1) there);
+* HKY85 substitutions along every branch at `mutation_rate` substitutions per
+  site per unit branch length (equal base frequencies, kappa = 2);
+* coverage Uniform(0, 10000), printed with decimals so that the default
+  transcript-ID regex (transcripts.py:8) parses it, distinct per gene;
+* ids "NODE_cov_{cov}_g{gene}_i{iso}".
+
+Extras for correctness runs: a fraction of genes gets a second isoform with a
+skipped internal segment (alternative splicing), and short indels can be added.
+Gene ids are permuted per taxon so nothing can rely on ortholog ids matching.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+
+import numpy as np
+
+_BASES = np.frombuffer(b"ACGT", dtype=np.uint8)
+
+
+@dataclasses.dataclass
+class Sample:
+    """One taxon's transcriptome, kept as flat arrays (FASTA-free)."""
+    name: str
+    seq: np.ndarray          # uint8 ASCII, all transcripts concatenated
+    tx_offsets: np.ndarray   # uint64, n_tx + 1
+    gene: np.ndarray         # int32 gene id per transcript
+    iso: np.ndarray          # int32 isoform id per transcript
+    cov: np.ndarray          # float64 coverage per transcript
+
+    @property
+    def n_tx(self):
+        return len(self.gene)
+
+    def ids(self):
+        return [f"NODE_cov_{c:.6f}_g{g}_i{i}" for c, g, i in
+                zip(self.cov, self.gene, self.iso)]
+
+    def transcript(self, t):
+        return self.seq[self.tx_offsets[t]:self.tx_offsets[t + 1]].tobytes().decode()
+
+    def write_fasta(self, path):
+        with open(path, "w") as f:
+            for t, name in enumerate(self.ids()):
+                f.write(f">{name}\n")
+                s = self.transcript(t)
+                for k in range(0, len(s), 80):
+                    f.write(s[k:k + 80] + "\n")
+
+
+def birth_death_tree(taxa, rng, birth=1.0, death=0.5):
+    """Grow a birth-death tree until `taxa` lineages are alive.
+
+    Returns (parent, branch_length, leaves) with node 0 the root.
+    """
+    while True:
+        parent, blen, start = [-1], [0.0], [0.0]
+        alive = [0]
+        t = 0.0
+        while 0 < len(alive) < taxa:
+            rate = len(alive) * (birth + death)
+            t += rng.exponential(1.0 / rate)
+            k = int(rng.integers(len(alive)))
+            node = alive.pop(k)
+            blen[node] = t - start[node]
+            if rng.random() < birth / (birth + death):
+                for _ in range(2):
+                    parent.append(node)
+                    blen.append(0.0)
+                    start.append(t)
+                    alive.append(len(parent) - 1)
+        if len(alive) == taxa:
+            t += rng.exponential(1.0 / (len(alive) * (birth + death)))
+            for a in alive:
+                blen[a] = t - start[a]
+            return np.array(parent), np.array(blen), sorted(alive)
+
+
+def _hky85_mutate(seq, expected_subs, rng, kappa=2.0):
+    """Substitutions on uint8 codes 0..3 (A C G T) for one branch."""
+    # with equal base frequencies HKY85's total rate splits into transitions
+    # (A<->G, C<->T) with weight kappa and two transversions with weight 1
+    n = seq.size
+    p_change = 1.0 - math.exp(-expected_subs)
+    k = rng.binomial(n, p_change)
+    if k == 0:
+        return seq
+    pos = rng.choice(n, size=k, replace=False)
+    r = rng.random(k) * (kappa + 2.0)
+    old = seq[pos]
+    transition = old ^ 2                  # A(0)<->G(2), C(1)<->T(3)
+    tv1 = old ^ 1
+    tv2 = old ^ 3
+    new = np.where(r < kappa, transition, np.where(r < kappa + 1.0, tv1, tv2))
+    out = seq.copy()
+    out[pos] = new.astype(np.uint8)
+    return out
+
+
+def _indels(gene_seqs, rate, rng):
+    """Short insertions/deletions (1-6 bp) at `rate` per base."""
+    out = []
+    for s in gene_seqs:
+        k = rng.binomial(s.size, rate)
+        if k == 0:
+            out.append(s)
+            continue
+        s = s.tolist()
+        for _ in range(k):
+            p = int(rng.integers(len(s)))
+            ln = int(rng.integers(1, 7))
+            if rng.random() < 0.5:
+                del s[p:p + ln]
+            else:
+                s[p:p] = rng.integers(0, 4, size=ln).tolist()
+        out.append(np.array(s, dtype=np.uint8))
+    return out
+
+
+def simulate(taxa, genes, seed=487, len_loc=1950, len_n=1000, len_p=0.1,
+             len_uniform=None, mutation_rate=0.01, p_iso2=0.0, indel_rate=0.0,
+             permute_genes=True, prefix="T"):
+    """Simulate `taxa` transcriptomes with `genes` orthologous genes each.
+
+    len_uniform=(lo, hi) draws lengths uniformly instead of loc + Binomial.
+    Returns (samples, tree) where tree = (parent, branch_length, leaves).
+    """
+    rng = np.random.default_rng(seed)
+    parent, blen, leaves = birth_death_tree(taxa, rng)
+    if len_uniform is not None:
+        lengths = rng.integers(len_uniform[0], len_uniform[1] + 1, size=genes)
+    else:
+        lengths = len_loc + rng.binomial(len_n, len_p, size=genes)
+    total = int(lengths.sum())
+    offs = np.zeros(genes + 1, dtype=np.int64)
+    offs[1:] = np.cumsum(lengths)
+    root = rng.integers(0, 4, size=total, dtype=np.uint8)
+    children = {}
+    for v, p in enumerate(parent):
+        if p >= 0:
+            children.setdefault(int(p), []).append(v)
+    # depth-first, keeping only the sequences still needed
+    seqs = {0: root}
+    leaf_seq = {}
+    stack = [0]
+    while stack:
+        v = stack.pop()
+        s = seqs.pop(v)
+        kids = children.get(v, [])
+        if not kids:
+            leaf_seq[v] = s
+            continue
+        for c in kids:
+            seqs[c] = _hky85_mutate(s, mutation_rate * blen[c], rng)
+            stack.append(c)
+    iso2 = rng.random(genes) < p_iso2
+    cov = rng.uniform(0, 10000, size=genes)
+    samples = []
+    for li, leaf in enumerate(leaves):
+        s = leaf_seq[leaf]
+        gseqs = [s[offs[g]:offs[g + 1]] for g in range(genes)]
+        if indel_rate > 0:
+            gseqs = _indels(gseqs, indel_rate, rng)
+        gid = (rng.permutation(genes) if permute_genes else np.arange(genes)) + 1
+        parts, gene_l, iso_l, cov_l = [], [], [], []
+        # per-taxon coverage jitter keeps top-n selection meaningful but distinct
+        tcov = cov * rng.uniform(0.9, 1.1, size=genes)
+        for g in range(genes):
+            parts.append(gseqs[g])
+            gene_l.append(gid[g]); iso_l.append(1); cov_l.append(tcov[g])
+            if iso2[g] and gseqs[g].size > 400:
+                a = int(rng.integers(100, gseqs[g].size // 2))
+                b = a + int(rng.integers(60, 160))
+                parts.append(np.concatenate([gseqs[g][:a], gseqs[g][b:]]))
+                gene_l.append(gid[g]); iso_l.append(2); cov_l.append(tcov[g] * 0.5)
+        lens = np.array([p.size for p in parts], dtype=np.uint64)
+        txo = np.zeros(len(parts) + 1, dtype=np.uint64)
+        txo[1:] = np.cumsum(lens)
+        codes = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+        samples.append(Sample(
+            name=f"{prefix}{li}",
+            seq=_BASES[codes],
+            tx_offsets=txo,
+            gene=np.array(gene_l, dtype=np.int32),
+            iso=np.array(iso_l, dtype=np.int32),
+            cov=np.array(cov_l, dtype=np.float64)))
+    return samples, (parent, blen, leaves)
+
+
+# BASELINE.json configs.
+CONFIGS = {
+    "C1": dict(taxa=4, genes=1000, seed=487),
+    "C2": dict(taxa=8, genes=10000, seed=488),
+    "C3": dict(taxa=32, genes=50000, seed=489, len_loc=950, len_n=100, len_p=0.5),
+    "C4": dict(taxa=64, genes=50000, seed=490, len_loc=950, len_n=100, len_p=0.5),
+    "C5": dict(taxa=128, genes=100000, seed=491, len_uniform=(200, 5000)),
+}

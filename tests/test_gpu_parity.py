@@ -1,0 +1,155 @@
+"""GPU parity: the HIP path against the CPU oracles, bit for bit.
+
+Alignment: oracle/align_oracle.c (restated megablast; parity vs BLAST itself is
+unpinned). Post-alignment: oracle/post_oracle.py, itself pinned
+to the reference by tests/golden/post_alignment.json -- and the engine is also
+run directly on those golden HSP tables (external-alignment mode).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle.parity import full_check
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "post_alignment.json")
+
+
+def _engine(**kw):
+    from rna_clique_amd.engine import Engine
+    return Engine(device=0, **kw)
+
+
+def _run_sim(samples, **kw):
+    eng = _engine(**kw)
+    for s in samples:
+        eng.add_sample(s.name, s.seq, s.tx_offsets, s.gene, s.iso)
+    eng.run()
+    return eng
+
+
+@pytest.mark.parametrize("seed,taxa,genes,iso,indel", [
+    (1, 3, 80, 0.0, 0.0),
+    (2, 4, 150, 0.2, 0.002),
+    (3, 5, 120, 0.1, 0.004),
+])
+def test_simulated_parity(native, seed, taxa, genes, iso, indel):
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(taxa, genes, seed=seed, p_iso2=iso, indel_rate=indel)
+    eng = _run_sim(samples)
+    msgs, summary = full_check(eng, samples)
+    assert not msgs, "\n".join(msgs[:10])
+    assert summary["hsps"] > 0 and summary["ideal_nodes"] > 0
+
+
+@pytest.mark.parametrize("top_matches,keep_all", [(1, True), (1, False), (2, True)])
+def test_simulated_parity_options(native, top_matches, keep_all):
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(4, 100, seed=11, p_iso2=0.3, indel_rate=0.003)
+    eng = _run_sim(samples, top_matches=top_matches, keep_all=keep_all)
+    msgs, _ = full_check(eng, samples, top_matches=top_matches, keep_all=keep_all,
+                         check_hsps=False)
+    assert not msgs, "\n".join(msgs[:10])
+
+
+def _golden_engine(fx, hc):
+    """Engine in external-alignment mode fed with a golden fixture's HSPs."""
+    from oracle.post_oracle import default_parse_id
+    from rna_clique_amd import _native as nat
+    samples = fx["samples"]
+    tx = {s: {} for s in samples}       # sample -> id -> (index)
+    for key, rows in fx["hits"].items():
+        q, s = key.split("|")
+        for r in rows:
+            h = dict(zip(hc, r))
+            tx[q].setdefault(h["qseqid"], len(tx[q]))
+            tx[s].setdefault(h["sseqid"], len(tx[s]))
+    eng = _engine(top_matches=fx["top_matches"], keep_all=fx["keep_all"])
+    for s in samples:
+        ids = sorted(tx[s], key=tx[s].get)
+        if not ids:
+            ids = ["NODE_cov_1.0_g999999_i1"]
+            tx[s][ids[0]] = 0
+        seq = np.frombuffer(b"ACGT" * 50 * len(ids), dtype=np.uint8)
+        offs = np.arange(len(ids) + 1, dtype=np.uint64) * 200
+        parsed = [default_parse_id(i) for i in ids]
+        eng.add_sample(s, seq, offs, [p[1] for p in parsed], [p[2] for p in parsed])
+    for key, rows in fx["hits"].items():
+        q, s = key.split("|")
+        arr = np.zeros(len(rows), dtype=nat.HSP_DTYPE)
+        for i, r in enumerate(rows):
+            h = dict(zip(hc, r))
+            arr[i]["q_tx"] = tx[q][h["qseqid"]]
+            arr[i]["s_tx"] = tx[s][h["sseqid"]]
+            for f in ("qstart", "qend", "sstart", "send", "length", "nident",
+                      "mismatch", "gaps", "gapopen"):
+                arr[i][f] = h[f]
+            arr[i]["bits10"] = int(round(h["bitscore"] * 10))
+            arr[i]["strand"] = 1 if h["sstrand"] == "minus" else 0
+        eng.add_hsps(samples.index(q), samples.index(s), arr)
+    eng.run()
+    return eng
+
+
+def test_golden_reference_tables(native):
+    """The engine's RBH/graph/filter/distance kernels reproduce the reference's
+    own outputs on the golden HSP tables (labels and row order included)."""
+    from oracle.parity import engine_rows_as_dicts
+    from rna_clique_amd._native import NativeError, RC_E_NO_IDEAL
+    d = json.load(open(GOLDEN))
+    cols, hc = d["columns"], d["hsp_columns"]
+    checked = 0
+    for fx in d["fixtures"]:
+        exp = fx["expected"]
+        if any(k != "matrix" for k in exp["errors"]):
+            continue   # the reference itself crashed (recorded quirk)
+        eng = _golden_engine(fx, hc)
+        samples = fx["samples"]
+        for key, rows in exp["tables"].items():
+            t1, t2 = key.split("|")
+            got = engine_rows_as_dicts(eng.pair_rows(samples.index(t1), samples.index(t2)))
+            want = [dict(zip(cols, r)) for r in rows]
+            keys = ["label", "qgene", "qiso", "sgene", "siso", "reverse", "bitscore",
+                    "nident", "length", "gaps", "qstart", "qend", "sstart", "send", "sstrand"]
+            assert [[g[k] for k in keys] for g in got] == [[w[k] for k in keys] for w in want], \
+                f"seed {fx['seed']} pair {key}"
+        edges = sorted(sorted([[samples[e["sample_a"]], int(e["gene_a"])],
+                               [samples[e["sample_b"]], int(e["gene_b"])]])
+                       for e in eng.edges())
+        assert edges == exp["edges"], f"seed {fx['seed']} edges"
+        s_, g_ = eng.ideal_nodes()
+        assert sorted([samples[a], int(b)] for a, b in zip(s_, g_)) == exp["valid"]
+        assert eng.stats()["sample_count"] == exp["sample_count"]
+        num, den = eng.pair_sums()
+        for key, (n_, d_) in exp["sums"].items():
+            t1, t2 = key.split("|")
+            a, b = samples.index(t1), samples.index(t2)
+            assert (int(num[a, b]), int(den[a, b])) == (n_, d_)
+        if exp["matrix"] is None:
+            with pytest.raises(NativeError) as ei:
+                eng.distance()
+            assert ei.value.code == RC_E_NO_IDEAL
+        else:
+            labels, mat = eng.distance()
+            assert labels == exp["matrix"]["labels"]
+            assert np.array_equal(mat, np.array(exp["matrix"]["values"]))
+        eng.close()
+        checked += 1
+    assert checked >= 15
+
+
+def test_repeat_runs_identical(native):
+    """Two runs of the same engine give identical results (deterministic)."""
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(4, 120, seed=5, p_iso2=0.2, indel_rate=0.002)
+    eng = _run_sim(samples)
+    h1 = [eng.hsps(q, s) for q in range(4) for s in range(4) if q != s]
+    _, m1 = eng.distance()
+    eng.run()
+    h2 = [eng.hsps(q, s) for q in range(4) for s in range(4) if q != s]
+    _, m2 = eng.distance()
+    assert all(np.array_equal(a, b) for a, b in zip(h1, h2))
+    assert np.array_equal(m1, m2)
