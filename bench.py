@@ -1,0 +1,187 @@
+"""Benchmark: sample-pairs/s of the whole pairwise-distance path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
+
+One step = one pass of the hot path over the whole synthetic batch with the
+inputs already resident in HBM: 2-bit pack -> seed index build -> seed-and-
+extend for every directed sample pair -> top-N + reciprocal best hits -> gene
+matches graph + ideal-clique filter -> restricted sums -> N x N distance matrix
+copied to the host. For N > 1 GPUs (torch.distributed.run, one rank per GPU)
+the query genes are sharded by sequence length, the per-(gene, sample) hits are
+exchanged with one RCCL all-gather, and every rank finishes the graph.
+
+Prints ONE JSON line (rank 0). See DESIGN.md §Measurement for the roofline
+model and the CPU baseline.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-pairs", type=int, default=1,
+                    help="sample pairs the CPU baseline times (2 directed searches each)")
+    return ap.parse_args()
+
+
+def algorithmic_bytes(samples, hsps_per_pair, word=28):
+    """B_pair = 8 (P_A + P_B) + (L_A + L_B) / 4 + 32 H_pair,
+    summed over all C(N, 2) pairs (P_X = seed positions at word size `word`)."""
+    import numpy as np
+    P, L = [], []
+    for s in samples:
+        lens = np.diff(s.tx_offsets.astype(np.int64))
+        P.append(int(np.maximum(lens - word + 1, 0).sum()))
+        L.append(int(lens.sum()))
+    n = len(samples)
+    tot = 0
+    for a in range(n):
+        for b in range(a + 1, n):
+            tot += 8 * (P[a] + P[b]) + (L[a] + L[b]) / 4
+    return tot + 32 * hsps_per_pair
+
+
+def cpu_baseline(samples, n_pairs=1):
+    """The C oracle (same algorithm, one core) on a bounded sample of the same
+    workload: `n_pairs` sample pairs, both directed searches each, plus the
+    post-alignment oracle on them. Returns pairs/s."""
+    from oracle.align import OracleDB
+    from oracle import post_oracle
+    from oracle.parity import hits_for_post
+    t0 = time.perf_counter()
+    done = 0
+    for k in range(n_pairs):
+        a, b = 2 * k, 2 * k + 1
+        sub = [samples[a], samples[b]]
+        db = OracleDB(sub)
+        hs = {(0, 1): db.align(0, 1), (1, 0): db.align(1, 0)}
+        hits = hits_for_post(sub, db, hs)
+        names = [s.name for s in sub]
+        post_oracle.run_pipeline(names, hits, post_oracle.default_parse_id)
+        done += 1
+    dt = time.perf_counter() - t0
+    return done / dt, dt
+
+
+def main():
+    args = parse_args()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    from rna_clique_amd.engine import Engine
+    from rna_clique_amd.simulate import simulate, CONFIGS
+    cfg = CONFIGS[args.config]
+    t_gen = time.perf_counter()
+    samples, _ = simulate(**cfg)
+    t_gen = time.perf_counter() - t_gen
+    n = len(samples)
+    pairs = n * (n - 1) // 2
+    eng = Engine(device=local_rank, shard_rank=rank, shard_count=world)
+    for s in samples:
+        eng.add_sample(s.name, s.seq, s.tx_offsets, s.gene, s.iso)
+    eng.upload()   # inputs resident in HBM before timing (H2D excluded)
+
+    def step():
+        if world == 1:
+            eng.run()
+        else:
+            eng.align()
+            mine = torch.from_numpy(eng.export_tops()).cuda()
+            sizes = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(world)]
+            dist.all_gather(sizes, torch.tensor([mine.numel()], device="cuda"))
+            mx = int(max(int(x) for x in sizes))
+            pad = torch.zeros(mx, dtype=torch.uint8, device="cuda")
+            pad[:mine.numel()] = mine
+            parts = [torch.empty(mx, dtype=torch.uint8, device="cuda") for _ in range(world)]
+            dist.all_gather(parts, pad)
+            allb = torch.cat([p[:int(sz)] for p, sz in zip(parts, sizes)]).cpu().numpy()
+            eng.import_tops(allb)
+            eng.finish()
+        return eng.distance()
+
+    for _ in range(args.warmup):
+        step()
+    align_ms = []
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        labels, mat = step()
+        align_ms.append(eng.timings()["align_kernel_ms"])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms_per_step = 1e3 * dt / args.steps
+    value = pairs * args.steps / dt
+    st = eng.stats()
+    tm = eng.timings()
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    # roofline of the dominant kernel (seed-and-extend), survey byte model
+    hsps = st["hsps"]
+    avg_align = sum(align_ms) / len(align_ms)
+    bytes_launch = algorithmic_bytes(samples, hsps) * (1.0 / world)
+    achieved = bytes_launch / (avg_align * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": "align_kernel", "kernel_ms": round(avg_align, 3),
+            "bytes_per_launch": int(bytes_launch)}
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        v, secs = cpu_baseline(samples, args.cpu_pairs)
+        cpu = {"value": round(v, 5), "unit": "sample-pairs/s", "cores": 1, "kind": "port",
+               "sample": f"{args.cpu_pairs} of {pairs} {args.config} sample pairs "
+                         f"(2 directed searches each + RBH/graph oracle), {secs:.1f} s"}
+    line = {
+        "metric": "sample-pairs/sec (all-vs-all alignment -> RBH graph -> distance matrix)",
+        "value": round(value, 3), "unit": "sample-pairs/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "u8/int32", "data": "synthetic (simulate.py, seeded, BASELINE configs)",
+        "config": {"workload": f"{args.config}: {n} samples x {cfg['genes']} genes",
+                   "pairs": pairs, "bases": int(sum(s.seq.size for s in samples)),
+                   "parallelism": f"query-gene shards x{world}"},
+        "roofline": roof, "cpu_baseline": cpu,
+        "phases_ms": {k: round(v, 3) for k, v in tm.items()},
+        "graph": {k: st[k] for k in ("hsps", "table_rows", "edges", "components",
+                                     "ideal_components", "sample_count")},
+        "gen_s": round(t_gen, 1),
+    }
+    print(json.dumps(line))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
