@@ -89,6 +89,8 @@ typedef struct rc_stats {
     int32_t pad;
     int64_t hsps;             /* HSPs of all directed searches after the e-value cut */
     int64_t table_rows;       /* rows of all gene matches tables */
+    int64_t seeds;            /* seeds (maximal exact runs >= W) of this engine's shard */
+    int64_t candidates;       /* (query tx, strand, subject tx) with >= 1 seed */
 } rc_stats;
 
 typedef struct rc_edge {
@@ -97,7 +99,8 @@ typedef struct rc_edge {
 
 typedef struct rc_timing {
     double pack_ms, index_ms, align_ms, topn_ms, rbh_ms, graph_ms, reduce_ms, total_ms;
-    double align_kernel_ms;   /* device time of the seed-and-extend kernel */
+    double seed_kernel_ms;    /* device time of the seed kernel (lookups, seeds) */
+    double align_kernel_ms;   /* device time of the extension kernel */
 } rc_timing;
 
 void rc_default_opts(rc_opts *opts);

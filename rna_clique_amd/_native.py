@@ -63,7 +63,8 @@ class RcStats(ctypes.Structure):
                 ("components", ctypes.c_int64), ("ideal_components", ctypes.c_int64),
                 ("ideal_nodes", ctypes.c_int64), ("sample_count", ctypes.c_int32),
                 ("pad", ctypes.c_int32), ("hsps", ctypes.c_int64),
-                ("table_rows", ctypes.c_int64)]
+                ("table_rows", ctypes.c_int64), ("seeds", ctypes.c_int64),
+                ("candidates", ctypes.c_int64)]
 
 
 EDGE_DTYPE = np.dtype([("sample_a", np.int32), ("gene_a", np.int32),
@@ -73,7 +74,7 @@ EDGE_DTYPE = np.dtype([("sample_a", np.int32), ("gene_a", np.int32),
 class RcTiming(ctypes.Structure):
     _fields_ = [(n, ctypes.c_double) for n in (
         "pack_ms", "index_ms", "align_ms", "topn_ms", "rbh_ms", "graph_ms",
-        "reduce_ms", "total_ms", "align_kernel_ms")]
+        "reduce_ms", "total_ms", "seed_kernel_ms", "align_kernel_ms")]
 
 
 assert HSP_DTYPE.itemsize == ctypes.sizeof(RcHsp)

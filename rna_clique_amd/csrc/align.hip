@@ -1,0 +1,624 @@
+// Seed-and-extend (the BLAST+ replacement), three kernels:
+//
+//   seed_kernel    one workgroup per query gene: 16-mer lookups at stride
+//                  W-15 on both strands of every isoform, canonical maximal
+//                  exact runs >= W (seeds), sorted per candidate
+//                  (query tx, strand, subject tx); candidates grouped by
+//                  subject sample.
+//   extend_kernel  one wave per candidate: query and subject staged in LDS,
+//                  greedy X-drop extension with one diagonal per lane,
+//                  containment skip, common-endpoint purge, e-value cut.
+//   group_*        per (query gene, subject sample): HSPs made contiguous
+//                  in candidate order (the order the oracle emits).
+//
+// Semantics: oracle/align_oracle.c ("RC-megablast v1"), bit for bit.
+#include "device.h"
+
+#include <climits>
+
+namespace rcg {
+
+constexpr int SBLOCK = 256;
+constexpr int SEED_CAP = 2048;
+constexpr int MAX_SAMPLES = 256;
+
+constexpr int EBLOCK = 256;
+constexpr int EWAVES = EBLOCK / 64;
+constexpr int STAGE_BASES = 8192;                 // staged transcript length limit
+constexpr int SW = STAGE_BASES / 32 + 2;          // words per staged orientation
+
+struct LSeed {
+    uint64_t k1;    // iso:7 | strand:1 | gtx:32 | x:24
+    uint32_t y, len;
+};
+
+// Oriented query geometry. strand 0: q; strand 1: revcomp(q).
+struct QGeo {
+    uint64_t qs;   // forward start
+    int Lq;
+};
+
+__device__ __forceinline__ uint64_t qfwd_pos(const QGeo &q, int strand, uint64_t total, int u)
+{
+    return strand ? (total - q.qs - (uint64_t)q.Lq + (uint64_t)u) : (q.qs + (uint64_t)u);
+}
+// walk leftwards from oriented position x (x-1, x-2, ...) as a forward walk
+__device__ __forceinline__ uint64_t qrev_pos(const QGeo &q, int strand, uint64_t total, int x)
+{
+    return strand ? (q.qs + (uint64_t)q.Lq - (uint64_t)x) : (total - q.qs - (uint64_t)x);
+}
+
+// ------------------------------------------------------------------------
+// seeds
+// ------------------------------------------------------------------------
+
+template <bool AMB>
+__global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParams P)
+{
+    const uint32_t g = P.gene_begin + blockIdx.x;
+    if (g >= P.gene_end) return;
+    const int tid = threadIdx.x;
+
+    __shared__ LSeed seeds[SEED_CAP];
+    __shared__ uint16_t seg_begin[SEED_CAP + 1];
+    __shared__ uint32_t it_lo[SBLOCK], it_pre[SBLOCK + 1], it_info[SBLOCK];
+    __shared__ uint64_t iso_start[MAX_ISO];
+    __shared__ uint32_t iso_len[MAX_ISO], iso_gtx[MAX_ISO], iso_pre[MAX_ISO + 1];
+    __shared__ uint32_t tcnt[MAX_SAMPLES], tpre[MAX_SAMPLES + 1];
+    __shared__ uint32_t sh_nseed, sh_flags, sh_nseg;
+    __shared__ unsigned long long sh_sbase, sh_cbase;
+
+    const int Q = db.gene_sample[g];
+    const uint32_t t0 = db.gene_tx_off[g];
+    const uint32_t niso = db.gene_tx_off[g + 1] - t0;
+    const int N = db.n_samples;
+    const uint64_t total = db.total;
+    const int stride = P.stride;
+    const uint32_t shard = blockIdx.x % NSHARD;
+    if (niso > (uint32_t)MAX_ISO || N > MAX_SAMPLES) {
+        if (tid == 0) atomicOr(P.status, 2u);
+        return;
+    }
+    for (uint32_t i = tid; i < niso; i += SBLOCK) {
+        const uint32_t gtx = db.gene_tx[t0 + i];
+        const TxInfo ti = db.tx[gtx];
+        iso_gtx[i] = gtx;
+        iso_start[i] = ti.start;
+        iso_len[i] = ti.len;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t pre = 0;
+        for (uint32_t i = 0; i < niso; i++) {
+            iso_pre[i] = pre;
+            const int L = (int)iso_len[i];
+            pre += (L >= W16) ? 2u * (uint32_t)((L - W16) / stride + 1) : 0u;
+        }
+        iso_pre[niso] = pre;
+    }
+    __syncthreads();
+    const uint32_t n_items = iso_pre[niso];
+    const uint32_t gl = g - P.gene_begin;
+
+    int T0 = 0, T1 = N;
+    while (T0 < N) {
+        if (tid == 0) {
+            sh_nseed = 0;
+            sh_flags = 0;
+        }
+        __syncthreads();
+        for (uint32_t ib = 0; ib < n_items; ib += SBLOCK) {
+            const uint32_t it = ib + tid;
+            uint32_t lo = 0, cnt = 0, info = 0;
+            if (it < n_items) {
+                uint32_t ii = 0;
+                while (ii + 1 < niso && iso_pre[ii + 1] <= it) ii++;
+                const uint32_t rem = it - iso_pre[ii];
+                const uint32_t ns = (iso_pre[ii + 1] - iso_pre[ii]) >> 1;
+                const int strand = rem >= ns ? 1 : 0;
+                const int p = (int)(rem - (strand ? ns : 0)) * stride;
+                info = ii | ((uint32_t)strand << 7) | ((uint32_t)p << 8);
+                QGeo qg = {iso_start[ii], (int)iso_len[ii]};
+                const uint64_t qp = qfwd_pos(qg, strand, total, p);
+                const uint64_t *QA = strand ? db.RC : db.F;
+                bool ok = true;
+                if (AMB) {
+                    const uint64_t *QM = strand ? db.ARC : db.AF;
+                    ok = (win(QM, qp) & 0xFFFFFFFFull) == 0;
+                }
+                if (ok) {
+                    const uint32_t key = (uint32_t)win(QA, qp);
+                    const uint32_t b = key >> (32 - ix.bits);
+                    uint32_t a0 = ix.bucket[b], a1 = ix.bucket[b + 1];
+                    while (a0 < a1 && ix.keys[a0] < key) a0++;
+                    uint32_t a2 = a0;
+                    while (a2 < a1 && ix.keys[a2] == key) a2++;
+                    lo = a0;
+                    cnt = a2 - a0;
+                }
+            }
+            it_lo[tid] = lo;
+            it_info[tid] = info;
+            it_pre[tid] = cnt;
+            __syncthreads();
+            if (tid == 0) {
+                uint32_t s = 0;
+                for (int i = 0; i < SBLOCK; i++) {
+                    const uint32_t c = it_pre[i];
+                    it_pre[i] = s;
+                    s += c;
+                }
+                it_pre[SBLOCK] = s;
+            }
+            __syncthreads();
+            const uint32_t nh = it_pre[SBLOCK];
+            for (uint32_t h = tid; h < nh; h += SBLOCK) {
+                int lo2 = 0, hi2 = SBLOCK;   // last k with it_pre[k] <= h
+                while (hi2 - lo2 > 1) {
+                    const int mid = (lo2 + hi2) >> 1;
+                    if (it_pre[mid] <= h) lo2 = mid; else hi2 = mid;
+                }
+                const int k = lo2;
+                const uint2 e = ix.ent[it_lo[k] + (h - it_pre[k])];
+                const TxInfo st = db.tx[e.x];
+                if (st.sample == Q || st.sample < T0 || st.sample >= T1) continue;
+                const uint32_t inf = it_info[k];
+                const uint32_t ii = inf & 127;
+                const int strand = (inf >> 7) & 1;
+                const int p = (int)(inf >> 8);
+                const int off = (int)e.y;
+                QGeo qg = {iso_start[ii], (int)iso_len[ii]};
+                const int maxl = min(min(p, off), stride);
+                const uint64_t *QL = strand ? db.F : db.RC;
+                const uint64_t *QLM = strand ? db.AF : db.ARC;
+                const int l = lcp<AMB>(QL, QLM, qrev_pos(qg, strand, total, p), db.RC, db.ARC,
+                                       total - st.start - (uint64_t)off, maxl);
+                if (l >= stride) continue;   // not canonical
+                const uint64_t *QR = strand ? db.RC : db.F;
+                const uint64_t *QRM = strand ? db.ARC : db.AF;
+                const int maxr = min(qg.Lq - p - W16, (int)st.len - off - W16);
+                const int r = lcp<AMB>(QR, QRM, qfwd_pos(qg, strand, total, p + W16), db.F, db.AF,
+                                       st.start + (uint64_t)off + W16, maxr);
+                const int len = l + W16 + r;
+                if (len < P.word) continue;
+                const uint32_t slot = atomicAdd(&sh_nseed, 1u);
+                if (slot < (uint32_t)SEED_CAP) {
+                    LSeed sd;
+                    sd.k1 = ((uint64_t)ii << 57) | ((uint64_t)strand << 56) | ((uint64_t)e.x << 24) |
+                            (uint64_t)(uint32_t)(p - l);
+                    sd.y = (uint32_t)(off - l);
+                    sd.len = (uint32_t)len;
+                    seeds[slot] = sd;
+                } else {
+                    atomicOr(&sh_flags, 1u);
+                }
+            }
+            __syncthreads();
+        }
+        if (sh_flags & 1u) {   // too many seeds: fewer subject samples per pass
+            if (T1 - T0 == 1) {
+                if (tid == 0) atomicOr(P.status, 2u);
+                return;
+            }
+            T1 = T0 + (T1 - T0) / 2;
+            __syncthreads();
+            continue;
+        }
+        const uint32_t nseed = sh_nseed;
+        // bitonic sort by (k1, y)
+        uint32_t np2 = 1;
+        while (np2 < nseed) np2 <<= 1;
+        for (uint32_t i = nseed + tid; i < np2; i += SBLOCK) {
+            seeds[i].k1 = ~0ull;
+            seeds[i].y = 0xFFFFFFFFu;
+        }
+        __syncthreads();
+        for (uint32_t kk = 2; kk <= np2; kk <<= 1) {
+            for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = tid; i < np2; i += SBLOCK) {
+                    const uint32_t ixj = i ^ j;
+                    if (ixj > i) {
+                        LSeed a = seeds[i], b = seeds[ixj];
+                        const bool gt = (a.k1 > b.k1) || (a.k1 == b.k1 && a.y > b.y);
+                        const bool up = (i & kk) == 0;
+                        if (gt == up) {
+                            seeds[i] = b;
+                            seeds[ixj] = a;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        // candidates (segments of equal (iso, strand, gtx))
+        if (tid == 0) {
+            uint32_t ns = 0;
+            for (uint32_t i = 0; i < nseed; i++)
+                if (i == 0 || (seeds[i].k1 >> 24) != (seeds[i - 1].k1 >> 24)) seg_begin[ns++] = (uint16_t)i;
+            seg_begin[ns] = (uint16_t)nseed;
+            sh_nseg = ns;
+        }
+        for (int T = tid; T < N; T += SBLOCK) tcnt[T] = 0;
+        __syncthreads();
+        const uint32_t nseg = sh_nseg;
+        for (uint32_t sg = tid; sg < nseg; sg += SBLOCK) {
+            const uint32_t gtx = (uint32_t)(seeds[seg_begin[sg]].k1 >> 24);
+            atomicAdd(&tcnt[db.tx[gtx].sample], 1u);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t s = 0;
+            for (int T = 0; T < N; T++) {
+                tpre[T] = s;
+                s += tcnt[T];
+            }
+            tpre[N] = s;
+            sh_sbase = nseed ? atomicAdd(&P.seed_count[shard], (unsigned long long)nseed) : 0ull;
+            sh_cbase = nseg ? atomicAdd(&P.cand_count[shard], (unsigned long long)nseg) : 0ull;
+            if (sh_sbase + nseed > P.seed_cap || sh_cbase + nseg > P.cand_cap) atomicOr(P.status, 1u);
+        }
+        __syncthreads();
+        const bool room = sh_sbase + nseed <= P.seed_cap && sh_cbase + nseg <= P.cand_cap;
+        const uint64_t sbase = (uint64_t)shard * P.seed_cap + sh_sbase;
+        const uint64_t cbase = (uint64_t)shard * P.cand_cap + sh_cbase;
+        if (room) {
+            for (uint32_t i = tid; i < nseed; i += SBLOCK) {
+                GSeed gs;
+                gs.x = (uint32_t)(seeds[i].k1 & 0xFFFFFFull);
+                gs.y = seeds[i].y;
+                gs.len = seeds[i].len;
+                P.seeds[sbase + i] = gs;
+            }
+            for (uint32_t sg = tid; sg < nseg; sg += SBLOCK) {
+                const uint32_t b0 = seg_begin[sg], b1 = seg_begin[sg + 1];
+                const uint64_t k1 = seeds[b0].k1;
+                const uint32_t gtx = (uint32_t)(k1 >> 24);
+                const int T = db.tx[gtx].sample;
+                uint32_t rk = 0;   // rank among earlier candidates of the same sample
+                for (uint32_t s2 = 0; s2 < sg; s2++)
+                    rk += db.tx[(uint32_t)(seeds[seg_begin[s2]].k1 >> 24)].sample == T;
+                Cand c;
+                c.seed_off = (uint32_t)(sbase + b0);
+                c.q_gtx = iso_gtx[(uint32_t)(k1 >> 57)];
+                c.s_gtx = gtx;
+                c.seed_cnt = (uint16_t)(b1 - b0);
+                c.strand = (uint8_t)((k1 >> 56) & 1);
+                c.pad = 0;
+                P.cands[cbase + tpre[T] + rk] = c;
+            }
+        }
+        for (int T = T0 + tid; T < T1; T += SBLOCK) {
+            const size_t gi = (size_t)gl * (size_t)N + (size_t)T;
+            P.gc_off[gi] = (uint32_t)(cbase + tpre[T]);
+            P.gc_cnt[gi] = tcnt[T];
+        }
+        T0 = T1;
+        T1 = N;
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------
+// extension
+// ------------------------------------------------------------------------
+
+struct ExtRes {
+    int score, i, j, d, g, o;
+};
+
+__device__ __forceinline__ int wave_max(int v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off));
+    return v;
+}
+
+// Greedy X-drop extension (oracle/align_oracle.c greedy_ext), one diagonal per
+// lane; A/B are forward walks (pa/pb = position of the first base). Stops as
+// soon as no live diagonal can still beat the best score (score + 2 * bases
+// left on the shorter side <= best): the result is unchanged.
+template <bool AMB>
+__device__ __forceinline__ ExtRes ext_wave(const uint64_t *A, const uint64_t *AA, uint64_t pa, int alen,
+                                           const uint64_t *B, const uint64_t *BA, uint64_t pb, int blen,
+                                           int X, int lane)
+{
+    const int k = lane + BAND_LO;
+    int R = -1, G = 0, O = 0, E = 0;
+    int r0 = 0;
+    if (lane == -BAND_LO) {
+        r0 = lcp<AMB>(A, AA, pa, B, BA, pb, min(alen, blen));
+        R = r0;
+    }
+    r0 = __shfl(r0, -BAND_LO);
+    ExtRes best = {2 * r0, r0, r0, 0, 0, 0};
+    if (2 * min(alen - r0, blen - r0) <= 0) return best;
+    for (int d = 1; d <= DMAX; ++d) {
+        const int goe = G | (O << 13) | (E << 26);
+        int Rl = __shfl_up(R, 1), Rr = __shfl_down(R, 1);
+        int gl = __shfl_up(goe, 1), gr = __shfl_down(goe, 1);
+        if (lane == 0) Rl = -1;
+        if (lane == 63) Rr = -1;
+        int ni = -1, ng = 0, no = 0, ne = 0;
+        if (R >= 0 && R < alen && R - k < blen) {
+            ni = R + 1; ng = G; no = O; ne = 0;
+        }
+        if (Rl >= 0 && Rl < alen) {
+            const int c = Rl + 1;
+            if (c > ni) {
+                ni = c;
+                ng = (gl & 8191) + 1;
+                no = ((gl >> 13) & 8191) + (((gl >> 26) & 3) == 1 ? 0 : 1);
+                ne = 1;
+            }
+        }
+        if (Rr >= 0 && Rr - (k + 1) < blen) {
+            const int c = Rr;
+            if (c > ni) {
+                ni = c;
+                ng = (gr & 8191) + 1;
+                no = ((gr >> 13) & 8191) + (((gr >> 26) & 3) == 2 ? 0 : 1);
+                ne = 2;
+            }
+        }
+        int score = INT_MIN, bound = INT_MIN;
+        if (ni >= 0 && ni - k >= 0) {
+            const int ja = ni - k;
+            const int m = min(alen - ni, blen - ja);
+            const int s = lcp<AMB>(A, AA, pa + (uint64_t)ni, B, BA, pb + (uint64_t)ja, m);
+            if (s > 0) {
+                ni += s;
+                ne = 0;
+            }
+            score = 2 * ni - k - 6 * d;
+            if (score < best.score - X) ni = -1;
+            else bound = score + 2 * (m - s);
+        } else {
+            ni = -1;
+        }
+        R = ni; G = ng; O = no; E = ne;
+        const bool live = ni >= 0;
+        const uint64_t lm = __ballot(live);
+        if (lm == 0) break;
+        const int mx = wave_max(live ? score : INT_MIN);
+        if (mx > best.score) {
+            const uint64_t tm = __ballot(live && score == mx);
+            const int bl = __ffsll((unsigned long long)tm) - 1;
+            best.score = mx;
+            best.i = __shfl(R, bl);
+            best.j = best.i - (bl + BAND_LO);
+            best.d = d;
+            best.g = __shfl(G, bl);
+            best.o = __shfl(O, bl);
+        }
+        if (wave_max(live ? bound : INT_MIN) <= best.score) break;
+    }
+    return best;
+}
+
+// copy 32-base windows [pos, pos + 32 * n) of a packed array into LDS
+__device__ __forceinline__ void stage(uint64_t *dst, const uint64_t *src, uint64_t pos, int n, int lane)
+{
+    for (int w = lane; w < n; w += 64) dst[w] = win(src, pos + 32 * (uint64_t)w);
+}
+
+// One candidate (all its seeds) on one wave. Positions: query walks on
+// (QF, QR) arrays whose oriented position u lives at qf0 + u / qr0 + u, the
+// subject walks on (TF, TR) arrays at tf0 + v / tr0 + v (see the oracle's
+// walker); in LDS the bases are 0.
+template <bool AMB>
+__device__ __forceinline__ void process_candidate(
+    const uint64_t *QF, const uint64_t *QFM, uint64_t qf0, const uint64_t *QR, const uint64_t *QRM, uint64_t qr0,
+    const uint64_t *TF, const uint64_t *TFM, uint64_t tf0, const uint64_t *TR, const uint64_t *TRM, uint64_t tr0,
+    int Lq, int Lt, int strand, const GSeed *sd, int ns, int X, int lane, int &bqa, int &bqb, int &bsa, int &bsb,
+    int &bsc, int &bd, int &bg, int &bo, int &bni, int &nh)
+{
+    // oriented query forward walk: strand 0 -> QF (forward), 1 -> QR (revcomp);
+    // leftwards walk from x: strand 0 -> QR at Lq - x, 1 -> QF at Lq - x
+    const uint64_t *AR = strand ? QR : QF;
+    const uint64_t *ARM = strand ? QRM : QFM;
+    const uint64_t ar0 = strand ? qr0 : qf0;
+    const uint64_t *AL = strand ? QF : QR;
+    const uint64_t *ALM = strand ? QFM : QRM;
+    const uint64_t al0 = strand ? qf0 : qr0;
+    nh = 0;
+    for (int si = 0; si < ns && nh < MAX_HSP; si++) {
+        const GSeed s = sd[si];
+        const int x = (int)s.x, y = (int)s.y, len = (int)s.len;
+        const bool inside = lane < nh && bqa <= x && x + len <= bqb && bsa <= y && y + len <= bsb;
+        if (__ballot(inside)) continue;
+        const ExtRes r = ext_wave<AMB>(AR, ARM, ar0 + (uint64_t)(x + len), Lq - (x + len), TF, TFM,
+                                       tf0 + (uint64_t)(y + len), Lt - (y + len), X, lane);
+        const ExtRes l = ext_wave<AMB>(AL, ALM, al0 + (uint64_t)(Lq - x), x, TR, TRM, tr0 + (uint64_t)(Lt - y), y,
+                                       X, lane);
+        if (lane == nh) {
+            bqa = x - l.i; bqb = x + len + r.i; bsa = y - l.j; bsb = y + len + r.j;
+            bsc = l.score + 2 * len + r.score;
+            bd = l.d + r.d; bg = l.g + r.g; bo = l.o + r.o;
+            bni = len + (l.i + l.j - 2 * l.d + l.g) / 2 + (r.i + r.j - 2 * r.d + r.g) / 2;
+        }
+        nh++;
+    }
+}
+
+template <bool AMB>
+__global__ __launch_bounds__(EBLOCK) void extend_kernel(Db db, ExtParams P)
+{
+    constexpr int NA = AMB ? 8 : 4;
+    __shared__ uint64_t stg[EWAVES][NA][SW];
+    __shared__ GSeed sseed[EWAVES][64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t total = db.total;
+    const uint64_t nwaves = (uint64_t)gridDim.x * EWAVES;
+    for (uint64_t li = (uint64_t)blockIdx.x * EWAVES + wid; li < P.n_cand; li += nwaves) {
+        int lo = 0, hi = NSHARD;   // shard of linear candidate li
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (P.shard_prefix[mid] <= li) lo = mid; else hi = mid;
+        }
+        const uint64_t ci = (uint64_t)lo * P.cand_cap + (li - P.shard_prefix[lo]);
+        const Cand cd = P.cands[ci];
+        const TxInfo qt = db.tx[cd.q_gtx], st = db.tx[cd.s_gtx];
+        const int Lq = (int)qt.len, Lt = (int)st.len;
+        const int strand = cd.strand;
+        const int ns = cd.seed_cnt;
+        // seeds: through LDS when few (the common case), else straight from HBM
+        const GSeed *sd = P.seeds + cd.seed_off;
+        if (ns <= 64) {
+            if (lane < ns) sseed[wid][lane] = sd[lane];
+            sd = sseed[wid];
+        }
+        int bqa = 0, bqb = 0, bsa = 0, bsb = 0, bsc = 0, bd = 0, bg = 0, bo = 0, bni = 0, nh = 0;
+        const uint64_t qr_g = total - qt.start - (uint64_t)Lq;   // revcomp(q) start in RC
+        const uint64_t tr_g = total - st.start - (uint64_t)Lt;
+        if (Lq + 32 <= STAGE_BASES && Lt + 32 <= STAGE_BASES) {
+            uint64_t *QF = stg[wid][0], *QR = stg[wid][1], *TF = stg[wid][2], *TR = stg[wid][3];
+            const int nq = (Lq >> 5) + 2, nt = (Lt >> 5) + 2;
+            stage(QF, db.F, qt.start, nq, lane);
+            stage(QR, db.RC, qr_g, nq, lane);
+            stage(TF, db.F, st.start, nt, lane);
+            stage(TR, db.RC, tr_g, nt, lane);
+            uint64_t *QFM = nullptr, *QRM = nullptr, *TFM = nullptr, *TRM = nullptr;
+            if (AMB) {
+                QFM = stg[wid][NA - 4]; QRM = stg[wid][NA - 3]; TFM = stg[wid][NA - 2]; TRM = stg[wid][NA - 1];
+                stage(QFM, db.AF, qt.start, nq, lane);
+                stage(QRM, db.ARC, qr_g, nq, lane);
+                stage(TFM, db.AF, st.start, nt, lane);
+                stage(TRM, db.ARC, tr_g, nt, lane);
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            process_candidate<AMB>(QF, QFM, 0, QR, QRM, 0, TF, TFM, 0, TR, TRM, 0, Lq, Lt, strand, sd, ns, P.xdrop,
+                                   lane, bqa, bqb, bsa, bsb, bsc, bd, bg, bo, bni, nh);
+        } else {
+            process_candidate<AMB>(db.F, db.AF, qt.start, db.RC, db.ARC, qr_g, db.F, db.AF, st.start, db.RC, db.ARC,
+                                   tr_g, Lq, Lt, strand, sd, ns, P.xdrop, lane, bqa, bqb, bsa, bsb, bsc, bd, bg, bo,
+                                   bni, nh);
+        }
+        // purge HSPs with common endpoints: by (score desc, index asc)
+        int rank = 0;
+        for (int j = 0; j < nh; j++) {
+            const int sj = __shfl(bsc, j);
+            if (lane < nh && (sj > bsc || (sj == bsc && j < lane))) rank++;
+        }
+        bool kept = false;
+        for (int rr = 0; rr < nh; rr++) {
+            const uint64_t m = __ballot(lane < nh && rank == rr);
+            const int i = __ffsll((unsigned long long)m) - 1;
+            const int qa = __shfl(bqa, i), sa = __shfl(bsa, i), qb = __shfl(bqb, i), sb2 = __shfl(bsb, i);
+            const bool conflict = kept && lane < nh && ((bqa == qa && bsa == sa) || (bqb == qb && bsb == sb2));
+            if (!__ballot(conflict) && lane == i) kept = true;
+        }
+        const int thr = P.thr[(size_t)st.sample * (size_t)(P.max_len + 1) + (size_t)Lq];
+        const bool out = kept && bsc >= thr;
+        const uint64_t om = __ballot(out);
+        const int nout = __popcll(om);
+        uint32_t obase = 0;
+        if (nout > 1 && lane == 0) {
+            const unsigned long long b = atomicAdd(P.ovf_count, (unsigned long long)(nout - 1));
+            if (b + (nout - 1) > P.ovf_cap) atomicOr(P.status, 1u);
+            obase = (uint32_t)b;
+        }
+        obase = __shfl(obase, 0);
+        if (out) {
+            const int rk = __popcll(om & ((1ull << lane) - 1ull));
+            DHsp h;
+            h.q_tx = cd.q_gtx;
+            h.s_tx = cd.s_gtx;
+            if (!strand) {
+                h.qstart = bqa + 1; h.qend = bqb; h.sstart = bsa + 1; h.send = bsb;
+            } else {
+                h.qstart = Lq - bqb + 1; h.qend = Lq - bqa; h.sstart = bsb; h.send = bsa + 1;
+            }
+            h.gaps = bg;
+            h.gapopen = bo;
+            h.mismatch = bd - bg;
+            h.nident = bni;
+            h.length = bni + (bd - bg) + bg;
+            h.score_half = bsc;
+            h.bits10 = P.bits10[bsc];
+            h.strand = strand;
+            if (rk == 0) P.cand_hsp[ci] = h;
+            else if ((uint64_t)obase + (rk - 1) < P.ovf_cap) P.ovf[obase + rk - 1] = h;
+        }
+        if (lane == 0) {
+            P.cand_nh[ci] = (uint8_t)nout;
+            P.cand_ovf[ci] = obase;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------
+// (gene, sample) groups
+// ------------------------------------------------------------------------
+
+__global__ void group_count_kernel(GroupParams P)
+{
+    const uint64_t n = (uint64_t)(P.gene_end - P.gene_begin) * (uint64_t)P.N;
+    for (uint64_t gi = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; gi < n;
+         gi += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t o = P.gc_off[gi], c = P.gc_cnt[gi];
+        uint32_t s = 0;
+        for (uint32_t i = 0; i < c; i++) s += P.cand_nh[o + i];
+        P.cnt[gi] = s;
+    }
+}
+
+__global__ void group_write_kernel(GroupParams P)
+{
+    const uint64_t n = (uint64_t)(P.gene_end - P.gene_begin) * (uint64_t)P.N;
+    for (uint64_t gi = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; gi < n;
+         gi += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t o = P.gc_off[gi], c = P.gc_cnt[gi];
+        uint64_t w = P.scan[gi];
+        const uint64_t gg = (uint64_t)P.gene_begin * P.N + gi;
+        P.grp_off[gg] = (uint32_t)w;
+        P.grp_cnt[gg] = P.cnt[gi];
+        for (uint32_t i = 0; i < c; i++) {
+            const uint32_t nh = P.cand_nh[o + i];
+            if (!nh) continue;
+            P.out[w++] = P.cand_hsp[o + i];
+            const uint32_t ov = P.cand_ovf[o + i];
+            for (uint32_t k = 1; k < nh; k++) P.out[w++] = P.ovf[ov + k - 1];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------
+
+void launch_seed(bool amb, const Db &db, const Index &ix, const SeedParams &P, hipStream_t st)
+{
+    const uint32_t n = P.gene_end - P.gene_begin;
+    if (n == 0) return;
+    if (amb)
+        hipLaunchKernelGGL(seed_kernel<true>, dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
+    else
+        hipLaunchKernelGGL(seed_kernel<false>, dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
+}
+
+void launch_extend(bool amb, const Db &db, const ExtParams &P, hipStream_t st)
+{
+    if (P.n_cand == 0) return;
+    uint64_t blocks = (P.n_cand + EWAVES - 1) / EWAVES;
+    const uint64_t cap = 256ull * 8;    // about two resident waves per SIMD slot; waves loop
+    if (blocks > cap) blocks = cap;
+    if (amb)
+        hipLaunchKernelGGL(extend_kernel<true>, dim3((unsigned)blocks), dim3(EBLOCK), 0, st, db, P);
+    else
+        hipLaunchKernelGGL(extend_kernel<false>, dim3((unsigned)blocks), dim3(EBLOCK), 0, st, db, P);
+}
+
+void launch_group(const GroupParams &P, int pass, hipStream_t st)
+{
+    const uint64_t n = (uint64_t)(P.gene_end - P.gene_begin) * (uint64_t)P.N;
+    if (!n) return;
+    uint64_t g = (n + 255) / 256;
+    if (g > 65536) g = 65536;
+    if (pass == 0)
+        hipLaunchKernelGGL(group_count_kernel, dim3((unsigned)g), dim3(256), 0, st, P);
+    else
+        hipLaunchKernelGGL(group_write_kernel, dim3((unsigned)g), dim3(256), 0, st, P);
+}
+
+}  // namespace rcg

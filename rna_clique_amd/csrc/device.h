@@ -65,20 +65,69 @@ struct Index {
     int32_t bits;
 };
 
-struct AlignParams {
-    int32_t word;               // W
-    int32_t stride;             // W - 16 + 1
-    int32_t xdrop;              // half units
-    int32_t max_len;            // longest transcript
-    const int32_t *thr;         // [n_samples][max_len + 1] min score_half
-    const int32_t *bits10;      // [2 * max_len + 2]
+constexpr int NSHARD = 256;    // output allocation shards (spread the atomics)
+
+// Seed (maximal exact run >= W) of one candidate, oriented query coordinates.
+struct GSeed {
+    uint32_t x, y, len;
+};
+
+// Candidate = (query transcript, strand, subject transcript) with >= 1 seed.
+struct Cand {
+    uint32_t seed_off;     // absolute index of its first seed (sorted by (x, y))
+    uint32_t q_gtx, s_gtx;
+    uint16_t seed_cnt;
+    uint8_t strand, pad;
+};
+
+// seed_kernel: per query gene, lookups -> canonical seeds -> candidates.
+struct SeedParams {
+    int32_t word;                 // W
+    int32_t stride;               // W - 16 + 1
     uint32_t gene_begin, gene_end;   // shard
-    DHsp *out;                  // scratch HSPs
-    uint64_t out_cap;
-    unsigned long long *out_count;
-    uint32_t *grp_off;          // [(g - gene_begin) * n_samples + T] scratch offset
-    uint32_t *grp_cnt;          // count
-    unsigned int *status;       // bit 0 scratch overflow, bit 1 gene limit
+    GSeed *seeds;
+    uint64_t seed_cap;            // per allocation shard
+    unsigned long long *seed_count;  // [NSHARD]
+    Cand *cands;
+    uint64_t cand_cap;            // per allocation shard
+    unsigned long long *cand_count;  // [NSHARD]
+    uint32_t *gc_off, *gc_cnt;    // [(g - gene_begin) * N + T] candidates of (gene, sample)
+    unsigned int *status;         // bit 0 overflow, bit 1 gene limit
+};
+
+// extend_kernel: one wave per candidate, greedy X-drop, purge, e-value cut.
+struct ExtParams {
+    int32_t xdrop;
+    int32_t max_len;
+    const int32_t *thr;           // [n_samples][max_len + 1] min score_half
+    const int32_t *bits10;        // [2 * max_len + 2]
+    const Cand *cands;
+    const GSeed *seeds;
+    const unsigned long long *shard_prefix;   // NSHARD + 1 prefix of candidate counts
+    uint64_t n_cand;
+    uint64_t cand_cap;
+    DHsp *cand_hsp;               // first HSP of each candidate (absolute index)
+    uint8_t *cand_nh;             // HSPs kept per candidate
+    uint32_t *cand_ovf;           // overflow offset of HSPs 2..nh
+    DHsp *ovf;
+    uint64_t ovf_cap;
+    unsigned long long *ovf_count;
+    unsigned int *status;         // bit 0 overflow
+};
+
+// group kernels: candidates of each (gene, sample) -> contiguous HSP groups.
+struct GroupParams {
+    uint32_t gene_begin, gene_end;
+    int32_t N;
+    const uint32_t *gc_off, *gc_cnt;   // shard-relative gene index
+    const uint8_t *cand_nh;
+    const DHsp *cand_hsp;
+    const uint32_t *cand_ovf;
+    const DHsp *ovf;
+    uint32_t *cnt;                // [(g - gene_begin) * N + T] HSPs per group
+    const uint64_t *scan;         // exclusive scan of cnt
+    uint32_t *grp_off, *grp_cnt;  // global-gene group table
+    DHsp *out;
 };
 
 // Parameters of the two reciprocal-best-hit passes.
@@ -99,5 +148,47 @@ struct RbhParams {
     DRow *rows;
     DEdge *edges;
 };
+
+// ------------------------------------------------------------------------
+// 2-bit windows
+// ------------------------------------------------------------------------
+
+// 32 bases starting at base position p (base i in bits 2i..2i+1).
+__device__ __forceinline__ uint64_t win(const uint64_t *__restrict__ a, uint64_t p)
+{
+    const uint64_t w = p >> 5;
+    const unsigned sh = (unsigned)(p & 31) * 2u;
+    const uint64_t lo = a[w];
+    if (sh == 0) return lo;
+    return (lo >> sh) | (a[w + 1] << (64u - sh));
+}
+
+// Longest common extension of two forward walks (at most maxn bases).
+// Ambiguous bases (mask 0b11) never match.
+template <bool AMB>
+__device__ __forceinline__ int lcp(const uint64_t *__restrict__ A, const uint64_t *__restrict__ AA,
+                                   uint64_t pa, const uint64_t *__restrict__ B,
+                                   const uint64_t *__restrict__ BA, uint64_t pb, int maxn)
+{
+    int n = 0;
+    while (n < maxn) {
+        uint64_t x = win(A, pa + n) ^ win(B, pb + n);
+        if (AMB) x |= win(AA, pa + n) | win(BA, pb + n);
+        if (x == 0) {
+            n += 32;
+            continue;
+        }
+        n += __builtin_ctzll(x) >> 1;
+        return n < maxn ? n : maxn;
+    }
+    return maxn > 0 ? maxn : 0;
+}
+
+__device__ __forceinline__ uint64_t rev2(uint64_t x)
+{
+    x = ((x >> 2) & 0x3333333333333333ull) | ((x & 0x3333333333333333ull) << 2);
+    x = ((x >> 4) & 0x0F0F0F0F0F0F0F0Full) | ((x & 0x0F0F0F0F0F0F0F0Full) << 4);
+    return __builtin_bswap64(x);
+}
 
 }  // namespace rcg

@@ -26,7 +26,9 @@ void launch_kmer_count(const TxInfo *, uint32_t, const uint64_t *, uint64_t *, h
 void launch_kmer_fill(bool, const TxInfo *, uint32_t, const uint64_t *, const uint64_t *, const uint64_t *,
                       uint32_t *, uint64_t *, hipStream_t);
 void launch_bucket_fill(const uint32_t *, uint64_t, int, uint32_t *, hipStream_t);
-void launch_align(bool, const Db &, const Index &, const AlignParams &, hipStream_t);
+void launch_seed(bool, const Db &, const Index &, const SeedParams &, hipStream_t);
+void launch_extend(bool, const Db &, const ExtParams &, hipStream_t);
+void launch_group(const GroupParams &, int, hipStream_t);
 
 void launch_rbh(const RbhParams &, int, hipStream_t);
 void launch_cc(const DEdge *, uint64_t, uint32_t, const int32_t *, int, uint32_t *, uint32_t *, uint32_t *,
@@ -220,7 +222,14 @@ struct rc_engine {
     DBuf<uint8_t> d_tmp;
     DBuf<int32_t> d_thr, d_bits10;
     DBuf<DHsp> d_hsp;
-    uint64_t hsp_cap_hint = 0;
+    DBuf<GSeed> d_seeds;
+    DBuf<Cand> d_cands;
+    DBuf<DHsp> d_cand_hsp, d_ovf;
+    DBuf<uint8_t> d_cand_nh;
+    DBuf<uint32_t> d_cand_ovf, d_gc_off, d_gc_cnt, d_gcount;
+    DBuf<uint64_t> d_gscan;
+    DBuf<unsigned long long> d_shard_cnt, d_shard_prefix;
+    uint64_t seed_cap = 0, cand_cap = 0, ovf_cap = 0;   // per-shard / total capacities
     DBuf<uint32_t> d_grp_off, d_grp_cnt;
     DBuf<unsigned long long> d_count;
     DBuf<unsigned int> d_status;
@@ -230,7 +239,7 @@ struct rc_engine {
     DBuf<uint64_t> d_off4;   // 4 * (n_items + 1)
     DBuf<DRow> d_rows;
     DBuf<DEdge> d_edges;
-    uint64_t n_rows = 0, n_edges = 0, n_hsps = 0;
+    uint64_t n_rows = 0, n_edges = 0, n_hsps = 0, n_seeds = 0, n_cands = 0;
     DBuf<uint32_t> d_parent, d_present, d_cnodes, d_cedges, d_sample_present;
     DBuf<uint8_t> d_ideal;
     DBuf<unsigned long long> d_stats, d_num, d_den;
@@ -240,7 +249,7 @@ struct rc_engine {
     // host results
     std::vector<unsigned long long> h_num, h_den, h_stats;
     rc_timing tm{};
-    hipEvent_t ev[12] = {};
+    hipEvent_t ev[16] = {};
 
     ~rc_engine()
     {
@@ -440,7 +449,7 @@ static int upload(rc_engine *e)
 
     // device copies
     const uint64_t total = e->seq.size();
-    const uint64_t nwords = (total + 31) / 32 + 2;
+    const uint64_t nwords = (total + 31) / 32 + 4;
     CHK(e->d_ascii.ensure(total + 64));
     HIPCHK(hipMemcpyAsync(e->d_ascii.p, e->seq.data(), total, hipMemcpyHostToDevice, e->st));
     CHK(e->d_F.ensure(nwords));
@@ -661,62 +670,163 @@ static int do_align(rc_engine *e)
     uint32_t g0, g1;
     shard_range(e, g0, g1);
     const uint32_t n_genes = (uint32_t)e->gene_sample.size();
+    const uint64_t sg = (uint64_t)(g1 - g0);
     const size_t ngrp = (size_t)n_genes * N;
+    const size_t nsgrp = (size_t)sg * N;
     CHK(e->d_grp_off.ensure(ngrp));
     CHK(e->d_grp_cnt.ensure(ngrp));
-    if (e->hsp_cap_hint == 0) e->hsp_cap_hint = (uint64_t)(g1 - g0) * (uint64_t)std::max(N - 1, 1) * 2 + 1024;
+    CHK(e->d_gc_off.ensure(nsgrp));
+    CHK(e->d_gc_cnt.ensure(nsgrp));
+    CHK(e->d_gcount.ensure(nsgrp + 1));
+    CHK(e->d_gscan.ensure(nsgrp + 1));
+    CHK(e->d_shard_cnt.ensure(2 * NSHARD));
+    CHK(e->d_shard_prefix.ensure(NSHARD + 1));
+    if (e->seed_cap == 0) {
+        const uint64_t nb = std::max<uint64_t>(sg, 1) * (uint64_t)std::max(N - 1, 1);
+        e->seed_cap = nb * 16 / NSHARD + 4096;
+        e->cand_cap = nb * 2 / NSHARD + 1024;
+        e->ovf_cap = nb / 4 + 1024;
+    }
+    Db db = make_db(e);
     Index ix;
-    for (int attempt = 0; attempt < 3; attempt++) {
-        CHK(e->d_hsp.ensure(e->hsp_cap_hint));
-        HIPCHK(hipMemsetAsync(e->d_grp_cnt.p, 0, ngrp * 4, e->st));
-        HIPCHK(hipMemsetAsync(e->d_grp_off.p, 0, ngrp * 4, e->st));
-        HIPCHK(hipMemsetAsync(e->d_count.p, 0, 4 * sizeof(unsigned long long), e->st));
+    ix.keys = e->d_keys2.p;
+    ix.ent = reinterpret_cast<const uint2 *>(e->d_vals2.p);
+    ix.bucket = e->d_bucket.p;
+    ix.bits = e->index_bits;
+    // --- seeds ---
+    std::vector<unsigned long long> shard_cnt(2 * NSHARD);
+    for (int attempt = 0;; attempt++) {
+        if (attempt == 4) return fail(RC_E_NOMEM, "seed/candidate buffers kept overflowing");
+        if (e->seed_cap * NSHARD > 0xFFFFFFFFull || e->cand_cap * NSHARD > 0xFFFFFFFFull)
+            return fail(RC_E_LIMIT, "more than 2^32 seeds or candidates on one GPU: use more shards");
+        CHK(e->d_seeds.ensure(e->seed_cap * NSHARD));
+        CHK(e->d_cands.ensure(e->cand_cap * NSHARD));
+        HIPCHK(hipMemsetAsync(e->d_shard_cnt.p, 0, 2 * NSHARD * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
-        Db db = make_db(e);
-        ix.keys = e->d_keys2.p;
-        ix.ent = reinterpret_cast<const uint2 *>(e->d_vals2.p);
-        ix.bucket = e->d_bucket.p;
-        ix.bits = e->index_bits;
-        AlignParams P;
-        P.word = e->o.word_size;
-        P.stride = e->o.word_size - W16 + 1;
-        P.xdrop = e->o.xdrop_half;
-        P.max_len = e->max_len;
-        P.thr = e->d_thr.p;
-        P.bits10 = e->d_bits10.p;
-        P.gene_begin = g0;
-        P.gene_end = g1;
-        P.out = e->d_hsp.p;
-        P.out_cap = e->d_hsp.cap;
-        P.out_count = e->d_count.p;
-        // groups are indexed by global gene so that rc_finish sees one table
-        P.grp_off = e->d_grp_off.p + (size_t)g0 * N;
-        P.grp_cnt = e->d_grp_cnt.p + (size_t)g0 * N;
-        P.status = e->d_status.p;
+        SeedParams S;
+        S.word = e->o.word_size;
+        S.stride = e->o.word_size - W16 + 1;
+        S.gene_begin = g0;
+        S.gene_end = g1;
+        S.seeds = e->d_seeds.p;
+        S.seed_cap = e->seed_cap;
+        S.seed_count = e->d_shard_cnt.p;
+        S.cands = e->d_cands.p;
+        S.cand_cap = e->cand_cap;
+        S.cand_count = e->d_shard_cnt.p + NSHARD;
+        S.gc_off = e->d_gc_off.p;
+        S.gc_cnt = e->d_gc_cnt.p;
+        S.status = e->d_status.p;
         HIPCHK(hipEventRecord(e->ev[3], e->st));
-        launch_align(e->has_amb, db, ix, P, e->st);
+        launch_seed(e->has_amb, db, ix, S, e->st);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(e->ev[4], e->st));
-        unsigned long long cnt = 0;
+        HIPCHK(hipEventRecord(e->ev[9], e->st));
         unsigned int status = 0;
-        HIPCHK(hipMemcpyAsync(&cnt, e->d_count.p, sizeof cnt, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipMemcpyAsync(shard_cnt.data(), e->d_shard_cnt.p, 2 * NSHARD * 8, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipStreamSynchronize(e->st));
         if (status & 2u)
-            return fail(RC_E_LIMIT, "a query gene exceeds the per-gene seed/HSP capacity against a single sample");
-        if (status & 1u) {
-            e->hsp_cap_hint = (uint64_t)(cnt * 1.25) + 1024;
-            continue;
+            return fail(RC_E_LIMIT, "a query gene has too many seeds against a single sample (or > 127 isoforms)");
+        if (!(status & 1u)) break;
+        uint64_t ms = 0, mc = 0;
+        for (int i = 0; i < NSHARD; i++) {
+            ms = std::max<uint64_t>(ms, shard_cnt[i]);
+            mc = std::max<uint64_t>(mc, shard_cnt[NSHARD + i]);
         }
-        e->n_hsps = cnt;
-        e->tm.pack_ms = ev_ms(e, 0, 1);
-        e->tm.index_ms = ev_ms(e, 1, 2);
-        e->tm.align_ms = ev_ms(e, 2, 4);
-        e->tm.align_kernel_ms = ev_ms(e, 3, 4);
-        e->aligned = true;
-        return RC_OK;
+        e->seed_cap = std::max<uint64_t>(e->seed_cap, ms * 5 / 4 + 4096);
+        e->cand_cap = std::max<uint64_t>(e->cand_cap, mc * 5 / 4 + 1024);
     }
-    return fail(RC_E_NOMEM, "HSP scratch kept overflowing");
+    std::vector<unsigned long long> prefix(NSHARD + 1, 0);
+    for (int i = 0; i < NSHARD; i++) prefix[i + 1] = prefix[i] + shard_cnt[NSHARD + i];
+    const uint64_t n_cand = prefix[NSHARD];
+    e->n_seeds = 0;
+    for (int i = 0; i < NSHARD; i++) e->n_seeds += shard_cnt[i];
+    e->n_cands = n_cand;
+    HIPCHK(hipMemcpyAsync(e->d_shard_prefix.p, prefix.data(), (NSHARD + 1) * 8, hipMemcpyHostToDevice, e->st));
+    // --- extension ---
+    const uint64_t slots = e->cand_cap * NSHARD;
+    CHK(e->d_cand_hsp.ensure(slots));
+    CHK(e->d_cand_nh.ensure(slots));
+    CHK(e->d_cand_ovf.ensure(slots));
+    for (int attempt = 0;; attempt++) {
+        if (attempt == 4) return fail(RC_E_NOMEM, "HSP overflow buffer kept overflowing");
+        CHK(e->d_ovf.ensure(e->ovf_cap));
+        HIPCHK(hipMemsetAsync(e->d_count.p, 0, 4 * sizeof(unsigned long long), e->st));
+        HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
+        ExtParams X;
+        X.xdrop = e->o.xdrop_half;
+        X.max_len = e->max_len;
+        X.thr = e->d_thr.p;
+        X.bits10 = e->d_bits10.p;
+        X.cands = e->d_cands.p;
+        X.seeds = e->d_seeds.p;
+        X.shard_prefix = e->d_shard_prefix.p;
+        X.n_cand = n_cand;
+        X.cand_cap = e->cand_cap;
+        X.cand_hsp = e->d_cand_hsp.p;
+        X.cand_nh = e->d_cand_nh.p;
+        X.cand_ovf = e->d_cand_ovf.p;
+        X.ovf = e->d_ovf.p;
+        X.ovf_cap = e->ovf_cap;
+        X.ovf_count = e->d_count.p;
+        X.status = e->d_status.p;
+        HIPCHK(hipEventRecord(e->ev[10], e->st));
+        launch_extend(e->has_amb, db, X, e->st);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(e->ev[11], e->st));
+        unsigned long long ovn = 0;
+        unsigned int status = 0;
+        HIPCHK(hipMemcpyAsync(&ovn, e->d_count.p, sizeof ovn, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipStreamSynchronize(e->st));
+        if (!(status & 1u)) break;
+        e->ovf_cap = ovn * 5 / 4 + 1024;
+    }
+    // --- groups: (query gene, subject sample) -> contiguous HSPs ---
+    GroupParams G;
+    G.gene_begin = g0;
+    G.gene_end = g1;
+    G.N = N;
+    G.gc_off = e->d_gc_off.p;
+    G.gc_cnt = e->d_gc_cnt.p;
+    G.cand_nh = e->d_cand_nh.p;
+    G.cand_hsp = e->d_cand_hsp.p;
+    G.cand_ovf = e->d_cand_ovf.p;
+    G.ovf = e->d_ovf.p;
+    G.cnt = e->d_gcount.p;
+    HIPCHK(hipMemsetAsync(e->d_grp_cnt.p, 0, ngrp * 4, e->st));
+    HIPCHK(hipMemsetAsync(e->d_grp_off.p, 0, ngrp * 4, e->st));
+    HIPCHK(hipMemsetAsync(e->d_gcount.p + nsgrp, 0, 4, e->st));
+    launch_group(G, 0, e->st);
+    {
+        size_t tmp = 0;
+        HIPCHK(rocprim::exclusive_scan(nullptr, tmp, e->d_gcount.p, e->d_gscan.p, (uint64_t)0, nsgrp + 1,
+                                       rocprim::plus<uint64_t>(), e->st));
+        CHK(e->d_tmp.ensure(tmp));
+        HIPCHK(rocprim::exclusive_scan(e->d_tmp.p, tmp, e->d_gcount.p, e->d_gscan.p, (uint64_t)0, nsgrp + 1,
+                                       rocprim::plus<uint64_t>(), e->st));
+    }
+    uint64_t nh = 0;
+    HIPCHK(hipMemcpyAsync(&nh, e->d_gscan.p + nsgrp, 8, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    if (nh > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "more than 2^32 HSPs on one GPU: use more shards");
+    CHK(e->d_hsp.ensure(nh));
+    G.scan = e->d_gscan.p;
+    G.grp_off = e->d_grp_off.p;
+    G.grp_cnt = e->d_grp_cnt.p;
+    G.out = e->d_hsp.p;
+    launch_group(G, 1, e->st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(e->ev[4], e->st));
+    HIPCHK(hipEventSynchronize(e->ev[4]));
+    e->n_hsps = nh;
+    e->tm.pack_ms = ev_ms(e, 0, 1);
+    e->tm.index_ms = ev_ms(e, 1, 2);
+    e->tm.align_ms = ev_ms(e, 2, 4);
+    e->tm.seed_kernel_ms = ev_ms(e, 3, 9);
+    e->tm.align_kernel_ms = ev_ms(e, 10, 11);
+    e->aligned = true;
+    return RC_OK;
 }
 
 static int do_finish(rc_engine *e)
@@ -951,6 +1061,8 @@ int rc_graph_stats(rc_engine *e, rc_stats *s)
     s->pad = 0;
     s->edges = (int64_t)e->n_edges;
     s->hsps = (int64_t)e->n_hsps;
+    s->seeds = (int64_t)e->n_seeds;
+    s->candidates = (int64_t)e->n_cands;
     s->table_rows = (int64_t)e->n_rows;
     return RC_OK;
 }

@@ -19,48 +19,6 @@
 namespace rcg {
 
 // ------------------------------------------------------------------------
-// 2-bit windows
-// ------------------------------------------------------------------------
-
-// 32 bases starting at base position p (base i in bits 2i..2i+1).
-__device__ __forceinline__ uint64_t win(const uint64_t *__restrict__ a, uint64_t p)
-{
-    const uint64_t w = p >> 5;
-    const unsigned sh = (unsigned)(p & 31) * 2u;
-    const uint64_t lo = a[w];
-    if (sh == 0) return lo;
-    return (lo >> sh) | (a[w + 1] << (64u - sh));
-}
-
-// Longest common extension of two forward walks (at most maxn bases).
-// Ambiguous bases (mask 0b11) never match.
-template <bool AMB>
-__device__ __forceinline__ int lcp(const uint64_t *__restrict__ A, const uint64_t *__restrict__ AA,
-                                   uint64_t pa, const uint64_t *__restrict__ B,
-                                   const uint64_t *__restrict__ BA, uint64_t pb, int maxn)
-{
-    int n = 0;
-    while (n < maxn) {
-        uint64_t x = win(A, pa + n) ^ win(B, pb + n);
-        if (AMB) x |= win(AA, pa + n) | win(BA, pb + n);
-        if (x == 0) {
-            n += 32;
-            continue;
-        }
-        n += __builtin_ctzll(x) >> 1;
-        return n < maxn ? n : maxn;
-    }
-    return maxn > 0 ? maxn : 0;
-}
-
-__device__ __forceinline__ uint64_t rev2(uint64_t x)
-{
-    x = ((x >> 2) & 0x3333333333333333ull) | ((x & 0x3333333333333333ull) << 2);
-    x = ((x >> 4) & 0x0F0F0F0F0F0F0F0Full) | ((x & 0x0F0F0F0F0F0F0F0Full) << 4);
-    return __builtin_bswap64(x);
-}
-
-// ------------------------------------------------------------------------
 // pack
 // ------------------------------------------------------------------------
 
@@ -211,454 +169,6 @@ __global__ void bucket_fill_kernel(const uint32_t *__restrict__ keys, uint64_t n
         const uint64_t lo = (i > 0) ? pb + 1 : 0;
         const uint64_t hi = (i < n) ? b : nb;
         for (uint64_t x = lo; x <= hi && x <= nb; x++) bucket[x] = (uint32_t)i;
-    }
-}
-
-// ------------------------------------------------------------------------
-// alignment
-// ------------------------------------------------------------------------
-
-constexpr int ABLOCK = 256;
-constexpr int NWAVE = ABLOCK / 64;
-constexpr int SEED_CAP = 2048;
-constexpr int HSP_CAP = 128;
-constexpr int MAX_SAMPLES = 256;
-
-struct LSeed {
-    uint64_t k1;    // iso:7 | strand:1 | gtx:32 | x:24
-    uint32_t y, len;
-};
-
-struct ExtRes {
-    int score, i, j, d, g, o;
-};
-
-__device__ __forceinline__ int wave_max(int v)
-{
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off));
-    return v;
-}
-
-// Greedy X-drop extension (oracle/align_oracle.c greedy_ext), one diagonal per
-// lane. Returns wave-uniform values.
-template <bool AMB>
-__device__ ExtRes ext_wave(const uint64_t *A, const uint64_t *AA, uint64_t pa, int alen,
-                           const uint64_t *B, const uint64_t *BA, uint64_t pb, int blen, int X,
-                           int lane)
-{
-    const int k = lane + BAND_LO;
-    int R = -1, G = 0, O = 0, E = 0;
-    int r0 = 0;
-    if (lane == -BAND_LO) {
-        r0 = lcp<AMB>(A, AA, pa, B, BA, pb, min(alen, blen));
-        R = r0;
-    }
-    r0 = __shfl(r0, -BAND_LO);
-    ExtRes best = {2 * r0, r0, r0, 0, 0, 0};
-    for (int d = 1; d <= DMAX; ++d) {
-        const int goe = G | (O << 13) | (E << 26);
-        int Rl = __shfl_up(R, 1), Rr = __shfl_down(R, 1);
-        int gl = __shfl_up(goe, 1), gr = __shfl_down(goe, 1);
-        if (lane == 0) Rl = -1;
-        if (lane == 63) Rr = -1;
-        int ni = -1, ng = 0, no = 0, ne = 0;
-        if (R >= 0 && R < alen && R - k < blen) {
-            ni = R + 1; ng = G; no = O; ne = 0;
-        }
-        if (Rl >= 0 && Rl < alen) {
-            const int c = Rl + 1;
-            if (c > ni) {
-                ni = c;
-                ng = (gl & 8191) + 1;
-                no = ((gl >> 13) & 8191) + (((gl >> 26) & 3) == 1 ? 0 : 1);
-                ne = 1;
-            }
-        }
-        if (Rr >= 0 && Rr - (k + 1) < blen) {
-            const int c = Rr;
-            if (c > ni) {
-                ni = c;
-                ng = (gr & 8191) + 1;
-                no = ((gr >> 13) & 8191) + (((gr >> 26) & 3) == 2 ? 0 : 1);
-                ne = 2;
-            }
-        }
-        int score = INT_MIN;
-        if (ni >= 0 && ni - k >= 0) {
-            const int ja = ni - k;
-            const int m = min(alen - ni, blen - ja);
-            const int s = lcp<AMB>(A, AA, pa + (uint64_t)ni, B, BA, pb + (uint64_t)ja, m);
-            if (s > 0) {
-                ni += s;
-                ne = 0;
-            }
-            score = 2 * ni - k - 6 * d;
-            if (score < best.score - X) ni = -1;
-        } else {
-            ni = -1;
-        }
-        R = ni; G = ng; O = no; E = ne;
-        const bool live = ni >= 0;
-        const uint64_t lm = __ballot(live);
-        if (lm == 0) break;
-        const int mx = wave_max(live ? score : INT_MIN);
-        if (mx > best.score) {
-            const uint64_t tm = __ballot(live && score == mx);
-            const int bl = __ffsll((unsigned long long)tm) - 1;
-            best.score = mx;
-            best.i = __shfl(R, bl);
-            best.j = best.i - (bl + BAND_LO);
-            best.d = d;
-            best.g = __shfl(G, bl);
-            best.o = __shfl(O, bl);
-        }
-    }
-    return best;
-}
-
-// Oriented query helpers. strand 0: q; strand 1: revcomp(q).
-struct QGeo {
-    uint64_t qs;   // forward start
-    int Lq;
-};
-
-// array/position of the forward walk of oriented position u
-__device__ __forceinline__ uint64_t qfwd_pos(const QGeo &q, int strand, uint64_t total, int u)
-{
-    return strand ? (total - q.qs - (uint64_t)q.Lq + (uint64_t)u) : (q.qs + (uint64_t)u);
-}
-// array/position of the walk leftwards from oriented position x (x-1, x-2, ...)
-__device__ __forceinline__ uint64_t qrev_pos(const QGeo &q, int strand, uint64_t total, int x)
-{
-    return strand ? (q.qs + (uint64_t)q.Lq - (uint64_t)x) : (total - q.qs - (uint64_t)x);
-}
-
-template <bool AMB>
-__global__ __launch_bounds__(ABLOCK) void align_kernel(Db db, Index ix, AlignParams P)
-{
-    const uint32_t g = P.gene_begin + blockIdx.x;
-    if (g >= P.gene_end) return;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-
-    __shared__ LSeed seeds[SEED_CAP];
-    __shared__ uint16_t seg_begin[SEED_CAP + 1];
-    __shared__ uint32_t it_lo[ABLOCK], it_pre[ABLOCK + 1], it_info[ABLOCK];
-    __shared__ uint64_t iso_start[MAX_ISO];
-    __shared__ uint32_t iso_len[MAX_ISO], iso_gtx[MAX_ISO], iso_pre[MAX_ISO + 1];
-    __shared__ DHsp hbuf[HSP_CAP];
-    __shared__ uint32_t hkey[HSP_CAP];
-    __shared__ uint16_t hord[HSP_CAP];
-    __shared__ uint32_t tcnt[MAX_SAMPLES], tpre[MAX_SAMPLES + 1];
-    __shared__ uint32_t sh_nseed, sh_nhsp, sh_flags, sh_nseg;
-    __shared__ unsigned long long sh_base;
-
-    const int Q = db.gene_sample[g];
-    const uint32_t t0 = db.gene_tx_off[g];
-    const uint32_t niso = db.gene_tx_off[g + 1] - t0;
-    const int N = db.n_samples;
-    const uint64_t total = db.total;
-    const int stride = P.stride;
-    if (niso > (uint32_t)MAX_ISO || N > MAX_SAMPLES) {
-        if (tid == 0) atomicOr(P.status, 2u);
-        return;
-    }
-    for (uint32_t i = tid; i < niso; i += ABLOCK) {
-        const uint32_t gtx = db.gene_tx[t0 + i];
-        const TxInfo ti = db.tx[gtx];
-        iso_gtx[i] = gtx;
-        iso_start[i] = ti.start;
-        iso_len[i] = ti.len;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t pre = 0;
-        for (uint32_t i = 0; i < niso; i++) {
-            iso_pre[i] = pre;
-            const int L = (int)iso_len[i];
-            pre += (L >= W16) ? 2u * (uint32_t)((L - W16) / stride + 1) : 0u;
-        }
-        iso_pre[niso] = pre;
-    }
-    __syncthreads();
-    const uint32_t n_items = iso_pre[niso];
-    const uint32_t gl = g - P.gene_begin;
-
-    int T0 = 0, T1 = N;
-    while (T0 < N) {
-        if (tid == 0) {
-            sh_nseed = 0;
-            sh_nhsp = 0;
-            sh_flags = 0;
-        }
-        __syncthreads();
-        // ---------------- seeds ----------------
-        for (uint32_t ib = 0; ib < n_items; ib += ABLOCK) {
-            const uint32_t it = ib + tid;
-            uint32_t lo = 0, cnt = 0, info = 0;
-            if (it < n_items) {
-                uint32_t ii = 0;
-                while (ii + 1 < niso && iso_pre[ii + 1] <= it) ii++;
-                const uint32_t rem = it - iso_pre[ii];
-                const uint32_t ns = (iso_pre[ii + 1] - iso_pre[ii]) >> 1;
-                const int strand = rem >= ns ? 1 : 0;
-                const int p = (int)(rem - (strand ? ns : 0)) * stride;
-                info = ii | ((uint32_t)strand << 7) | ((uint32_t)p << 8);
-                QGeo qg = {iso_start[ii], (int)iso_len[ii]};
-                const uint64_t qp = qfwd_pos(qg, strand, total, p);
-                const uint64_t *QA = strand ? db.RC : db.F;
-                bool ok = true;
-                if (AMB) {
-                    const uint64_t *QM = strand ? db.ARC : db.AF;
-                    ok = (win(QM, qp) & 0xFFFFFFFFull) == 0;
-                }
-                if (ok) {
-                    const uint32_t key = (uint32_t)win(QA, qp);
-                    const uint32_t b = key >> (32 - ix.bits);
-                    uint32_t a0 = ix.bucket[b], a1 = ix.bucket[b + 1];
-                    while (a0 < a1 && ix.keys[a0] < key) a0++;
-                    uint32_t a2 = a0;
-                    while (a2 < a1 && ix.keys[a2] == key) a2++;
-                    lo = a0;
-                    cnt = a2 - a0;
-                }
-            }
-            it_lo[tid] = lo;
-            it_info[tid] = info;
-            it_pre[tid] = cnt;
-            __syncthreads();
-            if (tid == 0) {
-                uint32_t s = 0;
-                for (int i = 0; i < ABLOCK; i++) {
-                    const uint32_t c = it_pre[i];
-                    it_pre[i] = s;
-                    s += c;
-                }
-                it_pre[ABLOCK] = s;
-            }
-            __syncthreads();
-            const uint32_t nh = it_pre[ABLOCK];
-            for (uint32_t h = tid; h < nh; h += ABLOCK) {
-                int lo2 = 0, hi2 = ABLOCK;   // last k with it_pre[k] <= h
-                while (hi2 - lo2 > 1) {
-                    const int mid = (lo2 + hi2) >> 1;
-                    if (it_pre[mid] <= h) lo2 = mid; else hi2 = mid;
-                }
-                const int k = lo2;
-                const uint2 e = ix.ent[it_lo[k] + (h - it_pre[k])];
-                const TxInfo st = db.tx[e.x];
-                if (st.sample == Q || st.sample < T0 || st.sample >= T1) continue;
-                const uint32_t inf = it_info[k];
-                const uint32_t ii = inf & 127;
-                const int strand = (inf >> 7) & 1;
-                const int p = (int)(inf >> 8);
-                const int off = (int)e.y;
-                QGeo qg = {iso_start[ii], (int)iso_len[ii]};
-                const int maxl = min(min(p, off), stride);
-                const uint64_t *QL = strand ? db.F : db.RC;
-                const uint64_t *QLM = strand ? db.AF : db.ARC;
-                const int l = lcp<AMB>(QL, QLM, qrev_pos(qg, strand, total, p), db.RC, db.ARC,
-                                       total - st.start - (uint64_t)off, maxl);
-                if (l >= stride) continue;
-                const uint64_t *QR = strand ? db.RC : db.F;
-                const uint64_t *QRM = strand ? db.ARC : db.AF;
-                const int maxr = min(qg.Lq - p - W16, (int)st.len - off - W16);
-                const int r = lcp<AMB>(QR, QRM, qfwd_pos(qg, strand, total, p + W16), db.F, db.AF,
-                                       st.start + (uint64_t)off + W16, maxr);
-                const int len = l + W16 + r;
-                if (len < P.word) continue;
-                const uint32_t slot = atomicAdd(&sh_nseed, 1u);
-                if (slot < (uint32_t)SEED_CAP) {
-                    LSeed sd;
-                    sd.k1 = ((uint64_t)ii << 57) | ((uint64_t)strand << 56) | ((uint64_t)e.x << 24) |
-                            (uint64_t)(uint32_t)(p - l);
-                    sd.y = (uint32_t)(off - l);
-                    sd.len = (uint32_t)len;
-                    seeds[slot] = sd;
-                } else {
-                    atomicOr(&sh_flags, 1u);
-                }
-            }
-            __syncthreads();
-        }
-        if (sh_flags & 1u) {
-            if (T1 - T0 == 1) {
-                if (tid == 0) atomicOr(P.status, 2u);
-                return;
-            }
-            T1 = T0 + (T1 - T0) / 2;
-            __syncthreads();
-            continue;
-        }
-        const uint32_t nseed = sh_nseed;
-        // ---------------- sort seeds by (k1, y) ----------------
-        uint32_t np2 = 1;
-        while (np2 < nseed) np2 <<= 1;
-        for (uint32_t i = nseed + tid; i < np2; i += ABLOCK) {
-            seeds[i].k1 = ~0ull;
-            seeds[i].y = 0xFFFFFFFFu;
-        }
-        __syncthreads();
-        for (uint32_t kk = 2; kk <= np2; kk <<= 1) {
-            for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
-                for (uint32_t i = tid; i < np2; i += ABLOCK) {
-                    const uint32_t ixj = i ^ j;
-                    if (ixj > i) {
-                        LSeed a = seeds[i], b = seeds[ixj];
-                        const bool gt = (a.k1 > b.k1) || (a.k1 == b.k1 && a.y > b.y);
-                        const bool up = (i & kk) == 0;
-                        if (gt == up) {
-                            seeds[i] = b;
-                            seeds[ixj] = a;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-        }
-        // ---------------- candidates (segments) ----------------
-        if (tid == 0) {
-            uint32_t ns = 0;
-            for (uint32_t i = 0; i < nseed; i++)
-                if (i == 0 || (seeds[i].k1 >> 24) != (seeds[i - 1].k1 >> 24)) seg_begin[ns++] = (uint16_t)i;
-            seg_begin[ns] = (uint16_t)nseed;
-            sh_nseg = ns;
-        }
-        __syncthreads();
-        const uint32_t nseg = sh_nseg;
-        for (uint32_t sg = wid; sg < nseg; sg += NWAVE) {
-            const uint32_t sb = seg_begin[sg], se = seg_begin[sg + 1];
-            const uint64_t k1 = seeds[sb].k1;
-            const uint32_t ii = (uint32_t)(k1 >> 57);
-            const int strand = (int)((k1 >> 56) & 1);
-            const uint32_t stx = (uint32_t)(k1 >> 24);
-            const TxInfo st = db.tx[stx];
-            QGeo qg = {iso_start[ii], (int)iso_len[ii]};
-            const int Lq = qg.Lq, Lt = (int)st.len;
-            const uint64_t *QR = strand ? db.RC : db.F;
-            const uint64_t *QRM = strand ? db.ARC : db.AF;
-            const uint64_t *QL = strand ? db.F : db.RC;
-            const uint64_t *QLM = strand ? db.AF : db.ARC;
-            int bqa = 0, bqb = 0, bsa = 0, bsb = 0, bsc = 0, bd = 0, bg = 0, bo = 0, bni = 0;
-            int nh = 0;
-            for (uint32_t si = sb; si < se && nh < MAX_HSP; si++) {
-                const int x = (int)(uint32_t)(seeds[si].k1 & 0xFFFFFFull);
-                const int y = (int)seeds[si].y, len = (int)seeds[si].len;
-                const bool inside = lane < nh && bqa <= x && x + len <= bqb && bsa <= y && y + len <= bsb;
-                if (__ballot(inside)) continue;
-                const ExtRes r = ext_wave<AMB>(QR, QRM, qfwd_pos(qg, strand, total, x + len), Lq - (x + len),
-                                               db.F, db.AF, st.start + (uint64_t)(y + len), Lt - (y + len),
-                                               P.xdrop, lane);
-                const ExtRes l = ext_wave<AMB>(QL, QLM, qrev_pos(qg, strand, total, x), x, db.RC, db.ARC,
-                                               total - st.start - (uint64_t)y, y, P.xdrop, lane);
-                if (lane == nh) {
-                    bqa = x - l.i; bqb = x + len + r.i; bsa = y - l.j; bsb = y + len + r.j;
-                    bsc = l.score + 2 * len + r.score;
-                    bd = l.d + r.d; bg = l.g + r.g; bo = l.o + r.o;
-                    bni = len + (l.i + l.j - 2 * l.d + l.g) / 2 + (r.i + r.j - 2 * r.d + r.g) / 2;
-                }
-                nh++;
-            }
-            // purge HSPs with common endpoints: by (score desc, index asc)
-            int rank = 0;
-            for (int j = 0; j < nh; j++) {
-                const int sj = __shfl(bsc, j);
-                if (lane < nh && (sj > bsc || (sj == bsc && j < lane))) rank++;
-            }
-            bool kept = false;
-            for (int rr = 0; rr < nh; rr++) {
-                const uint64_t m = __ballot(lane < nh && rank == rr);
-                const int i = __ffsll((unsigned long long)m) - 1;
-                const int qa = __shfl(bqa, i), sa = __shfl(bsa, i), qb = __shfl(bqb, i), sb2 = __shfl(bsb, i);
-                const bool conflict = kept && lane < nh &&
-                                      ((bqa == qa && bsa == sa) || (bqb == qb && bsb == sb2));
-                if (!__ballot(conflict) && lane == i) kept = true;
-            }
-            const int thr = P.thr[(size_t)st.sample * (size_t)(P.max_len + 1) + (size_t)Lq];
-            const bool out = kept && bsc >= thr;
-            const uint64_t om = __ballot(out);
-            uint32_t wbase = 0;
-            if (lane == 0 && om) wbase = atomicAdd(&sh_nhsp, (uint32_t)__popcll(om));
-            wbase = __shfl(wbase, 0);
-            if (out) {
-                const uint32_t slot = wbase + (uint32_t)__popcll(om & ((1ull << lane) - 1ull));
-                if (slot < (uint32_t)HSP_CAP) {
-                    DHsp h;
-                    h.q_tx = iso_gtx[ii];
-                    h.s_tx = stx;
-                    if (!strand) {
-                        h.qstart = bqa + 1; h.qend = bqb; h.sstart = bsa + 1; h.send = bsb;
-                    } else {
-                        h.qstart = Lq - bqb + 1; h.qend = Lq - bqa; h.sstart = bsb; h.send = bsa + 1;
-                    }
-                    h.gaps = bg;
-                    h.gapopen = bo;
-                    h.mismatch = bd - bg;
-                    h.nident = bni;
-                    h.length = bni + (bd - bg) + bg;
-                    h.score_half = bsc;
-                    h.bits10 = P.bits10[bsc];
-                    h.strand = strand;
-                    hbuf[slot] = h;
-                    hkey[slot] = (sg << 3) | (uint32_t)lane;
-                } else {
-                    atomicOr(&sh_flags, 2u);
-                }
-            }
-        }
-        __syncthreads();
-        if (sh_flags & 2u) {
-            if (T1 - T0 == 1) {
-                if (tid == 0) atomicOr(P.status, 2u);
-                return;
-            }
-            T1 = T0 + (T1 - T0) / 2;
-            __syncthreads();
-            continue;
-        }
-        // ---------------- order HSPs and group them by subject sample ----------------
-        const uint32_t nhsp = sh_nhsp;
-        for (uint32_t i = tid; i < nhsp; i += ABLOCK) {
-            uint32_t r = 0;
-            const uint32_t ki = hkey[i];
-            for (uint32_t j = 0; j < nhsp; j++) r += hkey[j] < ki;
-            hord[r] = (uint16_t)i;   // keys are unique
-        }
-        for (int T = tid; T < N; T += ABLOCK) tcnt[T] = 0;
-        __syncthreads();
-        for (uint32_t i = tid; i < nhsp; i += ABLOCK) {
-            const int T = db.tx[hbuf[i].s_tx].sample;
-            atomicAdd(&tcnt[T], 1u);
-        }
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t s = 0;
-            for (int T = 0; T < N; T++) {
-                tpre[T] = s;
-                s += tcnt[T];
-            }
-            tpre[N] = s;
-            sh_base = nhsp ? atomicAdd(P.out_count, (unsigned long long)nhsp) : 0ull;
-            if (sh_base + nhsp > P.out_cap) atomicOr(P.status, 1u);
-        }
-        __syncthreads();
-        const unsigned long long base = sh_base;
-        const bool room = base + nhsp <= P.out_cap;
-        for (uint32_t r = tid; r < nhsp; r += ABLOCK) {
-            const uint32_t i = hord[r];
-            const int T = db.tx[hbuf[i].s_tx].sample;
-            uint32_t rk = 0;   // rank among earlier (ordered) HSPs of the same sample
-            for (uint32_t r2 = 0; r2 < r; r2++) rk += db.tx[hbuf[hord[r2]].s_tx].sample == T;
-            if (room) P.out[base + tpre[T] + rk] = hbuf[i];
-        }
-        for (int T = T0 + tid; T < T1; T += ABLOCK) {
-            const size_t gi = (size_t)gl * (size_t)N + (size_t)T;
-            P.grp_off[gi] = (uint32_t)(base + tpre[T]);
-            P.grp_cnt[gi] = tcnt[T];
-        }
-        T0 = T1;
-        T1 = N;
-        __syncthreads();
     }
 }
 
@@ -1146,16 +656,6 @@ void launch_bucket_fill(const uint32_t *keys, uint64_t n, int bits, uint32_t *bu
 {
     hipLaunchKernelGGL(bucket_fill_kernel, dim3(grid_for(n + 1, 256)), dim3(256), 0, st, keys, n, bits,
                        bucket);
-}
-
-void launch_align(bool amb, const Db &db, const Index &ix, const AlignParams &P, hipStream_t st)
-{
-    const uint32_t n = P.gene_end - P.gene_begin;
-    if (n == 0) return;
-    if (amb)
-        hipLaunchKernelGGL(align_kernel<true>, dim3(n), dim3(ABLOCK), 0, st, db, ix, P);
-    else
-        hipLaunchKernelGGL(align_kernel<false>, dim3(n), dim3(ABLOCK), 0, st, db, ix, P);
 }
 
 void launch_rbh(const RbhParams &P, int pass, hipStream_t st)
