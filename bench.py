@@ -174,7 +174,7 @@ def main():
                    "parallelism": f"query-gene shards x{world}"},
         "roofline": roof, "cpu_baseline": cpu,
         "phases_ms": {k: round(v, 3) for k, v in tm.items()},
-        "graph": {k: st[k] for k in ("hsps", "table_rows", "edges", "components",
+        "graph": {k: st[k] for k in ("seeds", "candidates", "hsps", "table_rows", "edges", "components",
                                      "ideal_components", "sample_count")},
         "gen_s": round(t_gen, 1),
     }

@@ -52,6 +52,30 @@ __device__ __forceinline__ uint64_t qrev_pos(const QGeo &q, int strand, uint64_t
 // seeds
 // ------------------------------------------------------------------------
 
+// Exclusive scan of one value per thread over a SBLOCK-thread block.
+__device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *wsum, uint32_t &total)
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < SBLOCK / 64; i++) {
+        const uint32_t w = wsum[i];
+        if (i < wid) before += w;
+        tot += w;
+    }
+    __syncthreads();
+    total = tot;
+    return before + x - v;
+}
+
 template <bool AMB>
 __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParams P)
 {
@@ -65,7 +89,9 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
     __shared__ uint64_t iso_start[MAX_ISO];
     __shared__ uint32_t iso_len[MAX_ISO], iso_gtx[MAX_ISO], iso_pre[MAX_ISO + 1];
     __shared__ uint32_t tcnt[MAX_SAMPLES], tpre[MAX_SAMPLES + 1];
-    __shared__ uint32_t sh_nseed, sh_flags, sh_nseg;
+    __shared__ uint8_t seg_T[SEED_CAP];
+    __shared__ uint32_t wsum[SBLOCK / 64];
+    __shared__ uint32_t sh_nseed, sh_flags;
     __shared__ unsigned long long sh_sbase, sh_cbase;
 
     const int Q = db.gene_sample[g];
@@ -139,17 +165,9 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
             }
             it_lo[tid] = lo;
             it_info[tid] = info;
-            it_pre[tid] = cnt;
-            __syncthreads();
-            if (tid == 0) {
-                uint32_t s = 0;
-                for (int i = 0; i < SBLOCK; i++) {
-                    const uint32_t c = it_pre[i];
-                    it_pre[i] = s;
-                    s += c;
-                }
-                it_pre[SBLOCK] = s;
-            }
+            uint32_t tot;
+            it_pre[tid] = block_exscan(cnt, wsum, tot);
+            if (tid == 0) it_pre[SBLOCK] = tot;
             __syncthreads();
             const uint32_t nh = it_pre[SBLOCK];
             for (uint32_t h = tid; h < nh; h += SBLOCK) {
@@ -230,29 +248,33 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
                 __syncthreads();
             }
         }
-        // candidates (segments of equal (iso, strand, gtx))
-        if (tid == 0) {
-            uint32_t ns = 0;
-            for (uint32_t i = 0; i < nseed; i++)
-                if (i == 0 || (seeds[i].k1 >> 24) != (seeds[i - 1].k1 >> 24)) seg_begin[ns++] = (uint16_t)i;
-            seg_begin[ns] = (uint16_t)nseed;
-            sh_nseg = ns;
+        // candidates (segments of equal (iso, strand, gtx)), block-parallel
+        uint32_t nseg = 0;
+        for (uint32_t c0 = 0; c0 < nseed; c0 += SBLOCK) {
+            const uint32_t i = c0 + tid;
+            const uint32_t f = (i < nseed && (i == 0 || (seeds[i].k1 >> 24) != (seeds[i - 1].k1 >> 24))) ? 1u : 0u;
+            uint32_t tot;
+            const uint32_t pos = nseg + block_exscan(f, wsum, tot);
+            if (f) seg_begin[pos] = (uint16_t)i;
+            nseg += tot;
         }
+        if (tid == 0) seg_begin[nseg] = (uint16_t)nseed;
         for (int T = tid; T < N; T += SBLOCK) tcnt[T] = 0;
         __syncthreads();
-        const uint32_t nseg = sh_nseg;
         for (uint32_t sg = tid; sg < nseg; sg += SBLOCK) {
             const uint32_t gtx = (uint32_t)(seeds[seg_begin[sg]].k1 >> 24);
-            atomicAdd(&tcnt[db.tx[gtx].sample], 1u);
+            const int T = db.tx[gtx].sample;
+            seg_T[sg] = (uint8_t)T;
+            atomicAdd(&tcnt[T], 1u);
         }
         __syncthreads();
+        {
+            uint32_t tot;
+            const uint32_t v = tid < N ? tcnt[tid] : 0u;
+            const uint32_t pre = block_exscan(v, wsum, tot);
+            if (tid < N) tpre[tid] = pre;
+        }
         if (tid == 0) {
-            uint32_t s = 0;
-            for (int T = 0; T < N; T++) {
-                tpre[T] = s;
-                s += tcnt[T];
-            }
-            tpre[N] = s;
             sh_sbase = nseed ? atomicAdd(&P.seed_count[shard], (unsigned long long)nseed) : 0ull;
             sh_cbase = nseg ? atomicAdd(&P.cand_count[shard], (unsigned long long)nseg) : 0ull;
             if (sh_sbase + nseed > P.seed_cap || sh_cbase + nseg > P.cand_cap) atomicOr(P.status, 1u);
@@ -273,10 +295,9 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
                 const uint32_t b0 = seg_begin[sg], b1 = seg_begin[sg + 1];
                 const uint64_t k1 = seeds[b0].k1;
                 const uint32_t gtx = (uint32_t)(k1 >> 24);
-                const int T = db.tx[gtx].sample;
+                const int T = seg_T[sg];
                 uint32_t rk = 0;   // rank among earlier candidates of the same sample
-                for (uint32_t s2 = 0; s2 < sg; s2++)
-                    rk += db.tx[(uint32_t)(seeds[seg_begin[s2]].k1 >> 24)].sample == T;
+                for (uint32_t s2 = 0; s2 < sg; s2++) rk += seg_T[s2] == T;
                 Cand c;
                 c.seed_off = (uint32_t)(sbase + b0);
                 c.q_gtx = iso_gtx[(uint32_t)(k1 >> 57)];
@@ -306,11 +327,28 @@ struct ExtRes {
     int score, i, j, d, g, o;
 };
 
+// Max over the wave: DPP inside rows of 16 (xor 1, xor 2, half-row mirror,
+// row mirror), then the four row maxima through readlane. No LDS round trips.
 __device__ __forceinline__ int wave_max(int v)
 {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off));
-    return v;
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false));  // row_mirror
+    const int a = max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16));
+    const int b = max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48));
+    return max(a, b);
+}
+
+// lane l <- lane l-1 (lane 0 gets `edge`) / lane l <- lane l+1 (lane 63 gets `edge`):
+// gfx9-family DPP wavefront shifts, one VALU op each.
+__device__ __forceinline__ int from_lower(int v, int edge)
+{
+    return __builtin_amdgcn_update_dpp(edge, v, 0x138, 0xF, 0xF, false);   // wave_shr:1
+}
+__device__ __forceinline__ int from_upper(int v, int edge)
+{
+    return __builtin_amdgcn_update_dpp(edge, v, 0x130, 0xF, 0xF, false);   // wave_shl:1
 }
 
 // Greedy X-drop extension (oracle/align_oracle.c greedy_ext), one diagonal per
@@ -329,15 +367,13 @@ __device__ __forceinline__ ExtRes ext_wave(const uint64_t *A, const uint64_t *AA
         r0 = lcp<AMB>(A, AA, pa, B, BA, pb, min(alen, blen));
         R = r0;
     }
-    r0 = __shfl(r0, -BAND_LO);
+    r0 = __builtin_amdgcn_readlane(r0, -BAND_LO);
     ExtRes best = {2 * r0, r0, r0, 0, 0, 0};
     if (2 * min(alen - r0, blen - r0) <= 0) return best;
     for (int d = 1; d <= DMAX; ++d) {
         const int goe = G | (O << 13) | (E << 26);
-        int Rl = __shfl_up(R, 1), Rr = __shfl_down(R, 1);
-        int gl = __shfl_up(goe, 1), gr = __shfl_down(goe, 1);
-        if (lane == 0) Rl = -1;
-        if (lane == 63) Rr = -1;
+        const int Rl = from_lower(R, -1), Rr = from_upper(R, -1);
+        const int gl = from_lower(goe, 0), gr = from_upper(goe, 0);
         int ni = -1, ng = 0, no = 0, ne = 0;
         if (R >= 0 && R < alen && R - k < blen) {
             ni = R + 1; ng = G; no = O; ne = 0;
@@ -379,18 +415,18 @@ __device__ __forceinline__ ExtRes ext_wave(const uint64_t *A, const uint64_t *AA
         const bool live = ni >= 0;
         const uint64_t lm = __ballot(live);
         if (lm == 0) break;
-        const int mx = wave_max(live ? score : INT_MIN);
-        if (mx > best.score) {
+        if (__ballot(live && score > best.score)) {
+            const int mx = wave_max(live ? score : INT_MIN);
             const uint64_t tm = __ballot(live && score == mx);
             const int bl = __ffsll((unsigned long long)tm) - 1;
             best.score = mx;
-            best.i = __shfl(R, bl);
+            best.i = __builtin_amdgcn_readlane(R, bl);
             best.j = best.i - (bl + BAND_LO);
             best.d = d;
-            best.g = __shfl(G, bl);
-            best.o = __shfl(O, bl);
+            best.g = __builtin_amdgcn_readlane(G, bl);
+            best.o = __builtin_amdgcn_readlane(O, bl);
         }
-        if (wave_max(live ? bound : INT_MIN) <= best.score) break;
+        if (!__ballot(live && bound > best.score)) break;
     }
     return best;
 }
@@ -497,14 +533,15 @@ __global__ __launch_bounds__(EBLOCK) void extend_kernel(Db db, ExtParams P)
         // purge HSPs with common endpoints: by (score desc, index asc)
         int rank = 0;
         for (int j = 0; j < nh; j++) {
-            const int sj = __shfl(bsc, j);
+            const int sj = __builtin_amdgcn_readlane(bsc, j);
             if (lane < nh && (sj > bsc || (sj == bsc && j < lane))) rank++;
         }
         bool kept = false;
         for (int rr = 0; rr < nh; rr++) {
             const uint64_t m = __ballot(lane < nh && rank == rr);
             const int i = __ffsll((unsigned long long)m) - 1;
-            const int qa = __shfl(bqa, i), sa = __shfl(bsa, i), qb = __shfl(bqb, i), sb2 = __shfl(bsb, i);
+            const int qa = __builtin_amdgcn_readlane(bqa, i), sa = __builtin_amdgcn_readlane(bsa, i);
+            const int qb = __builtin_amdgcn_readlane(bqb, i), sb2 = __builtin_amdgcn_readlane(bsb, i);
             const bool conflict = kept && lane < nh && ((bqa == qa && bsa == sa) || (bqb == qb && bsb == sb2));
             if (!__ballot(conflict) && lane == i) kept = true;
         }
@@ -518,7 +555,7 @@ __global__ __launch_bounds__(EBLOCK) void extend_kernel(Db db, ExtParams P)
             if (b + (nout - 1) > P.ovf_cap) atomicOr(P.status, 1u);
             obase = (uint32_t)b;
         }
-        obase = __shfl(obase, 0);
+        obase = __builtin_amdgcn_readlane(obase, 0);
         if (out) {
             const int rk = __popcll(om & ((1ull << lane) - 1ull));
             DHsp h;
