@@ -355,9 +355,9 @@ __device__ __forceinline__ int from_upper(int v, int edge)
 // lane; A/B are forward walks (pa/pb = position of the first base). Stops as
 // soon as no live diagonal can still beat the best score (score + 2 * bases
 // left on the shorter side <= best): the result is unchanged.
-template <bool AMB>
-__device__ __forceinline__ ExtRes ext_wave(const uint64_t *A, const uint64_t *AA, uint64_t pa, int alen,
-                                           const uint64_t *B, const uint64_t *BA, uint64_t pb, int blen,
+template <bool AMB, typename PT>
+__device__ __forceinline__ ExtRes ext_wave(const uint64_t *A, const uint64_t *AA, PT pa, int alen,
+                                           const uint64_t *B, const uint64_t *BA, PT pb, int blen,
                                            int X, int lane)
 {
     const int k = lane + BAND_LO;
@@ -400,7 +400,7 @@ __device__ __forceinline__ ExtRes ext_wave(const uint64_t *A, const uint64_t *AA
         if (ni >= 0 && ni - k >= 0) {
             const int ja = ni - k;
             const int m = min(alen - ni, blen - ja);
-            const int s = lcp<AMB>(A, AA, pa + (uint64_t)ni, B, BA, pb + (uint64_t)ja, m);
+            const int s = lcp<AMB>(A, AA, pa + (PT)ni, B, BA, pb + (PT)ja, m);
             if (s > 0) {
                 ni += s;
                 ne = 0;
@@ -434,17 +434,17 @@ __device__ __forceinline__ ExtRes ext_wave(const uint64_t *A, const uint64_t *AA
 // copy 32-base windows [pos, pos + 32 * n) of a packed array into LDS
 __device__ __forceinline__ void stage(uint64_t *dst, const uint64_t *src, uint64_t pos, int n, int lane)
 {
-    for (int w = lane; w < n; w += 64) dst[w] = win(src, pos + 32 * (uint64_t)w);
+    for (int w = lane; w < n; w += 64) dst[w] = win<uint64_t>(src, pos + 32 * (uint64_t)w);
 }
 
 // One candidate (all its seeds) on one wave. Positions: query walks on
 // (QF, QR) arrays whose oriented position u lives at qf0 + u / qr0 + u, the
 // subject walks on (TF, TR) arrays at tf0 + v / tr0 + v (see the oracle's
 // walker); in LDS the bases are 0.
-template <bool AMB>
+template <bool AMB, typename PT>
 __device__ __forceinline__ void process_candidate(
-    const uint64_t *QF, const uint64_t *QFM, uint64_t qf0, const uint64_t *QR, const uint64_t *QRM, uint64_t qr0,
-    const uint64_t *TF, const uint64_t *TFM, uint64_t tf0, const uint64_t *TR, const uint64_t *TRM, uint64_t tr0,
+    const uint64_t *QF, const uint64_t *QFM, PT qf0, const uint64_t *QR, const uint64_t *QRM, PT qr0,
+    const uint64_t *TF, const uint64_t *TFM, PT tf0, const uint64_t *TR, const uint64_t *TRM, PT tr0,
     int Lq, int Lt, int strand, const GSeed *sd, int ns, int X, int lane, int &bqa, int &bqb, int &bsa, int &bsb,
     int &bsc, int &bd, int &bg, int &bo, int &bni, int &nh)
 {
@@ -452,20 +452,20 @@ __device__ __forceinline__ void process_candidate(
     // leftwards walk from x: strand 0 -> QR at Lq - x, 1 -> QF at Lq - x
     const uint64_t *AR = strand ? QR : QF;
     const uint64_t *ARM = strand ? QRM : QFM;
-    const uint64_t ar0 = strand ? qr0 : qf0;
+    const PT ar0 = strand ? qr0 : qf0;
     const uint64_t *AL = strand ? QF : QR;
     const uint64_t *ALM = strand ? QFM : QRM;
-    const uint64_t al0 = strand ? qf0 : qr0;
+    const PT al0 = strand ? qf0 : qr0;
     nh = 0;
     for (int si = 0; si < ns && nh < MAX_HSP; si++) {
         const GSeed s = sd[si];
         const int x = (int)s.x, y = (int)s.y, len = (int)s.len;
         const bool inside = lane < nh && bqa <= x && x + len <= bqb && bsa <= y && y + len <= bsb;
         if (__ballot(inside)) continue;
-        const ExtRes r = ext_wave<AMB>(AR, ARM, ar0 + (uint64_t)(x + len), Lq - (x + len), TF, TFM,
-                                       tf0 + (uint64_t)(y + len), Lt - (y + len), X, lane);
-        const ExtRes l = ext_wave<AMB>(AL, ALM, al0 + (uint64_t)(Lq - x), x, TR, TRM, tr0 + (uint64_t)(Lt - y), y,
-                                       X, lane);
+        const ExtRes r = ext_wave<AMB, PT>(AR, ARM, ar0 + (PT)(x + len), Lq - (x + len), TF, TFM,
+                                           tf0 + (PT)(y + len), Lt - (y + len), X, lane);
+        const ExtRes l = ext_wave<AMB, PT>(AL, ALM, al0 + (PT)(Lq - x), x, TR, TRM, tr0 + (PT)(Lt - y), y,
+                                           X, lane);
         if (lane == nh) {
             bqa = x - l.i; bqb = x + len + r.i; bsa = y - l.j; bsb = y + len + r.j;
             bsc = l.score + 2 * len + r.score;
@@ -523,12 +523,12 @@ __global__ __launch_bounds__(EBLOCK) void extend_kernel(Db db, ExtParams P)
             }
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            process_candidate<AMB>(QF, QFM, 0, QR, QRM, 0, TF, TFM, 0, TR, TRM, 0, Lq, Lt, strand, sd, ns, P.xdrop,
-                                   lane, bqa, bqb, bsa, bsb, bsc, bd, bg, bo, bni, nh);
+            process_candidate<AMB, uint32_t>(QF, QFM, 0u, QR, QRM, 0u, TF, TFM, 0u, TR, TRM, 0u, Lq, Lt, strand, sd,
+                                             ns, P.xdrop, lane, bqa, bqb, bsa, bsb, bsc, bd, bg, bo, bni, nh);
         } else {
-            process_candidate<AMB>(db.F, db.AF, qt.start, db.RC, db.ARC, qr_g, db.F, db.AF, st.start, db.RC, db.ARC,
-                                   tr_g, Lq, Lt, strand, sd, ns, P.xdrop, lane, bqa, bqb, bsa, bsb, bsc, bd, bg, bo,
-                                   bni, nh);
+            process_candidate<AMB, uint64_t>(db.F, db.AF, qt.start, db.RC, db.ARC, qr_g, db.F, db.AF, st.start, db.RC,
+                                             db.ARC, tr_g, Lq, Lt, strand, sd, ns, P.xdrop, lane, bqa, bqb, bsa, bsb,
+                                             bsc, bd, bg, bo, bni, nh);
         }
         // purge HSPs with common endpoints: by (score desc, index asc)
         int rank = 0;

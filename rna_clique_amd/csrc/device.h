@@ -153,27 +153,30 @@ struct RbhParams {
 // 2-bit windows
 // ------------------------------------------------------------------------
 
-// 32 bases starting at base position p (base i in bits 2i..2i+1).
-__device__ __forceinline__ uint64_t win(const uint64_t *__restrict__ a, uint64_t p)
+// 32 bases starting at base position p (base i in bits 2i..2i+1). Branchless:
+// both words are read (arrays carry padding words), (hi << 1) << (63 - sh)
+// is hi << (64 - sh) for sh > 0 and 0 for sh == 0.
+template <typename PT>
+__device__ __forceinline__ uint64_t win(const uint64_t *__restrict__ a, PT p)
 {
-    const uint64_t w = p >> 5;
+    const PT w = p >> 5;
     const unsigned sh = (unsigned)(p & 31) * 2u;
-    const uint64_t lo = a[w];
-    if (sh == 0) return lo;
-    return (lo >> sh) | (a[w + 1] << (64u - sh));
+    const uint64_t lo = a[w], hi = a[w + 1];
+    return (lo >> sh) | ((hi << 1) << (63u - sh));
 }
 
 // Longest common extension of two forward walks (at most maxn bases).
-// Ambiguous bases (mask 0b11) never match.
-template <bool AMB>
-__device__ __forceinline__ int lcp(const uint64_t *__restrict__ A, const uint64_t *__restrict__ AA,
-                                   uint64_t pa, const uint64_t *__restrict__ B,
-                                   const uint64_t *__restrict__ BA, uint64_t pb, int maxn)
+// Ambiguous bases (mask 0b11) never match. PT: 32-bit positions for LDS-staged
+// sequences, 64-bit for the global arrays.
+template <bool AMB, typename PT>
+__device__ __forceinline__ int lcp(const uint64_t *__restrict__ A, const uint64_t *__restrict__ AA, PT pa,
+                                   const uint64_t *__restrict__ B, const uint64_t *__restrict__ BA, PT pb,
+                                   int maxn)
 {
     int n = 0;
     while (n < maxn) {
-        uint64_t x = win(A, pa + n) ^ win(B, pb + n);
-        if (AMB) x |= win(AA, pa + n) | win(BA, pb + n);
+        uint64_t x = win(A, pa + (PT)n) ^ win(B, pb + (PT)n);
+        if (AMB) x |= win(AA, pa + (PT)n) | win(BA, pb + (PT)n);
         if (x == 0) {
             n += 32;
             continue;
