@@ -25,7 +25,6 @@ constexpr int MAX_SAMPLES = 256;
 constexpr int EBLOCK = 256;
 constexpr int EWAVES = EBLOCK / 64;
 constexpr int STAGE_BASES = 8192;                 // staged transcript length limit
-constexpr int SW = STAGE_BASES / 32 + 2;          // words per staged orientation
 
 struct LSeed {
     uint64_t k1;    // iso:7 | strand:1 | gtx:32 | x:24
@@ -340,8 +339,8 @@ __device__ __forceinline__ int wave_max(int v)
     return max(a, b);
 }
 
-// lane l <- lane l-1 (lane 0 gets `edge`) / lane l <- lane l+1 (lane 63 gets `edge`):
-// gfx9-family DPP wavefront shifts, one VALU op each.
+// lane l <- lane l-1 (lane 0 gets `edge`) / lane l <- lane l+1 (lane 63 gets
+// `edge`): gfx9-family DPP wavefront shifts, one VALU op each.
 __device__ __forceinline__ int from_lower(int v, int edge)
 {
     return __builtin_amdgcn_update_dpp(edge, v, 0x138, 0xF, 0xF, false);   // wave_shr:1
@@ -351,121 +350,126 @@ __device__ __forceinline__ int from_upper(int v, int edge)
     return __builtin_amdgcn_update_dpp(edge, v, 0x130, 0xF, 0xF, false);   // wave_shl:1
 }
 
-// Greedy X-drop extension (oracle/align_oracle.c greedy_ext), one diagonal per
-// lane; A/B are forward walks (pa/pb = position of the first base). Stops as
-// soon as no live diagonal can still beat the best score (score + 2 * bases
-// left on the shorter side <= best): the result is unchanged.
-template <bool AMB, typename PT>
-__device__ __forceinline__ ExtRes ext_wave(const uint64_t *A, const uint64_t *AA, PT pa, int alen,
-                                           const uint64_t *B, const uint64_t *BA, PT pb, int blen,
-                                           int X, int lane)
+// 32 bases starting at base p of a packed array viewed as dwords (16 bases
+// each): three dword loads and two funnel shifts (v_alignbit_b32).
+template <typename PT>
+__device__ __forceinline__ uint64_t win3(const uint32_t *__restrict__ a, PT p)
 {
-    const int k = lane + BAND_LO;
-    int R = -1, G = 0, O = 0, E = 0;
-    int r0 = 0;
-    if (lane == -BAND_LO) {
-        r0 = lcp<AMB>(A, AA, pa, B, BA, pb, min(alen, blen));
-        R = r0;
+    const PT i = p >> 4;
+    const uint32_t sh = ((uint32_t)p & 15u) * 2u;
+    const uint32_t w0 = a[i], w1 = a[i + 1], w2 = a[i + 2];
+    const uint32_t lo = __builtin_amdgcn_alignbit(w1, w0, sh);
+    const uint32_t hi = __builtin_amdgcn_alignbit(w2, w1, sh);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Matching bases walking forward from (pa, pb) (BACK = false) or backwards
+// from (pa - 1, pb - 1) (BACK = true; the window ending at p is read at p - 32
+// and the first mismatch is its highest differing base), at most maxn.
+template <bool AMB, bool BACK, typename PT>
+__device__ __forceinline__ int slide(const uint32_t *A, const uint32_t *AM, PT pa, const uint32_t *B,
+                                     const uint32_t *BM, PT pb, int maxn)
+{
+    int n = 0;
+    while (n < maxn) {
+        const PT qa = BACK ? pa - (PT)(n + 32) : pa + (PT)n;
+        const PT qb = BACK ? pb - (PT)(n + 32) : pb + (PT)n;
+        uint64_t x = win3(A, qa) ^ win3(B, qb);
+        if (AMB) x |= win3(AM, qa) | win3(BM, qb);
+        if (x == 0) {
+            n += 32;
+            continue;
+        }
+        n += (BACK ? __builtin_clzll(x) : __builtin_ctzll(x)) >> 1;
+        return n < maxn ? n : maxn;
     }
+    return maxn > 0 ? maxn : 0;
+}
+
+// Greedy X-drop extension (oracle/align_oracle.c greedy_ext), one diagonal per
+// lane of the wave. A / B: oriented query and subject; the walk starts at
+// (pa, pb) forward, or at (pa - 1, pb - 1) backwards. Branch-free step; the
+// per-lane gap state G | O << 13 | E << 26 travels in one register. Stops as
+// soon as no live diagonal can still beat the best score (score + 2 x bases
+// left on the shorter side <= best): the result is unchanged.
+template <bool AMB, bool BACK, typename PT>
+__device__ __forceinline__ ExtRes ext_wave(const uint32_t *A, const uint32_t *AM, PT pa, int alen,
+                                           const uint32_t *B, const uint32_t *BM, PT pb, int blen, int X,
+                                           int lane)
+{
+    constexpr int EBIT = 26, OBIT = 13;
+    constexpr int GMASK = 8191;
+    const int k = lane + BAND_LO;
+    int r0 = 0;
+    if (lane == -BAND_LO) r0 = slide<AMB, BACK, PT>(A, AM, pa, B, BM, pb, min(alen, blen));
     r0 = __builtin_amdgcn_readlane(r0, -BAND_LO);
     ExtRes best = {2 * r0, r0, r0, 0, 0, 0};
-    if (2 * min(alen - r0, blen - r0) <= 0) return best;
+    if (min(alen, blen) - r0 <= 0) return best;
+    int R = lane == -BAND_LO ? r0 : -1;
+    int goe = 0;
     for (int d = 1; d <= DMAX; ++d) {
-        const int goe = G | (O << 13) | (E << 26);
         const int Rl = from_lower(R, -1), Rr = from_upper(R, -1);
         const int gl = from_lower(goe, 0), gr = from_upper(goe, 0);
-        int ni = -1, ng = 0, no = 0, ne = 0;
-        if (R >= 0 && R < alen && R - k < blen) {
-            ni = R + 1; ng = G; no = O; ne = 0;
-        }
-        if (Rl >= 0 && Rl < alen) {
-            const int c = Rl + 1;
-            if (c > ni) {
-                ni = c;
-                ng = (gl & 8191) + 1;
-                no = ((gl >> 13) & 8191) + (((gl >> 26) & 3) == 1 ? 0 : 1);
-                ne = 1;
-            }
-        }
-        if (Rr >= 0 && Rr - (k + 1) < blen) {
-            const int c = Rr;
-            if (c > ni) {
-                ni = c;
-                ng = (gr & 8191) + 1;
-                no = ((gr >> 13) & 8191) + (((gr >> 26) & 3) == 2 ? 0 : 1);
-                ne = 2;
-            }
-        }
+        // candidates; ties prefer mismatch, then insertion, then deletion
+        const int cm = (R >= 0 && R < alen && R - k < blen) ? R + 1 : -1;
+        const int ci = (Rl >= 0 && Rl < alen) ? Rl + 1 : -1;
+        const int cd = (Rr >= 0 && Rr - (k + 1) < blen) ? Rr : -1;
+        int ni = max(max(cm, ci), cd);
+        const bool fm = ni >= 0 && cm == ni, fi = !fm && ci == ni;
+        const int gi = (gl & ~(3 << EBIT)) + 1 + ((((gl >> EBIT) & 3) == 1) ? 0 : (1 << OBIT)) + (1 << EBIT);
+        const int gd = (gr & ~(3 << EBIT)) + 1 + ((((gr >> EBIT) & 3) == 2) ? 0 : (1 << OBIT)) + (2 << EBIT);
+        int ng = fm ? (goe & ~(3 << EBIT)) : (fi ? gi : gd);
         int score = INT_MIN, bound = INT_MIN;
-        if (ni >= 0 && ni - k >= 0) {
+        if (ni >= 0) {
             const int ja = ni - k;
             const int m = min(alen - ni, blen - ja);
-            const int s = lcp<AMB>(A, AA, pa + (PT)ni, B, BA, pb + (PT)ja, m);
-            if (s > 0) {
-                ni += s;
-                ne = 0;
-            }
+            const int s = slide<AMB, BACK, PT>(A, AM, BACK ? pa - (PT)ni : pa + (PT)ni, B, BM,
+                                               BACK ? pb - (PT)ja : pb + (PT)ja, m);
+            ni += s;
+            if (s > 0) ng &= ~(3 << EBIT);
             score = 2 * ni - k - 6 * d;
             if (score < best.score - X) ni = -1;
-            else bound = score + 2 * (m - s);
-        } else {
-            ni = -1;
+            bound = score + 2 * (m - s);
         }
-        R = ni; G = ng; O = no; E = ne;
+        R = ni;
+        goe = ng;
         const bool live = ni >= 0;
-        const uint64_t lm = __ballot(live);
-        if (lm == 0) break;
+        if (!__ballot(live)) break;
         if (__ballot(live && score > best.score)) {
-            const int mx = wave_max(live ? score : INT_MIN);
-            const uint64_t tm = __ballot(live && score == mx);
-            const int bl = __ffsll((unsigned long long)tm) - 1;
-            best.score = mx;
+            // (score, lowest lane) as one key: score * 64 + (63 - lane)
+            const int mk = wave_max(live ? score * 64 + (63 - lane) : INT_MIN);
+            const int bl = 63 - (mk & 63);
+            best.score = mk >> 6;
             best.i = __builtin_amdgcn_readlane(R, bl);
             best.j = best.i - (bl + BAND_LO);
             best.d = d;
-            best.g = __builtin_amdgcn_readlane(G, bl);
-            best.o = __builtin_amdgcn_readlane(O, bl);
+            const int bg = __builtin_amdgcn_readlane(goe, bl);
+            best.g = bg & GMASK;
+            best.o = (bg >> OBIT) & GMASK;
         }
         if (!__ballot(live && bound > best.score)) break;
     }
     return best;
 }
 
-// copy 32-base windows [pos, pos + 32 * n) of a packed array into LDS
-__device__ __forceinline__ void stage(uint64_t *dst, const uint64_t *src, uint64_t pos, int n, int lane)
-{
-    for (int w = lane; w < n; w += 64) dst[w] = win<uint64_t>(src, pos + 32 * (uint64_t)w);
-}
-
-// One candidate (all its seeds) on one wave. Positions: query walks on
-// (QF, QR) arrays whose oriented position u lives at qf0 + u / qr0 + u, the
-// subject walks on (TF, TR) arrays at tf0 + v / tr0 + v (see the oracle's
-// walker); in LDS the bases are 0.
+// One candidate (all its seeds) on one wave. QO: oriented query (its base u at
+// qo + u), TF: subject forward (base v at tf + v); right extensions walk
+// forward from the seed end, left extensions backwards from the seed start.
 template <bool AMB, typename PT>
-__device__ __forceinline__ void process_candidate(
-    const uint64_t *QF, const uint64_t *QFM, PT qf0, const uint64_t *QR, const uint64_t *QRM, PT qr0,
-    const uint64_t *TF, const uint64_t *TFM, PT tf0, const uint64_t *TR, const uint64_t *TRM, PT tr0,
-    int Lq, int Lt, int strand, const GSeed *sd, int ns, int X, int lane, int &bqa, int &bqb, int &bsa, int &bsb,
-    int &bsc, int &bd, int &bg, int &bo, int &bni, int &nh)
+__device__ __forceinline__ void process_candidate(const uint32_t *QO, const uint32_t *QOM, PT qo, const uint32_t *TF,
+                                                  const uint32_t *TFM, PT tf, int Lq, int Lt, const GSeed *sd,
+                                                  int ns, int X, int lane, int &bqa, int &bqb, int &bsa, int &bsb,
+                                                  int &bsc, int &bd, int &bg, int &bo, int &bni, int &nh)
 {
-    // oriented query forward walk: strand 0 -> QF (forward), 1 -> QR (revcomp);
-    // leftwards walk from x: strand 0 -> QR at Lq - x, 1 -> QF at Lq - x
-    const uint64_t *AR = strand ? QR : QF;
-    const uint64_t *ARM = strand ? QRM : QFM;
-    const PT ar0 = strand ? qr0 : qf0;
-    const uint64_t *AL = strand ? QF : QR;
-    const uint64_t *ALM = strand ? QFM : QRM;
-    const PT al0 = strand ? qf0 : qr0;
     nh = 0;
     for (int si = 0; si < ns && nh < MAX_HSP; si++) {
         const GSeed s = sd[si];
         const int x = (int)s.x, y = (int)s.y, len = (int)s.len;
         const bool inside = lane < nh && bqa <= x && x + len <= bqb && bsa <= y && y + len <= bsb;
         if (__ballot(inside)) continue;
-        const ExtRes r = ext_wave<AMB, PT>(AR, ARM, ar0 + (PT)(x + len), Lq - (x + len), TF, TFM,
-                                           tf0 + (PT)(y + len), Lt - (y + len), X, lane);
-        const ExtRes l = ext_wave<AMB, PT>(AL, ALM, al0 + (PT)(Lq - x), x, TR, TRM, tr0 + (PT)(Lt - y), y,
-                                           X, lane);
+        const ExtRes r = ext_wave<AMB, false, PT>(QO, QOM, qo + (PT)(x + len), Lq - (x + len), TF, TFM,
+                                                  tf + (PT)(y + len), Lt - (y + len), X, lane);
+        const ExtRes l = ext_wave<AMB, true, PT>(QO, QOM, qo + (PT)x, x, TF, TFM, tf + (PT)y, y, X, lane);
         if (lane == nh) {
             bqa = x - l.i; bqb = x + len + r.i; bsa = y - l.j; bsb = y + len + r.j;
             bsc = l.score + 2 * len + r.score;
@@ -476,11 +480,21 @@ __device__ __forceinline__ void process_candidate(
     }
 }
 
+constexpr int SPAD = 32;                               // front pad of staged sequences (bases)
+constexpr int SW2 = (STAGE_BASES + SPAD) / 32 + 3;     // u64 words per staged sequence
+
+// stage bases [pos, pos + L) of a packed global array at LDS base SPAD
+__device__ __forceinline__ void stage_seq(uint64_t *dst, const uint64_t *src, uint64_t pos, int L, int lane)
+{
+    const int nw = (L >> 5) + 3;
+    for (int w = lane; w < nw; w += 64) dst[w] = w ? win<uint64_t>(src, pos + 32 * (uint64_t)(w - 1)) : 0ull;
+}
+
 template <bool AMB>
 __global__ __launch_bounds__(EBLOCK) void extend_kernel(Db db, ExtParams P)
 {
-    constexpr int NA = AMB ? 8 : 4;
-    __shared__ uint64_t stg[EWAVES][NA][SW];
+    constexpr int NA = AMB ? 4 : 2;
+    __shared__ uint64_t stg[EWAVES][NA][SW2];
     __shared__ GSeed sseed[EWAVES][64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint64_t total = db.total;
@@ -504,31 +518,34 @@ __global__ __launch_bounds__(EBLOCK) void extend_kernel(Db db, ExtParams P)
             sd = sseed[wid];
         }
         int bqa = 0, bqb = 0, bsa = 0, bsb = 0, bsc = 0, bd = 0, bg = 0, bo = 0, bni = 0, nh = 0;
-        const uint64_t qr_g = total - qt.start - (uint64_t)Lq;   // revcomp(q) start in RC
-        const uint64_t tr_g = total - st.start - (uint64_t)Lt;
-        if (Lq + 32 <= STAGE_BASES && Lt + 32 <= STAGE_BASES) {
-            uint64_t *QF = stg[wid][0], *QR = stg[wid][1], *TF = stg[wid][2], *TR = stg[wid][3];
-            const int nq = (Lq >> 5) + 2, nt = (Lt >> 5) + 2;
-            stage(QF, db.F, qt.start, nq, lane);
-            stage(QR, db.RC, qr_g, nq, lane);
-            stage(TF, db.F, st.start, nt, lane);
-            stage(TR, db.RC, tr_g, nt, lane);
-            uint64_t *QFM = nullptr, *QRM = nullptr, *TFM = nullptr, *TRM = nullptr;
+        // oriented query: q (forward array) or revcomp(q) (reverse-complement array)
+        const uint64_t *QA = strand ? db.RC : db.F;
+        const uint64_t *QAM = strand ? db.ARC : db.AF;
+        const uint64_t q0 = strand ? total - qt.start - (uint64_t)Lq : qt.start;
+        if (Lq + SPAD <= STAGE_BASES && Lt + SPAD <= STAGE_BASES) {
+            uint64_t *QO = stg[wid][0], *TF = stg[wid][1];
+            stage_seq(QO, QA, q0, Lq, lane);
+            stage_seq(TF, db.F, st.start, Lt, lane);
+            const uint32_t *QOM = nullptr, *TFM = nullptr;
             if (AMB) {
-                QFM = stg[wid][NA - 4]; QRM = stg[wid][NA - 3]; TFM = stg[wid][NA - 2]; TRM = stg[wid][NA - 1];
-                stage(QFM, db.AF, qt.start, nq, lane);
-                stage(QRM, db.ARC, qr_g, nq, lane);
-                stage(TFM, db.AF, st.start, nt, lane);
-                stage(TRM, db.ARC, tr_g, nt, lane);
+                stage_seq(stg[wid][2], QAM, q0, Lq, lane);
+                stage_seq(stg[wid][3], db.AF, st.start, Lt, lane);
+                QOM = reinterpret_cast<const uint32_t *>(stg[wid][2]);
+                TFM = reinterpret_cast<const uint32_t *>(stg[wid][3]);
             }
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            process_candidate<AMB, uint32_t>(QF, QFM, 0u, QR, QRM, 0u, TF, TFM, 0u, TR, TRM, 0u, Lq, Lt, strand, sd,
+            process_candidate<AMB, uint32_t>(reinterpret_cast<const uint32_t *>(QO), QOM, (uint32_t)SPAD,
+                                             reinterpret_cast<const uint32_t *>(TF), TFM, (uint32_t)SPAD, Lq, Lt, sd,
                                              ns, P.xdrop, lane, bqa, bqb, bsa, bsb, bsc, bd, bg, bo, bni, nh);
         } else {
-            process_candidate<AMB, uint64_t>(db.F, db.AF, qt.start, db.RC, db.ARC, qr_g, db.F, db.AF, st.start, db.RC,
-                                             db.ARC, tr_g, Lq, Lt, strand, sd, ns, P.xdrop, lane, bqa, bqb, bsa, bsb,
-                                             bsc, bd, bg, bo, bni, nh);
+            // global arrays carry two zero words in front, so backward windows
+            // of the first transcript stay in bounds (positions may go to -32)
+            process_candidate<AMB, int64_t>(reinterpret_cast<const uint32_t *>(QA),
+                                            reinterpret_cast<const uint32_t *>(QAM), (int64_t)q0,
+                                            reinterpret_cast<const uint32_t *>(db.F),
+                                            reinterpret_cast<const uint32_t *>(db.AF), (int64_t)st.start, Lq, Lt,
+                                            sd, ns, P.xdrop, lane, bqa, bqb, bsa, bsb, bsc, bd, bg, bo, bni, nh);
         }
         // purge HSPs with common endpoints: by (score desc, index asc)
         int rank = 0;

@@ -42,6 +42,7 @@ void launch_distance(const unsigned long long *, const unsigned long long *, con
 using namespace rcg;
 
 static thread_local std::string g_err;
+static const size_t FRONT_PAD = 2;   // zero words in front of every packed array
 
 static int fail(int code, const std::string &msg)
 {
@@ -452,11 +453,17 @@ static int upload(rc_engine *e)
     const uint64_t nwords = (total + 31) / 32 + 4;
     CHK(e->d_ascii.ensure(total + 64));
     HIPCHK(hipMemcpyAsync(e->d_ascii.p, e->seq.data(), total, hipMemcpyHostToDevice, e->st));
-    CHK(e->d_F.ensure(nwords));
-    CHK(e->d_RC.ensure(nwords));
+    // packed arrays carry FRONT_PAD zero words in front (backward windows of
+    // the first transcript read them); the kernels see p + FRONT_PAD
+    CHK(e->d_F.ensure(nwords + FRONT_PAD));
+    CHK(e->d_RC.ensure(nwords + FRONT_PAD));
+    HIPCHK(hipMemsetAsync(e->d_F.p, 0, (nwords + FRONT_PAD) * 8, e->st));
+    HIPCHK(hipMemsetAsync(e->d_RC.p, 0, (nwords + FRONT_PAD) * 8, e->st));
     if (e->has_amb) {
-        CHK(e->d_AF.ensure(nwords));
-        CHK(e->d_ARC.ensure(nwords));
+        CHK(e->d_AF.ensure(nwords + FRONT_PAD));
+        CHK(e->d_ARC.ensure(nwords + FRONT_PAD));
+        HIPCHK(hipMemsetAsync(e->d_AF.p, 0, (nwords + FRONT_PAD) * 8, e->st));
+        HIPCHK(hipMemsetAsync(e->d_ARC.p, 0, (nwords + FRONT_PAD) * 8, e->st));
     }
     std::vector<TxInfo> txi(n_tx);
     for (uint32_t t = 0; t < n_tx; t++) {
@@ -529,7 +536,7 @@ static int build_index(rc_engine *e)
     if (amb) {
         CHK(e->d_kcnt.ensure(n_tx + 1));
         HIPCHK(hipMemsetAsync(e->d_kcnt.p, 0, (n_tx + 1) * sizeof(uint64_t), e->st));
-        if (n_tx) launch_kmer_count(e->d_tx.p, n_tx, e->d_AF.p, e->d_kcnt.p, e->st);
+        if (n_tx) launch_kmer_count(e->d_tx.p, n_tx, e->d_AF.p + FRONT_PAD, e->d_kcnt.p, e->st);
         size_t tmp = 0;
         HIPCHK(rocprim::exclusive_scan(nullptr, tmp, e->d_kcnt.p, e->d_kpos_off.p, (uint64_t)0, (size_t)n_tx + 1,
                                        rocprim::plus<uint64_t>(), e->st));
@@ -543,7 +550,8 @@ static int build_index(rc_engine *e)
     CHK(e->d_keys2.ensure(npos));
     CHK(e->d_vals.ensure(npos));
     CHK(e->d_vals2.ensure(npos));
-    if (n_tx) launch_kmer_fill(amb, e->d_tx.p, n_tx, e->d_F.p, e->d_AF.p, e->d_kpos_off.p, e->d_keys.p, e->d_vals.p,
+    if (n_tx) launch_kmer_fill(amb, e->d_tx.p, n_tx, e->d_F.p + FRONT_PAD, amb ? e->d_AF.p + FRONT_PAD : nullptr,
+                               e->d_kpos_off.p, e->d_keys.p, e->d_vals.p,
                                e->st);
     size_t tmp = 0;
     HIPCHK(rocprim::radix_sort_pairs(nullptr, tmp, e->d_keys.p, e->d_keys2.p, e->d_vals.p, e->d_vals2.p, (size_t)npos,
@@ -560,10 +568,10 @@ static int build_index(rc_engine *e)
 static Db make_db(rc_engine *e)
 {
     Db db;
-    db.F = e->d_F.p;
-    db.RC = e->d_RC.p;
-    db.AF = e->has_amb ? e->d_AF.p : nullptr;
-    db.ARC = e->has_amb ? e->d_ARC.p : nullptr;
+    db.F = e->d_F.p + FRONT_PAD;
+    db.RC = e->d_RC.p + FRONT_PAD;
+    db.AF = e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr;
+    db.ARC = e->has_amb ? e->d_ARC.p + FRONT_PAD : nullptr;
     db.total = e->seq.size();
     db.tx = e->d_tx.p;
     db.tx_gene = e->d_tx_gene.p;
@@ -658,8 +666,8 @@ static int do_align(rc_engine *e)
     const uint64_t total = e->seq.size();
     const uint64_t nwords = (total + 31) / 32 + 2;
     HIPCHK(hipEventRecord(e->ev[0], e->st));
-    launch_pack(e->d_ascii.p, total, nwords, e->d_F.p, e->d_RC.p, e->has_amb ? e->d_AF.p : nullptr,
-                e->has_amb ? e->d_ARC.p : nullptr, e->st);
+    launch_pack(e->d_ascii.p, total, nwords, e->d_F.p + FRONT_PAD, e->d_RC.p + FRONT_PAD,
+                e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr, e->has_amb ? e->d_ARC.p + FRONT_PAD : nullptr, e->st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e->ev[1], e->st));
     CHK(build_index(e));
