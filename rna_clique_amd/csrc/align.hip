@@ -462,21 +462,32 @@ __device__ __forceinline__ void process_candidate(const uint32_t *QO, const uint
                                                   int &bsc, int &bd, int &bg, int &bo, int &bni, int &nh)
 {
     nh = 0;
-    for (int si = 0; si < ns && nh < MAX_HSP; si++) {
-        const GSeed s = sd[si];
-        const int x = (int)s.x, y = (int)s.y, len = (int)s.len;
-        const bool inside = lane < nh && bqa <= x && x + len <= bqb && bsa <= y && y + len <= bsb;
-        if (__ballot(inside)) continue;
-        const ExtRes r = ext_wave<AMB, false, PT>(QO, QOM, qo + (PT)(x + len), Lq - (x + len), TF, TFM,
-                                                  tf + (PT)(y + len), Lt - (y + len), X, lane);
-        const ExtRes l = ext_wave<AMB, true, PT>(QO, QOM, qo + (PT)x, x, TF, TFM, tf + (PT)y, y, X, lane);
-        if (lane == nh) {
-            bqa = x - l.i; bqb = x + len + r.i; bsa = y - l.j; bsb = y + len + r.j;
-            bsc = l.score + 2 * len + r.score;
-            bd = l.d + r.d; bg = l.g + r.g; bo = l.o + r.o;
-            bni = len + (l.i + l.j - 2 * l.d + l.g) / 2 + (r.i + r.j - 2 * r.d + r.g) / 2;
+    for (int c0 = 0; c0 < ns && nh < MAX_HSP; c0 += 64) {
+        // lane i holds seed c0 + i; the loop broadcasts them with readlane
+        int sx = 0, sy = 0, sl = 0;
+        if (c0 + lane < ns) {
+            const GSeed g = sd[c0 + lane];
+            sx = (int)g.x;
+            sy = (int)g.y;
+            sl = (int)g.len;
         }
-        nh++;
+        const int nc = min(ns - c0, 64);
+        for (int si = 0; si < nc && nh < MAX_HSP; si++) {
+            const int x = __builtin_amdgcn_readlane(sx, si), y = __builtin_amdgcn_readlane(sy, si);
+            const int len = __builtin_amdgcn_readlane(sl, si);
+            const bool inside = lane < nh && bqa <= x && x + len <= bqb && bsa <= y && y + len <= bsb;
+            if (__ballot(inside)) continue;
+            const ExtRes r = ext_wave<AMB, false, PT>(QO, QOM, qo + (PT)(x + len), Lq - (x + len), TF, TFM,
+                                                      tf + (PT)(y + len), Lt - (y + len), X, lane);
+            const ExtRes l = ext_wave<AMB, true, PT>(QO, QOM, qo + (PT)x, x, TF, TFM, tf + (PT)y, y, X, lane);
+            if (lane == nh) {
+                bqa = x - l.i; bqb = x + len + r.i; bsa = y - l.j; bsb = y + len + r.j;
+                bsc = l.score + 2 * len + r.score;
+                bd = l.d + r.d; bg = l.g + r.g; bo = l.o + r.o;
+                bni = len + (l.i + l.j - 2 * l.d + l.g) / 2 + (r.i + r.j - 2 * r.d + r.g) / 2;
+            }
+            nh++;
+        }
     }
 }
 
@@ -495,28 +506,44 @@ __global__ __launch_bounds__(EBLOCK) void extend_kernel(Db db, ExtParams P)
 {
     constexpr int NA = AMB ? 4 : 2;
     __shared__ uint64_t stg[EWAVES][NA][SW2];
-    __shared__ GSeed sseed[EWAVES][64];
+    __shared__ unsigned long long sprefix[NSHARD + 1];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i <= NSHARD; i += EBLOCK) sprefix[i] = P.shard_prefix[i];
+    __syncthreads();
     const uint64_t total = db.total;
     const uint64_t nwaves = (uint64_t)gridDim.x * EWAVES;
-    for (uint64_t li = (uint64_t)blockIdx.x * EWAVES + wid; li < P.n_cand; li += nwaves) {
-        int lo = 0, hi = NSHARD;   // shard of linear candidate li
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (P.shard_prefix[mid] <= li) lo = mid; else hi = mid;
+    int shard = 0;   // advances monotonically with li
+    uint64_t li = (uint64_t)blockIdx.x * EWAVES + wid;
+    auto locate = [&](uint64_t l) -> uint64_t {
+        while (shard + 1 < NSHARD && sprefix[shard + 1] <= l) shard++;
+        return (uint64_t)shard * P.cand_cap + (l - sprefix[shard]);
+    };
+    // software pipeline: the next candidate's record and transcripts are in
+    // flight while the current one is extended
+    Cand ncd{};
+    TxInfo nqt{}, nst{};
+    uint64_t nci = 0;
+    if (li < P.n_cand) {
+        nci = locate(li);
+        ncd = P.cands[nci];
+        nqt = db.tx[ncd.q_gtx];
+        nst = db.tx[ncd.s_gtx];
+    }
+    for (; li < P.n_cand; li += nwaves) {
+        const uint64_t ci = nci;
+        const Cand cd = ncd;
+        const TxInfo qt = nqt, st = nst;
+        const uint64_t lnext = li + nwaves;
+        if (lnext < P.n_cand) {
+            nci = locate(lnext);
+            ncd = P.cands[nci];
+            nqt = db.tx[ncd.q_gtx];
+            nst = db.tx[ncd.s_gtx];
         }
-        const uint64_t ci = (uint64_t)lo * P.cand_cap + (li - P.shard_prefix[lo]);
-        const Cand cd = P.cands[ci];
-        const TxInfo qt = db.tx[cd.q_gtx], st = db.tx[cd.s_gtx];
         const int Lq = (int)qt.len, Lt = (int)st.len;
         const int strand = cd.strand;
         const int ns = cd.seed_cnt;
-        // seeds: through LDS when few (the common case), else straight from HBM
         const GSeed *sd = P.seeds + cd.seed_off;
-        if (ns <= 64) {
-            if (lane < ns) sseed[wid][lane] = sd[lane];
-            sd = sseed[wid];
-        }
         int bqa = 0, bqb = 0, bsa = 0, bsb = 0, bsc = 0, bd = 0, bg = 0, bo = 0, bni = 0, nh = 0;
         // oriented query: q (forward array) or revcomp(q) (reverse-complement array)
         const uint64_t *QA = strand ? db.RC : db.F;
