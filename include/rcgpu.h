@@ -101,6 +101,8 @@ typedef struct rc_timing {
     double pack_ms, index_ms, align_ms, topn_ms, rbh_ms, graph_ms, reduce_ms, total_ms;
     double seed_kernel_ms;    /* device time of the seed kernel (lookups, seeds) */
     double align_kernel_ms;   /* device time of the extension kernel */
+    double ext_steps;         /* greedy X-drop steps executed (wave-level) */
+    double ext_calls;         /* greedy extensions (left + right per HSP attempt) */
 } rc_timing;
 
 void rc_default_opts(rc_opts *opts);

@@ -74,7 +74,8 @@ EDGE_DTYPE = np.dtype([("sample_a", np.int32), ("gene_a", np.int32),
 class RcTiming(ctypes.Structure):
     _fields_ = [(n, ctypes.c_double) for n in (
         "pack_ms", "index_ms", "align_ms", "topn_ms", "rbh_ms", "graph_ms",
-        "reduce_ms", "total_ms", "seed_kernel_ms", "align_kernel_ms")]
+        "reduce_ms", "total_ms", "seed_kernel_ms", "align_kernel_ms", "ext_steps",
+        "ext_calls")]
 
 
 assert HSP_DTYPE.itemsize == ctypes.sizeof(RcHsp)

@@ -395,7 +395,7 @@ __device__ __forceinline__ int slide(const uint32_t *A, const uint32_t *AM, PT p
 template <bool AMB, bool BACK, typename PT>
 __device__ __forceinline__ ExtRes ext_wave(const uint32_t *A, const uint32_t *AM, PT pa, int alen,
                                            const uint32_t *B, const uint32_t *BM, PT pb, int blen, int X,
-                                           int lane)
+                                           int lane, uint32_t &steps)
 {
     constexpr int EBIT = 26, OBIT = 13;
     constexpr int GMASK = 8191;
@@ -408,6 +408,7 @@ __device__ __forceinline__ ExtRes ext_wave(const uint32_t *A, const uint32_t *AM
     int R = lane == -BAND_LO ? r0 : -1;
     int goe = 0;
     for (int d = 1; d <= DMAX; ++d) {
+        steps++;
         const int Rl = from_lower(R, -1), Rr = from_upper(R, -1);
         const int gl = from_lower(goe, 0), gr = from_upper(goe, 0);
         // candidates; ties prefer mismatch, then insertion, then deletion
@@ -459,7 +460,8 @@ template <bool AMB, typename PT>
 __device__ __forceinline__ void process_candidate(const uint32_t *QO, const uint32_t *QOM, PT qo, const uint32_t *TF,
                                                   const uint32_t *TFM, PT tf, int Lq, int Lt, const GSeed *sd,
                                                   int ns, int X, int lane, int &bqa, int &bqb, int &bsa, int &bsb,
-                                                  int &bsc, int &bd, int &bg, int &bo, int &bni, int &nh)
+                                                  int &bsc, int &bd, int &bg, int &bo, int &bni, int &nh,
+                                                  uint32_t &steps, uint32_t &exts)
 {
     nh = 0;
     for (int c0 = 0; c0 < ns && nh < MAX_HSP; c0 += 64) {
@@ -478,8 +480,10 @@ __device__ __forceinline__ void process_candidate(const uint32_t *QO, const uint
             const bool inside = lane < nh && bqa <= x && x + len <= bqb && bsa <= y && y + len <= bsb;
             if (__ballot(inside)) continue;
             const ExtRes r = ext_wave<AMB, false, PT>(QO, QOM, qo + (PT)(x + len), Lq - (x + len), TF, TFM,
-                                                      tf + (PT)(y + len), Lt - (y + len), X, lane);
-            const ExtRes l = ext_wave<AMB, true, PT>(QO, QOM, qo + (PT)x, x, TF, TFM, tf + (PT)y, y, X, lane);
+                                                      tf + (PT)(y + len), Lt - (y + len), X, lane, steps);
+            const ExtRes l = ext_wave<AMB, true, PT>(QO, QOM, qo + (PT)x, x, TF, TFM, tf + (PT)y, y, X, lane,
+                                                     steps);
+            exts += 2;
             if (lane == nh) {
                 bqa = x - l.i; bqb = x + len + r.i; bsa = y - l.j; bsb = y + len + r.j;
                 bsc = l.score + 2 * len + r.score;
@@ -520,6 +524,7 @@ __global__ __launch_bounds__(EBLOCK) void extend_kernel(Db db, ExtParams P)
     };
     // software pipeline: the next candidate's record and transcripts are in
     // flight while the current one is extended
+    uint32_t steps = 0, exts = 0, ncands = 0;
     Cand ncd{};
     TxInfo nqt{}, nst{};
     uint64_t nci = 0;
@@ -544,6 +549,7 @@ __global__ __launch_bounds__(EBLOCK) void extend_kernel(Db db, ExtParams P)
         const int strand = cd.strand;
         const int ns = cd.seed_cnt;
         const GSeed *sd = P.seeds + cd.seed_off;
+        ncands++;
         int bqa = 0, bqb = 0, bsa = 0, bsb = 0, bsc = 0, bd = 0, bg = 0, bo = 0, bni = 0, nh = 0;
         // oriented query: q (forward array) or revcomp(q) (reverse-complement array)
         const uint64_t *QA = strand ? db.RC : db.F;
@@ -564,7 +570,8 @@ __global__ __launch_bounds__(EBLOCK) void extend_kernel(Db db, ExtParams P)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             process_candidate<AMB, uint32_t>(reinterpret_cast<const uint32_t *>(QO), QOM, (uint32_t)SPAD,
                                              reinterpret_cast<const uint32_t *>(TF), TFM, (uint32_t)SPAD, Lq, Lt, sd,
-                                             ns, P.xdrop, lane, bqa, bqb, bsa, bsb, bsc, bd, bg, bo, bni, nh);
+                                             ns, P.xdrop, lane, bqa, bqb, bsa, bsb, bsc, bd, bg, bo, bni, nh, steps,
+                                             exts);
         } else {
             // global arrays carry two zero words in front, so backward windows
             // of the first transcript stay in bounds (positions may go to -32)
@@ -572,7 +579,8 @@ __global__ __launch_bounds__(EBLOCK) void extend_kernel(Db db, ExtParams P)
                                             reinterpret_cast<const uint32_t *>(QAM), (int64_t)q0,
                                             reinterpret_cast<const uint32_t *>(db.F),
                                             reinterpret_cast<const uint32_t *>(db.AF), (int64_t)st.start, Lq, Lt,
-                                            sd, ns, P.xdrop, lane, bqa, bqb, bsa, bsb, bsc, bd, bg, bo, bni, nh);
+                                            sd, ns, P.xdrop, lane, bqa, bqb, bsa, bsb, bsc, bd, bg, bo, bni, nh,
+                                            steps, exts);
         }
         // purge HSPs with common endpoints: by (score desc, index asc)
         int rank = 0;
@@ -625,6 +633,11 @@ __global__ __launch_bounds__(EBLOCK) void extend_kernel(Db db, ExtParams P)
             P.cand_nh[ci] = (uint8_t)nout;
             P.cand_ovf[ci] = obase;
         }
+    }
+    if (lane == 0 && P.counters) {
+        atomicAdd(&P.counters[0], (unsigned long long)steps);
+        atomicAdd(&P.counters[1], (unsigned long long)exts);
+        atomicAdd(&P.counters[2], (unsigned long long)ncands);
     }
 }
 

@@ -113,6 +113,7 @@ struct ExtParams {
     uint64_t ovf_cap;
     unsigned long long *ovf_count;
     unsigned int *status;         // bit 0 overflow
+    unsigned long long *counters; // [0] greedy steps, [1] extensions, [2] candidates (one atomic per wave)
 };
 
 // group kernels: candidates of each (gene, sample) -> contiguous HSP groups.

@@ -778,15 +778,19 @@ static int do_align(rc_engine *e)
         X.ovf_cap = e->ovf_cap;
         X.ovf_count = e->d_count.p;
         X.status = e->d_status.p;
+        X.counters = e->d_count.p + 1;
         HIPCHK(hipEventRecord(e->ev[10], e->st));
         launch_extend(e->has_amb, db, X, e->st);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e->ev[11], e->st));
-        unsigned long long ovn = 0;
+        unsigned long long ovn = 0, ctr[3] = {0, 0, 0};
         unsigned int status = 0;
         HIPCHK(hipMemcpyAsync(&ovn, e->d_count.p, sizeof ovn, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipMemcpyAsync(ctr, e->d_count.p + 1, sizeof ctr, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipStreamSynchronize(e->st));
+        e->tm.ext_steps = (double)ctr[0];
+        e->tm.ext_calls = (double)ctr[1];
         if (!(status & 1u)) break;
         e->ovf_cap = ovn * 5 / 4 + 1024;
     }
