@@ -350,55 +350,40 @@ __device__ __forceinline__ int from_upper(int v, int edge)
     return __builtin_amdgcn_update_dpp(edge, v, 0x130, 0xF, 0xF, false);   // wave_shl:1
 }
 
-// 64 bases starting at base p of a packed array viewed as dwords (16 bases
-// each): five dword loads and four funnel shifts (v_alignbit_b32).
+// 32 bases starting at base p of a packed array viewed as dwords (16 bases
+// each): three dword loads and two funnel shifts (v_alignbit_b32).
 template <typename PT>
-__device__ __forceinline__ void win5(const uint32_t *__restrict__ a, PT p, uint64_t &lo, uint64_t &hi)
+__device__ __forceinline__ uint64_t win3(const uint32_t *__restrict__ a, PT p)
 {
     const PT i = p >> 4;
     const uint32_t sh = ((uint32_t)p & 15u) * 2u;
-    const uint32_t w0 = a[i], w1 = a[i + 1], w2 = a[i + 2], w3 = a[i + 3], w4 = a[i + 4];
-    lo = ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32) | __builtin_amdgcn_alignbit(w1, w0, sh);
-    hi = ((uint64_t)__builtin_amdgcn_alignbit(w4, w3, sh) << 32) | __builtin_amdgcn_alignbit(w3, w2, sh);
+    const uint32_t w0 = a[i], w1 = a[i + 1], w2 = a[i + 2];
+    const uint32_t lo = __builtin_amdgcn_alignbit(w1, w0, sh);
+    const uint32_t hi = __builtin_amdgcn_alignbit(w2, w1, sh);
+    return ((uint64_t)hi << 32) | lo;
 }
 
 // Matching bases walking forward from (pa, pb) (BACK = false) or backwards
-// from (pa - 1, pb - 1) (BACK = true: the 64-base window ending at p is read
-// at p - 64 and the first mismatch is its highest differing base), at most
-// maxn (<= 0: nothing). Wave-uniform loop, predicated body: no divergent
-// branches; finished lanes read a clamped, in-bounds window.
+// from (pa - 1, pb - 1) (BACK = true; the window ending at p is read at p - 32
+// and the first mismatch is its highest differing base), at most maxn.
 template <bool AMB, bool BACK, typename PT>
 __device__ __forceinline__ int slide(const uint32_t *A, const uint32_t *AM, PT pa, const uint32_t *B,
                                      const uint32_t *BM, PT pb, int maxn)
 {
     int n = 0;
-    bool more = maxn > 0;
-    while (__ballot(more)) {
-        const PT off = more ? (PT)(BACK ? n + 64 : n) : (PT)(BACK ? 64 : 0);
-        const PT qa = more ? (BACK ? pa - off : pa + off) : (BACK ? (PT)64 : (PT)0);
-        const PT qb = more ? (BACK ? pb - off : pb + off) : (BACK ? (PT)64 : (PT)0);
-        uint64_t alo, ahi, blo, bhi;
-        win5(A, qa, alo, ahi);
-        win5(B, qb, blo, bhi);
-        uint64_t xl = alo ^ blo, xh = ahi ^ bhi;
-        if (AMB) {
-            uint64_t mlo, mhi, nlo, nhi;
-            win5(AM, qa, mlo, mhi);
-            win5(BM, qb, nlo, nhi);
-            xl |= mlo | nlo;
-            xh |= mhi | nhi;
+    while (n < maxn) {
+        const PT qa = BACK ? pa - (PT)(n + 32) : pa + (PT)n;
+        const PT qb = BACK ? pb - (PT)(n + 32) : pb + (PT)n;
+        uint64_t x = win3(A, qa) ^ win3(B, qb);
+        if (AMB) x |= win3(AM, qa) | win3(BM, qb);
+        if (x == 0) {
+            n += 32;
+            continue;
         }
-        // BACK: the base next to p is the top of the window (xh's high bits)
-        const uint64_t first = BACK ? xh : xl, second = BACK ? xl : xh;
-        const int c1 = BACK ? __builtin_clzll(first | 1ull) : __builtin_ctzll(first | (1ull << 63));
-        const int c2 = BACK ? __builtin_clzll(second | 1ull) : __builtin_ctzll(second | (1ull << 63));
-        const int adv = first ? (c1 >> 1) : (second ? 32 + (c2 >> 1) : 64);
-        if (more) {
-            n += adv;
-            more = adv == 64 && n < maxn;
-        }
+        n += (BACK ? __builtin_clzll(x) : __builtin_ctzll(x)) >> 1;
+        return n < maxn ? n : maxn;
     }
-    return n < maxn ? n : (maxn > 0 ? maxn : 0);
+    return maxn > 0 ? maxn : 0;
 }
 
 // Greedy X-drop extension (oracle/align_oracle.c greedy_ext), one diagonal per
@@ -415,7 +400,8 @@ __device__ __forceinline__ ExtRes ext_wave(const uint32_t *A, const uint32_t *AM
     constexpr int EBIT = 26, OBIT = 13;
     constexpr int GMASK = 8191;
     const int k = lane + BAND_LO;
-    int r0 = slide<AMB, BACK, PT>(A, AM, pa, B, BM, pb, lane == -BAND_LO ? min(alen, blen) : 0);
+    int r0 = 0;
+    if (lane == -BAND_LO) r0 = slide<AMB, BACK, PT>(A, AM, pa, B, BM, pb, min(alen, blen));
     r0 = __builtin_amdgcn_readlane(r0, -BAND_LO);
     ExtRes best = {2 * r0, r0, r0, 0, 0, 0};
     if (min(alen, blen) - r0 <= 0) return best;
@@ -434,17 +420,18 @@ __device__ __forceinline__ ExtRes ext_wave(const uint32_t *A, const uint32_t *AM
         const int gi = (gl & ~(3 << EBIT)) + 1 + ((((gl >> EBIT) & 3) == 1) ? 0 : (1 << OBIT)) + (1 << EBIT);
         const int gd = (gr & ~(3 << EBIT)) + 1 + ((((gr >> EBIT) & 3) == 2) ? 0 : (1 << OBIT)) + (2 << EBIT);
         int ng = fm ? (goe & ~(3 << EBIT)) : (fi ? gi : gd);
-        const bool cand = ni >= 0;
-        const int nic = cand ? ni : 0;
-        const int ja = nic - k;
-        const int m = cand ? min(alen - nic, blen - ja) : 0;
-        const int s = slide<AMB, BACK, PT>(A, AM, BACK ? pa - (PT)nic : pa + (PT)nic, B, BM,
-                                           BACK ? pb - (PT)ja : pb + (PT)ja, m);
-        ni = cand ? ni + s : -1;
-        ng = (s > 0) ? (ng & ~(3 << EBIT)) : ng;
-        const int score = 2 * ni - k - 6 * d;
-        const int bound = score + 2 * (m - s);
-        ni = (cand && score >= best.score - X) ? ni : -1;
+        int score = INT_MIN, bound = INT_MIN;
+        if (ni >= 0) {
+            const int ja = ni - k;
+            const int m = min(alen - ni, blen - ja);
+            const int s = slide<AMB, BACK, PT>(A, AM, BACK ? pa - (PT)ni : pa + (PT)ni, B, BM,
+                                               BACK ? pb - (PT)ja : pb + (PT)ja, m);
+            ni += s;
+            if (s > 0) ng &= ~(3 << EBIT);
+            score = 2 * ni - k - 6 * d;
+            if (score < best.score - X) ni = -1;
+            bound = score + 2 * (m - s);
+        }
         R = ni;
         goe = ng;
         const bool live = ni >= 0;
@@ -508,16 +495,14 @@ __device__ __forceinline__ void process_candidate(const uint32_t *QO, const uint
     }
 }
 
-constexpr int SPAD = 64;                               // front pad of staged sequences (bases)
-constexpr int SW2 = (STAGE_BASES + SPAD) / 32 + 4;     // u64 words per staged sequence
+constexpr int SPAD = 32;                               // front pad of staged sequences (bases)
+constexpr int SW2 = (STAGE_BASES + SPAD) / 32 + 3;     // u64 words per staged sequence
 
-// stage bases [pos, pos + L) of a packed global array at LDS base SPAD (the
-// two front words stay zero: backward 64-base windows read them)
+// stage bases [pos, pos + L) of a packed global array at LDS base SPAD
 __device__ __forceinline__ void stage_seq(uint64_t *dst, const uint64_t *src, uint64_t pos, int L, int lane)
 {
-    const int nw = ((L + SPAD) >> 5) + 4;
-    for (int w = lane; w < nw; w += 64)
-        dst[w] = w >= 2 ? win<uint64_t>(src, pos + 32 * (uint64_t)(w - 2)) : 0ull;
+    const int nw = (L >> 5) + 3;
+    for (int w = lane; w < nw; w += 64) dst[w] = w ? win<uint64_t>(src, pos + 32 * (uint64_t)(w - 1)) : 0ull;
 }
 
 template <bool AMB>
