@@ -33,6 +33,11 @@
  *  5. Purge HSPs sharing a start or end point (keep higher score, then earlier),
  *     keep HSPs whose e-value <= evalue (Karlin-Altschul, lambda 1.28, K 0.46,
  *     H 0.85, alpha 1.5, beta -2 for 1/-2 linear; BLAST length adjustment).
+ *  5b. Symmetry: both directed searches of a sample pair find the same seed set
+ *     (every maximal exact run >= W), so candidates are extended once, with the
+ *     lower-numbered sample as query; the other direction reports the mirror
+ *     images under its own e-value cut. (BLAST runs the two searches
+ *     independently; this is where the restatement departs from it.)
  *  6. Bitscore as BLAST prints it (integer-truncated above 99.9) in tenths.
  */
 #include <math.h>
@@ -349,9 +354,26 @@ static void push_hsp(hsp_vec *hv, const orc_hsp *h)
     hv->v[hv->n++] = *h;
 }
 
+/* A kept (purged) HSP of a candidate, before any e-value cut. */
+typedef struct {
+    uint32_t qtx, stx;
+    int32_t strand, hidx;      /* hidx: index in the candidate's HSP list */
+    int32_t qa, qb, sa, sb, score, d, g, o, nident, Lq, Lt;
+} core_hsp;
+
+typedef struct { core_hsp *v; uint64_t n, cap; } core_vec;
+
+static void push_core(core_vec *cv, const core_hsp *h)
+{
+    if (cv->n == cv->cap) {
+        cv->cap = cv->cap ? 2 * cv->cap : 1024;
+        cv->v = (core_hsp *)realloc(cv->v, cv->cap * sizeof(core_hsp));
+    }
+    cv->v[cv->n++] = *h;
+}
+
 static void process_candidate(const seqdb *db, uint32_t qtx, int strand, uint32_t stx,
-                              const seed *sd, int ns, int32_t X, int32_t thr,
-                              double ss, hsp_vec *out)
+                              const seed *sd, int ns, int32_t X, core_vec *out)
 {
     hsp_box H[MAX_HSP];
     int nh = 0;
@@ -394,45 +416,57 @@ static void process_candidate(const seqdb *db, uint32_t qtx, int strand, uint32_
         keep[i] = ok;
     }
     for (int i = 0; i < nh; i++) {
-        if (!keep[i] || H[i].score < thr) continue;
-        const hsp_box *b = &H[i];
-        orc_hsp o;
-        memset(&o, 0, sizeof o);
-        o.q_tx = qtx; o.s_tx = stx; o.strand = strand;
-        if (!strand) {
-            o.qstart = b->qa + 1; o.qend = b->qb; o.sstart = b->sa + 1; o.send = b->sb;
-        } else {
-            o.qstart = Lq - b->qb + 1; o.qend = Lq - b->qa; o.sstart = b->sb; o.send = b->sa + 1;
-        }
-        o.gaps = b->g; o.gapopen = b->o; o.mismatch = b->d - b->g; o.nident = b->nident;
-        o.length = o.nident + o.mismatch + o.gaps;
-        o.score_half = b->score;
-        o.bits10 = bits10_of(b->score);
-        o.evalue = evalue_of(ss, b->score);
-        push_hsp(out, &o);
+        if (!keep[i]) continue;
+        core_hsp c;
+        c.qtx = qtx; c.stx = stx; c.strand = strand; c.hidx = i;
+        c.qa = H[i].qa; c.qb = H[i].qb; c.sa = H[i].sa; c.sb = H[i].sb;
+        c.score = H[i].score; c.d = H[i].d; c.g = H[i].g; c.o = H[i].o; c.nident = H[i].nident;
+        c.Lq = Lq; c.Lt = Lt;
+        push_core(out, &c);
     }
 }
 
-/* Directed search: every gene of query sample Q (genes in ascending global gene
- * order, isoforms in input order) against subject sample T. Output order:
- * (gene, isoform, strand, subject tx, HSP). gene_tx: CSR over transcripts. */
-int orc_align(const char *seq, uint64_t total_len, const uint64_t *tx_start,
-              const int32_t *tx_sample, uint32_t n_tx,
-              const uint32_t *gene_tx_off, const uint32_t *gene_tx, uint32_t n_genes,
-              const int32_t *gene_sample, int32_t qsample, int32_t tsample,
-              const orc_params *P, orc_hsp **out, uint64_t *n_out)
+/* BLAST-tabular record of a core HSP, from the computing direction's view
+ * (mirror = 0) or from the other direction's (mirror = 1: query and subject
+ * swap; on the minus strand the subject coordinates run backwards). */
+static orc_hsp to_record(const core_hsp *c, int mirror)
 {
-    if (P->word_size < W16 || P->word_size > 64) return -1;
-    uint8_t *codes = (uint8_t *)malloc(total_len ? total_len : 1);
-    for (uint64_t i = 0; i < total_len; i++) codes[i] = code_of(seq[i]);
+    orc_hsp o;
+    int32_t qs, qe, ss, se;
+    memset(&o, 0, sizeof o);
+    if (!c->strand) {
+        qs = c->qa + 1; qe = c->qb; ss = c->sa + 1; se = c->sb;
+    } else {
+        qs = c->Lq - c->qb + 1; qe = c->Lq - c->qa; ss = c->sb; se = c->sa + 1;
+    }
+    if (!mirror) {
+        o.q_tx = c->qtx; o.s_tx = c->stx;
+        o.qstart = qs; o.qend = qe; o.sstart = ss; o.send = se;
+    } else {
+        o.q_tx = c->stx; o.s_tx = c->qtx;
+        if (!c->strand) { o.qstart = ss; o.qend = se; o.sstart = qs; o.send = qe; }
+        else { o.qstart = se; o.qend = ss; o.sstart = qe; o.send = qs; }
+    }
+    o.strand = c->strand;
+    o.gaps = c->g; o.gapopen = c->o; o.mismatch = c->d - c->g; o.nident = c->nident;
+    o.length = o.nident + o.mismatch + o.gaps;
+    o.score_half = c->score;
+    o.bits10 = bits10_of(c->score);
+    return o;
+}
+
+/* Core search: every gene of query sample Q (genes in ascending global gene
+ * order, isoforms in input order) against subject sample T. Output order:
+ * (gene, isoform, strand, subject tx, HSP index). No e-value cut. */
+static void core_search(const uint8_t *codes, const uint64_t *tx_start, const int32_t *tx_sample,
+                        uint32_t n_tx, const uint32_t *gene_tx_off, const uint32_t *gene_tx,
+                        uint32_t n_genes, const int32_t *gene_sample, int32_t qsample,
+                        int32_t tsample, const orc_params *P, core_vec *cv)
+{
     seqdb db = {codes, tx_start, tx_sample, n_tx};
     sindex ix;
     build_index(&db, tsample, &ix);
-    int64_t dblen = 0, dbn = 0;
-    for (uint32_t t = 0; t < n_tx; t++)
-        if (tx_sample[t] == tsample) { dblen += (int64_t)(tx_start[t + 1] - tx_start[t]); dbn++; }
     const int32_t s = P->word_size - W16 + 1;
-    hsp_vec hv = {0, 0, 0};
     seed *sd = NULL;
     uint64_t sdcap = 0;
     for (uint32_t g = 0; g < n_genes; g++) {
@@ -441,8 +475,6 @@ int orc_align(const char *seq, uint64_t total_len, const uint64_t *tx_start,
             uint32_t q = gene_tx[ii];
             uint64_t qs = tx_start[q];
             int32_t Lq = (int32_t)(tx_start[q + 1] - qs);
-            double ss = search_space(Lq, dblen, dbn);
-            int32_t thr = score_threshold(ss, P->evalue);
             for (int strand = 0; strand < 2; strand++) {
                 uint64_t nsd = 0;
                 for (int32_t p = 0; p + W16 <= Lq; p += s) {
@@ -485,8 +517,7 @@ int orc_align(const char *seq, uint64_t total_len, const uint64_t *tx_start,
                 for (uint64_t i = 0; i < nsd;) {
                     uint64_t j = i;
                     while (j < nsd && sd[j].tx == sd[i].tx) j++;
-                    process_candidate(&db, q, strand, sd[i].tx, sd + i, (int)(j - i),
-                                      P->xdrop_half, thr, ss, &hv);
+                    process_candidate(&db, q, strand, sd[i].tx, sd + i, (int)(j - i), P->xdrop_half, cv);
                     i = j;
                 }
             }
@@ -494,6 +525,79 @@ int orc_align(const char *seq, uint64_t total_len, const uint64_t *tx_start,
     }
     free(sd);
     free(ix.e);
+}
+
+/* ordering of mirrored records: (query gene, query isoform position, strand,
+ * subject tx, HSP index) */
+typedef struct { uint64_t k1, k2; orc_hsp h; } keyed_hsp;
+
+static int keyed_cmp(const void *pa, const void *pb)
+{
+    const keyed_hsp *a = (const keyed_hsp *)pa, *b = (const keyed_hsp *)pb;
+    if (a->k1 != b->k1) return a->k1 < b->k1 ? -1 : 1;
+    if (a->k2 != b->k2) return a->k2 < b->k2 ? -1 : 1;
+    return 0;
+}
+
+/* Directed search (query sample Q, subject sample T). Symmetric spec: the
+ * candidates of a sample pair are extended once, with the lower-numbered
+ * sample as query; the other direction's HSPs are their mirror images. Each
+ * direction applies its own e-value cut (its query length and subject DB).
+ * Output order: (query gene, isoform, strand, subject tx, HSP index). */
+int orc_align(const char *seq, uint64_t total_len, const uint64_t *tx_start,
+              const int32_t *tx_sample, uint32_t n_tx,
+              const uint32_t *gene_tx_off, const uint32_t *gene_tx, uint32_t n_genes,
+              const int32_t *gene_sample, int32_t qsample, int32_t tsample,
+              const orc_params *P, orc_hsp **out, uint64_t *n_out)
+{
+    if (P->word_size < W16 || P->word_size > 64 || qsample == tsample) return -1;
+    uint8_t *codes = (uint8_t *)malloc(total_len ? total_len : 1);
+    for (uint64_t i = 0; i < total_len; i++) codes[i] = code_of(seq[i]);
+    int64_t dblen = 0, dbn = 0;   /* subject sample of this direction */
+    for (uint32_t t = 0; t < n_tx; t++)
+        if (tx_sample[t] == tsample) { dblen += (int64_t)(tx_start[t + 1] - tx_start[t]); dbn++; }
+    const int mirror = qsample > tsample;
+    core_vec cv = {0, 0, 0};
+    core_search(codes, tx_start, tx_sample, n_tx, gene_tx_off, gene_tx, n_genes, gene_sample,
+                mirror ? tsample : qsample, mirror ? qsample : tsample, P, &cv);
+    hsp_vec hv = {0, 0, 0};
+    if (!mirror) {
+        for (uint64_t i = 0; i < cv.n; i++) {
+            const core_hsp *c = &cv.v[i];
+            const double ss = search_space(c->Lq, dblen, dbn);
+            if (c->score < score_threshold(ss, P->evalue)) continue;
+            orc_hsp o = to_record(c, 0);
+            o.evalue = evalue_of(ss, c->score);
+            push_hsp(&hv, &o);
+        }
+    } else {
+        /* position of each transcript inside its gene, and its gene */
+        uint32_t *tx_gene = (uint32_t *)malloc((n_tx ? n_tx : 1) * sizeof(uint32_t));
+        uint32_t *tx_pos = (uint32_t *)malloc((n_tx ? n_tx : 1) * sizeof(uint32_t));
+        for (uint32_t g = 0; g < n_genes; g++)
+            for (uint32_t ii = gene_tx_off[g]; ii < gene_tx_off[g + 1]; ii++) {
+                tx_gene[gene_tx[ii]] = g;
+                tx_pos[gene_tx[ii]] = ii - gene_tx_off[g];
+            }
+        keyed_hsp *kv = (keyed_hsp *)malloc((cv.n ? cv.n : 1) * sizeof(keyed_hsp));
+        uint64_t nk = 0;
+        for (uint64_t i = 0; i < cv.n; i++) {
+            const core_hsp *c = &cv.v[i];
+            const double ss = search_space(c->Lt, dblen, dbn);   /* query = c->stx */
+            if (c->score < score_threshold(ss, P->evalue)) continue;
+            kv[nk].h = to_record(c, 1);
+            kv[nk].h.evalue = evalue_of(ss, c->score);
+            kv[nk].k1 = ((uint64_t)tx_gene[c->stx] << 32) | ((uint64_t)tx_pos[c->stx] << 1) | (uint64_t)c->strand;
+            kv[nk].k2 = ((uint64_t)c->qtx << 8) | (uint64_t)c->hidx;
+            nk++;
+        }
+        qsort(kv, nk, sizeof(keyed_hsp), keyed_cmp);
+        for (uint64_t i = 0; i < nk; i++) push_hsp(&hv, &kv[i].h);
+        free(kv);
+        free(tx_gene);
+        free(tx_pos);
+    }
+    free(cv.v);
     free(codes);
     *out = hv.v;
     *n_out = hv.n;

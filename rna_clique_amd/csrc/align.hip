@@ -125,7 +125,10 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
     const uint32_t n_items = iso_pre[niso];
     const uint32_t gl = g - P.gene_begin;
 
-    int T0 = 0, T1 = N;
+    // subject samples of this shard: higher-numbered samples only (symmetric
+    // spec: the pair's other direction is the mirror image)
+    const uint64_t tm[4] = {P.tmask[4 * Q], P.tmask[4 * Q + 1], P.tmask[4 * Q + 2], P.tmask[4 * Q + 3]};
+    int T0 = Q + 1, T1 = N;
     while (T0 < N) {
         if (tid == 0) {
             sh_nseed = 0;
@@ -178,7 +181,7 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
                 const int k = lo2;
                 const uint2 e = ix.ent[it_lo[k] + (h - it_pre[k])];
                 const TxInfo st = db.tx[e.x];
-                if (st.sample == Q || st.sample < T0 || st.sample >= T1) continue;
+                if (st.sample < T0 || st.sample >= T1 || !((tm[st.sample >> 6] >> (st.sample & 63)) & 1)) continue;
                 const uint32_t inf = it_info[k];
                 const uint32_t ii = inf & 127;
                 const int strand = (inf >> 7) & 1;
@@ -597,8 +600,12 @@ __global__ __launch_bounds__(EBLOCK) void extend_kernel(Db db, ExtParams P)
             const bool conflict = kept && lane < nh && ((bqa == qa && bsa == sa) || (bqb == qb && bsb == sb2));
             if (!__ballot(conflict) && lane == i) kept = true;
         }
-        const int thr = P.thr[(size_t)st.sample * (size_t)(P.max_len + 1) + (size_t)Lq];
-        const bool out = kept && bsc >= thr;
+        // e-value cut of each direction: query->subject (query length, subject
+        // DB) and the mirrored one (subject length, query sample's DB)
+        const int thr_f = P.thr[(size_t)st.sample * (size_t)(P.max_len + 1) + (size_t)Lq];
+        const int thr_r = P.thr[(size_t)qt.sample * (size_t)(P.max_len + 1) + (size_t)Lt];
+        const bool pf = bsc >= thr_f, pr = bsc >= thr_r;
+        const bool out = kept && (pf || pr);
         const uint64_t om = __ballot(out);
         const int nout = __popcll(om);
         uint32_t obase = 0;
@@ -625,7 +632,7 @@ __global__ __launch_bounds__(EBLOCK) void extend_kernel(Db db, ExtParams P)
             h.length = bni + (bd - bg) + bg;
             h.score_half = bsc;
             h.bits10 = P.bits10[bsc];
-            h.strand = strand;
+            h.strand = strand | (pf ? HSP_FWD : 0) | (pr ? HSP_REV : 0) | (lane << HSP_IDX_SHIFT);
             if (rk == 0) P.cand_hsp[ci] = h;
             else if ((uint64_t)obase + (rk - 1) < P.ovf_cap) P.ovf[obase + rk - 1] = h;
         }
@@ -652,7 +659,13 @@ __global__ void group_count_kernel(GroupParams P)
          gi += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t o = P.gc_off[gi], c = P.gc_cnt[gi];
         uint32_t s = 0;
-        for (uint32_t i = 0; i < c; i++) s += P.cand_nh[o + i];
+        for (uint32_t i = 0; i < c; i++) {
+            const uint32_t nh = P.cand_nh[o + i];
+            if (!nh) continue;
+            s += (P.cand_hsp[o + i].strand & HSP_FWD) ? 1u : 0u;
+            const uint32_t ov = P.cand_ovf[o + i];
+            for (uint32_t k = 1; k < nh; k++) s += (P.ovf[ov + k - 1].strand & HSP_FWD) ? 1u : 0u;
+        }
         P.cnt[gi] = s;
     }
 }
@@ -665,14 +678,102 @@ __global__ void group_write_kernel(GroupParams P)
         const uint32_t o = P.gc_off[gi], c = P.gc_cnt[gi];
         uint64_t w = P.scan[gi];
         const uint64_t gg = (uint64_t)P.gene_begin * P.N + gi;
-        P.grp_off[gg] = (uint32_t)w;
-        P.grp_cnt[gg] = P.cnt[gi];
+        if (P.cnt[gi]) {
+            P.grp_off[gg] = (uint32_t)w;
+            P.grp_cnt[gg] = P.cnt[gi];
+        }
         for (uint32_t i = 0; i < c; i++) {
             const uint32_t nh = P.cand_nh[o + i];
             if (!nh) continue;
-            P.out[w++] = P.cand_hsp[o + i];
+            const DHsp &h0 = P.cand_hsp[o + i];
+            if (h0.strand & HSP_FWD) P.out[w++] = h0;
             const uint32_t ov = P.cand_ovf[o + i];
-            for (uint32_t k = 1; k < nh; k++) P.out[w++] = P.ovf[ov + k - 1];
+            for (uint32_t k = 1; k < nh; k++)
+                if (P.ovf[ov + k - 1].strand & HSP_FWD) P.out[w++] = P.ovf[ov + k - 1];
+        }
+    }
+}
+
+// the mirror image of a query->subject HSP, as the subject->query search reports it
+__device__ __forceinline__ DHsp mirror_hsp(const DHsp &h)
+{
+    DHsp m = h;
+    m.q_tx = h.s_tx;
+    m.s_tx = h.q_tx;
+    if (!(h.strand & 1)) {
+        m.qstart = h.sstart; m.qend = h.send; m.sstart = h.qstart; m.send = h.qend;
+    } else {
+        m.qstart = h.send; m.qend = h.sstart; m.sstart = h.qend; m.send = h.qstart;
+    }
+    return m;
+}
+
+// candidate slot of linear candidate index li
+__device__ __forceinline__ uint64_t cand_slot(const GroupParams &P, uint64_t li)
+{
+    int lo = 0, hi = NSHARD;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (P.shard_prefix[mid] <= li) lo = mid; else hi = mid;
+    }
+    return (uint64_t)lo * P.cand_cap + (li - P.shard_prefix[lo]);
+}
+
+// pass 0: count mirrored HSPs per (gene of the subject tx, query sample);
+// pass 1: scatter them (order fixed later by mirror_sort_kernel)
+__global__ void mirror_scatter_kernel(GroupParams P, int pass)
+{
+    for (uint64_t li = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; li < P.n_cand;
+         li += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t ci = cand_slot(P, li);
+        const uint32_t nh = P.cand_nh[ci];
+        if (!nh) continue;
+        const uint32_t ov = P.cand_ovf[ci];
+        for (uint32_t k = 0; k < nh; k++) {
+            const DHsp &h = k ? P.ovf[ov + k - 1] : P.cand_hsp[ci];
+            if (!(h.strand & HSP_REV)) continue;
+            const uint64_t gi = (uint64_t)P.tx_gene[h.s_tx] * P.N + (uint64_t)P.tx[h.q_tx].sample;
+            if (pass == 0) {
+                atomicAdd(&P.mcnt[gi], 1u);
+            } else {
+                const uint64_t slot = P.mbase + P.mscan[gi] + atomicAdd(&P.mcur[gi], 1u);
+                P.out[slot] = mirror_hsp(h);
+                // order: (isoform position, strand) then (subject tx, index)
+                P.mkey[2 * (slot - P.mbase)] = ((uint64_t)P.tx_pos[h.s_tx] << 1) | (uint64_t)(h.strand & 1);
+                P.mkey[2 * (slot - P.mbase) + 1] =
+                    ((uint64_t)h.q_tx << 8) | (uint64_t)((h.strand >> HSP_IDX_SHIFT) & 7);
+            }
+        }
+    }
+}
+
+// sort each mirrored group by its order keys (groups are small) and fill the
+// group table
+__global__ void mirror_sort_kernel(GroupParams P)
+{
+    const uint64_t n = (uint64_t)P.n_genes * (uint64_t)P.N;
+    for (uint64_t gi = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; gi < n;
+         gi += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t c = P.mcnt[gi];
+        if (!c) continue;
+        const uint64_t b = P.mscan[gi];
+        P.grp_off[gi] = (uint32_t)(P.mbase + b);
+        P.grp_cnt[gi] = c;
+        for (uint32_t i = 1; i < c; i++) {
+            const uint64_t k1 = P.mkey[2 * (b + i)], k2 = P.mkey[2 * (b + i) + 1];
+            const DHsp h = P.out[P.mbase + b + i];
+            uint32_t j = i;
+            while (j > 0) {
+                const uint64_t p1 = P.mkey[2 * (b + j - 1)], p2 = P.mkey[2 * (b + j - 1) + 1];
+                if (p1 < k1 || (p1 == k1 && p2 < k2)) break;
+                P.mkey[2 * (b + j)] = p1;
+                P.mkey[2 * (b + j) + 1] = p2;
+                P.out[P.mbase + b + j] = P.out[P.mbase + b + j - 1];
+                j--;
+            }
+            P.mkey[2 * (b + j)] = k1;
+            P.mkey[2 * (b + j) + 1] = k2;
+            P.out[P.mbase + b + j] = h;
         }
     }
 }
@@ -705,14 +806,21 @@ void launch_extend(bool amb, const Db &db, const ExtParams &P, hipStream_t st)
 
 void launch_group(const GroupParams &P, int pass, hipStream_t st)
 {
-    const uint64_t n = (uint64_t)(P.gene_end - P.gene_begin) * (uint64_t)P.N;
+    // 0 direct count, 1 direct write, 2 mirror count, 3 mirror scatter, 4 mirror sort
+    uint64_t n = (uint64_t)(P.gene_end - P.gene_begin) * (uint64_t)P.N;
+    if (pass == 2 || pass == 3) n = P.n_cand;
+    if (pass == 4) n = (uint64_t)P.n_genes * (uint64_t)P.N;
     if (!n) return;
     uint64_t g = (n + 255) / 256;
     if (g > 65536) g = 65536;
     if (pass == 0)
         hipLaunchKernelGGL(group_count_kernel, dim3((unsigned)g), dim3(256), 0, st, P);
-    else
+    else if (pass == 1)
         hipLaunchKernelGGL(group_write_kernel, dim3((unsigned)g), dim3(256), 0, st, P);
+    else if (pass == 2 || pass == 3)
+        hipLaunchKernelGGL(mirror_scatter_kernel, dim3((unsigned)g), dim3(256), 0, st, P, pass - 2);
+    else
+        hipLaunchKernelGGL(mirror_sort_kernel, dim3((unsigned)g), dim3(256), 0, st, P);
 }
 
 }  // namespace rcg

@@ -92,6 +92,7 @@ struct SeedParams {
     uint64_t cand_cap;            // per allocation shard
     unsigned long long *cand_count;  // [NSHARD]
     uint32_t *gc_off, *gc_cnt;    // [(g - gene_begin) * N + T] candidates of (gene, sample)
+    const uint64_t *tmask;        // [n_samples][4] subject samples (> query sample) of this shard
     unsigned int *status;         // bit 0 overflow, bit 1 gene limit
 };
 
@@ -116,7 +117,15 @@ struct ExtParams {
     unsigned long long *counters; // [0] greedy steps, [1] extensions, [2] candidates (one atomic per wave)
 };
 
+// DHsp.strand carries, besides the strand (bit 0), the direction flags of a
+// freshly extended HSP (bit 1: passes the query->subject e-value cut, bit 2:
+// passes the mirrored direction's) and its index in the candidate (bits 3-5).
+constexpr int HSP_FWD = 2, HSP_REV = 4, HSP_IDX_SHIFT = 3;
+
 // group kernels: candidates of each (gene, sample) -> contiguous HSP groups.
+// Direct groups (gene of the query sample, higher subject sample) come in
+// candidate order; mirrored groups (gene of the higher sample, lower sample)
+// are counted, scattered and sorted by (isoform, strand, subject tx, index).
 struct GroupParams {
     uint32_t gene_begin, gene_end;
     int32_t N;
@@ -125,10 +134,21 @@ struct GroupParams {
     const DHsp *cand_hsp;
     const uint32_t *cand_ovf;
     const DHsp *ovf;
-    uint32_t *cnt;                // [(g - gene_begin) * N + T] HSPs per group
+    uint32_t *cnt;                // [(g - gene_begin) * N + T] direct HSPs per group
     const uint64_t *scan;         // exclusive scan of cnt
     uint32_t *grp_off, *grp_cnt;  // global-gene group table
     DHsp *out;
+    // mirrored groups, over all candidates
+    const unsigned long long *shard_prefix;
+    uint64_t n_cand, cand_cap;
+    const uint32_t *tx_gene, *tx_pos;   // gene of a transcript, its position in the gene
+    const TxInfo *tx;
+    uint32_t *mcnt;               // [gene * N + T]
+    const uint64_t *mscan;        // exclusive scan of mcnt
+    uint32_t *mcur;               // scatter cursors [gene * N + T]
+    uint64_t mbase;               // first output slot of the mirrored region
+    uint64_t *mkey;               // order keys of the mirrored region (parallel to out)
+    uint32_t n_genes;
 };
 
 // Parameters of the two reciprocal-best-hit passes.

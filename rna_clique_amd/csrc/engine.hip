@@ -228,7 +228,8 @@ struct rc_engine {
     DBuf<DHsp> d_cand_hsp, d_ovf;
     DBuf<uint8_t> d_cand_nh;
     DBuf<uint32_t> d_cand_ovf, d_gc_off, d_gc_cnt, d_gcount;
-    DBuf<uint64_t> d_gscan;
+    DBuf<uint64_t> d_gscan, d_mscan, d_mkey, d_tmask;
+    DBuf<uint32_t> d_mcnt, d_mcur, d_tx_pos;
     DBuf<unsigned long long> d_shard_cnt, d_shard_prefix;
     uint64_t seed_cap = 0, cand_cap = 0, ovf_cap = 0;   // per-shard / total capacities
     DBuf<uint32_t> d_grp_off, d_grp_cnt;
@@ -480,6 +481,10 @@ static int upload(rc_engine *e)
     };
     CHK(up(e->d_tx, txi));
     CHK(up(e->d_tx_gene, e->tx_gene));
+    std::vector<uint32_t> tx_pos(n_tx, 0);
+    for (uint32_t g = 0; g < n_genes; g++)
+        for (uint32_t i = e->gene_tx_off[g]; i < e->gene_tx_off[g + 1]; i++) tx_pos[e->gene_tx[i]] = i - e->gene_tx_off[g];
+    CHK(up(e->d_tx_pos, tx_pos));
     CHK(up(e->d_gene_tx_off, e->gene_tx_off));
     CHK(up(e->d_gene_tx, e->gene_tx));
     CHK(up(e->d_gene_sample, e->gene_sample));
@@ -584,32 +589,52 @@ static Db make_db(rc_engine *e)
     return db;
 }
 
-static void shard_range(rc_engine *e, uint32_t &g0, uint32_t &g1)
+// Shard plan: the sample pairs in itertools.combinations order, cut into
+// shard_count contiguous ranges of about equal sequence length (L_a + L_b per
+// pair). Every pair is aligned once, lower-numbered sample as query, so each
+// (gene, sample) group belongs to exactly one shard. Returns the query-gene
+// range to scan and, per query sample, the bit set of its subject samples.
+static void shard_plan(rc_engine *e, uint32_t &g0, uint32_t &g1, std::vector<uint64_t> &tmask)
 {
-    // contiguous gene ranges of roughly equal sequence length
-    const uint32_t n_genes = (uint32_t)e->gene_sample.size();
-    if (e->o.shard_count == 1) {
-        g0 = 0;
-        g1 = n_genes;
+    const int N = (int)e->samples.size();
+    tmask.assign((size_t)4 * N, 0);
+    const size_t np = e->pair_a.size();
+    double tot = 0;
+    for (size_t p = 0; p < np; p++) tot += (double)(e->db_len[e->pair_a[p]] + e->db_len[e->pair_b[p]]);
+    const int R = e->o.shard_count, r = e->o.shard_rank;
+    size_t p0 = 0, p1 = np;
+    if (R > 1) {
+        p0 = p1 = np;
+        bool have0 = false;
+        double acc = 0;
+        for (size_t p = 0; p < np; p++) {
+            const double mid = acc + 0.5 * (double)(e->db_len[e->pair_a[p]] + e->db_len[e->pair_b[p]]);
+            const int owner = tot > 0 ? std::min(R - 1, (int)(mid / tot * R)) : 0;
+            if (owner == r && !have0) {
+                p0 = p;
+                have0 = true;
+            }
+            if (owner > r) {
+                p1 = p;
+                break;
+            }
+            acc += (double)(e->db_len[e->pair_a[p]] + e->db_len[e->pair_b[p]]);
+        }
+        if (!have0) p0 = p1 = np;
+    }
+    int smin = N, smax = -1;
+    for (size_t p = p0; p < p1; p++) {
+        const int qa = e->pair_a[p], sb = e->pair_b[p];
+        tmask[4 * qa + (sb >> 6)] |= 1ull << (sb & 63);
+        smin = std::min(smin, qa);
+        smax = std::max(smax, qa);
+    }
+    if (smax < 0) {
+        g0 = g1 = 0;
         return;
     }
-    const uint64_t total = e->seq.size();
-    auto cut = [&](int r) -> uint32_t {
-        if (r <= 0) return 0;
-        if (r >= e->o.shard_count) return n_genes;
-        const uint64_t target = total * (uint64_t)r / (uint64_t)e->o.shard_count;
-        uint64_t acc = 0;
-        for (uint32_t g = 0; g < n_genes; g++) {
-            if (acc >= target) return g;
-            for (uint32_t i = e->gene_tx_off[g]; i < e->gene_tx_off[g + 1]; i++) {
-                const uint32_t t = e->gene_tx[i];
-                acc += e->tx_start[t + 1] - e->tx_start[t];
-            }
-        }
-        return n_genes;
-    };
-    g0 = cut(e->o.shard_rank);
-    g1 = cut(e->o.shard_rank + 1);
+    g0 = e->sample_gene_begin[smin];
+    g1 = e->sample_gene_begin[smax + 1];
 }
 
 // External HSPs -> device groups in canonical (query gene, subject sample) order.
@@ -676,7 +701,10 @@ static int do_align(rc_engine *e)
 
     const int N = (int)e->samples.size();
     uint32_t g0, g1;
-    shard_range(e, g0, g1);
+    std::vector<uint64_t> tmask;
+    shard_plan(e, g0, g1, tmask);
+    CHK(e->d_tmask.ensure(tmask.size()));
+    HIPCHK(hipMemcpyAsync(e->d_tmask.p, tmask.data(), tmask.size() * 8, hipMemcpyHostToDevice, e->st));
     const uint32_t n_genes = (uint32_t)e->gene_sample.size();
     const uint64_t sg = (uint64_t)(g1 - g0);
     const size_t ngrp = (size_t)n_genes * N;
@@ -711,6 +739,7 @@ static int do_align(rc_engine *e)
         CHK(e->d_cands.ensure(e->cand_cap * NSHARD));
         HIPCHK(hipMemsetAsync(e->d_shard_cnt.p, 0, 2 * NSHARD * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
+        if (nsgrp) HIPCHK(hipMemsetAsync(e->d_gc_cnt.p, 0, nsgrp * 4, e->st));
         SeedParams S;
         S.word = e->o.word_size;
         S.stride = e->o.word_size - W16 + 1;
@@ -724,6 +753,7 @@ static int do_align(rc_engine *e)
         S.cand_count = e->d_shard_cnt.p + NSHARD;
         S.gc_off = e->d_gc_off.p;
         S.gc_cnt = e->d_gc_cnt.p;
+        S.tmask = e->d_tmask.p;
         S.status = e->d_status.p;
         HIPCHK(hipEventRecord(e->ev[3], e->st));
         launch_seed(e->has_amb, db, ix, S, e->st);
@@ -795,7 +825,10 @@ static int do_align(rc_engine *e)
         e->ovf_cap = ovn * 5 / 4 + 1024;
     }
     // --- groups: (query gene, subject sample) -> contiguous HSPs ---
-    GroupParams G;
+    // Direct groups (query sample < subject sample) come first in d_hsp, in
+    // candidate order; mirrored groups (the subject->query direction of the
+    // same alignments) follow, each sorted into the order that search emits.
+    GroupParams G{};
     G.gene_begin = g0;
     G.gene_end = g1;
     G.N = N;
@@ -806,28 +839,52 @@ static int do_align(rc_engine *e)
     G.cand_ovf = e->d_cand_ovf.p;
     G.ovf = e->d_ovf.p;
     G.cnt = e->d_gcount.p;
+    G.shard_prefix = e->d_shard_prefix.p;
+    G.n_cand = n_cand;
+    G.cand_cap = e->cand_cap;
+    G.tx_gene = e->d_tx_gene.p;
+    G.tx_pos = e->d_tx_pos.p;
+    G.tx = e->d_tx.p;
+    G.n_genes = n_genes;
+    CHK(e->d_mcnt.ensure(ngrp + 1));
+    CHK(e->d_mcur.ensure(ngrp));
+    CHK(e->d_mscan.ensure(ngrp + 1));
+    G.mcnt = e->d_mcnt.p;
+    G.mcur = e->d_mcur.p;
     HIPCHK(hipMemsetAsync(e->d_grp_cnt.p, 0, ngrp * 4, e->st));
     HIPCHK(hipMemsetAsync(e->d_grp_off.p, 0, ngrp * 4, e->st));
     HIPCHK(hipMemsetAsync(e->d_gcount.p + nsgrp, 0, 4, e->st));
+    HIPCHK(hipMemsetAsync(e->d_mcnt.p, 0, (ngrp + 1) * 4, e->st));
+    HIPCHK(hipMemsetAsync(e->d_mcur.p, 0, ngrp * 4, e->st));
     launch_group(G, 0, e->st);
-    {
+    launch_group(G, 2, e->st);
+    auto exscan = [&](const uint32_t *in, uint64_t *out, size_t n) -> int {
         size_t tmp = 0;
-        HIPCHK(rocprim::exclusive_scan(nullptr, tmp, e->d_gcount.p, e->d_gscan.p, (uint64_t)0, nsgrp + 1,
-                                       rocprim::plus<uint64_t>(), e->st));
+        HIPCHK(rocprim::exclusive_scan(nullptr, tmp, in, out, (uint64_t)0, n, rocprim::plus<uint64_t>(), e->st));
         CHK(e->d_tmp.ensure(tmp));
-        HIPCHK(rocprim::exclusive_scan(e->d_tmp.p, tmp, e->d_gcount.p, e->d_gscan.p, (uint64_t)0, nsgrp + 1,
-                                       rocprim::plus<uint64_t>(), e->st));
-    }
-    uint64_t nh = 0;
-    HIPCHK(hipMemcpyAsync(&nh, e->d_gscan.p + nsgrp, 8, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(rocprim::exclusive_scan(e->d_tmp.p, tmp, in, out, (uint64_t)0, n, rocprim::plus<uint64_t>(), e->st));
+        return RC_OK;
+    };
+    CHK(exscan(e->d_gcount.p, e->d_gscan.p, nsgrp + 1));
+    CHK(exscan(e->d_mcnt.p, e->d_mscan.p, ngrp + 1));
+    uint64_t nd = 0, nm = 0;
+    HIPCHK(hipMemcpyAsync(&nd, e->d_gscan.p + nsgrp, 8, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipMemcpyAsync(&nm, e->d_mscan.p + ngrp, 8, hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
+    const uint64_t nh = nd + nm;
     if (nh > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "more than 2^32 HSPs on one GPU: use more shards");
     CHK(e->d_hsp.ensure(nh));
+    CHK(e->d_mkey.ensure(2 * nm + 2));
     G.scan = e->d_gscan.p;
+    G.mscan = e->d_mscan.p;
     G.grp_off = e->d_grp_off.p;
     G.grp_cnt = e->d_grp_cnt.p;
     G.out = e->d_hsp.p;
+    G.mbase = nd;
+    G.mkey = e->d_mkey.p;
     launch_group(G, 1, e->st);
+    launch_group(G, 3, e->st);
+    launch_group(G, 4, e->st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e->ev[4], e->st));
     HIPCHK(hipEventSynchronize(e->ev[4]));
@@ -950,7 +1007,7 @@ static rc_hsp to_rc_hsp(rc_engine *e, const DHsp &d, int qs_, int ss_)
     h.s_tx = d.s_tx - e->samples[ss_].tx_begin;
     h.qstart = d.qstart; h.qend = d.qend; h.sstart = d.sstart; h.send = d.send;
     h.length = d.length; h.nident = d.nident; h.mismatch = d.mismatch; h.gaps = d.gaps;
-    h.gapopen = d.gapopen; h.score_half = d.score_half; h.bits10 = d.bits10; h.strand = d.strand;
+    h.gapopen = d.gapopen; h.score_half = d.score_half; h.bits10 = d.bits10; h.strand = d.strand & 1;
     const int64_t qlen = (int64_t)(e->tx_start[d.q_tx + 1] - e->tx_start[d.q_tx]);
     h.evalue = stats::evalue(stats::search_space(qlen, e->db_len[ss_], e->db_n[ss_]), d.score_half);
     return h;
@@ -1180,24 +1237,13 @@ int rc_export_tops(rc_engine *e, void *buf, uint64_t cap, uint64_t *n, int on_de
     if (!e || !n) return fail(RC_E_ARG, "null argument");
     if (!e->aligned) return fail(RC_E_STATE, "rc_export_tops before rc_align");
     CHK(set_device(e));
-    const int N = (int)e->samples.size();
-    uint32_t g0, g1;
-    shard_range(e, g0, g1);
-    std::vector<uint32_t> off, cnt;
-    CHK(copy_groups(e, off, cnt));
-    uint64_t tot = 0;
-    for (size_t i = (size_t)g0 * N; i < (size_t)g1 * N; i++) tot += cnt[i];
+    // d_hsp holds exactly this shard's groups, each contiguous
+    const uint64_t tot = e->n_hsps;
     *n = tot;
     if (!buf) return RC_OK;
     if (cap < tot) return fail(RC_E_CAPACITY, "buffer too small");
-    uint64_t w = 0;
-    for (size_t i = (size_t)g0 * N; i < (size_t)g1 * N; i++) {
-        if (!cnt[i]) continue;
-        DHsp *dst = reinterpret_cast<DHsp *>(buf) + w;
-        HIPCHK(hipMemcpy(dst, e->d_hsp.p + off[i], cnt[i] * sizeof(DHsp),
-                         on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost));
-        w += cnt[i];
-    }
+    if (tot)
+        HIPCHK(hipMemcpy(buf, e->d_hsp.p, tot * sizeof(DHsp), on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost));
     return RC_OK;
 }
 
