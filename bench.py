@@ -7,7 +7,8 @@ inputs already resident in HBM: 2-bit pack -> seed index build -> seed-and-
 extend for every directed sample pair -> top-N + reciprocal best hits -> gene
 matches graph + ideal-clique filter -> restricted sums -> N x N distance matrix
 copied to the host. For N > 1 GPUs (torch.distributed.run, one rank per GPU)
-the query genes are sharded by sequence length, the per-(gene, sample) hits are
+the sample pairs are sharded by sequence length (rc_plan_shards), every rank
+aligns its pairs and runs reciprocal best hits for them, the graph edges are
 exchanged with one RCCL all-gather, and every rank finishes the graph.
 
 Prints ONE JSON line (rank 0). See DESIGN.md §Measurement for the roofline
@@ -91,6 +92,7 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl")
+    from rna_clique_amd import distributed
     from rna_clique_amd.engine import Engine
     from rna_clique_amd.simulate import simulate, CONFIGS
     cfg = CONFIGS[args.config]
@@ -108,18 +110,7 @@ def main():
         if world == 1:
             eng.run()
         else:
-            eng.align()
-            mine = torch.from_numpy(eng.export_tops()).cuda()
-            sizes = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(world)]
-            dist.all_gather(sizes, torch.tensor([mine.numel()], device="cuda"))
-            mx = int(max(int(x) for x in sizes))
-            pad = torch.zeros(mx, dtype=torch.uint8, device="cuda")
-            pad[:mine.numel()] = mine
-            parts = [torch.empty(mx, dtype=torch.uint8, device="cuda") for _ in range(world)]
-            dist.all_gather(parts, pad)
-            allb = torch.cat([p[:int(sz)] for p, sz in zip(parts, sizes)]).cpu().numpy()
-            eng.import_tops(allb)
-            eng.finish()
+            distributed.sharded_run(eng)
         return eng.distance()
 
     for _ in range(args.warmup):
@@ -171,7 +162,7 @@ def main():
         "dtype": "u8/int32", "data": "synthetic (simulate.py, seeded, BASELINE configs)",
         "config": {"workload": f"{args.config}: {n} samples x {cfg['genes']} genes",
                    "pairs": pairs, "bases": int(sum(s.seq.size for s in samples)),
-                   "parallelism": f"query-gene shards x{world}"},
+                   "parallelism": f"sample-pair shards x{world}"},
         "roofline": roof, "cpu_baseline": cpu,
         "phases_ms": {k: round(v, 3) for k, v in tm.items()},
         "graph": {k: st[k] for k in ("seeds", "candidates", "hsps", "table_rows", "edges", "components",

@@ -129,22 +129,35 @@ int rc_add_hsps(rc_engine *eng, int32_t q, int32_t s, const rc_hsp *hsps, uint64
  * are resident in HBM and rc_run repeats the whole path from them. */
 int rc_upload(rc_engine *eng);
 
-/* Phases. rc_run = rc_align + rc_finish. rc_align runs the seed-and-extend
- * kernel for the query genes of this engine's shard; rc_finish runs top-N,
- * reciprocal best hits, the graph, the ideal filter and the pair sums over the
- * top hits of all shards (see rc_export_tops / rc_import_tops). */
+/* Phases. rc_run = rc_align + rc_finish (single shard).
+ *
+ * Sharded use (shard_count > 1, one engine per GPU, every engine given the
+ * same samples): the C(N,2) sample pairs, in combinations order, are cut into
+ * shard_count contiguous ranges of about equal sequence length; rc_align runs
+ * seed-and-extend for this shard's pairs only, and rc_finish the top-N and
+ * reciprocal-best-hit step for them, producing this shard's gene matches
+ * tables and graph edges. The gene matches graph and the ideal-clique filter
+ * are global, so the edges are then exchanged (one all-gather) and every shard
+ * passes the concatenation to rc_import_edges, which runs connected
+ * components, the ideal filter and the pair sums over all edges. Tables
+ * (rc_pair_rows) stay on the shard that owns the pair. */
 int rc_run(rc_engine *eng);
 int rc_align(rc_engine *eng);
 int rc_finish(rc_engine *eng);
 
-/* Multi-GPU exchange of per-(query gene, subject sample) top hits. Records are
- * opaque, fixed-size (rc_top_record_size() bytes). export: the records of this
- * shard into a caller buffer (host or device pointer, `on_device` says which);
- * import: replace this engine's top hits by the concatenation of all shards'
- * records (in shard order). */
-uint64_t rc_top_record_size(void);
-int rc_export_tops(rc_engine *eng, void *buf, uint64_t cap, uint64_t *n, int on_device);
-int rc_import_tops(rc_engine *eng, const void *buf, uint64_t n, int on_device);
+/* Edge records are opaque and fixed-size (rc_edge_record_size() bytes).
+ * export: this shard's edges into a caller buffer (host or device pointer,
+ * `on_device` says which; buf == NULL queries the count); import: all shards'
+ * edges, concatenated in any order, then the graph phase. */
+uint64_t rc_edge_record_size(void);
+int rc_export_edges(rc_engine *eng, void *buf, uint64_t cap, uint64_t *n, int on_device);
+int rc_import_edges(rc_engine *eng, const void *buf, uint64_t n, int on_device);
+/* This shard's sample-pair range [first, last) in combinations order. */
+int rc_shard_pairs(rc_engine *eng, int64_t *first, int64_t *last);
+/* The split itself (no device needed): pair_first[shard_count + 1], shard r
+ * owns pairs [pair_first[r], pair_first[r + 1]). sample_bases = total bases
+ * of each sample's transcripts. */
+int rc_plan_shards(const int64_t *sample_bases, int32_t n_samples, int32_t shard_count, int64_t *pair_first);
 
 /* Results (after rc_run / rc_finish). */
 int rc_hsps(rc_engine *eng, int32_t q, int32_t s, rc_hsp *buf, uint64_t cap, uint64_t *n);
@@ -158,6 +171,24 @@ int rc_pair_sums(rc_engine *eng, int64_t *num, int64_t *den);
  * Returns RC_E_NO_IDEAL when some pair has no ideal rows. */
 int rc_distance(rc_engine *eng, const int32_t *order, double *out);
 int rc_timings(rc_engine *eng, rc_timing *t);
+
+/* ---- FASTA input (host only; fasta.cpp) ----------------------------------
+ * Replaces the Bio.SeqIO passes of TopGeneSelector (select_top_genes.py:108-127)
+ * and the Bio.SeqIO.write of select_top_and_save (select_top_genes_all.py:12-46).
+ * A title is the header line without '>' and trailing whitespace; a sequence is
+ * the record's lines right-stripped and joined, ' ' and '\r' removed. `keep`
+ * (one byte per record, NULL = all) selects records for select/write. */
+typedef struct rc_fasta rc_fasta;
+int rc_fasta_open(const char *path, rc_fasta **out);
+int rc_fasta_close(rc_fasta *f);
+int rc_fasta_info(const rc_fasta *f, uint64_t *n_records, uint64_t *n_bases, uint64_t *title_bytes);
+/* titles concatenated into buf (title_bytes), offsets[n_records + 1];
+ * seq_lens[n_records] (may be NULL) */
+int rc_fasta_titles(const rc_fasta *f, char *buf, uint64_t *offsets, uint64_t *seq_lens);
+/* selected sequences concatenated into seq; tx_offsets[n_selected + 1] */
+int rc_fasta_select(const rc_fasta *f, const uint8_t *keep, uint8_t *seq, uint64_t *tx_offsets);
+/* selected records as Bio.SeqIO.write(..., "fasta") writes them (width 60) */
+int rc_fasta_write(const rc_fasta *f, const uint8_t *keep, const char *path, int32_t width);
 
 #ifdef __cplusplus
 }

@@ -98,9 +98,11 @@ SIGNATURES = {
     "rc_run": (ctypes.c_int, [VP]),
     "rc_align": (ctypes.c_int, [VP]),
     "rc_finish": (ctypes.c_int, [VP]),
-    "rc_top_record_size": (ctypes.c_uint64, []),
-    "rc_export_tops": (ctypes.c_int, [VP, VP, ctypes.c_uint64, P(ctypes.c_uint64), ctypes.c_int]),
-    "rc_import_tops": (ctypes.c_int, [VP, VP, ctypes.c_uint64, ctypes.c_int]),
+    "rc_edge_record_size": (ctypes.c_uint64, []),
+    "rc_export_edges": (ctypes.c_int, [VP, VP, ctypes.c_uint64, P(ctypes.c_uint64), ctypes.c_int]),
+    "rc_import_edges": (ctypes.c_int, [VP, VP, ctypes.c_uint64, ctypes.c_int]),
+    "rc_shard_pairs": (ctypes.c_int, [VP, P(ctypes.c_int64), P(ctypes.c_int64)]),
+    "rc_plan_shards": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.c_int32, VP]),
     "rc_hsps": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.c_int32, VP, ctypes.c_uint64,
                                P(ctypes.c_uint64)]),
     "rc_pair_rows": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.c_int32, VP, ctypes.c_uint64,
@@ -111,6 +113,12 @@ SIGNATURES = {
     "rc_pair_sums": (ctypes.c_int, [VP, VP, VP]),
     "rc_distance": (ctypes.c_int, [VP, VP, VP]),
     "rc_timings": (ctypes.c_int, [VP, P(RcTiming)]),
+    "rc_fasta_open": (ctypes.c_int, [ctypes.c_char_p, P(VP)]),
+    "rc_fasta_close": (ctypes.c_int, [VP]),
+    "rc_fasta_info": (ctypes.c_int, [VP, P(ctypes.c_uint64), P(ctypes.c_uint64), P(ctypes.c_uint64)]),
+    "rc_fasta_titles": (ctypes.c_int, [VP, VP, VP, VP]),
+    "rc_fasta_select": (ctypes.c_int, [VP, VP, VP, VP]),
+    "rc_fasta_write": (ctypes.c_int, [VP, VP, ctypes.c_char_p, ctypes.c_int32]),
 }
 
 _lib = None

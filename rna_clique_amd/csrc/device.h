@@ -161,7 +161,7 @@ struct RbhParams {
     const uint32_t *pair_item_begin;     // n_pairs + 1
     const int32_t *pair_a, *pair_b;
     int32_t n_pairs, N, top_n, keep_all;
-    uint64_t n_items;
+    uint64_t item0, n_items;             // this shard's items [item0, item0 + n_items)
     // pass 0 outputs (per item)
     uint32_t *n_rows, *n_fsel, *n_rsel, *n_edges;
     // pass 1 inputs (exclusive scans) and outputs

@@ -31,6 +31,7 @@ void launch_extend(bool, const Db &, const ExtParams &, hipStream_t);
 void launch_group(const GroupParams &, int, hipStream_t);
 
 void launch_rbh(const RbhParams &, int, hipStream_t);
+void launch_gather_rows(const DHsp *, const DRow *, uint64_t, DHsp *, hipStream_t);
 void launch_cc(const DEdge *, uint64_t, uint32_t, const int32_t *, int, uint32_t *, uint32_t *, uint32_t *,
                uint32_t *, uint32_t *, uint8_t *, unsigned long long *, hipStream_t);
 void launch_pair_sums(const DEdge *, uint64_t, const uint32_t *, const uint8_t *, unsigned long long *,
@@ -48,6 +49,11 @@ static int fail(int code, const std::string &msg)
 {
     g_err = msg;
     return code;
+}
+
+int rcg_fail(int code, const std::string &msg)
+{
+    return fail(code, msg);
 }
 
 #define HIPCHK(x)                                                                                    \
@@ -210,6 +216,10 @@ struct rc_engine {
 
     // state
     bool uploaded = false, aligned = false, finished = false;
+    // this shard's sample pairs [pair0, pair1) and their items [item0, item1)
+    uint64_t pair0 = 0, pair1 = 0, item0 = 0, item1 = 0;
+    uint64_t n_local_edges = 0;
+    bool rbh_done = false;
 
     // device buffers
     DBuf<uint8_t> d_ascii;
@@ -240,6 +250,7 @@ struct rc_engine {
     DBuf<uint32_t> d_cnt4;   // 4 * (n_items + 1)
     DBuf<uint64_t> d_off4;   // 4 * (n_items + 1)
     DBuf<DRow> d_rows;
+    DBuf<DHsp> d_gather;
     DBuf<DEdge> d_edges;
     uint64_t n_rows = 0, n_edges = 0, n_hsps = 0, n_seeds = 0, n_cands = 0;
     DBuf<uint32_t> d_parent, d_present, d_cnodes, d_cedges, d_sample_present;
@@ -279,7 +290,7 @@ void rc_default_opts(rc_opts *o)
 
 const char *rc_last_error(void) { return g_err.c_str(); }
 
-uint64_t rc_top_record_size(void) { return sizeof(DHsp); }
+uint64_t rc_edge_record_size(void) { return sizeof(DEdge); }
 
 int rc_create(const rc_opts *opts, rc_engine **out)
 {
@@ -379,6 +390,9 @@ int rc_add_hsps(rc_engine *e, int32_t q, int32_t s, const rc_hsp *h, uint64_t n)
 
 // Build gene numbering, tables and upload everything that does not change
 // between runs. Inputs are then resident in HBM; rc_run repacks from them.
+static void shard_pairs(rc_engine *e);
+extern "C" int rc_plan_shards(const int64_t *, int32_t, int32_t, int64_t *);
+
 static int upload(rc_engine *e)
 {
     if (e->uploaded) return RC_OK;
@@ -448,6 +462,8 @@ static int upload(rc_engine *e)
             e->pair_item_begin.push_back((uint32_t)items);
         }
     e->n_items = items;
+    if (N > 256) return fail(RC_E_LIMIT, "more than 256 samples per engine");
+    shard_pairs(e);
 
     // device copies
     const uint64_t total = e->seq.size();
@@ -589,41 +605,27 @@ static Db make_db(rc_engine *e)
     return db;
 }
 
-// Shard plan: the sample pairs in itertools.combinations order, cut into
-// shard_count contiguous ranges of about equal sequence length (L_a + L_b per
-// pair). Every pair is aligned once, lower-numbered sample as query, so each
-// (gene, sample) group belongs to exactly one shard. Returns the query-gene
-// range to scan and, per query sample, the bit set of its subject samples.
+static void shard_pairs(rc_engine *e)
+{
+    const int N = (int)e->samples.size();
+    std::vector<int64_t> bases(N), first(e->o.shard_count + 1);
+    for (int i = 0; i < N; i++) bases[i] = e->db_len[i];
+    rc_plan_shards(bases.data(), N, e->o.shard_count, first.data());
+    e->pair0 = (uint64_t)first[e->o.shard_rank];
+    e->pair1 = (uint64_t)first[e->o.shard_rank + 1];
+    e->item0 = e->pair_item_begin[e->pair0];
+    e->item1 = e->pair_item_begin[e->pair1];
+}
+
+// Seed plan of this shard: every owned pair is aligned once, lower-numbered
+// sample as query. Returns the query-gene range to scan and, per query sample,
+// the bit set of its subject samples.
 static void shard_plan(rc_engine *e, uint32_t &g0, uint32_t &g1, std::vector<uint64_t> &tmask)
 {
     const int N = (int)e->samples.size();
     tmask.assign((size_t)4 * N, 0);
-    const size_t np = e->pair_a.size();
-    double tot = 0;
-    for (size_t p = 0; p < np; p++) tot += (double)(e->db_len[e->pair_a[p]] + e->db_len[e->pair_b[p]]);
-    const int R = e->o.shard_count, r = e->o.shard_rank;
-    size_t p0 = 0, p1 = np;
-    if (R > 1) {
-        p0 = p1 = np;
-        bool have0 = false;
-        double acc = 0;
-        for (size_t p = 0; p < np; p++) {
-            const double mid = acc + 0.5 * (double)(e->db_len[e->pair_a[p]] + e->db_len[e->pair_b[p]]);
-            const int owner = tot > 0 ? std::min(R - 1, (int)(mid / tot * R)) : 0;
-            if (owner == r && !have0) {
-                p0 = p;
-                have0 = true;
-            }
-            if (owner > r) {
-                p1 = p;
-                break;
-            }
-            acc += (double)(e->db_len[e->pair_a[p]] + e->db_len[e->pair_b[p]]);
-        }
-        if (!have0) p0 = p1 = np;
-    }
     int smin = N, smax = -1;
-    for (size_t p = p0; p < p1; p++) {
+    for (uint64_t p = e->pair0; p < e->pair1; p++) {
         const int qa = e->pair_a[p], sb = e->pair_b[p];
         tmask[4 * qa + (sb >> 6)] |= 1ull << (sb & 63);
         smin = std::min(smin, qa);
@@ -677,7 +679,7 @@ static int do_align(rc_engine *e)
 {
     CHK(upload(e));
     CHK(set_device(e));
-    e->aligned = e->finished = false;
+    e->aligned = e->finished = e->rbh_done = false;
     e->tm = rc_timing{};
     if (e->external) {
         HIPCHK(hipEventRecord(e->ev[0], e->st));
@@ -898,14 +900,15 @@ static int do_align(rc_engine *e)
     return RC_OK;
 }
 
-static int do_finish(rc_engine *e)
+// Top-N + reciprocal best hits for this shard's items -> table rows, edges.
+static int do_rbh(rc_engine *e)
 {
     if (!e->aligned) return fail(RC_E_STATE, "rc_finish before rc_align");
     CHK(set_device(e));
     const int N = (int)e->samples.size();
-    const uint32_t n_genes = (uint32_t)e->gene_sample.size();
-    const uint64_t ni = e->n_items;
+    const uint64_t ni = e->item1 - e->item0;
     const size_t np = e->pair_a.size();
+    e->finished = false;
     HIPCHK(hipEventRecord(e->ev[5], e->st));
     CHK(e->d_cnt4.ensure(4 * (ni + 1)));
     CHK(e->d_off4.ensure(4 * (ni + 1)));
@@ -924,6 +927,7 @@ static int do_finish(rc_engine *e)
     R.N = N;
     R.top_n = e->o.top_matches;
     R.keep_all = e->o.keep_all;
+    R.item0 = e->item0;
     R.n_items = ni;
     R.n_rows = e->d_cnt4.p;
     R.n_fsel = e->d_cnt4.p + (ni + 1);
@@ -947,6 +951,7 @@ static int do_finish(rc_engine *e)
     HIPCHK(hipStreamSynchronize(e->st));
     e->n_rows = tot[0];
     e->n_edges = tot[3];
+    e->n_local_edges = tot[3];
     CHK(e->d_rows.ensure(e->n_rows));
     CHK(e->d_edges.ensure(e->n_edges));
     R.row_off = e->d_off4.p;
@@ -958,7 +963,22 @@ static int do_finish(rc_engine *e)
     launch_rbh(R, 1, e->st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e->ev[6], e->st));
-    // graph
+    HIPCHK(hipEventSynchronize(e->ev[6]));
+    e->tm.rbh_ms = ev_ms(e, 5, 6);
+    e->rbh_done = true;
+    return RC_OK;
+}
+
+// Gene matches graph over d_edges[0, n_edges): connected components, ideal
+// filter, restricted pair sums.
+static int do_graph(rc_engine *e)
+{
+    if (!e->rbh_done) return fail(RC_E_STATE, "graph phase before rc_finish");
+    CHK(set_device(e));
+    const int N = (int)e->samples.size();
+    const uint32_t n_genes = (uint32_t)e->gene_sample.size();
+    const size_t np = e->pair_a.size();
+    HIPCHK(hipEventRecord(e->ev[6], e->st));
     CHK(e->d_parent.ensure(n_genes));
     CHK(e->d_present.ensure(n_genes));
     CHK(e->d_cnodes.ensure(n_genes));
@@ -988,11 +1008,17 @@ static int do_finish(rc_engine *e)
     HIPCHK(hipMemcpyAsync(e->h_stats.data(), e->d_stats.p, 8 * 8, hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipEventRecord(e->ev[8], e->st));
     HIPCHK(hipStreamSynchronize(e->st));
-    e->tm.rbh_ms = ev_ms(e, 5, 6);
     e->tm.graph_ms = ev_ms(e, 6, 7);
     e->tm.reduce_ms = ev_ms(e, 7, 8);
     e->tm.total_ms = e->tm.pack_ms + e->tm.index_ms + e->tm.align_ms + e->tm.rbh_ms + e->tm.graph_ms + e->tm.reduce_ms;
     e->finished = true;
+    return RC_OK;
+}
+
+static int do_finish(rc_engine *e)
+{
+    CHK(do_rbh(e));
+    if (e->o.shard_count == 1) return do_graph(e);
     return RC_OK;
 }
 
@@ -1047,7 +1073,7 @@ int rc_finish(rc_engine *e)
 int rc_run(rc_engine *e)
 {
     if (!e) return fail(RC_E_ARG, "null engine");
-    if (e->o.shard_count != 1) return fail(RC_E_STATE, "sharded engines use rc_align / rc_import_tops / rc_finish");
+    if (e->o.shard_count != 1) return fail(RC_E_STATE, "sharded engines use rc_align / rc_finish / rc_import_edges");
     CHK(do_align(e));
     return do_finish(e);
 }
@@ -1082,23 +1108,31 @@ int rc_hsps(rc_engine *e, int32_t q, int32_t s, rc_hsp *buf, uint64_t cap, uint6
 int rc_pair_rows(rc_engine *e, int32_t s1, int32_t s2, rc_row *buf, uint64_t cap, uint64_t *n)
 {
     if (!e || !n) return fail(RC_E_ARG, "null argument");
-    if (!e->finished) return fail(RC_E_STATE, "no results yet");
+    if (!e->rbh_done) return fail(RC_E_STATE, "no results yet");
     const int N = (int)e->samples.size();
     if (s1 < 0 || s1 >= N || s2 < 0 || s2 >= N || s1 >= s2) return fail(RC_E_ARG, "need s1 < s2 (input order)");
     CHK(set_device(e));
-    const int p = e->pair_index[s1 * N + s2];
-    const uint64_t ib = e->pair_item_begin[p], ie = e->pair_item_begin[p + 1];
+    const uint64_t p = (uint64_t)e->pair_index[s1 * N + s2];
+    if (p < e->pair0 || p >= e->pair1) return fail(RC_E_ARG, "pair belongs to another shard");
+    const uint64_t ib = e->pair_item_begin[p] - e->item0, ie = e->pair_item_begin[p + 1] - e->item0;
     uint64_t r0 = 0, r1 = 0;
     HIPCHK(hipMemcpy(&r0, e->d_off4.p + ib, 8, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(&r1, e->d_off4.p + ie, 8, hipMemcpyDeviceToHost));
-    *n = r1 - r0;
+    const uint64_t nr = r1 - r0;
+    *n = nr;
     if (!buf) return RC_OK;
-    if (cap < r1 - r0) return fail(RC_E_CAPACITY, "buffer too small");
-    std::vector<DRow> rows(r1 - r0);
-    if (!rows.empty()) HIPCHK(hipMemcpy(rows.data(), e->d_rows.p + r0, rows.size() * sizeof(DRow), hipMemcpyDeviceToHost));
-    for (size_t i = 0; i < rows.size(); i++) {
-        DHsp d;
-        HIPCHK(hipMemcpy(&d, e->d_hsp.p + rows[i].hsp, sizeof(DHsp), hipMemcpyDeviceToHost));
+    if (cap < nr) return fail(RC_E_CAPACITY, "buffer too small");
+    if (!nr) return RC_OK;
+    std::vector<DRow> rows(nr);
+    std::vector<DHsp> hs(nr);
+    CHK(e->d_gather.ensure(nr));
+    launch_gather_rows(e->d_hsp.p, e->d_rows.p + r0, nr, e->d_gather.p, e->st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(rows.data(), e->d_rows.p + r0, nr * sizeof(DRow), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipMemcpyAsync(hs.data(), e->d_gather.p, nr * sizeof(DHsp), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    for (uint64_t i = 0; i < nr; i++) {
+        const DHsp &d = hs[i];
         rc_row &r = buf[i];
         const bool rev = rows[i].reverse != 0;
         // forward rows: query in s2, subject in s1; reverse rows the other way round
@@ -1232,53 +1266,75 @@ int rc_timings(rc_engine *e, rc_timing *t)
     return RC_OK;
 }
 
-int rc_export_tops(rc_engine *e, void *buf, uint64_t cap, uint64_t *n, int on_device)
+int rc_export_edges(rc_engine *e, void *buf, uint64_t cap, uint64_t *n, int on_device)
 {
     if (!e || !n) return fail(RC_E_ARG, "null argument");
-    if (!e->aligned) return fail(RC_E_STATE, "rc_export_tops before rc_align");
+    if (!e->rbh_done) return fail(RC_E_STATE, "rc_export_edges before rc_finish");
     CHK(set_device(e));
-    // d_hsp holds exactly this shard's groups, each contiguous
-    const uint64_t tot = e->n_hsps;
+    const uint64_t tot = e->n_local_edges;
     *n = tot;
     if (!buf) return RC_OK;
     if (cap < tot) return fail(RC_E_CAPACITY, "buffer too small");
+    if (e->n_edges != e->n_local_edges) return fail(RC_E_STATE, "edges already replaced by rc_import_edges");
     if (tot)
-        HIPCHK(hipMemcpy(buf, e->d_hsp.p, tot * sizeof(DHsp), on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(buf, e->d_edges.p, tot * sizeof(DEdge), on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost));
     return RC_OK;
 }
 
-int rc_import_tops(rc_engine *e, const void *buf, uint64_t n, int on_device)
+int rc_import_edges(rc_engine *e, const void *buf, uint64_t n, int on_device)
 {
     if (!e || (n && !buf)) return fail(RC_E_ARG, "null argument");
-    CHK(upload(e));
+    if (!e->rbh_done) return fail(RC_E_STATE, "rc_import_edges before rc_finish");
     CHK(set_device(e));
-    const int N = (int)e->samples.size();
-    std::vector<DHsp> all(n);
-    if (n)
-        HIPCHK(hipMemcpy(all.data(), buf, n * sizeof(DHsp), on_device ? hipMemcpyDeviceToHost : hipMemcpyHostToHost));
-    const size_t ngrp = (size_t)e->gene_sample.size() * N;
-    std::vector<uint32_t> off(ngrp, 0), cnt(ngrp, 0);
-    size_t prev = (size_t)-1;
-    for (uint64_t i = 0; i < n; i++) {
-        if (all[i].q_tx >= e->tx_gene.size() || all[i].s_tx >= e->tx_sample.size())
-            return fail(RC_E_ARG, "record out of range");
-        const size_t gi = (size_t)e->tx_gene[all[i].q_tx] * N + e->tx_sample[all[i].s_tx];
-        if (gi != prev) {
-            if (cnt[gi]) return fail(RC_E_ARG, "records are not grouped by (gene, sample)");
-            off[gi] = (uint32_t)i;
-        }
-        cnt[gi]++;
-        prev = gi;
+    const uint32_t ng = (uint32_t)e->gene_sample.size();
+    const uint64_t np = e->pair_a.size();
+    if (!on_device && n) {
+        const DEdge *ed = static_cast<const DEdge *>(buf);
+        for (uint64_t i = 0; i < n; i++)
+            if (ed[i].a >= ng || ed[i].b >= ng || ed[i].pair >= np) return fail(RC_E_ARG, "edge record out of range");
     }
-    CHK(e->d_hsp.ensure(n));
-    CHK(e->d_grp_off.ensure(ngrp));
-    CHK(e->d_grp_cnt.ensure(ngrp));
-    if (n) HIPCHK(hipMemcpy(e->d_hsp.p, all.data(), n * sizeof(DHsp), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(e->d_grp_off.p, off.data(), ngrp * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(e->d_grp_cnt.p, cnt.data(), ngrp * 4, hipMemcpyHostToDevice));
-    e->n_hsps = n;
-    e->aligned = true;
-    e->finished = false;
+    CHK(e->d_edges.ensure(n));
+    if (n)
+        HIPCHK(hipMemcpy(e->d_edges.p, buf, n * sizeof(DEdge), on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+    e->n_edges = n;
+    e->n_local_edges = 0;   // the local edges are gone
+    return do_graph(e);
+}
+
+// The sample pairs in itertools.combinations order, cut into shard_count
+// contiguous ranges of about equal sequence length (L_a + L_b per pair, the
+// byte model of SURVEY.md §8d): pair p goes to the shard whose share of the
+// total holds the midpoint of p's cost interval.
+int rc_plan_shards(const int64_t *sample_bases, int32_t n_samples, int32_t shard_count, int64_t *pair_first)
+{
+    if (!pair_first || shard_count < 1 || n_samples < 0 || (n_samples && !sample_bases))
+        return fail(RC_E_ARG, "bad argument");
+    std::vector<double> cum(1, 0.0);
+    for (int a = 0; a < n_samples; a++)
+        for (int b = a + 1; b < n_samples; b++)
+            cum.push_back(cum.back() + (double)(sample_bases[a] + sample_bases[b]));
+    const int64_t np = (int64_t)cum.size() - 1;
+    const double tot = cum.back();
+    int64_t p = 0;
+    for (int r = 0; r < shard_count; r++) {
+        pair_first[r] = p;
+        while (p < np) {
+            const int owner = tot > 0 ? std::min(shard_count - 1, (int)(0.5 * (cum[p] + cum[p + 1]) / tot * shard_count))
+                                      : (int)((p * shard_count) / np);
+            if (owner > r) break;
+            p++;
+        }
+    }
+    pair_first[shard_count] = np;
+    return RC_OK;
+}
+
+int rc_shard_pairs(rc_engine *e, int64_t *first, int64_t *last)
+{
+    if (!e || !first || !last) return fail(RC_E_ARG, "null argument");
+    CHK(upload(e));
+    *first = (int64_t)e->pair0;
+    *last = (int64_t)e->pair1;
     return RC_OK;
 }
 

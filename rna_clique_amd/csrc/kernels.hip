@@ -218,8 +218,10 @@ __device__ __forceinline__ uint32_t desc_rank(const DHsp *h, uint32_t off, uint3
 
 __global__ void rbh_kernel(RbhParams P, int pass)
 {
-    for (uint64_t item = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; item < P.n_items;
-         item += (uint64_t)gridDim.x * blockDim.x) {
+    // items [item0, item0 + n_items) of this shard; per-item arrays are local
+    for (uint64_t li = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; li < P.n_items;
+         li += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t item = P.item0 + li;
         int lo = 0, hi = P.n_pairs;
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
@@ -277,11 +279,11 @@ __global__ void rbh_kernel(RbhParams P, int pass)
         // (keep "first": only the first such row)
         uint32_t prev_a = 0;
         bool have_prev = false, done = false;
-        uint64_t row_w = pass ? P.row_off[item] : 0, edge_w = pass ? P.edge_off[item] : 0;
-        const uint64_t fsel_base = pass ? P.fsel_off[item] - P.fsel_off[P.pair_item_begin[pr]] : 0;
+        uint64_t row_w = pass ? P.row_off[li] : 0, edge_w = pass ? P.edge_off[li] : 0;
+        const uint64_t fsel_base = pass ? P.fsel_off[li] - P.fsel_off[P.pair_item_begin[pr] - P.item0] : 0;
         const uint64_t fsel_pair_total =
-            pass ? P.fsel_off[P.pair_item_begin[pr + 1]] - P.fsel_off[P.pair_item_begin[pr]] : 0;
-        const uint64_t rsel_base = pass ? P.rsel_off[item] - P.rsel_off[P.pair_item_begin[pr]] : 0;
+            pass ? P.fsel_off[P.pair_item_begin[pr + 1] - P.item0] - P.fsel_off[P.pair_item_begin[pr] - P.item0] : 0;
+        const uint64_t rsel_base = pass ? P.rsel_off[li] - P.rsel_off[P.pair_item_begin[pr] - P.item0] : 0;
         while (fsel && !done) {
             // next smallest a among selected F rows
             bool found = false;
@@ -413,10 +415,10 @@ __global__ void rbh_kernel(RbhParams P, int pass)
             }
         }
         if (!pass) {
-            P.n_rows[item] = nrows;
-            P.n_fsel[item] = fsel;
-            P.n_rsel[item] = rsel;
-            P.n_edges[item] = nedges;
+            P.n_rows[li] = nrows;
+            P.n_fsel[li] = fsel;
+            P.n_rsel[li] = rsel;
+            P.n_edges[li] = nedges;
         }
     }
 }
@@ -627,6 +629,13 @@ static inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 65536
     return (unsigned)g;
 }
 
+// rows -> their HSP records, for copying one pair's table to the host
+__global__ void gather_rows_kernel(const DHsp *hsp, const DRow *rows, uint64_t n, DHsp *out)
+{
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = hsp[rows[i].hsp];
+}
+
 void launch_pack(const uint8_t *ascii, uint64_t total, uint64_t nwords, uint64_t *F, uint64_t *RC,
                  uint64_t *AF, uint64_t *ARC, hipStream_t st)
 {
@@ -693,6 +702,12 @@ void launch_distance(const unsigned long long *num, const unsigned long long *de
     if (!n) return;
     hipLaunchKernelGGL(distance_kernel, dim3((n + 255) / 256), dim3(256), 0, st, num, den, pair_index, order, N,
                        out, status);
+}
+
+void launch_gather_rows(const DHsp *hsp, const DRow *rows, uint64_t n, DHsp *out, hipStream_t st)
+{
+    if (!n) return;
+    hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, hsp, rows, n, out);
 }
 
 }  // namespace rcg

@@ -1,0 +1,91 @@
+"""Multi-GPU: one engine per GPU, sample pairs sharded, one edge exchange.
+
+SURVEY.md §8e. Every rank loads the same samples. rc_plan_shards cuts the
+C(N,2) pairs (combinations order) into contiguous ranges of equal sequence
+length; each rank aligns its pairs (seed + extend, both directions at once)
+and runs top-N / reciprocal best hits for them, which yields its share of the
+gene matches tables and graph edges. The ideal-clique filter needs the whole
+graph, so the edge records (20 B each: two node ids, the pair, and the edge's
+nident and length - gaps sums) are all-gathered once -- over RCCL on GPUs,
+gloo on CPU -- and every rank runs connected components, the ideal filter and
+the pair sums over all of them. That is the only collective on the data path.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native as nat
+
+
+def world(process_group=None):
+    """(world size, rank) of an initialised torch.distributed group, else (1, 0)."""
+    try:
+        import torch.distributed as dist
+    except ImportError:
+        return 1, 0
+    if not dist.is_available() or not dist.is_initialized():
+        return 1, 0
+    return dist.get_world_size(process_group), dist.get_rank(process_group)
+
+
+def plan_shards(sample_bases, shard_count):
+    """pair_first[shard_count + 1] from rc_plan_shards (no device needed)."""
+    b = np.ascontiguousarray(sample_bases, dtype=np.int64)
+    out = np.zeros(shard_count + 1, dtype=np.int64)
+    nat.check(nat.lib().rc_plan_shards(b.ctypes.data_as(ctypes.c_void_p), len(b), int(shard_count),
+                                       out.ctypes.data_as(ctypes.c_void_p)))
+    return out
+
+
+def all_gather_records(local, record_size, process_group=None, device=None):
+    """Variable-length all-gather of fixed-size records.
+
+    `local` is a uint8 tensor (CUDA for RCCL, CPU for gloo) holding this
+    rank's records. Returns (concatenation of every rank's records in rank
+    order, record count). Sizes go first, then one padded all-gather."""
+    import torch
+    import torch.distributed as dist
+    W = dist.get_world_size(process_group)
+    dev = local.device if device is None else device
+    n = torch.tensor([local.numel() // record_size], dtype=torch.int64, device=dev)
+    counts = [torch.zeros_like(n) for _ in range(W)]
+    dist.all_gather(counts, n, group=process_group)
+    counts = [int(c.item()) for c in counts]
+    mx = max(counts) * record_size
+    if mx == 0:
+        return torch.zeros(0, dtype=torch.uint8, device=dev), 0
+    send = torch.zeros(mx, dtype=torch.uint8, device=dev)
+    send[:local.numel()] = local
+    recv = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(W)]
+    dist.all_gather(recv, send, group=process_group)
+    out = torch.cat([r[:c * record_size] for r, c in zip(recv, counts)])
+    return out, sum(counts)
+
+
+def exchange_edges(eng, process_group=None):
+    """All-gather the shards' graph edges and run the graph phase on them.
+    The engine must have run align() and finish()."""
+    import torch
+    import torch.distributed as dist
+    rs = eng.edge_record_size()
+    on_gpu = dist.get_backend(process_group) != "gloo" and torch.cuda.is_available()
+    if on_gpu:
+        n = eng.local_edge_count()
+        local = torch.empty(max(n * rs, 1), dtype=torch.uint8, device="cuda")[:n * rs]
+        eng.export_edges(local)            # device-to-device, engine stream synced
+        allt, total = all_gather_records(local, rs, process_group)
+        torch.cuda.current_stream().synchronize()   # engine runs on its own stream
+        eng.import_edges(allt.contiguous(), total)
+    else:
+        local = torch.from_numpy(eng.export_edges())
+        allt, total = all_gather_records(local, rs, process_group)
+        eng.import_edges(allt.numpy())
+
+
+def sharded_run(eng, process_group=None):
+    """rc_run for a sharded engine: align + RBH locally, exchange, graph."""
+    eng.align()
+    eng.finish()
+    exchange_edges(eng, process_group)

@@ -89,24 +89,54 @@ class Engine:
     def finish(self):
         nat.check(nat.lib().rc_finish(self._h))
 
-    def export_tops(self):
+    def shard_pairs(self):
+        """[first, last) of this shard's sample pairs in combinations order."""
+        a, b = ctypes.c_int64(), ctypes.c_int64()
+        nat.check(nat.lib().rc_shard_pairs(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    def local_edge_count(self):
+        n = ctypes.c_uint64()
+        nat.check(nat.lib().rc_export_edges(self._h, None, 0, ctypes.byref(n), 0))
+        return n.value
+
+    @staticmethod
+    def edge_record_size():
+        return int(nat.lib().rc_edge_record_size())
+
+    def export_edges(self, out=None):
+        """This shard's graph edges as opaque records: into `out` (a CUDA
+        uint8 tensor, written device-to-device) or a new host uint8 array."""
         L = nat.lib()
         n = ctypes.c_uint64()
-        nat.check(L.rc_export_tops(self._h, None, 0, ctypes.byref(n), 0))
-        rs = L.rc_top_record_size()
+        nat.check(L.rc_export_edges(self._h, None, 0, ctypes.byref(n), 0))
+        rs = self.edge_record_size()
+        if out is not None:
+            if out.numel() < n.value * rs:
+                raise ValueError("edge buffer too small")
+            if n.value:
+                nat.check(L.rc_export_edges(self._h, ctypes.c_void_p(out.data_ptr()), n.value,
+                                            ctypes.byref(n), 1))
+            return n.value
         buf = np.zeros(n.value * rs, dtype=np.uint8)
-        nat.check(L.rc_export_tops(self._h, buf.ctypes.data_as(ctypes.c_void_p),
-                                   n.value, ctypes.byref(n), 0))
+        if n.value:
+            nat.check(L.rc_export_edges(self._h, buf.ctypes.data_as(ctypes.c_void_p), n.value,
+                                        ctypes.byref(n), 0))
         return buf
 
-    def import_tops(self, buf):
+    def import_edges(self, buf, n=None):
+        """All shards' edges (host uint8 array, or CUDA tensor + record count)
+        -> graph, ideal filter, pair sums."""
         L = nat.lib()
-        rs = L.rc_top_record_size()
-        buf = np.ascontiguousarray(buf, dtype=np.uint8)
-        if len(buf) % rs:
-            raise ValueError("record buffer size is not a multiple of the record size")
-        nat.check(L.rc_import_tops(self._h, buf.ctypes.data_as(ctypes.c_void_p),
-                                   len(buf) // rs, 0))
+        rs = self.edge_record_size()
+        if isinstance(buf, np.ndarray):
+            buf = np.ascontiguousarray(buf, dtype=np.uint8)
+            if len(buf) % rs:
+                raise ValueError("edge buffer size is not a multiple of the record size")
+            nat.check(L.rc_import_edges(self._h, buf.ctypes.data_as(ctypes.c_void_p), len(buf) // rs, 0))
+        else:
+            n = buf.numel() // rs if n is None else int(n)
+            nat.check(L.rc_import_edges(self._h, ctypes.c_void_p(buf.data_ptr()), n, 1))
 
     # ------------------------------------------------------------- results
     def _sized(self, fn, dtype, *args):

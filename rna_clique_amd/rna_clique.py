@@ -1,0 +1,112 @@
+"""rna_clique(): the reference's top-level API over the GPU engine.
+
+Same parameters and return value as the reference (rna_clique.py:28-178):
+top-genes selection per input directory -> all-pairs alignment, gene matches
+tables, gene matches graph and ideal-clique filter -> SampleSimilarity, with
+the distance matrix written to `output_matrix` under key "matrix".
+
+What changes underneath:
+* steps 2-6 run in librcgpu.so (hand-written HIP for gfx950) for the whole
+  pair set at once instead of C(N,2) pairs of blastn subprocesses plus pandas
+  and networkx;
+* `cache_dir` (BLAST DB cache) is accepted and unused: the seed index lives in
+  HBM and is rebuilt per run;
+* gene matches tables are written to `out_dir_2` as `{s1}--{s2}.pkl`
+  (write_table's pickle form, gene_matches_tables.py:42-56) when
+  `table_format="pkl"`; "none" skips them; "h5" needs PyTables;
+* `output_graph` is the networkx pickle of build_graph (filtering_step.py:
+  158-159); pass None to skip building it (it is the slowest host step);
+* `jobs` bounds the host threads of the top-genes step.
+"""
+from __future__ import annotations
+
+import itertools
+import multiprocessing
+import os
+import pickle
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+from typing import Callable, Iterable, Optional
+
+from .engine import Engine
+from .h5 import write_matrix
+from .select_top_genes import select_top_sample
+from .similarity import NoIdealComponentsError, SampleSimilarity  # noqa: F401
+from .tables import pair_table, write_table
+from .transcripts import TranscriptID, TranscriptIDParseError, default_gene_re  # noqa: F401
+
+
+def select_all(dirs, out_dir_1, transcripts, top_genes, id_parser, jobs=1):
+    """select_top_and_save over every input directory (filtering_step.py:
+    129-143), in input order."""
+    dirs = [Path(d) for d in dirs]
+    Path(out_dir_1).mkdir(parents=True, exist_ok=True)
+    work = lambda d: select_top_sample(out_dir_1, transcripts, d, top_genes, id_parser)  # noqa: E731
+    if jobs <= 1 or len(dirs) <= 1:
+        return [work(d) for d in dirs]
+    with ThreadPoolExecutor(max_workers=min(jobs, len(dirs))) as ex:
+        return list(ex.map(work, dirs))
+
+
+def run_engine(samples, top_matches=1, evalue=1e-99, keep_all=True, device=0,
+               process_group=None, **engine_kwargs) -> Engine:
+    """Load the samples (labels = top-genes FASTA paths) and run the whole
+    path. With an initialised torch.distributed group of size > 1 the sample
+    pairs are sharded across ranks (see distributed.py)."""
+    from . import distributed
+    world, rank = distributed.world(process_group)
+    eng = Engine(top_matches=top_matches, keep_all=keep_all, evalue=evalue,
+                 device=device, shard_rank=rank, shard_count=world, **engine_kwargs)
+    for s in samples:
+        eng.add_sample(str(s.path), s.seq, s.tx_offsets, s.gene, s.iso)
+    if world == 1:
+        eng.run()
+    else:
+        distributed.sharded_run(eng, process_group)
+    return eng
+
+
+def rna_clique(
+        dirs: Iterable[Path],
+        out_dir_1: Path,
+        out_dir_2: Optional[Path],
+        cache_dir: Optional[Path],
+        output_graph: Optional[Path],
+        output_matrix: Optional[Path],
+        top_genes: int,
+        transcripts: str = "transcripts.fasta",
+        top_matches: int = 1,
+        id_parser: Callable[[str], TranscriptID] = TranscriptID.parser_from_re(default_gene_re),
+        evalue: float = 1e-99,
+        keep_all: bool = True,
+        store_dfs: bool = False,
+        jobs: int = multiprocessing.cpu_count() - 1,
+        *,
+        device: int = 0,
+        table_format: str = "pkl",
+        process_group=None,
+) -> tuple[SampleSimilarity, dict[Path, str]]:
+    """Full RNA-clique analysis of the transcriptomes in `dirs` (see the
+    module docstring for what differs from the reference underneath).
+
+    Returns (SampleSimilarity, {top-genes FASTA path: sample name})."""
+    samples = select_all(dirs, out_dir_1, transcripts, top_genes, id_parser, max(1, jobs))
+    pts = {s.path: s.name for s in samples}
+    eng = run_engine(samples, top_matches, evalue, keep_all, device, process_group)
+    sim = SampleSimilarity(eng, store_dfs=store_dfs)
+    from . import distributed
+    writer = distributed.world(process_group)[1] == 0
+    if writer and out_dir_2 is not None and table_format != "none":
+        out_dir_2 = Path(out_dir_2)
+        out_dir_2.mkdir(parents=True, exist_ok=True)
+        for a, b in itertools.combinations(range(len(samples)), 2):
+            t = pair_table(eng, a, b)
+            write_table(t, out_dir_2 / f"{samples[a].name}--{samples[b].name}.{table_format}")
+    if writer and output_graph is not None:
+        tmp = str(output_graph) + ".tmp"
+        with open(tmp, "wb") as f:
+            pickle.dump(sim.graph, f, pickle.HIGHEST_PROTOCOL)
+        os.replace(tmp, output_graph)
+    if writer and output_matrix is not None:
+        write_matrix(sim.get_dissimilarity_df(), output_matrix)
+    return sim, pts

@@ -1,0 +1,112 @@
+"""Gene matches tables and graph in the reference's in-memory and on-disk forms.
+
+The engine keeps every table on the GPU; these helpers materialise them only
+when a caller asks (store_dfs, od2 files, graph.pkl):
+
+* `pair_table` -> the DataFrame HomologFinder.get_match_table returns plus the
+  ssample/qsample columns find_homologs_and_save adds (find_all_pairs.py:57-88;
+  schema docs/formats.md:231-252), with the index labels the reference keeps.
+* `build_graph` -> the networkx Graph build_graph.py:40-68 makes from those
+  tables, with the same node and edge insertion order.
+* `write_table` -> gene_matches_tables.py:42-56 (.pkl via pandas; .h5 needs
+  PyTables, which this image does not have).
+"""
+from __future__ import annotations
+
+import numbers
+from pathlib import Path
+
+import numpy as np
+import pandas as pd
+
+TABLE_COLUMNS = ["pident", "length", "mismatch", "gapopen", "qstart", "qend", "sstart",
+                 "send", "evalue", "bitscore", "gaps", "nident", "sstrand", "qgene",
+                 "qiso", "sgene", "siso", "reverse", "ssample", "qsample"]
+
+
+def blast_evalue(e):
+    """E-value as BLAST's tabular output prints it, read back as a float:
+    "0.0" below 1e-180, else three significant digits (the form shown in
+    docs/formats.md:262, e.g. 8.75e-152)."""
+    e = np.asarray(e, dtype=np.float64)
+    txt = np.char.mod("%.2e", e)
+    out = txt.astype(np.float64)
+    out[e < 1.0e-180] = 0.0
+    return out
+
+
+def blast_pident(nident, length):
+    """pident = 100 * nident / length printed with 3 decimals."""
+    p = 100.0 * np.asarray(nident, dtype=np.float64) / np.maximum(np.asarray(length), 1)
+    return np.char.mod("%.3f", p).astype(np.float64)
+
+
+def shrink_df(df: pd.DataFrame) -> pd.DataFrame:
+    """Downcast integer columns (find_homologs.py:58-80)."""
+    df = df.copy()
+    for col in df.columns:
+        if issubclass(df[col].dtype.type, numbers.Integral):
+            df[col] = pd.to_numeric(pd.to_numeric(df[col], downcast="integer"),
+                                    downcast="unsigned")
+    return df
+
+
+def rows_to_table(rows: np.ndarray, ssample: str, qsample: str) -> pd.DataFrame:
+    """Engine rows (ROW_DTYPE) of one sample pair -> reference table."""
+    h = rows["hsp"]
+    df = pd.DataFrame({
+        "pident": blast_pident(h["nident"], h["length"]),
+        "length": h["length"], "mismatch": h["mismatch"], "gapopen": h["gapopen"],
+        "qstart": h["qstart"], "qend": h["qend"], "sstart": h["sstart"], "send": h["send"],
+        "evalue": blast_evalue(h["evalue"]),
+        "bitscore": h["bits10"].astype(np.float64) / 10.0,
+        "gaps": h["gaps"], "nident": h["nident"],
+        "sstrand": np.where(h["strand"] != 0, "minus", "plus"),
+        "qgene": rows["qgene"], "qiso": rows["qiso"],
+        "sgene": rows["sgene"], "siso": rows["siso"],
+        "reverse": rows["reverse"].astype(bool),
+    }, index=pd.Index(rows["label"].astype(np.int64)))
+    df = shrink_df(df)
+    df["ssample"] = pd.Categorical([ssample] * len(df))
+    df["qsample"] = pd.Categorical([qsample] * len(df))
+    return df[TABLE_COLUMNS]
+
+
+def pair_table(engine, a: int, b: int, labels=None) -> pd.DataFrame:
+    """Gene matches table of samples a < b (a = t1 = ssample, b = t2 = qsample)."""
+    labels = labels or engine.labels
+    return rows_to_table(engine.pair_rows(a, b), labels[a], labels[b])
+
+
+def write_table(df: pd.DataFrame, path: Path):
+    """gene_matches_tables.py:42-56."""
+    path = Path(path)
+    if path.suffix == ".pkl":
+        df.to_pickle(path)
+    elif path.suffix == ".h5":
+        df.to_hdf(path, key="gene_matches", format="table")   # needs PyTables
+    else:
+        raise ValueError(f"Could not determine file type for extension {path.suffix}.")
+
+
+def build_graph(tables):
+    """build_graph.py:40-68 over (ssample, qsample, rows) triples or DataFrames:
+    per table, the s-nodes, then the q-nodes, then the edges, in row order."""
+    import networkx as nx
+    g = nx.Graph()
+    for t in tables:
+        if isinstance(t, pd.DataFrame):
+            ss = t["ssample"].astype(object).to_numpy()
+            qs = t["qsample"].astype(object).to_numpy()
+            sg = t["sgene"].to_numpy()
+            qg = t["qgene"].to_numpy()
+            sn = list(zip(ss, sg.tolist()))
+            qn = list(zip(qs, qg.tolist()))
+        else:
+            ssample, qsample, rows = t
+            sn = [(ssample, x) for x in rows["sgene"].tolist()]
+            qn = [(qsample, x) for x in rows["qgene"].tolist()]
+        g.add_nodes_from(sn)
+        g.add_nodes_from(qn)
+        g.add_edges_from(zip(sn, qn))
+    return g
