@@ -58,6 +58,21 @@ def algorithmic_bytes(samples, hsps_per_pair, word=28):
     return tot + 32 * hsps_per_pair
 
 
+def traffic_from_profile(config, world):
+    """HBM bytes per step of the seed + extend kernels from the committed PMC
+    profile (profiles/<round>/<config>_pmc.json, FETCH_SIZE doubled per the
+    gfx950 note + WRITE_SIZE; collected with scripts/gpu_pmc.sh), or None."""
+    import glob
+    if world != 1:
+        return None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"{config}_pmc.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d.get("traffic_bytes_seed_extend")
+
+
 def cpu_baseline(samples, n_pairs=1):
     """The C oracle (same algorithm, one core) on a bounded sample of the same
     workload: `n_pairs` sample pairs, both directed searches each, plus the
@@ -115,14 +130,15 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    align_ms = []
+    kern_ms = []
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         labels, mat = step()
-        align_ms.append(eng.timings()["align_kernel_ms"])
+        tmi = eng.timings()
+        kern_ms.append(tmi["seed_kernel_ms"] + tmi["align_kernel_ms"])
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -139,14 +155,17 @@ def main():
         if dist:
             dist.destroy_process_group()
         return
-    # roofline of the dominant kernel (seed-and-extend), survey byte model
+    # roofline of the dominant kernel pair (seed + extend), SURVEY.md §8d byte
+    # model over this rank's share of the pairs; time = HIP events on the
+    # engine's stream around the two launches
     hsps = st["hsps"]
-    avg_align = sum(align_ms) / len(align_ms)
+    avg_k = sum(kern_ms) / len(kern_ms)
     bytes_launch = algorithmic_bytes(samples, hsps) * (1.0 / world)
-    achieved = bytes_launch / (avg_align * 1e-3) / 1e9
+    achieved = bytes_launch / (avg_k * 1e-3) / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": "align_kernel", "kernel_ms": round(avg_align, 3),
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic_from_profile(args.config, world),
+            "kernel": "seed_kernel + extend_kernel", "kernel_ms": round(avg_k, 3),
             "bytes_per_launch": int(bytes_launch)}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:

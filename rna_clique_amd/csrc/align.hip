@@ -19,7 +19,7 @@
 namespace rcg {
 
 constexpr int SBLOCK = 256;
-constexpr int SEED_CAP = 2048;
+constexpr int SEED_CAP = 1024;
 constexpr int MAX_SAMPLES = 256;
 
 constexpr int EBLOCK = 256;
@@ -84,7 +84,8 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
 
     __shared__ LSeed seeds[SEED_CAP];
     __shared__ uint16_t seg_begin[SEED_CAP + 1];
-    __shared__ uint32_t it_lo[SBLOCK], it_pre[SBLOCK + 1], it_info[SBLOCK];
+    __shared__ uint32_t it_lo[SBLOCK], it_cnt[SBLOCK], it_pre[SBLOCK + 1], it_info[SBLOCK];
+    __shared__ uint32_t sh_carry_lo, sh_carry_cnt;
     __shared__ uint64_t iso_start[MAX_ISO];
     __shared__ uint32_t iso_len[MAX_ISO], iso_gtx[MAX_ISO], iso_pre[MAX_ISO + 1];
     __shared__ uint32_t tcnt[MAX_SAMPLES], tpre[MAX_SAMPLES + 1];
@@ -135,6 +136,12 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
             sh_flags = 0;
         }
         __syncthreads();
+        // words p of the oriented query at stride s, one per thread; each
+        // word's index run narrowed to the subject transcripts of [T0, T1)
+        // (runs are sorted by (transcript, offset), transcripts sample-major)
+        const uint32_t txb0 = db.sample_tx_begin[T0], txb1 = db.sample_tx_begin[T1];
+        const bool join = stride <= W16;   // canonical test through the previous word's run
+        if (tid == 0) sh_carry_cnt = 0;
         for (uint32_t ib = 0; ib < n_items; ib += SBLOCK) {
             const uint32_t it = ib + tid;
             uint32_t lo = 0, cnt = 0, info = 0;
@@ -157,21 +164,43 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
                 if (ok) {
                     const uint32_t key = (uint32_t)win(QA, qp);
                     const uint32_t b = key >> (32 - ix.bits);
-                    uint32_t a0 = ix.bucket[b], a1 = ix.bucket[b + 1];
-                    while (a0 < a1 && ix.keys[a0] < key) a0++;
+                    const uint32_t b0 = ix.bucket[b], b1 = ix.bucket[b + 1];
+                    // key run inside the bucket: lower and upper bound
+                    uint32_t a0 = b0, h = b1;
+                    while (a0 < h) {
+                        const uint32_t m = (a0 + h) >> 1;
+                        if (ix.keys[m] < key) a0 = m + 1; else h = m;
+                    }
                     uint32_t a2 = a0;
-                    while (a2 < a1 && ix.keys[a2] == key) a2++;
-                    lo = a0;
-                    cnt = a2 - a0;
+                    h = b1;
+                    while (a2 < h) {
+                        const uint32_t m = (a2 + h) >> 1;
+                        if (ix.keys[m] <= key) a2 = m + 1; else h = m;
+                    }
+                    // first entry with transcript >= txb0, first with >= txb1
+                    uint32_t l0 = a0, h0 = a2;
+                    while (l0 < h0) {
+                        const uint32_t m = (l0 + h0) >> 1;
+                        if (ix.ent[m].x < txb0) l0 = m + 1; else h0 = m;
+                    }
+                    uint32_t l1 = l0, h1 = a2;
+                    while (l1 < h1) {
+                        const uint32_t m = (l1 + h1) >> 1;
+                        if (ix.ent[m].x < txb1) l1 = m + 1; else h1 = m;
+                    }
+                    lo = l0;
+                    cnt = l1 - l0;
                 }
             }
             it_lo[tid] = lo;
+            it_cnt[tid] = cnt;
             it_info[tid] = info;
             uint32_t tot;
             it_pre[tid] = block_exscan(cnt, wsum, tot);
             if (tid == 0) it_pre[SBLOCK] = tot;
             __syncthreads();
             const uint32_t nh = it_pre[SBLOCK];
+            const uint32_t carry_lo = sh_carry_lo, carry_cnt = sh_carry_cnt;
             for (uint32_t h = tid; h < nh; h += SBLOCK) {
                 int lo2 = 0, hi2 = SBLOCK;   // last k with it_pre[k] <= h
                 while (hi2 - lo2 > 1) {
@@ -180,13 +209,34 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
                 }
                 const int k = lo2;
                 const uint2 e = ix.ent[it_lo[k] + (h - it_pre[k])];
-                const TxInfo st = db.tx[e.x];
-                if (st.sample < T0 || st.sample >= T1 || !((tm[st.sample >> 6] >> (st.sample & 63)) & 1)) continue;
                 const uint32_t inf = it_info[k];
-                const uint32_t ii = inf & 127;
-                const int strand = (inf >> 7) & 1;
                 const int p = (int)(inf >> 8);
                 const int off = (int)e.y;
+                if (join && p >= stride && off >= stride) {
+                    // the maximal run reaches back to p - s iff the previous
+                    // word hits (transcript, off - s): then not canonical
+                    uint32_t plo = k ? it_lo[k - 1] : carry_lo, pcnt = k ? it_cnt[k - 1] : carry_cnt;
+                    const uint32_t ty = (uint32_t)(off - stride);
+                    while (pcnt > 0) {
+                        const uint32_t half = pcnt >> 1;
+                        const uint2 f = ix.ent[plo + half];
+                        if (f.x < e.x || (f.x == e.x && f.y < ty)) {
+                            plo += half + 1;
+                            pcnt -= half + 1;
+                        } else {
+                            pcnt = half;
+                        }
+                    }
+                    const uint32_t pend = k ? it_lo[k - 1] + it_cnt[k - 1] : carry_lo + carry_cnt;
+                    if (plo < pend) {
+                        const uint2 f = ix.ent[plo];
+                        if (f.x == e.x && f.y == ty) continue;
+                    }
+                }
+                const TxInfo st = db.tx[e.x];
+                if (!((tm[st.sample >> 6] >> (st.sample & 63)) & 1)) continue;
+                const uint32_t ii = inf & 127;
+                const int strand = (inf >> 7) & 1;
                 QGeo qg = {iso_start[ii], (int)iso_len[ii]};
                 const int maxl = min(min(p, off), stride);
                 const uint64_t *QL = strand ? db.F : db.RC;
@@ -214,6 +264,10 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
                 }
             }
             __syncthreads();
+            if (tid == SBLOCK - 1) {
+                sh_carry_lo = lo;
+                sh_carry_cnt = cnt;
+            }
         }
         if (sh_flags & 1u) {   // too many seeds: fewer subject samples per pass
             if (T1 - T0 == 1) {
@@ -521,6 +575,7 @@ __global__ __launch_bounds__(EBLOCK) void extend_kernel(Db db, ExtParams P)
     const uint64_t nwaves = (uint64_t)gridDim.x * EWAVES;
     int shard = 0;   // advances monotonically with li
     uint64_t li = (uint64_t)blockIdx.x * EWAVES + wid;
+    const uint64_t n_work = P.n_cand;
     auto locate = [&](uint64_t l) -> uint64_t {
         while (shard + 1 < NSHARD && sprefix[shard + 1] <= l) shard++;
         return (uint64_t)shard * P.cand_cap + (l - sprefix[shard]);
@@ -531,18 +586,18 @@ __global__ __launch_bounds__(EBLOCK) void extend_kernel(Db db, ExtParams P)
     Cand ncd{};
     TxInfo nqt{}, nst{};
     uint64_t nci = 0;
-    if (li < P.n_cand) {
+    if (li < n_work) {
         nci = locate(li);
         ncd = P.cands[nci];
         nqt = db.tx[ncd.q_gtx];
         nst = db.tx[ncd.s_gtx];
     }
-    for (; li < P.n_cand; li += nwaves) {
+    for (; li < n_work; li += nwaves) {
         const uint64_t ci = nci;
         const Cand cd = ncd;
         const TxInfo qt = nqt, st = nst;
         const uint64_t lnext = li + nwaves;
-        if (lnext < P.n_cand) {
+        if (lnext < n_work) {
             nci = locate(lnext);
             ncd = P.cands[nci];
             nqt = db.tx[ncd.q_gtx];

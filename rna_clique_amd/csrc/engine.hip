@@ -530,7 +530,7 @@ static int upload(rc_engine *e)
     CHK(up(e->d_thr, thr));
     CHK(up(e->d_bits10, b10));
     CHK(e->d_status.ensure(4));
-    CHK(e->d_count.ensure(4));
+    CHK(e->d_count.ensure(8));
     HIPCHK(hipStreamSynchronize(e->st));
     int bits = 16;
     while (bits < 30 && (1ull << bits) < e->n_kpos) bits++;
@@ -791,7 +791,7 @@ static int do_align(rc_engine *e)
     for (int attempt = 0;; attempt++) {
         if (attempt == 4) return fail(RC_E_NOMEM, "HSP overflow buffer kept overflowing");
         CHK(e->d_ovf.ensure(e->ovf_cap));
-        HIPCHK(hipMemsetAsync(e->d_count.p, 0, 4 * sizeof(unsigned long long), e->st));
+        HIPCHK(hipMemsetAsync(e->d_count.p, 0, 8 * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
         ExtParams X;
         X.xdrop = e->o.xdrop_half;

@@ -45,6 +45,19 @@ def test_simulated_parity(native, seed, taxa, genes, iso, indel):
     assert summary["hsps"] > 0 and summary["ideal_nodes"] > 0
 
 
+@pytest.mark.parametrize("lens,indel", [((200, 9000), 0.002), (None, 0.03)])
+def test_simulated_parity_long_and_gappy(native, lens, indel):
+    """Long transcripts (past the LDS staging limit, global-memory path) and
+    indel-rich pairs (wide live bands)."""
+    from rna_clique_amd.simulate import simulate
+    kw = {"len_uniform": lens} if lens else {}
+    samples, _ = simulate(4, 60, seed=21, p_iso2=0.2, indel_rate=indel, **kw)
+    eng = _run_sim(samples)
+    msgs, summary = full_check(eng, samples)
+    assert not msgs, "\n".join(msgs[:10])
+    assert summary["hsps"] > 0
+
+
 @pytest.mark.parametrize("top_matches,keep_all", [(1, True), (1, False), (2, True)])
 def test_simulated_parity_options(native, top_matches, keep_all):
     from rna_clique_amd.simulate import simulate
