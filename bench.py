@@ -36,6 +36,7 @@ def parse_args():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--cpu-pairs", type=int, default=1,
                     help="sample pairs the CPU baseline times (2 directed searches each)")
     return ap.parse_args()
@@ -100,13 +101,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch as _t
+    ndev = max(1, _t.cuda.device_count())
+    device = local_rank % ndev   # one GPU per rank; ranks share a GPU only in rehearsals
     import numpy as np
     import torch
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(device)
+        dist.init_process_group(args.backend)
     from rna_clique_amd import distributed
     from rna_clique_amd.engine import Engine
     from rna_clique_amd.simulate import simulate, CONFIGS
@@ -116,7 +120,7 @@ def main():
     t_gen = time.perf_counter() - t_gen
     n = len(samples)
     pairs = n * (n - 1) // 2
-    eng = Engine(device=local_rank, shard_rank=rank, shard_count=world)
+    eng = Engine(device=device, shard_rank=rank, shard_count=world)
     for s in samples:
         eng.add_sample(s.name, s.seq, s.tx_offsets, s.gene, s.iso)
     eng.upload()   # inputs resident in HBM before timing (H2D excluded)
@@ -144,7 +148,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda" if args.backend != "gloo" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms_per_step = 1e3 * dt / args.steps

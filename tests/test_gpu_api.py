@@ -135,3 +135,50 @@ def test_matrix_h5_from_run(native, tmp_path):
     f = h.open(tmp_path / "m.h5")
     assert np.array_equal(h.doubles(f, "/matrix/block0_values"), df.to_numpy())
     assert h.strings(f, "/matrix/axis1") == list(df.index)
+
+
+def _shard_worker(rank, world, port, q):
+    import os as _os
+    import torch.distributed as dist
+    _os.environ["MASTER_ADDR"] = "127.0.0.1"
+    _os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rna_clique_amd import distributed
+        from rna_clique_amd.engine import Engine
+        from rna_clique_amd.simulate import simulate
+        samples, _ = simulate(5, 100, seed=31, p_iso2=0.2, indel_rate=0.002)
+        eng = _load(Engine(device=0, shard_rank=rank, shard_count=world), samples)
+        distributed.sharded_run(eng)
+        q.put((rank, eng.distance()[1].tobytes(), eng.stats()["edges"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_processes_share_the_pairs(native):
+    """world_size 2, one engine per process on the same GPU, gloo exchange:
+    the same distances as one engine."""
+    import socket
+    import torch.multiprocessing as mp
+    from rna_clique_amd.engine import Engine
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(5, 100, seed=31, p_iso2=0.2, indel_rate=0.002)
+    ref = _load(Engine(device=0), samples)
+    ref.run()
+    want = ref.distance()[1]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for _, blob, edges in got:
+        assert np.frombuffer(blob, dtype=np.float64).reshape(want.shape).tobytes() == want.tobytes()
+        assert edges == ref.stats()["edges"]
