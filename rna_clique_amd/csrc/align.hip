@@ -137,9 +137,9 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
         }
         __syncthreads();
         // words p of the oriented query at stride s, one per thread; each
-        // word's index run narrowed to the subject transcripts of [T0, T1)
-        // (runs are sorted by (transcript, offset), transcripts sample-major)
-        const uint32_t txb0 = db.sample_tx_begin[T0], txb1 = db.sample_tx_begin[T1];
+        // word's index run narrowed to the bases of subject samples [T0, T1)
+        // (runs hold ascending global positions; samples are contiguous)
+        const uint32_t pb0 = (uint32_t)db.sample_pos_begin[T0], pb1 = (uint32_t)db.sample_pos_begin[T1];
         const bool join = stride <= W16;   // canonical test through the previous word's run
         if (tid == 0) sh_carry_cnt = 0;
         for (uint32_t ib = 0; ib < n_items; ib += SBLOCK) {
@@ -164,29 +164,21 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
                 if (ok) {
                     const uint32_t key = (uint32_t)win(QA, qp);
                     const uint32_t b = key >> (32 - ix.bits);
-                    const uint32_t b0 = ix.bucket[b], b1 = ix.bucket[b + 1];
-                    // key run inside the bucket: lower and upper bound
-                    uint32_t a0 = b0, h = b1;
-                    while (a0 < h) {
-                        const uint32_t m = (a0 + h) >> 1;
-                        if (ix.keys[m] < key) a0 = m + 1; else h = m;
-                    }
-                    uint32_t a2 = a0;
-                    h = b1;
-                    while (a2 < h) {
-                        const uint32_t m = (a2 + h) >> 1;
-                        if (ix.keys[m] <= key) a2 = m + 1; else h = m;
-                    }
-                    // first entry with transcript >= txb0, first with >= txb1
-                    uint32_t l0 = a0, h0 = a2;
+                    // entries of the k-mer with position in [pb0, pb1): lower
+                    // bounds of (key, pb0) and (key, pb1) inside the bucket
+                    const uint64_t k0 = ((uint64_t)key << 32) | pb0, k1 = ((uint64_t)key << 32) | pb1;
+                    uint32_t l0 = ix.bucket[b], h0 = ix.bucket[b + 1];
+                    uint32_t h1 = h0;
                     while (l0 < h0) {
                         const uint32_t m = (l0 + h0) >> 1;
-                        if (ix.ent[m].x < txb0) l0 = m + 1; else h0 = m;
+                        const uint64_t v = ix.ent[m];
+                        if (v < k0) l0 = m + 1; else h0 = m;
+                        if (v >= k1) h1 = min(h1, m);
                     }
-                    uint32_t l1 = l0, h1 = a2;
+                    uint32_t l1 = l0;
                     while (l1 < h1) {
                         const uint32_t m = (l1 + h1) >> 1;
-                        if (ix.ent[m].x < txb1) l1 = m + 1; else h1 = m;
+                        if (ix.ent[m] < k1) l1 = m + 1; else h1 = m;
                     }
                     lo = l0;
                     cnt = l1 - l0;
@@ -208,19 +200,19 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
                     if (it_pre[mid] <= h) lo2 = mid; else hi2 = mid;
                 }
                 const int k = lo2;
-                const uint2 e = ix.ent[it_lo[k] + (h - it_pre[k])];
+                const uint64_t ev = ix.ent[it_lo[k] + (h - it_pre[k])];
+                const uint32_t pos = (uint32_t)ev;
                 const uint32_t inf = it_info[k];
                 const int p = (int)(inf >> 8);
-                const int off = (int)e.y;
-                if (join && p >= stride && off >= stride) {
+                if (join && p >= stride) {
                     // the maximal run reaches back to p - s iff the previous
-                    // word hits (transcript, off - s): then not canonical
+                    // word hits position pos - s (an indexed window never
+                    // crosses a transcript boundary, so then off >= s too)
                     uint32_t plo = k ? it_lo[k - 1] : carry_lo, pcnt = k ? it_cnt[k - 1] : carry_cnt;
-                    const uint32_t ty = (uint32_t)(off - stride);
+                    const uint32_t tp = pos - (uint32_t)stride;
                     while (pcnt > 0) {
                         const uint32_t half = pcnt >> 1;
-                        const uint2 f = ix.ent[plo + half];
-                        if (f.x < e.x || (f.x == e.x && f.y < ty)) {
+                        if ((uint32_t)ix.ent[plo + half] < tp) {
                             plo += half + 1;
                             pcnt -= half + 1;
                         } else {
@@ -228,13 +220,12 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
                         }
                     }
                     const uint32_t pend = k ? it_lo[k - 1] + it_cnt[k - 1] : carry_lo + carry_cnt;
-                    if (plo < pend) {
-                        const uint2 f = ix.ent[plo];
-                        if (f.x == e.x && f.y == ty) continue;
-                    }
+                    if (plo < pend && (uint32_t)ix.ent[plo] == tp) continue;
                 }
-                const TxInfo st = db.tx[e.x];
+                TxInfo st;
+                const uint32_t stx = tx_of_pos(db, ix, pos, st);
                 if (!((tm[st.sample >> 6] >> (st.sample & 63)) & 1)) continue;
+                const int off = (int)(pos - (uint32_t)st.start);
                 const uint32_t ii = inf & 127;
                 const int strand = (inf >> 7) & 1;
                 QGeo qg = {iso_start[ii], (int)iso_len[ii]};
@@ -254,7 +245,7 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
                 const uint32_t slot = atomicAdd(&sh_nseed, 1u);
                 if (slot < (uint32_t)SEED_CAP) {
                     LSeed sd;
-                    sd.k1 = ((uint64_t)ii << 57) | ((uint64_t)strand << 56) | ((uint64_t)e.x << 24) |
+                    sd.k1 = ((uint64_t)ii << 57) | ((uint64_t)strand << 56) | ((uint64_t)stx << 24) |
                             (uint64_t)(uint32_t)(p - l);
                     sd.y = (uint32_t)(off - l);
                     sd.len = (uint32_t)len;

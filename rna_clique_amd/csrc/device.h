@@ -55,15 +55,29 @@ struct Db {
     const int32_t *gene_sample;
     const uint32_t *sample_gene_begin;       // n_samples + 1
     const uint32_t *sample_tx_begin;         // n_samples + 1
+    const uint64_t *sample_pos_begin;        // n_samples + 1: first base of each sample
     int32_t n_samples;
 };
 
+// 16-mer index: one u64 per indexed position, (k-mer << 32) | global base
+// position, sorted by k-mer (stable, so positions ascend inside a k-mer run);
+// bucket[b] = first entry whose k-mer has top `bits` bits >= b.
 struct Index {
-    const uint32_t *keys;       // sorted 16-mer keys
-    const uint2 *ent;           // (gtx, offset) in key order
+    const uint64_t *ent;
     const uint32_t *bucket;     // 2^bits + 1 offsets
+    const uint32_t *pos_tx;     // transcript holding base (p >> POS_TX_SHIFT) << POS_TX_SHIFT
     int32_t bits;
 };
+constexpr int POS_TX_SHIFT = 8;
+
+// transcript of a global base position: the block table, then forward
+__device__ __forceinline__ uint32_t tx_of_pos(const Db &db, const Index &ix, uint32_t pos, TxInfo &ti)
+{
+    uint32_t t = ix.pos_tx[pos >> POS_TX_SHIFT];
+    ti = db.tx[t];
+    while ((uint64_t)pos >= ti.start + ti.len) ti = db.tx[++t];
+    return t;
+}
 
 constexpr int NSHARD = 256;    // output allocation shards (spread the atomics)
 

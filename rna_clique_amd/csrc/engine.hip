@@ -24,8 +24,8 @@ namespace rcg {
 void launch_pack(const uint8_t *, uint64_t, uint64_t, uint64_t *, uint64_t *, uint64_t *, uint64_t *, hipStream_t);
 void launch_kmer_count(const TxInfo *, uint32_t, const uint64_t *, uint64_t *, hipStream_t);
 void launch_kmer_fill(bool, const TxInfo *, uint32_t, const uint64_t *, const uint64_t *, const uint64_t *,
-                      uint32_t *, uint64_t *, hipStream_t);
-void launch_bucket_fill(const uint32_t *, uint64_t, int, uint32_t *, hipStream_t);
+                      uint64_t *, hipStream_t);
+void launch_bucket_fill(const uint64_t *, uint64_t, int, uint32_t *, hipStream_t);
 void launch_seed(bool, const Db &, const Index &, const SeedParams &, hipStream_t);
 void launch_extend(bool, const Db &, const ExtParams &, hipStream_t);
 void launch_group(const GroupParams &, int, hipStream_t);
@@ -228,8 +228,9 @@ struct rc_engine {
     DBuf<uint32_t> d_tx_gene, d_gene_tx_off, d_gene_tx, d_sample_gene_begin, d_sample_tx_begin;
     DBuf<int32_t> d_gene_sample;
     DBuf<uint64_t> d_kpos_off, d_kcnt;
-    DBuf<uint32_t> d_keys, d_keys2, d_bucket;
-    DBuf<uint64_t> d_vals, d_vals2;
+    DBuf<uint64_t> d_ent, d_ent2;   // (k-mer << 32 | position), unsorted / sorted
+    DBuf<uint32_t> d_bucket, d_pos_tx;
+    DBuf<uint64_t> d_sample_pos;
     DBuf<uint8_t> d_tmp;
     DBuf<int32_t> d_thr, d_bits10;
     DBuf<DHsp> d_hsp;
@@ -517,6 +518,22 @@ static int upload(rc_engine *e)
         koff[t + 1] = koff[t] + (uint64_t)(L >= W16 ? L - W16 + 1 : 0);
     }
     CHK(up(e->d_kpos_off, koff));
+    // base position -> transcript, per 2^POS_TX_SHIFT-base block; first base of each sample
+    if (total >= (1ull << 32)) return fail(RC_E_LIMIT, "more than 2^32 bases on one GPU: shard the samples");
+    // (host vectors outlive the async copies: the stream is synchronized below)
+    std::vector<uint32_t> pos_tx((total >> POS_TX_SHIFT) + 2, 0);
+    std::vector<uint64_t> spos(N + 1);
+    {
+        uint32_t t = 0;
+        for (size_t b = 0; b < pos_tx.size(); b++) {
+            const uint64_t p = (uint64_t)b << POS_TX_SHIFT;
+            while (t + 1 < n_tx && e->tx_start[t + 1] <= p) t++;
+            pos_tx[b] = t;
+        }
+        CHK(up(e->d_pos_tx, pos_tx));
+        for (int si = 0; si <= N; si++) spos[si] = si < N ? e->tx_start[e->sample_tx_begin[si]] : total;
+        CHK(up(e->d_sample_pos, spos));
+    }
     e->n_kpos = koff[n_tx];   // upper bound; exact count for the no-ambiguity case
     if (e->n_kpos > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "more than 2^32 seed positions on one GPU");
     // statistics tables
@@ -567,21 +584,22 @@ static int build_index(rc_engine *e)
         HIPCHK(hipMemcpyAsync(&npos, e->d_kpos_off.p + n_tx, sizeof(uint64_t), hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipStreamSynchronize(e->st));
     }
-    CHK(e->d_keys.ensure(npos));
-    CHK(e->d_keys2.ensure(npos));
-    CHK(e->d_vals.ensure(npos));
-    CHK(e->d_vals2.ensure(npos));
+    CHK(e->d_ent.ensure(npos));
+    CHK(e->d_ent2.ensure(npos));
     if (n_tx) launch_kmer_fill(amb, e->d_tx.p, n_tx, e->d_F.p + FRONT_PAD, amb ? e->d_AF.p + FRONT_PAD : nullptr,
-                               e->d_kpos_off.p, e->d_keys.p, e->d_vals.p,
-                               e->st);
+                               e->d_kpos_off.p, e->d_ent.p, e->st);
+    // sort on the k-mer (bits 32..63); the fill order is position order and the
+    // onesweep radix sort is stable, so positions stay ascending per k-mer.
+    // rocPRIM sorts up to 2^20 items with a merge sort that did not keep that
+    // order for a partial bit range: there, sort all 64 bits (same result,
+    // positions are unique).
+    const unsigned bb = npos <= (1ull << 20) ? 0u : 32u;
     size_t tmp = 0;
-    HIPCHK(rocprim::radix_sort_pairs(nullptr, tmp, e->d_keys.p, e->d_keys2.p, e->d_vals.p, e->d_vals2.p, (size_t)npos,
-                                     0, 32, e->st));
+    HIPCHK(rocprim::radix_sort_keys(nullptr, tmp, e->d_ent.p, e->d_ent2.p, (size_t)npos, bb, 64u, e->st));
     CHK(e->d_tmp.ensure(tmp));
-    HIPCHK(rocprim::radix_sort_pairs(e->d_tmp.p, tmp, e->d_keys.p, e->d_keys2.p, e->d_vals.p, e->d_vals2.p,
-                                     (size_t)npos, 0, 32, e->st));
+    HIPCHK(rocprim::radix_sort_keys(e->d_tmp.p, tmp, e->d_ent.p, e->d_ent2.p, (size_t)npos, bb, 64u, e->st));
     CHK(e->d_bucket.ensure((1ull << e->index_bits) + 1));
-    launch_bucket_fill(e->d_keys2.p, npos, e->index_bits, e->d_bucket.p, e->st);
+    launch_bucket_fill(e->d_ent2.p, npos, e->index_bits, e->d_bucket.p, e->st);
     e->n_kpos = npos;
     return RC_OK;
 }
@@ -601,6 +619,7 @@ static Db make_db(rc_engine *e)
     db.gene_sample = e->d_gene_sample.p;
     db.sample_gene_begin = e->d_sample_gene_begin.p;
     db.sample_tx_begin = e->d_sample_tx_begin.p;
+    db.sample_pos_begin = e->d_sample_pos.p;
     db.n_samples = (int32_t)e->samples.size();
     return db;
 }
@@ -727,9 +746,9 @@ static int do_align(rc_engine *e)
     }
     Db db = make_db(e);
     Index ix;
-    ix.keys = e->d_keys2.p;
-    ix.ent = reinterpret_cast<const uint2 *>(e->d_vals2.p);
+    ix.ent = e->d_ent2.p;
     ix.bucket = e->d_bucket.p;
+    ix.pos_tx = e->d_pos_tx.p;
     ix.bits = e->index_bits;
     // --- seeds ---
     std::vector<unsigned long long> shard_cnt(2 * NSHARD);

@@ -112,8 +112,7 @@ __global__ __launch_bounds__(256) void kmer_fill_kernel(const TxInfo *__restrict
                                                         const uint64_t *__restrict__ F,
                                                         const uint64_t *__restrict__ AF,
                                                         const uint64_t *__restrict__ out_off,
-                                                        uint32_t *__restrict__ keys,
-                                                        uint64_t *__restrict__ vals)
+                                                        uint64_t *__restrict__ ent)
 {
     const uint32_t t = blockIdx.x;
     if (t >= n_tx) return;
@@ -131,10 +130,7 @@ __global__ __launch_bounds__(256) void kmer_fill_kernel(const TxInfo *__restrict
             if (AMB) ok = (win(AF, ti.start + o) & 0xFFFFFFFFull) == 0;
         }
         if (!AMB) {
-            if (ok) {
-                keys[base + o] = key;
-                vals[base + o] = (uint64_t)t | ((uint64_t)o << 32);
-            }
+            if (ok) ent[base + o] = ((uint64_t)key << 32) | (ti.start + (uint64_t)o);
         } else {
             const uint64_t m = __ballot(ok);
             const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -147,8 +143,7 @@ __global__ __launch_bounds__(256) void kmer_fill_kernel(const TxInfo *__restrict
                 tot += wcnt[i];
             }
             if (ok) {
-                keys[base + woff + before] = key;
-                vals[base + woff + before] = (uint64_t)t | ((uint64_t)o << 32);
+                ent[base + woff + before] = ((uint64_t)key << 32) | (ti.start + (uint64_t)o);
             }
             base += tot;
             __syncthreads();
@@ -157,15 +152,15 @@ __global__ __launch_bounds__(256) void kmer_fill_kernel(const TxInfo *__restrict
 }
 
 // bucket[b] = first sorted index whose key >> (32 - bits) >= b, b in [0, 2^bits].
-__global__ void bucket_fill_kernel(const uint32_t *__restrict__ keys, uint64_t n, int bits,
+__global__ void bucket_fill_kernel(const uint64_t *__restrict__ ent, uint64_t n, int bits,
                                    uint32_t *__restrict__ bucket)
 {
-    const unsigned sh = 32u - (unsigned)bits;
+    const unsigned sh = 64u - (unsigned)bits;
     const uint64_t nb = 1ull << bits;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i <= n;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t b = (i < n) ? (uint64_t)(keys[i] >> sh) : nb + 1;
-        const uint64_t pb = (i > 0) ? (uint64_t)(keys[i - 1] >> sh) : 0;
+        const uint64_t b = (i < n) ? (ent[i] >> sh) : nb + 1;
+        const uint64_t pb = (i > 0) ? (ent[i - 1] >> sh) : 0;
         const uint64_t lo = (i > 0) ? pb + 1 : 0;
         const uint64_t hi = (i < n) ? b : nb;
         for (uint64_t x = lo; x <= hi && x <= nb; x++) bucket[x] = (uint32_t)i;
@@ -651,20 +646,17 @@ void launch_kmer_count(const TxInfo *tx, uint32_t n_tx, const uint64_t *AF, uint
 }
 
 void launch_kmer_fill(bool amb, const TxInfo *tx, uint32_t n_tx, const uint64_t *F, const uint64_t *AF,
-                      const uint64_t *out_off, uint32_t *keys, uint64_t *vals, hipStream_t st)
+                      const uint64_t *out_off, uint64_t *ent, hipStream_t st)
 {
     if (amb)
-        hipLaunchKernelGGL(kmer_fill_kernel<true>, dim3(n_tx), dim3(256), 0, st, tx, n_tx, F, AF, out_off,
-                           keys, vals);
+        hipLaunchKernelGGL(kmer_fill_kernel<true>, dim3(n_tx), dim3(256), 0, st, tx, n_tx, F, AF, out_off, ent);
     else
-        hipLaunchKernelGGL(kmer_fill_kernel<false>, dim3(n_tx), dim3(256), 0, st, tx, n_tx, F, AF, out_off,
-                           keys, vals);
+        hipLaunchKernelGGL(kmer_fill_kernel<false>, dim3(n_tx), dim3(256), 0, st, tx, n_tx, F, AF, out_off, ent);
 }
 
-void launch_bucket_fill(const uint32_t *keys, uint64_t n, int bits, uint32_t *bucket, hipStream_t st)
+void launch_bucket_fill(const uint64_t *ent, uint64_t n, int bits, uint32_t *bucket, hipStream_t st)
 {
-    hipLaunchKernelGGL(bucket_fill_kernel, dim3(grid_for(n + 1, 256)), dim3(256), 0, st, keys, n, bits,
-                       bucket);
+    hipLaunchKernelGGL(bucket_fill_kernel, dim3(grid_for(n + 1, 256)), dim3(256), 0, st, ent, n, bits, bucket);
 }
 
 void launch_rbh(const RbhParams &P, int pass, hipStream_t st)
