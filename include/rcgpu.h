@@ -103,6 +103,8 @@ typedef struct rc_timing {
     double align_kernel_ms;   /* device time of the extension kernel */
     double ext_steps;         /* greedy X-drop steps executed (wave-level) */
     double ext_calls;         /* greedy extensions (left + right per HSP attempt) */
+    double ext_fullband;      /* extensions recomputed with the full 64-diagonal band */
+    double ext_deferred;      /* candidates past the two-candidate staging slot */
 } rc_timing;
 
 void rc_default_opts(rc_opts *opts);

@@ -24,7 +24,19 @@ constexpr int MAX_SAMPLES = 256;
 
 constexpr int EBLOCK = 256;
 constexpr int EWAVES = EBLOCK / 64;
+#ifndef EXT_MIN_WAVES
+#define EXT_MIN_WAVES 8
+#endif
 constexpr int STAGE_BASES = 8192;                 // staged transcript length limit
+
+// wave-uniform copies (SGPR) of values the compiler cannot prove uniform
+// (LDS and vector-memory loads at a uniform address)
+__device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t rfl(uint64_t v)
+{
+    return ((uint64_t)rfl((uint32_t)(v >> 32)) << 32) | rfl((uint32_t)v);
+}
 
 struct LSeed {
     uint64_t k1;    // iso:7 | strand:1 | gtx:32 | x:24
@@ -554,7 +566,7 @@ __device__ __forceinline__ void stage_seq(uint64_t *dst, const uint64_t *src, ui
 }
 
 template <bool AMB>
-__global__ __launch_bounds__(EBLOCK) void extend_kernel(Db db, ExtParams P)
+__global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, ExtParams P)
 {
     constexpr int NA = AMB ? 4 : 2;
     __shared__ uint64_t stg[EWAVES][NA][SW2];
@@ -566,34 +578,23 @@ __global__ __launch_bounds__(EBLOCK) void extend_kernel(Db db, ExtParams P)
     const uint64_t nwaves = (uint64_t)gridDim.x * EWAVES;
     int shard = 0;   // advances monotonically with li
     uint64_t li = (uint64_t)blockIdx.x * EWAVES + wid;
-    const uint64_t n_work = P.n_cand;
+    // list mode (P.defer set): the candidates extend_dual_kernel deferred
+    const bool list = P.defer != nullptr;
+    const uint64_t n_work = list ? (uint64_t)*P.defer_count : P.n_cand;
+    // candidate slots are wave-uniform: keep them (and what is loaded through
+    // them) in scalar registers
     auto locate = [&](uint64_t l) -> uint64_t {
+        if (list) return rfl((uint64_t)P.defer[l]);
         while (shard + 1 < NSHARD && sprefix[shard + 1] <= l) shard++;
-        return (uint64_t)shard * P.cand_cap + (l - sprefix[shard]);
+        return rfl((uint64_t)((uint64_t)shard * P.cand_cap + (l - sprefix[shard])));
     };
-    // software pipeline: the next candidate's record and transcripts are in
-    // flight while the current one is extended
+    const Cand *__restrict__ cands = P.cands;
+    const TxInfo *__restrict__ txs = db.tx;
     uint32_t steps = 0, exts = 0, ncands = 0;
-    Cand ncd{};
-    TxInfo nqt{}, nst{};
-    uint64_t nci = 0;
-    if (li < n_work) {
-        nci = locate(li);
-        ncd = P.cands[nci];
-        nqt = db.tx[ncd.q_gtx];
-        nst = db.tx[ncd.s_gtx];
-    }
     for (; li < n_work; li += nwaves) {
-        const uint64_t ci = nci;
-        const Cand cd = ncd;
-        const TxInfo qt = nqt, st = nst;
-        const uint64_t lnext = li + nwaves;
-        if (lnext < n_work) {
-            nci = locate(lnext);
-            ncd = P.cands[nci];
-            nqt = db.tx[ncd.q_gtx];
-            nst = db.tx[ncd.s_gtx];
-        }
+        const uint64_t ci = locate(li);
+        const Cand cd = cands[ci];
+        const TxInfo qt = txs[cd.q_gtx], st = txs[cd.s_gtx];
         const int Lq = (int)qt.len, Lt = (int)st.len;
         const int strand = cd.strand;
         const int ns = cd.seed_cnt;
@@ -841,13 +842,13 @@ void launch_seed(bool amb, const Db &db, const Index &ix, const SeedParams &P, h
 void launch_extend(bool amb, const Db &db, const ExtParams &P, hipStream_t st)
 {
     if (P.n_cand == 0) return;
-    uint64_t blocks = (P.n_cand + EWAVES - 1) / EWAVES;
-    const uint64_t cap = 256ull * 8;    // about two resident waves per SIMD slot; waves loop
-    if (blocks > cap) blocks = cap;
+    ExtParams W = P;
+    W.defer = nullptr;
+    const uint64_t blocks = 256ull * 8;
     if (amb)
-        hipLaunchKernelGGL(extend_kernel<true>, dim3((unsigned)blocks), dim3(EBLOCK), 0, st, db, P);
+        hipLaunchKernelGGL(extend_kernel<true>, dim3((unsigned)blocks), dim3(EBLOCK), 0, st, db, W);
     else
-        hipLaunchKernelGGL(extend_kernel<false>, dim3((unsigned)blocks), dim3(EBLOCK), 0, st, db, P);
+        hipLaunchKernelGGL(extend_kernel<false>, dim3((unsigned)blocks), dim3(EBLOCK), 0, st, db, W);
 }
 
 void launch_group(const GroupParams &P, int pass, hipStream_t st)

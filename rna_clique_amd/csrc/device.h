@@ -128,13 +128,21 @@ struct ExtParams {
     uint64_t ovf_cap;
     unsigned long long *ovf_count;
     unsigned int *status;         // bit 0 overflow
-    unsigned long long *counters; // [0] greedy steps, [1] extensions, [2] candidates (one atomic per wave)
+    unsigned long long *counters; // [0] greedy steps, [1] extensions, [2] candidates (one atomic per wave),
+                                  // [4] full-band recomputations
+    // two-candidate kernel: staging slot (u64 words per sequence) and the
+    // candidates it defers to the one-wave kernel (transcripts past the slot)
+    int32_t dsw;
+    uint32_t *defer;
+    unsigned long long *defer_count;
 };
 
 // DHsp.strand carries, besides the strand (bit 0), the direction flags of a
 // freshly extended HSP (bit 1: passes the query->subject e-value cut, bit 2:
 // passes the mirrored direction's) and its index in the candidate (bits 3-5).
 constexpr int HSP_FWD = 2, HSP_REV = 4, HSP_IDX_SHIFT = 3;
+
+constexpr int DSTAGE_MAX = 4096;   // longest transcript the two-candidate extension stages
 
 // group kernels: candidates of each (gene, sample) -> contiguous HSP groups.
 // Direct groups (gene of the query sample, higher subject sample) come in

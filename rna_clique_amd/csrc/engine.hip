@@ -238,7 +238,7 @@ struct rc_engine {
     DBuf<Cand> d_cands;
     DBuf<DHsp> d_cand_hsp, d_ovf;
     DBuf<uint8_t> d_cand_nh;
-    DBuf<uint32_t> d_cand_ovf, d_gc_off, d_gc_cnt, d_gcount;
+    DBuf<uint32_t> d_cand_ovf, d_gc_off, d_gc_cnt, d_gcount, d_defer;
     DBuf<uint64_t> d_gscan, d_mscan, d_mkey, d_tmask;
     DBuf<uint32_t> d_mcnt, d_mcur, d_tx_pos;
     DBuf<unsigned long long> d_shard_cnt, d_shard_prefix;
@@ -807,6 +807,7 @@ static int do_align(rc_engine *e)
     CHK(e->d_cand_hsp.ensure(slots));
     CHK(e->d_cand_nh.ensure(slots));
     CHK(e->d_cand_ovf.ensure(slots));
+    CHK(e->d_defer.ensure(std::max<uint64_t>(n_cand, 1)));
     for (int attempt = 0;; attempt++) {
         if (attempt == 4) return fail(RC_E_NOMEM, "HSP overflow buffer kept overflowing");
         CHK(e->d_ovf.ensure(e->ovf_cap));
@@ -830,11 +831,14 @@ static int do_align(rc_engine *e)
         X.ovf_count = e->d_count.p;
         X.status = e->d_status.p;
         X.counters = e->d_count.p + 1;
+        X.dsw = (std::min(e->max_len, DSTAGE_MAX) >> 5) + 3;
+        X.defer = e->d_defer.p;
+        X.defer_count = e->d_count.p + 6;
         HIPCHK(hipEventRecord(e->ev[10], e->st));
         launch_extend(e->has_amb, db, X, e->st);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e->ev[11], e->st));
-        unsigned long long ovn = 0, ctr[3] = {0, 0, 0};
+        unsigned long long ovn = 0, ctr[6] = {0, 0, 0, 0, 0, 0};
         unsigned int status = 0;
         HIPCHK(hipMemcpyAsync(&ovn, e->d_count.p, sizeof ovn, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipMemcpyAsync(ctr, e->d_count.p + 1, sizeof ctr, hipMemcpyDeviceToHost, e->st));
@@ -842,6 +846,8 @@ static int do_align(rc_engine *e)
         HIPCHK(hipStreamSynchronize(e->st));
         e->tm.ext_steps = (double)ctr[0];
         e->tm.ext_calls = (double)ctr[1];
+        e->tm.ext_fullband = (double)ctr[4];
+        e->tm.ext_deferred = (double)ctr[5];
         if (!(status & 1u)) break;
         e->ovf_cap = ovn * 5 / 4 + 1024;
     }
