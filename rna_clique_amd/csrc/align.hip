@@ -696,6 +696,446 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
 }
 
 // ------------------------------------------------------------------------
+// extension, four candidates per wave: one 16-lane DPP row per candidate
+// ------------------------------------------------------------------------
+//
+// The greedy frontier of a near-identical transcript pair stays within a few
+// diagonals of the seed's, so most of the 64-diagonal band of extend_kernel is
+// dead lanes. Here each 16-lane row of the wave runs its own candidate over
+// the sub-band of diagonals [-8, 7] (row lane rl <-> diagonal rl - 8). The
+// sub-band computes exactly what the full band computes as long as no live
+// diagonal reaches its edge lanes (a diagonal outside can only be entered
+// from a live neighbour); the first time an edge lane is live while the
+// extension continues, the candidate is handed to extend_kernel (list mode)
+// whole. Rows advance independently (their own seeds, extensions,
+// candidates): a row that finishes an extension does its bookkeeping while
+// the other rows wait one transition, then all rows step together.
+
+#ifndef ROW_MIN_WAVES
+#define ROW_MIN_WAVES 6
+#endif
+
+// max over the 16 lanes of each DPP row, in every lane of the row
+__device__ __forceinline__ int row_max(int v)
+{
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false));  // row_mirror
+    return v;
+}
+
+// Sub-band rows of RW = 16 lanes (one DPP row) or 32 lanes (half a wave).
+// lane rl <- rl - 1 inside the row (rl 0 gets `edge`); FIX: also at the
+// half-wave seam (needed for the frontier, not for values only read where
+// the frontier neighbour is live)
+template <int RW, bool FIX>
+__device__ __forceinline__ int rw_from_lower(int v, int edge, int rl)
+{
+    if constexpr (RW == 16) {
+        return __builtin_amdgcn_update_dpp(edge, v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    } else {
+        const int x = __builtin_amdgcn_update_dpp(edge, v, 0x138, 0xF, 0xF, false);   // wave_shr:1
+        return (FIX && rl == 0) ? edge : x;
+    }
+}
+// lane rl <- rl + 1 inside the row (rl RW - 1 gets `edge`)
+template <int RW, bool FIX>
+__device__ __forceinline__ int rw_from_upper(int v, int edge, int rl)
+{
+    if constexpr (RW == 16) {
+        return __builtin_amdgcn_update_dpp(edge, v, 0x101, 0xF, 0xF, false);   // row_shl:1
+    } else {
+        const int x = __builtin_amdgcn_update_dpp(edge, v, 0x130, 0xF, 0xF, false);   // wave_shl:1
+        return (FIX && rl == RW - 1) ? edge : x;
+    }
+}
+// max over the row, in every lane of the row
+template <int RW>
+__device__ __forceinline__ int rw_max(int v)
+{
+    v = row_max(v);
+    if constexpr (RW == 32) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);   // DPP rows 0<->1, 2<->3
+        v = max((int)r[0], (int)r[1]);
+    }
+    return v;
+}
+// bit r set iff some lane of row r is set in a wave mask (scalar work)
+template <int RW>
+__device__ __forceinline__ uint32_t rw_bits(uint64_t m)
+{
+    if constexpr (RW == 16)
+        return ((m & 0xFFFFull) ? 1u : 0u) | ((m & 0xFFFF0000ull) ? 2u : 0u) | ((m & 0xFFFF00000000ull) ? 4u : 0u) |
+               ((m >> 48) ? 8u : 0u);
+    else
+        return ((uint32_t)m ? 1u : 0u) | ((m >> 32) ? 2u : 0u);
+}
+// the RW bits of this lane's row in a wave mask
+template <int RW>
+__device__ __forceinline__ uint32_t rw_mask(uint64_t m, int row)
+{
+    return (uint32_t)(m >> (RW * row)) & (RW == 32 ? 0xFFFFFFFFu : 0xFFFFu);
+}
+
+// Matching bases from (pa, pb) forward, or from (pa - 1, pb - 1) backwards, at
+// most maxn; positions index one LDS dword array (16 bases per dword); masks
+// (AMB) sit `moff` bases after the sequences.
+template <bool AMB>
+__device__ __forceinline__ int slide_dir(const uint32_t *S, uint32_t pa, uint32_t pb, int maxn, bool back,
+                                         uint32_t moff)
+{
+    int n = 0;
+    while (n < maxn) {
+        const uint32_t qa = back ? pa - (uint32_t)(n + 32) : pa + (uint32_t)n;
+        const uint32_t qb = back ? pb - (uint32_t)(n + 32) : pb + (uint32_t)n;
+        uint64_t x = win3(S, qa) ^ win3(S, qb);
+        if (AMB) x |= win3(S, qa + moff) | win3(S, qb + moff);
+        if (x == 0) {
+            n += 32;
+            continue;
+        }
+        n += (back ? __builtin_clzll(x) : __builtin_ctzll(x)) >> 1;
+        return n < maxn ? n : maxn;
+    }
+    return maxn > 0 ? maxn : 0;
+}
+
+// per-row bookkeeping in LDS
+enum { RM_CLO, RM_CHI, RM_QTX, RM_STX, RM_LQ, RM_LT, RM_STRAND, RM_SOFF, RM_X, RM_Y, RM_LEN,
+       RM_RSC, RM_RI, RM_RJ, RM_RD, RM_RGO, RM_N };
+enum { HB_QA, HB_QB, HB_SA, HB_SB, HB_SC, HB_D, HB_G, HB_O, HB_NI, HB_N };
+// row actions
+enum { A_FETCH, A_SEED, A_RDONE, A_LDONE, A_ABORT, A_STEP, A_DONE };
+
+template <bool AMB, int RW>
+__global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db db, ExtParams P)
+{
+    constexpr int RROWS = EBLOCK / RW;   // rows per block
+    constexpr int RC0 = RW / 2;          // row lane of diagonal 0
+    constexpr int NA = AMB ? 4 : 2;
+    constexpr int EBIT = 26, OBIT = 13;
+    constexpr int GMASK = 8191;
+    extern __shared__ uint64_t rstg[];                    // [RROWS][NA][sw]
+    __shared__ unsigned long long sprefix[NSHARD + 1];
+    __shared__ int rmeta[RROWS][RM_N];
+    __shared__ int rbox[RROWS][MAX_HSP][HB_N];
+    for (int i = threadIdx.x; i <= NSHARD; i += EBLOCK) sprefix[i] = P.shard_prefix[i];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, rl = lane & (RW - 1), row = lane / RW;
+    const int rs = threadIdx.x / RW;                      // row slot in the block
+    const int k = rl - RC0;                               // this lane's diagonal
+    const int sw = P.dsw;                                 // u64 words per staged sequence
+    const int smax = (sw - 4) * 32;                       // longest staged transcript + SPAD
+    const uint32_t *S = reinterpret_cast<const uint32_t *>(rstg);
+    uint64_t *qst = rstg + (size_t)rs * NA * sw, *tst = qst + sw;
+    const uint32_t qbase = (uint32_t)(rs * NA * sw) * 32u + SPAD, tbase = qbase + 32u * (uint32_t)sw;
+    const uint32_t moff = 64u * (uint32_t)sw;
+    int *meta = rmeta[rs];
+    const uint64_t total = db.total;
+    const uint64_t nrows = (uint64_t)gridDim.x * RROWS;
+    uint64_t li = (uint64_t)blockIdx.x * RROWS + rs;
+    int shard = 0;
+    const int X = P.xdrop;
+
+    int act = A_FETCH;
+    // extension state: frontier (R, gap state), winner record, row-uniform best
+    int R = -1, goe = 0, wi = 0, wg = 0, wd = 0, best = 0, bl = RC0, d = 0;
+    uint32_t pa = 0, pb = 0;
+    int alen = 0, blen = 0;
+    bool back = false;
+    // candidate state (row-uniform) and the seed chunk (lane rl: seed cb + rl)
+    int ns = 0, nh = 0, si = 0, cb = -1, sx = 0, sy = 0, sl = 0;
+    uint32_t steps = 0, exts = 0, ncands = 0, nover = 0;
+
+    auto ext_init = [&](int done_act) {
+        int r0 = 0;
+        if (rl == RC0) r0 = slide_dir<AMB>(S, pa, pb, min(alen, blen), back, moff);
+        r0 = __shfl(r0, RW * row + RC0);
+        best = 2 * r0;
+        bl = RC0;
+        if (rl == RC0) {
+            wi = r0;
+            wg = 0;
+            wd = 0;
+        }
+        R = rl == RC0 ? r0 : -1;
+        goe = 0;
+        d = 0;
+        exts++;
+        act = (min(alen, blen) - r0 <= 0) ? done_act : A_STEP;
+    };
+
+    for (;;) {
+        // ---------------- transitions ----------------
+        while (act != A_STEP && act != A_DONE) {
+            if (act == A_FETCH) {
+                if (li >= P.n_cand) {
+                    act = A_DONE;
+                    continue;
+                }
+                while (shard + 1 < NSHARD && sprefix[shard + 1] <= li) shard++;
+                const uint64_t ci = (uint64_t)shard * P.cand_cap + (li - sprefix[shard]);
+                const Cand cd = P.cands[ci];
+                const TxInfo qt = db.tx[cd.q_gtx], st = db.tx[cd.s_gtx];
+                const int Lq = (int)qt.len, Lt = (int)st.len;
+                if (Lq + SPAD > smax || Lt + SPAD > smax) {
+                    if (rl == 0) {
+                        const unsigned long long di = atomicAdd(P.defer_count, 1ull);
+                        P.defer[di] = (uint32_t)ci;
+                    }
+                    li += nrows;
+                    continue;
+                }
+                const uint64_t q0 = cd.strand ? total - qt.start - (uint64_t)Lq : qt.start;
+                const uint64_t *QA = cd.strand ? db.RC : db.F;
+                const int nwq = (Lq >> 5) + 3, nwt = (Lt >> 5) + 3;
+                for (int w = rl; w < nwq; w += RW) qst[w] = w ? win<uint64_t>(QA, q0 + 32 * (uint64_t)(w - 1)) : 0ull;
+                for (int w = rl; w < nwt; w += RW) tst[w] = w ? win<uint64_t>(db.F, st.start + 32 * (uint64_t)(w - 1)) : 0ull;
+                if (AMB) {
+                    const uint64_t *QM = cd.strand ? db.ARC : db.AF;
+                    for (int w = rl; w < nwq; w += RW) qst[2 * sw + w] = w ? win<uint64_t>(QM, q0 + 32 * (uint64_t)(w - 1)) : 0ull;
+                    for (int w = rl; w < nwt; w += RW) tst[2 * sw + w] = w ? win<uint64_t>(db.AF, st.start + 32 * (uint64_t)(w - 1)) : 0ull;
+                }
+                if (rl == 0) {
+                    meta[RM_CLO] = (int)(uint32_t)ci;
+                    meta[RM_CHI] = (int)(uint32_t)(ci >> 32);
+                    meta[RM_QTX] = (int)cd.q_gtx;
+                    meta[RM_STX] = (int)cd.s_gtx;
+                    meta[RM_LQ] = Lq;
+                    meta[RM_LT] = Lt;
+                    meta[RM_STRAND] = cd.strand;
+                    meta[RM_SOFF] = (int)cd.seed_off;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                ns = cd.seed_cnt;
+                nh = 0;
+                si = 0;
+                cb = -1;
+                ncands++;
+                act = A_SEED;
+            } else if (act == A_SEED) {
+                if (nh >= MAX_HSP || si >= ns) {
+                    // ---- candidate done: purge, e-value cut, output ----
+                    const uint64_t ci = (uint64_t)(uint32_t)meta[RM_CLO] | ((uint64_t)(uint32_t)meta[RM_CHI] << 32);
+                    const int Lq = meta[RM_LQ], Lt = meta[RM_LT], strand = meta[RM_STRAND];
+                    const uint32_t q_gtx = (uint32_t)meta[RM_QTX], s_gtx = (uint32_t)meta[RM_STX];
+                    const bool mine = rl < nh;
+                    const int *hb = rbox[rs][mine ? rl : 0];
+                    const int bqa = hb[HB_QA], bqb = hb[HB_QB], bsa = hb[HB_SA], bsb = hb[HB_SB];
+                    const int bsc = hb[HB_SC];
+                    bool kept = mine && rl == 0;
+                    if (nh > 1) {
+                        int rank = 0;
+                        for (int j = 0; j < nh; j++) {
+                            const int sj = rbox[rs][j][HB_SC];
+                            if (mine && (sj > bsc || (sj == bsc && j < rl))) rank++;
+                        }
+                        kept = false;
+                        for (int rr = 0; rr < nh; rr++) {
+                            const uint32_t m = rw_mask<RW>(__ballot(mine && rank == rr), row);
+                            const int i = __builtin_ctz(m);
+                            const int *hi = rbox[rs][i];
+                            const bool conflict = kept && mine && ((bqa == hi[HB_QA] && bsa == hi[HB_SA]) ||
+                                                                   (bqb == hi[HB_QB] && bsb == hi[HB_SB]));
+                            if (!rw_mask<RW>(__ballot(conflict), row) && rl == i) kept = true;
+                        }
+                    }
+                    const int qs = db.tx[q_gtx].sample, ss = db.tx[s_gtx].sample;
+                    const int thr_f = P.thr[(size_t)ss * (size_t)(P.max_len + 1) + (size_t)Lq];
+                    const int thr_r = P.thr[(size_t)qs * (size_t)(P.max_len + 1) + (size_t)Lt];
+                    const bool pf = bsc >= thr_f, pr = bsc >= thr_r;
+                    const bool out = kept && (pf || pr);
+                    const uint32_t om = rw_mask<RW>(__ballot(out), row);
+                    const int nout = __popc(om);
+                    uint32_t obase = 0;
+                    if (nout > 1 && rl == 0) {
+                        const unsigned long long b = atomicAdd(P.ovf_count, (unsigned long long)(nout - 1));
+                        if (b + (nout - 1) > P.ovf_cap) atomicOr(P.status, 1u);
+                        obase = (uint32_t)b;
+                    }
+                    obase = __shfl(obase, RW * row);
+                    if (out) {
+                        const int rk = __popc(om & ((1u << rl) - 1u));
+                        DHsp h;
+                        h.q_tx = q_gtx;
+                        h.s_tx = s_gtx;
+                        if (!strand) {
+                            h.qstart = bqa + 1; h.qend = bqb; h.sstart = bsa + 1; h.send = bsb;
+                        } else {
+                            h.qstart = Lq - bqb + 1; h.qend = Lq - bqa; h.sstart = bsb; h.send = bsa + 1;
+                        }
+                        const int bd = hb[HB_D], bg = hb[HB_G], bni = hb[HB_NI];
+                        h.gaps = bg;
+                        h.gapopen = hb[HB_O];
+                        h.mismatch = bd - bg;
+                        h.nident = bni;
+                        h.length = bni + (bd - bg) + bg;
+                        h.score_half = bsc;
+                        h.bits10 = P.bits10[bsc];
+                        h.strand = strand | (pf ? HSP_FWD : 0) | (pr ? HSP_REV : 0) | (rl << HSP_IDX_SHIFT);
+                        if (rk == 0) P.cand_hsp[ci] = h;
+                        else if ((uint64_t)obase + (rk - 1) < P.ovf_cap) P.ovf[obase + rk - 1] = h;
+                    }
+                    if (rl == 0) {
+                        P.cand_nh[ci] = (uint8_t)nout;
+                        P.cand_ovf[ci] = obase;
+                    }
+                    li += nrows;
+                    act = A_FETCH;
+                    continue;
+                }
+                // next seed not inside a kept box, searched 16 at a time
+                const int c0 = si & ~(RW - 1);
+                if (c0 != cb) {
+                    cb = c0;
+                    if (cb + rl < ns) {
+                        const GSeed g = P.seeds[(uint32_t)meta[RM_SOFF] + (uint32_t)(cb + rl)];
+                        sx = (int)g.x;
+                        sy = (int)g.y;
+                        sl = (int)g.len;
+                    }
+                }
+                const int idx = cb + rl;
+                bool contained = false;
+                for (int j = 0; j < nh; j++) {
+                    const int *hj = rbox[rs][j];
+                    contained |= hj[HB_QA] <= sx && sx + sl <= hj[HB_QB] && hj[HB_SA] <= sy && sy + sl <= hj[HB_SB];
+                }
+                const uint32_t m = rw_mask<RW>(__ballot(idx >= si && idx < ns && !contained), row);
+                if (!m) {
+                    si = cb + RW;
+                    continue;
+                }
+                const int f = __builtin_ctz(m);
+                const int x = __shfl(sx, RW * row + f), y = __shfl(sy, RW * row + f), len = __shfl(sl, RW * row + f);
+                si = cb + f + 1;
+                if (rl == 0) {
+                    meta[RM_X] = x;
+                    meta[RM_Y] = y;
+                    meta[RM_LEN] = len;
+                }
+                const int Lq = meta[RM_LQ], Lt = meta[RM_LT];
+                pa = qbase + (uint32_t)(x + len);
+                alen = Lq - (x + len);
+                pb = tbase + (uint32_t)(y + len);
+                blen = Lt - (y + len);
+                back = false;
+                ext_init(A_RDONE);
+            } else if (act == A_RDONE || act == A_LDONE) {
+                const int src = RW * row + bl;
+                const int ei = __shfl(wi, src), ed = __shfl(wd, src), ego = __shfl(wg, src);
+                const int ej = ei - (bl - RC0);
+                const int x = meta[RM_X], y = meta[RM_Y], len = meta[RM_LEN];
+                if (act == A_RDONE) {
+                    if (rl == 0) {
+                        meta[RM_RSC] = best;
+                        meta[RM_RI] = ei;
+                        meta[RM_RJ] = ej;
+                        meta[RM_RD] = ed;
+                        meta[RM_RGO] = ego;
+                    }
+                    pa = qbase + (uint32_t)x;
+                    alen = x;
+                    pb = tbase + (uint32_t)y;
+                    blen = y;
+                    back = true;
+                    ext_init(A_LDONE);
+                } else {
+                    const int rsc = meta[RM_RSC], ri = meta[RM_RI], rj = meta[RM_RJ], rd = meta[RM_RD];
+                    const int rgo = meta[RM_RGO];
+                    const int lg = ego & GMASK, lo = (ego >> OBIT) & GMASK;
+                    const int rg = rgo & GMASK, ro = (rgo >> OBIT) & GMASK;
+                    if (rl == 0) {
+                        int *hb = rbox[rs][nh];
+                        hb[HB_QA] = x - ei;
+                        hb[HB_QB] = x + len + ri;
+                        hb[HB_SA] = y - ej;
+                        hb[HB_SB] = y + len + rj;
+                        hb[HB_SC] = best + 2 * len + rsc;
+                        hb[HB_D] = ed + rd;
+                        hb[HB_G] = lg + rg;
+                        hb[HB_O] = lo + ro;
+                        hb[HB_NI] = len + (ei + ej - 2 * ed + lg) / 2 + (ri + rj - 2 * rd + rg) / 2;
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    nh++;
+                    act = A_SEED;
+                }
+            } else {   // A_ABORT: the sub-band overflowed; extend_kernel redoes the candidate
+                if (rl == 0) {
+                    const unsigned long long di = atomicAdd(P.defer_count, 1ull);
+                    P.defer[di] = (uint32_t)meta[RM_CLO];
+                }
+                nover++;
+                li += nrows;
+                act = A_FETCH;
+            }
+        }
+        const bool ext = act == A_STEP;
+        if (!__ballot(ext)) break;
+        // ---------------- one greedy step of every extending row ----------------
+        if (ext) {
+            steps++;
+            d++;
+            const int Rl = rw_from_lower<RW, true>(R, -1, rl), Rr = rw_from_upper<RW, true>(R, -1, rl);
+            const int gl = rw_from_lower<RW, false>(goe, 0, rl), gr = rw_from_upper<RW, false>(goe, 0, rl);
+            const int cm = (R >= 0 && R < alen && R - k < blen) ? R + 1 : -1;
+            const int cil = (Rl >= 0 && Rl < alen) ? Rl + 1 : -1;
+            const int cd = (Rr >= 0 && Rr - (k + 1) < blen) ? Rr : -1;
+            int ni = max(max(cm, cil), cd);
+            const bool fm = ni >= 0 && cm == ni, fi = !fm && cil == ni;
+            const int gi = (gl & ~(3 << EBIT)) + 1 + ((((gl >> EBIT) & 3) == 1) ? 0 : (1 << OBIT)) + (1 << EBIT);
+            const int gd = (gr & ~(3 << EBIT)) + 1 + ((((gr >> EBIT) & 3) == 2) ? 0 : (1 << OBIT)) + (2 << EBIT);
+            int ng = fm ? (goe & ~(3 << EBIT)) : (fi ? gi : gd);
+            int score = INT_MIN, bound = INT_MIN;
+            if (ni >= 0) {
+                const int ja = ni - k;
+                const int m = min(alen - ni, blen - ja);
+                const int s = slide_dir<AMB>(S, back ? pa - (uint32_t)ni : pa + (uint32_t)ni,
+                                             back ? pb - (uint32_t)ja : pb + (uint32_t)ja, m, back, moff);
+                ni += s;
+                if (s > 0) ng &= ~(3 << EBIT);
+                score = 2 * ni - k - 6 * d;
+                if (score < best - X) ni = -1;
+                bound = score + 2 * (m - s);
+            }
+            R = ni;
+            goe = ng;
+            const bool live = ni >= 0;
+            const uint32_t rb_live = rw_bits<RW>(__ballot(live));
+            const uint32_t rb_imp = rw_bits<RW>(__ballot(live && score > best));
+            if (rb_imp) {
+                const int mk = rw_max<RW>(live ? score * RW + (RW - 1 - rl) : INT_MIN);
+                if ((rb_imp >> row) & 1) {
+                    best = mk >> (RW == 32 ? 5 : 4);
+                    bl = RW - 1 - (mk & (RW - 1));
+                    if (rl == bl) {
+                        wi = R;
+                        wg = goe;
+                        wd = d;
+                    }
+                }
+            }
+            const uint32_t rb_cont = rw_bits<RW>(__ballot(live && bound > best));
+            const uint32_t rb_edge = rw_bits<RW>(__ballot(live && (rl == 0 || rl == RW - 1)));
+            const bool cont = ((rb_live & rb_cont) >> row) & 1;
+            if (!cont || d >= DMAX) act = back ? A_LDONE : A_RDONE;
+            else if ((rb_edge >> row) & 1) act = A_ABORT;
+        }
+    }
+    if (rl == 0 && P.counters) {
+        atomicAdd(&P.counters[0], (unsigned long long)steps);
+        atomicAdd(&P.counters[1], (unsigned long long)exts);
+        atomicAdd(&P.counters[2], (unsigned long long)ncands);
+        atomicAdd(&P.counters[3], (unsigned long long)nover);
+    }
+}
+
+// ------------------------------------------------------------------------
 // (gene, sample) groups
 // ------------------------------------------------------------------------
 
@@ -845,6 +1285,33 @@ void launch_extend(bool amb, const Db &db, const ExtParams &P, hipStream_t st)
     ExtParams W = P;
     W.defer = nullptr;
     const uint64_t blocks = 256ull * 8;
+    if (amb)
+        hipLaunchKernelGGL(extend_kernel<true>, dim3((unsigned)blocks), dim3(EBLOCK), 0, st, db, W);
+    else
+        hipLaunchKernelGGL(extend_kernel<false>, dim3((unsigned)blocks), dim3(EBLOCK), 0, st, db, W);
+}
+
+// Row kernel over all candidates, then extend_kernel over the ones it deferred
+// (sub-band overflow, or transcripts longer than the row staging slot). The
+// deferred count stays on the device: the list launch reads it.
+void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_width, hipStream_t st)
+{
+    if (P.n_cand == 0) return;
+    ExtParams W = P;
+    const int rw = row_width == 16 ? 16 : 32;
+    const size_t lds = (size_t)(EBLOCK / rw) * (amb ? 4 : 2) * (size_t)P.dsw * 8;
+    const uint64_t blocks = 256ull * 8;
+    if (rw == 16) {
+        if (amb)
+            hipLaunchKernelGGL((extend_rows_kernel<true, 16>), dim3((unsigned)blocks), dim3(EBLOCK), lds, st, db, W);
+        else
+            hipLaunchKernelGGL((extend_rows_kernel<false, 16>), dim3((unsigned)blocks), dim3(EBLOCK), lds, st, db, W);
+    } else {
+        if (amb)
+            hipLaunchKernelGGL((extend_rows_kernel<true, 32>), dim3((unsigned)blocks), dim3(EBLOCK), lds, st, db, W);
+        else
+            hipLaunchKernelGGL((extend_rows_kernel<false, 32>), dim3((unsigned)blocks), dim3(EBLOCK), lds, st, db, W);
+    }
     if (amb)
         hipLaunchKernelGGL(extend_kernel<true>, dim3((unsigned)blocks), dim3(EBLOCK), 0, st, db, W);
     else

@@ -28,6 +28,7 @@ void launch_kmer_fill(bool, const TxInfo *, uint32_t, const uint64_t *, const ui
 void launch_bucket_fill(const uint64_t *, uint64_t, int, uint32_t *, hipStream_t);
 void launch_seed(bool, const Db &, const Index &, const SeedParams &, hipStream_t);
 void launch_extend(bool, const Db &, const ExtParams &, hipStream_t);
+void launch_extend_rows(bool, const Db &, const ExtParams &, int, hipStream_t);
 void launch_group(const GroupParams &, int, hipStream_t);
 
 void launch_rbh(const RbhParams &, int, hipStream_t);
@@ -831,11 +832,16 @@ static int do_align(rc_engine *e)
         X.ovf_count = e->d_count.p;
         X.status = e->d_status.p;
         X.counters = e->d_count.p + 1;
-        X.dsw = (std::min(e->max_len, DSTAGE_MAX) >> 5) + 3;
+        X.dsw = ((std::min(e->max_len, DSTAGE_MAX) + 32 + 31) >> 5) + 4;   // row staging slot (u64 words)
         X.defer = e->d_defer.p;
         X.defer_count = e->d_count.p + 6;
         HIPCHK(hipEventRecord(e->ev[10], e->st));
-        launch_extend(e->has_amb, db, X, e->st);
+        {
+            // sub-band row width of the extension (16 or 32 diagonals); RC_ROW_WIDTH overrides
+            const char *rwv = getenv("RC_ROW_WIDTH");
+            const int rw = rwv ? atoi(rwv) : 32;
+            launch_extend_rows(e->has_amb, db, X, rw, e->st);
+        }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e->ev[11], e->st));
         unsigned long long ovn = 0, ctr[6] = {0, 0, 0, 0, 0, 0};
@@ -846,7 +852,7 @@ static int do_align(rc_engine *e)
         HIPCHK(hipStreamSynchronize(e->st));
         e->tm.ext_steps = (double)ctr[0];
         e->tm.ext_calls = (double)ctr[1];
-        e->tm.ext_fullband = (double)ctr[4];
+        e->tm.ext_fullband = (double)ctr[3];
         e->tm.ext_deferred = (double)ctr[5];
         if (!(status & 1u)) break;
         e->ovf_cap = ovn * 5 / 4 + 1024;
