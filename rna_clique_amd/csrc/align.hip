@@ -835,7 +835,9 @@ __global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db d
     int *meta = rmeta[rs];
     const uint64_t total = db.total;
     const uint64_t nrows = (uint64_t)gridDim.x * RROWS;
-    uint64_t li = (uint64_t)blockIdx.x * RROWS + rs;
+    // candidates: static round robin (chunk 0) or chunks from a global counter
+    const int chunk = P.chunk;
+    uint64_t li = chunk ? 0 : (uint64_t)blockIdx.x * RROWS + rs, lend = 0;
     int shard = 0;
     const int X = P.xdrop;
 
@@ -871,6 +873,12 @@ __global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db d
         // ---------------- transitions ----------------
         while (act != A_STEP && act != A_DONE) {
             if (act == A_FETCH) {
+                if (chunk && li >= lend) {
+                    unsigned long long b = 0;
+                    if (rl == 0) b = atomicAdd(P.work, (unsigned long long)chunk);
+                    li = (uint64_t)__shfl((long long)b, RW * row);
+                    lend = li + (uint64_t)chunk;
+                }
                 if (li >= P.n_cand) {
                     act = A_DONE;
                     continue;
@@ -885,7 +893,7 @@ __global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db d
                         const unsigned long long di = atomicAdd(P.defer_count, 1ull);
                         P.defer[di] = (uint32_t)ci;
                     }
-                    li += nrows;
+                    li += chunk ? 1 : nrows;
                     continue;
                 }
                 const uint64_t q0 = cd.strand ? total - qt.start - (uint64_t)Lq : qt.start;
@@ -983,7 +991,7 @@ __global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db d
                         P.cand_nh[ci] = (uint8_t)nout;
                         P.cand_ovf[ci] = obase;
                     }
-                    li += nrows;
+                    li += chunk ? 1 : nrows;
                     act = A_FETCH;
                     continue;
                 }
@@ -1071,7 +1079,7 @@ __global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db d
                     P.defer[di] = (uint32_t)meta[RM_CLO];
                 }
                 nover++;
-                li += nrows;
+                li += chunk ? 1 : nrows;
                 act = A_FETCH;
             }
         }
@@ -1294,28 +1302,47 @@ void launch_extend(bool amb, const Db &db, const ExtParams &P, hipStream_t st)
 // Row kernel over all candidates, then extend_kernel over the ones it deferred
 // (sub-band overflow, or transcripts longer than the row staging slot). The
 // deferred count stays on the device: the list launch reads it.
+// One resident wave per SIMD slot: a grid past the resident capacity leaves a
+// partial second round of waves (static per-row work runs at low occupancy).
+template <typename K>
+static unsigned resident_blocks(K kernel, size_t lds)
+{
+    int dev = 0, cus = 256, per_cu = 1;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, EBLOCK, lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    return (unsigned)(cus * per_cu);
+}
+
+// Row kernel over all candidates, then extend_kernel over the ones it deferred
+// (sub-band overflow, or transcripts longer than the row staging slot). The
+// deferred count stays on the device: the list launch reads it.
 void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_width, hipStream_t st)
 {
     if (P.n_cand == 0) return;
     ExtParams W = P;
     const int rw = row_width == 16 ? 16 : 32;
     const size_t lds = (size_t)(EBLOCK / rw) * (amb ? 4 : 2) * (size_t)P.dsw * 8;
-    const uint64_t blocks = 256ull * 8;
+#define RC_LAUNCH_ROWS(A, RWV)                                                                            \
+    do {                                                                                                  \
+        auto kern = extend_rows_kernel<A, RWV>;                                                           \
+        hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, lds)), dim3(EBLOCK), lds, st, db, W);         \
+    } while (0)
     if (rw == 16) {
-        if (amb)
-            hipLaunchKernelGGL((extend_rows_kernel<true, 16>), dim3((unsigned)blocks), dim3(EBLOCK), lds, st, db, W);
-        else
-            hipLaunchKernelGGL((extend_rows_kernel<false, 16>), dim3((unsigned)blocks), dim3(EBLOCK), lds, st, db, W);
+        if (amb) RC_LAUNCH_ROWS(true, 16); else RC_LAUNCH_ROWS(false, 16);
     } else {
-        if (amb)
-            hipLaunchKernelGGL((extend_rows_kernel<true, 32>), dim3((unsigned)blocks), dim3(EBLOCK), lds, st, db, W);
-        else
-            hipLaunchKernelGGL((extend_rows_kernel<false, 32>), dim3((unsigned)blocks), dim3(EBLOCK), lds, st, db, W);
+        if (amb) RC_LAUNCH_ROWS(true, 32); else RC_LAUNCH_ROWS(false, 32);
     }
-    if (amb)
-        hipLaunchKernelGGL(extend_kernel<true>, dim3((unsigned)blocks), dim3(EBLOCK), 0, st, db, W);
-    else
-        hipLaunchKernelGGL(extend_kernel<false>, dim3((unsigned)blocks), dim3(EBLOCK), 0, st, db, W);
+#undef RC_LAUNCH_ROWS
+    if (amb) {
+        auto kern = extend_kernel<true>;
+        hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W);
+    } else {
+        auto kern = extend_kernel<false>;
+        hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W);
+    }
 }
 
 void launch_group(const GroupParams &P, int pass, hipStream_t st)

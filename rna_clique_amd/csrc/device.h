@@ -133,6 +133,8 @@ struct ExtParams {
     // two-candidate kernel: staging slot (u64 words per sequence) and the
     // candidates it defers to the one-wave kernel (transcripts past the slot)
     int32_t dsw;
+    int32_t chunk;                // row kernel: candidates per work grab (0: static round robin)
+    unsigned long long *work;     // row kernel: work counter
     uint32_t *defer;
     unsigned long long *defer_count;
 };

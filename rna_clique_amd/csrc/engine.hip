@@ -835,6 +835,11 @@ static int do_align(rc_engine *e)
         X.dsw = ((std::min(e->max_len, DSTAGE_MAX) + 32 + 31) >> 5) + 4;   // row staging slot (u64 words)
         X.defer = e->d_defer.p;
         X.defer_count = e->d_count.p + 6;
+        X.work = e->d_count.p + 7;
+        {
+            const char *cv = getenv("RC_ROW_CHUNK");
+            X.chunk = cv ? atoi(cv) : 4;
+        }
         HIPCHK(hipEventRecord(e->ev[10], e->st));
         {
             // sub-band row width of the extension (16 or 32 diagonals); RC_ROW_WIDTH overrides
