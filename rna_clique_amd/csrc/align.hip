@@ -15,6 +15,7 @@
 #include "device.h"
 
 #include <climits>
+#include <cstdlib>
 
 namespace rcg {
 
@@ -701,15 +702,17 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
 //
 // The greedy frontier of a near-identical transcript pair stays within a few
 // diagonals of the seed's, so most of the 64-diagonal band of extend_kernel is
-// dead lanes. Here each 16-lane row of the wave runs its own candidate over
-// the sub-band of diagonals [-8, 7] (row lane rl <-> diagonal rl - 8). The
-// sub-band computes exactly what the full band computes as long as no live
-// diagonal reaches its edge lanes (a diagonal outside can only be entered
-// from a live neighbour); the first time an edge lane is live while the
-// extension continues, the candidate is handed to extend_kernel (list mode)
-// whole. Rows advance independently (their own seeds, extensions,
-// candidates): a row that finishes an extension does its bookkeeping while
-// the other rows wait one transition, then all rows step together.
+// dead lanes. Here each row of RW lanes (16: one DPP row, 32: half a wave)
+// runs its own candidate over the sub-band of diagonals [-RW/2, RW/2 - 1]
+// (row lane rl <-> diagonal rl - RW/2). The sub-band computes exactly what the
+// full band computes as long as no live diagonal reaches its edge lanes (a
+// diagonal outside can only be entered from a live neighbour); the first time
+// an edge lane is live while the extension continues, the candidate is handed
+// to extend_kernel (list mode) whole. Rows advance independently (their own
+// seeds, extensions, candidates): a row that finishes an extension does its
+// bookkeeping while the other rows wait one transition, then all rows step
+// together. Every extension walks forward: a left extension runs on reversed
+// copies of both transcripts staged next to the forward ones.
 
 #ifndef ROW_MIN_WAVES
 #define ROW_MIN_WAVES 6
@@ -725,7 +728,6 @@ __device__ __forceinline__ int row_max(int v)
     return v;
 }
 
-// Sub-band rows of RW = 16 lanes (one DPP row) or 32 lanes (half a wave).
 // lane rl <- rl - 1 inside the row (rl 0 gets `edge`); FIX: also at the
 // half-wave seam (needed for the frontier, not for values only read where
 // the frontier neighbour is live)
@@ -778,27 +780,33 @@ __device__ __forceinline__ uint32_t rw_mask(uint64_t m, int row)
     return (uint32_t)(m >> (RW * row)) & (RW == 32 ? 0xFFFFFFFFu : 0xFFFFu);
 }
 
-// Matching bases from (pa, pb) forward, or from (pa - 1, pb - 1) backwards, at
-// most maxn; positions index one LDS dword array (16 bases per dword); masks
-// (AMB) sit `moff` bases after the sequences.
+// Matching bases from (pa, pb) forward, at most maxn; positions index one LDS
+// dword array (16 bases per dword); masks (AMB) sit `moff` bases further on.
 template <bool AMB>
-__device__ __forceinline__ int slide_dir(const uint32_t *S, uint32_t pa, uint32_t pb, int maxn, bool back,
-                                         uint32_t moff)
+__device__ __forceinline__ int slide_fwd(const uint32_t *S, uint32_t pa, uint32_t pb, int maxn, uint32_t moff)
 {
     int n = 0;
     while (n < maxn) {
-        const uint32_t qa = back ? pa - (uint32_t)(n + 32) : pa + (uint32_t)n;
-        const uint32_t qb = back ? pb - (uint32_t)(n + 32) : pb + (uint32_t)n;
-        uint64_t x = win3(S, qa) ^ win3(S, qb);
-        if (AMB) x |= win3(S, qa + moff) | win3(S, qb + moff);
+        uint64_t x = win3(S, pa + (uint32_t)n) ^ win3(S, pb + (uint32_t)n);
+        if (AMB) x |= win3(S, pa + (uint32_t)n + moff) | win3(S, pb + (uint32_t)n + moff);
         if (x == 0) {
             n += 32;
             continue;
         }
-        n += (back ? __builtin_clzll(x) : __builtin_ctzll(x)) >> 1;
+        n += __builtin_ctzll(x) >> 1;
         return n < maxn ? n : maxn;
     }
     return maxn > 0 ? maxn : 0;
+}
+
+// 32 bases at a signed base position of a packed global array (the arrays
+// carry two zero words in front, so p >= -64 stays in bounds)
+__device__ __forceinline__ uint64_t win_s(const uint64_t *__restrict__ a, int64_t p)
+{
+    const int64_t w = p >> 5;
+    const unsigned sh = (unsigned)(p & 31) * 2u;
+    const uint64_t lo = a[w], hi = a[w + 1];
+    return (lo >> sh) | ((hi << 1) << (63u - sh));
 }
 
 // per-row bookkeeping in LDS
@@ -808,18 +816,21 @@ enum { HB_QA, HB_QB, HB_SA, HB_SB, HB_SC, HB_D, HB_G, HB_O, HB_NI, HB_N };
 // row actions
 enum { A_FETCH, A_SEED, A_RDONE, A_LDONE, A_ABORT, A_STEP, A_DONE };
 
-template <bool AMB, int RW>
-__global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db db, ExtParams P)
+template <bool AMB, int RW, int MINW>
+__global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtParams P)
 {
     constexpr int RROWS = EBLOCK / RW;   // rows per block
     constexpr int RC0 = RW / 2;          // row lane of diagonal 0
-    constexpr int NA = AMB ? 4 : 2;
+    constexpr int NA = AMB ? 8 : 4;      // staged arrays per row: Q, T, Qrev, Trev (+ their masks)
     constexpr int EBIT = 26, OBIT = 13;
     constexpr int GMASK = 8191;
     extern __shared__ uint64_t rstg[];                    // [RROWS][NA][sw]
     __shared__ unsigned long long sprefix[NSHARD + 1];
     __shared__ int rmeta[RROWS][RM_N];
     __shared__ int rbox[RROWS][MAX_HSP][HB_N];
+    __shared__ int rseed[RROWS][3][RW];                   // seed chunk of each row: x, y, len
+    __shared__ unsigned int rcnt[4];                      // extensions, candidates, overflows
+    if (threadIdx.x < 4) rcnt[threadIdx.x] = 0;
     for (int i = threadIdx.x; i <= NSHARD; i += EBLOCK) sprefix[i] = P.shard_prefix[i];
     __syncthreads();
 
@@ -829,15 +840,16 @@ __global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db d
     const int sw = P.dsw;                                 // u64 words per staged sequence
     const int smax = (sw - 4) * 32;                       // longest staged transcript + SPAD
     const uint32_t *S = reinterpret_cast<const uint32_t *>(rstg);
-    uint64_t *qst = rstg + (size_t)rs * NA * sw, *tst = qst + sw;
-    const uint32_t qbase = (uint32_t)(rs * NA * sw) * 32u + SPAD, tbase = qbase + 32u * (uint32_t)sw;
-    const uint32_t moff = 64u * (uint32_t)sw;
+    uint64_t *stg = rstg + (size_t)rs * NA * sw;          // Q, T, Qr, Tr, [QM, TM, QMr, TMr]
+    const uint32_t bq = (uint32_t)(rs * NA * sw) * 32u + SPAD;   // base position of Q[0]
+    const uint32_t bt = bq + 32u * (uint32_t)sw, bqr = bt + 32u * (uint32_t)sw, btr = bqr + 32u * (uint32_t)sw;
+    const uint32_t moff = 128u * (uint32_t)sw;
     int *meta = rmeta[rs];
     const uint64_t total = db.total;
-    const uint64_t nrows = (uint64_t)gridDim.x * RROWS;
+    const uint32_t nrows = gridDim.x * RROWS;
     // candidates: static round robin (chunk 0) or chunks from a global counter
     const int chunk = P.chunk;
-    uint64_t li = chunk ? 0 : (uint64_t)blockIdx.x * RROWS + rs, lend = 0;
+    uint32_t li = chunk ? 0u : blockIdx.x * RROWS + rs, lend = 0;   // candidate counts < 2^32
     int shard = 0;
     const int X = P.xdrop;
 
@@ -846,14 +858,14 @@ __global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db d
     int R = -1, goe = 0, wi = 0, wg = 0, wd = 0, best = 0, bl = RC0, d = 0;
     uint32_t pa = 0, pb = 0;
     int alen = 0, blen = 0;
-    bool back = false;
     // candidate state (row-uniform) and the seed chunk (lane rl: seed cb + rl)
-    int ns = 0, nh = 0, si = 0, cb = -1, sx = 0, sy = 0, sl = 0;
-    uint32_t steps = 0, exts = 0, ncands = 0, nover = 0;
+    int ns = 0, nh = 0, si = 0, cb = -1;
+    int *sxa = rseed[rs][0], *sya = rseed[rs][1], *sla = rseed[rs][2];
+    unsigned long long steps = 0;                         // row steps (wave-uniform count)
 
     auto ext_init = [&](int done_act) {
         int r0 = 0;
-        if (rl == RC0) r0 = slide_dir<AMB>(S, pa, pb, min(alen, blen), back, moff);
+        if (rl == RC0) r0 = slide_fwd<AMB>(S, pa, pb, min(alen, blen), moff);
         r0 = __shfl(r0, RW * row + RC0);
         best = 2 * r0;
         bl = RC0;
@@ -865,8 +877,21 @@ __global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db d
         R = rl == RC0 ? r0 : -1;
         goe = 0;
         d = 0;
-        exts++;
+        if (rl == 0) atomicAdd(&rcnt[0], 1u);
         act = (min(alen, blen) - r0 <= 0) ? done_act : A_STEP;
+    };
+    auto stage_fwd = [&](uint64_t *dst, const uint64_t *src, uint64_t p0, int L) {
+        const int nw = (L >> 5) + 3;
+        for (int w = rl; w < nw; w += RW) dst[w] = w ? win<uint64_t>(src, p0 + 32 * (uint64_t)(w - 1)) : 0ull;
+    };
+    // reversed copy: word w >= 1 holds reversed bases 32 (w - 1) .. 32 w - 1,
+    // i.e. bases L - 32 w .. L - 32 (w - 1) - 1 in reverse order
+    auto stage_rev = [&](uint64_t *dst, const uint64_t *src, uint64_t p0, int L) {
+        const int nw = (L >> 5) + 3;
+        for (int w = rl; w < nw; w += RW) {
+            const int64_t gp = (int64_t)p0 + L - 32 * (int64_t)w;
+            dst[w] = (w && gp >= -64) ? rev2(win_s(src, gp)) : 0ull;
+        }
     };
 
     for (;;) {
@@ -876,8 +901,9 @@ __global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db d
                 if (chunk && li >= lend) {
                     unsigned long long b = 0;
                     if (rl == 0) b = atomicAdd(P.work, (unsigned long long)chunk);
-                    li = (uint64_t)__shfl((long long)b, RW * row);
-                    lend = li + (uint64_t)chunk;
+                    b = (unsigned long long)__shfl((long long)b, RW * row);
+                    li = b < P.n_cand ? (uint32_t)b : (uint32_t)P.n_cand;
+                    lend = li + (uint32_t)chunk;
                 }
                 if (li >= P.n_cand) {
                     act = A_DONE;
@@ -893,18 +919,21 @@ __global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db d
                         const unsigned long long di = atomicAdd(P.defer_count, 1ull);
                         P.defer[di] = (uint32_t)ci;
                     }
-                    li += chunk ? 1 : nrows;
+                    li += chunk ? 1u : nrows;
                     continue;
                 }
                 const uint64_t q0 = cd.strand ? total - qt.start - (uint64_t)Lq : qt.start;
                 const uint64_t *QA = cd.strand ? db.RC : db.F;
-                const int nwq = (Lq >> 5) + 3, nwt = (Lt >> 5) + 3;
-                for (int w = rl; w < nwq; w += RW) qst[w] = w ? win<uint64_t>(QA, q0 + 32 * (uint64_t)(w - 1)) : 0ull;
-                for (int w = rl; w < nwt; w += RW) tst[w] = w ? win<uint64_t>(db.F, st.start + 32 * (uint64_t)(w - 1)) : 0ull;
+                stage_fwd(stg, QA, q0, Lq);
+                stage_fwd(stg + sw, db.F, st.start, Lt);
+                stage_rev(stg + 2 * sw, QA, q0, Lq);
+                stage_rev(stg + 3 * sw, db.F, st.start, Lt);
                 if (AMB) {
                     const uint64_t *QM = cd.strand ? db.ARC : db.AF;
-                    for (int w = rl; w < nwq; w += RW) qst[2 * sw + w] = w ? win<uint64_t>(QM, q0 + 32 * (uint64_t)(w - 1)) : 0ull;
-                    for (int w = rl; w < nwt; w += RW) tst[2 * sw + w] = w ? win<uint64_t>(db.AF, st.start + 32 * (uint64_t)(w - 1)) : 0ull;
+                    stage_fwd(stg + 4 * sw, QM, q0, Lq);
+                    stage_fwd(stg + 5 * sw, db.AF, st.start, Lt);
+                    stage_rev(stg + 6 * sw, QM, q0, Lq);
+                    stage_rev(stg + 7 * sw, db.AF, st.start, Lt);
                 }
                 if (rl == 0) {
                     meta[RM_CLO] = (int)(uint32_t)ci;
@@ -922,7 +951,7 @@ __global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db d
                 nh = 0;
                 si = 0;
                 cb = -1;
-                ncands++;
+                if (rl == 0) atomicAdd(&rcnt[1], 1u);
                 act = A_SEED;
             } else if (act == A_SEED) {
                 if (nh >= MAX_HSP || si >= ns) {
@@ -991,22 +1020,25 @@ __global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db d
                         P.cand_nh[ci] = (uint8_t)nout;
                         P.cand_ovf[ci] = obase;
                     }
-                    li += chunk ? 1 : nrows;
+                    li += chunk ? 1u : nrows;
                     act = A_FETCH;
                     continue;
                 }
-                // next seed not inside a kept box, searched 16 at a time
+                // next seed not inside a kept box, searched RW at a time
                 const int c0 = si & ~(RW - 1);
                 if (c0 != cb) {
                     cb = c0;
                     if (cb + rl < ns) {
                         const GSeed g = P.seeds[(uint32_t)meta[RM_SOFF] + (uint32_t)(cb + rl)];
-                        sx = (int)g.x;
-                        sy = (int)g.y;
-                        sl = (int)g.len;
+                        sxa[rl] = (int)g.x;
+                        sya[rl] = (int)g.y;
+                        sla[rl] = (int)g.len;
                     }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
                 }
                 const int idx = cb + rl;
+                const int sx = sxa[rl], sy = sya[rl], sl = sla[rl];
                 bool contained = false;
                 for (int j = 0; j < nh; j++) {
                     const int *hj = rbox[rs][j];
@@ -1018,7 +1050,7 @@ __global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db d
                     continue;
                 }
                 const int f = __builtin_ctz(m);
-                const int x = __shfl(sx, RW * row + f), y = __shfl(sy, RW * row + f), len = __shfl(sl, RW * row + f);
+                const int x = sxa[f], y = sya[f], len = sla[f];
                 si = cb + f + 1;
                 if (rl == 0) {
                     meta[RM_X] = x;
@@ -1026,11 +1058,10 @@ __global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db d
                     meta[RM_LEN] = len;
                 }
                 const int Lq = meta[RM_LQ], Lt = meta[RM_LT];
-                pa = qbase + (uint32_t)(x + len);
+                pa = bq + (uint32_t)(x + len);
                 alen = Lq - (x + len);
-                pb = tbase + (uint32_t)(y + len);
+                pb = bt + (uint32_t)(y + len);
                 blen = Lt - (y + len);
-                back = false;
                 ext_init(A_RDONE);
             } else if (act == A_RDONE || act == A_LDONE) {
                 const int src = RW * row + bl;
@@ -1045,11 +1076,13 @@ __global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db d
                         meta[RM_RD] = ed;
                         meta[RM_RGO] = ego;
                     }
-                    pa = qbase + (uint32_t)x;
+                    // left extension: forward from reversed position L - x
+                    // (= base x - 1) of the reversed copies
+                    const int Lq = meta[RM_LQ], Lt = meta[RM_LT];
+                    pa = bqr + (uint32_t)(Lq - x);
                     alen = x;
-                    pb = tbase + (uint32_t)y;
+                    pb = btr + (uint32_t)(Lt - y);
                     blen = y;
-                    back = true;
                     ext_init(A_LDONE);
                 } else {
                     const int rsc = meta[RM_RSC], ri = meta[RM_RI], rj = meta[RM_RJ], rd = meta[RM_RD];
@@ -1078,33 +1111,36 @@ __global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db d
                     const unsigned long long di = atomicAdd(P.defer_count, 1ull);
                     P.defer[di] = (uint32_t)meta[RM_CLO];
                 }
-                nover++;
-                li += chunk ? 1 : nrows;
+                if (rl == 0) atomicAdd(&rcnt[2], 1u);
+                li += chunk ? 1u : nrows;
                 act = A_FETCH;
             }
         }
         const bool ext = act == A_STEP;
-        if (!__ballot(ext)) break;
+        const uint64_t mext = __ballot(ext);
+        if (!mext) break;
+        steps += (unsigned long long)__builtin_popcount(rw_bits<RW>(mext));
         // ---------------- one greedy step of every extending row ----------------
         if (ext) {
-            steps++;
             d++;
             const int Rl = rw_from_lower<RW, true>(R, -1, rl), Rr = rw_from_upper<RW, true>(R, -1, rl);
             const int gl = rw_from_lower<RW, false>(goe, 0, rl), gr = rw_from_upper<RW, false>(goe, 0, rl);
+            // candidates; ties prefer mismatch, then insertion, then deletion
             const int cm = (R >= 0 && R < alen && R - k < blen) ? R + 1 : -1;
             const int cil = (Rl >= 0 && Rl < alen) ? Rl + 1 : -1;
             const int cd = (Rr >= 0 && Rr - (k + 1) < blen) ? Rr : -1;
             int ni = max(max(cm, cil), cd);
             const bool fm = ni >= 0 && cm == ni, fi = !fm && cil == ni;
-            const int gi = (gl & ~(3 << EBIT)) + 1 + ((((gl >> EBIT) & 3) == 1) ? 0 : (1 << OBIT)) + (1 << EBIT);
-            const int gd = (gr & ~(3 << EBIT)) + 1 + ((((gr >> EBIT) & 3) == 2) ? 0 : (1 << OBIT)) + (2 << EBIT);
-            int ng = fm ? (goe & ~(3 << EBIT)) : (fi ? gi : gd);
+            // gap state of the chosen move: G | O << 13 | E << 26 (E: 1 insertion, 2 deletion)
+            const int src = fm ? goe : (fi ? gl : gr);
+            const int e = fm ? 0 : (fi ? 1 : 2);
+            const int pe = (src >> EBIT) & 3;
+            int ng = (src & ~(3 << EBIT)) + (fm ? 0 : 1 + (pe == e ? 0 : (1 << OBIT)) + (e << EBIT));
             int score = INT_MIN, bound = INT_MIN;
             if (ni >= 0) {
                 const int ja = ni - k;
                 const int m = min(alen - ni, blen - ja);
-                const int s = slide_dir<AMB>(S, back ? pa - (uint32_t)ni : pa + (uint32_t)ni,
-                                             back ? pb - (uint32_t)ja : pb + (uint32_t)ja, m, back, moff);
+                const int s = slide_fwd<AMB>(S, pa + (uint32_t)ni, pb + (uint32_t)ja, m, moff);
                 ni += s;
                 if (s > 0) ng &= ~(3 << EBIT);
                 score = 2 * ni - k - 6 * d;
@@ -1114,7 +1150,6 @@ __global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db d
             R = ni;
             goe = ng;
             const bool live = ni >= 0;
-            const uint32_t rb_live = rw_bits<RW>(__ballot(live));
             const uint32_t rb_imp = rw_bits<RW>(__ballot(live && score > best));
             if (rb_imp) {
                 const int mk = rw_max<RW>(live ? score * RW + (RW - 1 - rl) : INT_MIN);
@@ -1128,19 +1163,17 @@ __global__ __launch_bounds__(EBLOCK, ROW_MIN_WAVES) void extend_rows_kernel(Db d
                     }
                 }
             }
+            // bound >= score, so a lane that can still beat best is live
             const uint32_t rb_cont = rw_bits<RW>(__ballot(live && bound > best));
             const uint32_t rb_edge = rw_bits<RW>(__ballot(live && (rl == 0 || rl == RW - 1)));
-            const bool cont = ((rb_live & rb_cont) >> row) & 1;
-            if (!cont || d >= DMAX) act = back ? A_LDONE : A_RDONE;
+            const bool cont = (rb_cont >> row) & 1;
+            if (!cont || d >= DMAX) act = pa >= bqr ? A_LDONE : A_RDONE;
             else if ((rb_edge >> row) & 1) act = A_ABORT;
         }
     }
-    if (rl == 0 && P.counters) {
-        atomicAdd(&P.counters[0], (unsigned long long)steps);
-        atomicAdd(&P.counters[1], (unsigned long long)exts);
-        atomicAdd(&P.counters[2], (unsigned long long)ncands);
-        atomicAdd(&P.counters[3], (unsigned long long)nover);
-    }
+    if (lane == 0 && P.counters) atomicAdd(&P.counters[0], steps);
+    __syncthreads();
+    if (threadIdx.x < 3 && P.counters) atomicAdd(&P.counters[1 + threadIdx.x], (unsigned long long)rcnt[threadIdx.x]);
 }
 
 // ------------------------------------------------------------------------
@@ -1324,16 +1357,20 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
     if (P.n_cand == 0) return;
     ExtParams W = P;
     const int rw = row_width == 16 ? 16 : 32;
-    const size_t lds = (size_t)(EBLOCK / rw) * (amb ? 4 : 2) * (size_t)P.dsw * 8;
-#define RC_LAUNCH_ROWS(A, RWV)                                                                            \
+    const size_t lds = (size_t)(EBLOCK / rw) * (amb ? 8 : 4) * (size_t)P.dsw * 8;
+#define RC_LAUNCH_ROWS(A, RWV, MW)                                                                        \
     do {                                                                                                  \
-        auto kern = extend_rows_kernel<A, RWV>;                                                           \
+        auto kern = extend_rows_kernel<A, RWV, MW>;                                                       \
         hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, lds)), dim3(EBLOCK), lds, st, db, W);         \
     } while (0)
+    const char *mwv = getenv("RC_ROW_WAVES");
+    const int mw = mwv ? atoi(mwv) : ROW_MIN_WAVES;
     if (rw == 16) {
-        if (amb) RC_LAUNCH_ROWS(true, 16); else RC_LAUNCH_ROWS(false, 16);
+        if (amb) RC_LAUNCH_ROWS(true, 16, ROW_MIN_WAVES); else RC_LAUNCH_ROWS(false, 16, ROW_MIN_WAVES);
+    } else if (mw == 5) {
+        if (amb) RC_LAUNCH_ROWS(true, 32, 5); else RC_LAUNCH_ROWS(false, 32, 5);
     } else {
-        if (amb) RC_LAUNCH_ROWS(true, 32); else RC_LAUNCH_ROWS(false, 32);
+        if (amb) RC_LAUNCH_ROWS(true, 32, ROW_MIN_WAVES); else RC_LAUNCH_ROWS(false, 32, ROW_MIN_WAVES);
     }
 #undef RC_LAUNCH_ROWS
     if (amb) {
