@@ -26,7 +26,8 @@ def build_native(force=False, verbose=False):
     """Compile the HIP engine into rna_clique_amd/librcgpu.so."""
     if not force and not _stale():
         return OUT
-    cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", *SOURCES]
+    extra = os.environ.get("RC_EXTRA_FLAGS", "").split()
+    cmd = [HIPCC, *FLAGS, *extra, "-o", OUT + ".tmp", *SOURCES]
     res = subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"hipcc failed:\n{' '.join(cmd)}\n{res.stderr[-8000:]}")

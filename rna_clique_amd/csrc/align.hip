@@ -780,6 +780,27 @@ __device__ __forceinline__ uint32_t rw_mask(uint64_t m, int row)
     return (uint32_t)(m >> (RW * row)) & (RW == 32 ? 0xFFFFFFFFu : 0xFFFFu);
 }
 
+// spread a wave mask to whole rows: every lane of a row with a set lane (scalar work)
+template <int RW>
+__device__ __forceinline__ uint64_t rw_spread(uint64_t m)
+{
+    if constexpr (RW == 32) {
+        return ((m & 0xFFFFFFFFull) ? 0xFFFFFFFFull : 0ull) | ((m & 0xFFFFFFFF00000000ull) ? 0xFFFFFFFF00000000ull : 0ull);
+    } else {
+        uint64_t r = 0;
+        for (int i = 0; i < 4; i++)
+            if ((m >> (16 * i)) & 0xFFFFull) r |= 0xFFFFull << (16 * i);
+        return r;
+    }
+}
+// lane in mask ? a : b, one v_cndmask with the mask as the SGPR-pair condition
+__device__ __forceinline__ int lane_sel(uint64_t m, int a, int b)
+{
+    int r;
+    asm("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
+
 // Matching bases from (pa, pb) forward, at most maxn; positions index one LDS
 // dword array (16 bases per dword); masks (AMB) sit `moff` bases further on.
 template <bool AMB>
@@ -814,7 +835,8 @@ enum { RM_CLO, RM_CHI, RM_QTX, RM_STX, RM_LQ, RM_LT, RM_STRAND, RM_SOFF, RM_X, R
        RM_RSC, RM_RI, RM_RJ, RM_RD, RM_RGO, RM_N };
 enum { HB_QA, HB_QB, HB_SA, HB_SB, HB_SC, HB_D, HB_G, HB_O, HB_NI, HB_N };
 // row actions
-enum { A_FETCH, A_SEED, A_RDONE, A_LDONE, A_ABORT, A_STEP, A_DONE };
+// (transition actions < A_DONE; extending: A_STEP_R / A_STEP_L = their done action + 4)
+enum { A_FETCH, A_SEED, A_RDONE, A_LDONE, A_ABORT, A_DONE, A_STEP_R, A_STEP_L };
 
 template <bool AMB, int RW, int MINW>
 __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtParams P)
@@ -855,7 +877,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
 
     int act = A_FETCH;
     // extension state: frontier (R, gap state), winner record, row-uniform best
-    int R = -1, goe = 0, wi = 0, wg = 0, wd = 0, best = 0, bl = RC0, d = 0;
+    int R = -1, goe = 0, wi = 0, wg = 0, wd = 0, best = 0, bl = RC0, d6 = 0;   // d6 = 6 x greedy step
     uint32_t pa = 0, pb = 0;
     int alen = 0, blen = 0;
     // candidate state (row-uniform) and the seed chunk (lane rl: seed cb + rl)
@@ -876,9 +898,9 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
         }
         R = rl == RC0 ? r0 : -1;
         goe = 0;
-        d = 0;
+        d6 = 0;
         if (rl == 0) atomicAdd(&rcnt[0], 1u);
-        act = (min(alen, blen) - r0 <= 0) ? done_act : A_STEP;
+        act = (min(alen, blen) - r0 <= 0) ? done_act : done_act + (A_STEP_R - A_RDONE);
     };
     auto stage_fwd = [&](uint64_t *dst, const uint64_t *src, uint64_t p0, int L) {
         const int nw = (L >> 5) + 3;
@@ -894,9 +916,15 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
         }
     };
 
+#ifdef RC_ROW_TIMING
+    unsigned long long t_tr = 0, t_st = 0;
+#endif
     for (;;) {
+#ifdef RC_ROW_TIMING
+        const unsigned long long c0t = __builtin_readcyclecounter();
+#endif
         // ---------------- transitions ----------------
-        while (act != A_STEP && act != A_DONE) {
+        while (act < A_DONE) {
             if (act == A_FETCH) {
                 if (chunk && li >= lend) {
                     unsigned long long b = 0;
@@ -1065,7 +1093,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                 ext_init(A_RDONE);
             } else if (act == A_RDONE || act == A_LDONE) {
                 const int src = RW * row + bl;
-                const int ei = __shfl(wi, src), ed = __shfl(wd, src), ego = __shfl(wg, src);
+                const int ei = __shfl(wi, src), ed = __shfl(wd, src) / 6, ego = __shfl(wg, src);
                 const int ej = ei - (bl - RC0);
                 const int x = meta[RM_X], y = meta[RM_Y], len = meta[RM_LEN];
                 if (act == A_RDONE) {
@@ -1116,18 +1144,24 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                 act = A_FETCH;
             }
         }
-        const bool ext = act == A_STEP;
+#ifdef RC_ROW_TIMING
+        const unsigned long long c1t = __builtin_readcyclecounter();
+        t_tr += c1t - c0t;
+#endif
+        const bool ext = act >= A_STEP_R;
         const uint64_t mext = __ballot(ext);
         if (!mext) break;
         steps += (unsigned long long)__builtin_popcount(rw_bits<RW>(mext));
         // ---------------- one greedy step of every extending row ----------------
         if (ext) {
-            d++;
+            d6 += 6;
             const int Rl = rw_from_lower<RW, true>(R, -1, rl), Rr = rw_from_upper<RW, true>(R, -1, rl);
             const int gl = rw_from_lower<RW, false>(goe, 0, rl), gr = rw_from_upper<RW, false>(goe, 0, rl);
-            // candidates; ties prefer mismatch, then insertion, then deletion
-            const int cm = (R >= 0 && R < alen && R - k < blen) ? R + 1 : -1;
-            const int cil = (Rl >= 0 && Rl < alen) ? Rl + 1 : -1;
+            // candidates; ties prefer mismatch, then insertion, then deletion (a
+            // frontier value R >= 0 has j = R - k >= 0, so unsigned compares
+            // carry the lower bounds)
+            const int cm = ((uint32_t)R < (uint32_t)alen && (uint32_t)(R - k) < (uint32_t)blen) ? R + 1 : -1;
+            const int cil = ((uint32_t)Rl < (uint32_t)alen) ? Rl + 1 : -1;
             const int cd = (Rr >= 0 && Rr - (k + 1) < blen) ? Rr : -1;
             int ni = max(max(cm, cil), cd);
             const bool fm = ni >= 0 && cm == ni, fi = !fm && cil == ni;
@@ -1143,34 +1177,39 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                 const int s = slide_fwd<AMB>(S, pa + (uint32_t)ni, pb + (uint32_t)ja, m, moff);
                 ni += s;
                 if (s > 0) ng &= ~(3 << EBIT);
-                score = 2 * ni - k - 6 * d;
+                score = 2 * ni - k - d6;
                 if (score < best - X) ni = -1;
                 bound = score + 2 * (m - s);
             }
             R = ni;
             goe = ng;
             const bool live = ni >= 0;
-            const uint32_t rb_imp = rw_bits<RW>(__ballot(live && score > best));
-            if (rb_imp) {
+            // row-wide decisions as lane masks (scalar), applied with v_cndmask
+            const uint64_t mimp = rw_spread<RW>(__ballot(live && score > best));
+            if (mimp) {
                 const int mk = rw_max<RW>(live ? score * RW + (RW - 1 - rl) : INT_MIN);
-                if ((rb_imp >> row) & 1) {
-                    best = mk >> (RW == 32 ? 5 : 4);
-                    bl = RW - 1 - (mk & (RW - 1));
-                    if (rl == bl) {
-                        wi = R;
-                        wg = goe;
-                        wd = d;
-                    }
-                }
+                best = lane_sel(mimp, mk >> (RW == 32 ? 5 : 4), best);
+                bl = lane_sel(mimp, RW - 1 - (mk & (RW - 1)), bl);
+                const uint64_t mwin = mimp & __ballot(rl == bl);
+                wi = lane_sel(mwin, R, wi);
+                wg = lane_sel(mwin, goe, wg);
+                wd = lane_sel(mwin, d6, wd);
             }
             // bound >= score, so a lane that can still beat best is live
-            const uint32_t rb_cont = rw_bits<RW>(__ballot(live && bound > best));
-            const uint32_t rb_edge = rw_bits<RW>(__ballot(live && (rl == 0 || rl == RW - 1)));
-            const bool cont = (rb_cont >> row) & 1;
-            if (!cont || d >= DMAX) act = pa >= bqr ? A_LDONE : A_RDONE;
-            else if ((rb_edge >> row) & 1) act = A_ABORT;
+            const uint64_t mcont = rw_spread<RW>(__ballot(live && bound > best)) & __ballot(d6 < 6 * DMAX);
+            const uint64_t medge = rw_spread<RW>(__ballot(live && (rl == 0 || rl == RW - 1)));
+            act = lane_sel(mcont, lane_sel(medge, (int)A_ABORT, act), act - (A_STEP_R - A_RDONE));
         }
+#ifdef RC_ROW_TIMING
+        t_st += __builtin_readcyclecounter() - c1t;
+#endif
     }
+#ifdef RC_ROW_TIMING
+    if (lane == 0 && P.counters) {
+        atomicAdd(&P.counters[8], t_tr);
+        atomicAdd(&P.counters[9], t_st);
+    }
+#endif
     if (lane == 0 && P.counters) atomicAdd(&P.counters[0], steps);
     __syncthreads();
     if (threadIdx.x < 3 && P.counters) atomicAdd(&P.counters[1 + threadIdx.x], (unsigned long long)rcnt[threadIdx.x]);

@@ -548,7 +548,7 @@ static int upload(rc_engine *e)
     CHK(up(e->d_thr, thr));
     CHK(up(e->d_bits10, b10));
     CHK(e->d_status.ensure(4));
-    CHK(e->d_count.ensure(8));
+    CHK(e->d_count.ensure(16));
     HIPCHK(hipStreamSynchronize(e->st));
     int bits = 16;
     while (bits < 30 && (1ull << bits) < e->n_kpos) bits++;
@@ -812,7 +812,7 @@ static int do_align(rc_engine *e)
     for (int attempt = 0;; attempt++) {
         if (attempt == 4) return fail(RC_E_NOMEM, "HSP overflow buffer kept overflowing");
         CHK(e->d_ovf.ensure(e->ovf_cap));
-        HIPCHK(hipMemsetAsync(e->d_count.p, 0, 8 * sizeof(unsigned long long), e->st));
+        HIPCHK(hipMemsetAsync(e->d_count.p, 0, 16 * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
         ExtParams X;
         X.xdrop = e->o.xdrop_half;
@@ -849,7 +849,7 @@ static int do_align(rc_engine *e)
         }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e->ev[11], e->st));
-        unsigned long long ovn = 0, ctr[6] = {0, 0, 0, 0, 0, 0};
+        unsigned long long ovn = 0, ctr[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         unsigned int status = 0;
         HIPCHK(hipMemcpyAsync(&ovn, e->d_count.p, sizeof ovn, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipMemcpyAsync(ctr, e->d_count.p + 1, sizeof ctr, hipMemcpyDeviceToHost, e->st));
@@ -859,6 +859,8 @@ static int do_align(rc_engine *e)
         e->tm.ext_calls = (double)ctr[1];
         e->tm.ext_fullband = (double)ctr[3];
         e->tm.ext_deferred = (double)ctr[5];
+        if (ctr[8] || ctr[9])   // row kernel built with RC_ROW_TIMING: wave cycles in transitions / steps
+            fprintf(stderr, "row kernel wave-cycles: transitions %.4g steps %.4g\n", (double)ctr[8], (double)ctr[9]);
         if (!(status & 1u)) break;
         e->ovf_cap = ovn * 5 / 4 + 1024;
     }
