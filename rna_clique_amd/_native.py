@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librcgpu.so")
+# RC_LIB: an alternative build of the same library (e.g. the cycle-instrumented one)
+LIB_PATH = os.environ.get("RC_LIB") or os.path.join(HERE, "librcgpu.so")
 
 RC_OK = 0
 RC_E_ARG = -1

@@ -35,3 +35,14 @@ def build_native(force=False, verbose=False):
         print(res.stderr)
     os.replace(OUT + ".tmp", OUT)
     return OUT
+
+
+def build_timing():
+    """The same library with the row-extension cycle counters compiled in
+    (RC_ROW_TIMING), as librcgpu_timing.so, for profiling runs (RC_LIB=...)."""
+    out = os.path.join(HERE, "librcgpu_timing.so")
+    cmd = [HIPCC, *FLAGS, "-DRC_ROW_TIMING", "-o", out, *SOURCES]
+    res = subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"hipcc failed:\n{res.stderr[-8000:]}")
+    return out

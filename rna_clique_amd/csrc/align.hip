@@ -365,6 +365,14 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
                 c.seed_cnt = (uint16_t)(b1 - b0);
                 c.strand = (uint8_t)((k1 >> 56) & 1);
                 c.pad = 0;
+                const uint32_t qi = (uint32_t)(k1 >> 57);
+                c.q0 = c.strand ? total - iso_start[qi] - (uint64_t)iso_len[qi] : iso_start[qi];
+                const TxInfo st = db.tx[gtx];
+                c.s0 = st.start;
+                c.Lq = (int32_t)iso_len[qi];
+                c.Lt = (int32_t)st.len;
+                c.qsam = Q;
+                c.ssam = st.sample;
                 P.cands[cbase + tpre[T] + rk] = c;
             }
         }
@@ -830,12 +838,16 @@ __device__ __forceinline__ uint64_t win_s(const uint64_t *__restrict__ a, int64_
     return (lo >> sh) | ((hi << 1) << (63u - sh));
 }
 
-// per-row bookkeeping in LDS
-enum { RM_CLO, RM_CHI, RM_QTX, RM_STX, RM_LQ, RM_LT, RM_STRAND, RM_SOFF, RM_X, RM_Y, RM_LEN,
+// per-row bookkeeping in LDS: the candidate record (CAND_DWORDS dwords) and state
+enum { RM_REC = 0, RM_CLO = CAND_DWORDS, RM_CHI, RM_QB, RM_TB, RM_X, RM_Y, RM_LEN,
        RM_RSC, RM_RI, RM_RJ, RM_RD, RM_RGO, RM_N };
+// fields of the record (dword offsets, layout of Cand)
+enum { RC_SOFF = 0, RC_QTX = 1, RC_STX = 2, RC_CNT_STRAND = 3, RC_Q0 = 4, RC_S0 = 6, RC_LQ = 8, RC_LT = 9,
+       RC_QSAM = 10, RC_SSAM = 11 };
 enum { HB_QA, HB_QB, HB_SA, HB_SB, HB_SC, HB_D, HB_G, HB_O, HB_NI, HB_N };
-// row actions
-// (transition actions < A_DONE; extending: A_STEP_R / A_STEP_L = their done action + 4)
+// candidate progress and work cursors of a row
+enum { RS_NH, RS_SI, RS_CB, RS_LEND, RS_SHARD, RS_SHN, RS_N };
+// row actions (transition actions < A_DONE; extending: A_STEP_R / A_STEP_L = their done action + 4)
 enum { A_FETCH, A_SEED, A_RDONE, A_LDONE, A_ABORT, A_DONE, A_STEP_R, A_STEP_L };
 
 template <bool AMB, int RW, int MINW>
@@ -843,14 +855,20 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
 {
     constexpr int RROWS = EBLOCK / RW;   // rows per block
     constexpr int RC0 = RW / 2;          // row lane of diagonal 0
-    constexpr int NA = AMB ? 8 : 4;      // staged arrays per row: Q, T, Qrev, Trev (+ their masks)
+    constexpr int NA = AMB ? 8 : 4;      // staged arrays per row: Q, T (raw words), Qrev, Trev (+ masks)
     constexpr int EBIT = 26, OBIT = 13;
     constexpr int GMASK = 8191;
     extern __shared__ uint64_t rstg[];                    // [RROWS][NA][sw]
     __shared__ unsigned long long sprefix[NSHARD + 1];
-    __shared__ int rmeta[RROWS][RM_N];
-    __shared__ int rbox[RROWS][MAX_HSP][HB_N];
-    __shared__ int rseed[RROWS][3][RW];                   // seed chunk of each row: x, y, len
+    // per-row state that only transitions touch lives in LDS, one struct per
+    // row addressed off one base register
+    struct RowLds {
+        int meta[RM_N];
+        int st[RS_N];                    // candidate progress, work cursors
+        int box[MAX_HSP][HB_N];          // kept HSP boxes of the candidate
+        int seed[3][RW];                 // seed chunk: x, y, len
+    };
+    __shared__ RowLds rows_lds[RROWS];
     __shared__ unsigned int rcnt[4];                      // extensions, candidates, overflows
     if (threadIdx.x < 4) rcnt[threadIdx.x] = 0;
     for (int i = threadIdx.x; i <= NSHARD; i += EBLOCK) sprefix[i] = P.shard_prefix[i];
@@ -859,30 +877,54 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
     const int lane = threadIdx.x & 63, rl = lane & (RW - 1), row = lane / RW;
     const int rs = threadIdx.x / RW;                      // row slot in the block
     const int k = rl - RC0;                               // this lane's diagonal
-    const int sw = P.dsw;                                 // u64 words per staged sequence
-    const int smax = (sw - 4) * 32;                       // longest staged transcript + SPAD
+    const int sw = P.dsw;                                 // u64 words per staged array
     const uint32_t *S = reinterpret_cast<const uint32_t *>(rstg);
-    uint64_t *stg = rstg + (size_t)rs * NA * sw;          // Q, T, Qr, Tr, [QM, TM, QMr, TMr]
-    const uint32_t bq = (uint32_t)(rs * NA * sw) * 32u + SPAD;   // base position of Q[0]
-    const uint32_t bt = bq + 32u * (uint32_t)sw, bqr = bt + 32u * (uint32_t)sw, btr = bqr + 32u * (uint32_t)sw;
+    // two guard words in front: reversed staging reads up to 31 bases before an array
+    uint64_t *stg = rstg + 2 + (size_t)rs * NA * sw;      // Q, T, Qr, Tr, [QM, TM, QMr, TMr]
+    const uint32_t base0 = (uint32_t)(2 + rs * NA * sw) * 32u;   // base position of the row's Q array
+    const uint32_t bqr = base0 + 64u * (uint32_t)sw, btr = bqr + 32u * (uint32_t)sw;
     const uint32_t moff = 128u * (uint32_t)sw;
-    int *meta = rmeta[rs];
-    const uint64_t total = db.total;
-    const uint32_t nrows = gridDim.x * RROWS;
-    // candidates: static round robin (chunk 0) or chunks from a global counter
-    const int chunk = P.chunk;
-    uint32_t li = chunk ? 0u : blockIdx.x * RROWS + rs, lend = 0;   // candidate counts < 2^32
-    int shard = 0;
+    RowLds &RL = rows_lds[rs];
+    int *meta = RL.meta;
+    int *sxa = RL.seed[0], *sya = RL.seed[1], *sla = RL.seed[2];
+    int (*rbox_row)[HB_N] = RL.box;
     const int X = P.xdrop;
+    // candidates come in chunks from a global counter (P.chunk >= 1); the
+    // record of the next one is prefetched (one dword per lane) while the
+    // current one is extended
+    const uint32_t chunk = (uint32_t)max(P.chunk, 1);
+    const uint32_t ncand = (uint32_t)P.n_cand;
+    uint32_t lnx = 0;
+    auto grab = [&]() {
+        unsigned long long b = 0;
+        if (rl == 0) b = atomicAdd(P.work, (unsigned long long)chunk);
+        b = (unsigned long long)__shfl((long long)b, RW * row);
+        lnx = b < ncand ? (uint32_t)b : ncand;
+        if (rl == 0) RL.st[RS_LEND] = (int)(lnx + chunk);
+    };
+    // candidate slot of linear index l; the shard cursor (in LDS) only advances
+    auto slot = [&](uint32_t l, int which) -> uint64_t {
+        int sh = RL.st[which];
+        while (sh + 1 < NSHARD && sprefix[sh + 1] <= l) sh++;
+        if (rl == 0) RL.st[which] = sh;
+        return (uint64_t)sh * P.cand_cap + (l - sprefix[sh]);
+    };
+    auto load_rec = [&](uint32_t l) -> int {
+        if (l >= ncand || rl >= CAND_DWORDS) return 0;
+        return reinterpret_cast<const int *>(P.cands + slot(l, RS_SHN))[rl];
+    };
+    if (rl == 0) {
+        RL.st[RS_SHARD] = 0;
+        RL.st[RS_SHN] = 0;
+    }
+    grab();
+    int recv = load_rec(lnx);
 
     int act = A_FETCH;
     // extension state: frontier (R, gap state), winner record, row-uniform best
     int R = -1, goe = 0, wi = 0, wg = 0, wd = 0, best = 0, bl = RC0, d6 = 0;   // d6 = 6 x greedy step
     uint32_t pa = 0, pb = 0;
     int alen = 0, blen = 0;
-    // candidate state (row-uniform) and the seed chunk (lane rl: seed cb + rl)
-    int ns = 0, nh = 0, si = 0, cb = -1;
-    int *sxa = rseed[rs][0], *sya = rseed[rs][1], *sla = rseed[rs][2];
     unsigned long long steps = 0;                         // row steps (wave-uniform count)
 
     auto ext_init = [&](int done_act) {
@@ -902,17 +944,21 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
         if (rl == 0) atomicAdd(&rcnt[0], 1u);
         act = (min(alen, blen) - r0 <= 0) ? done_act : done_act + (A_STEP_R - A_RDONE);
     };
-    auto stage_fwd = [&](uint64_t *dst, const uint64_t *src, uint64_t p0, int L) {
-        const int nw = (L >> 5) + 3;
-        for (int w = rl; w < nw; w += RW) dst[w] = w ? win<uint64_t>(src, p0 + 32 * (uint64_t)(w - 1)) : 0ull;
+    auto seed_chunk = [&](int c0, int ns) {
+        if (c0 + rl < ns) {
+            const GSeed g = P.seeds[(uint32_t)meta[RM_REC + RC_SOFF] + (uint32_t)(c0 + rl)];
+            sxa[rl] = (int)g.x;
+            sya[rl] = (int)g.y;
+            sla[rl] = (int)g.len;
+        }
     };
-    // reversed copy: word w >= 1 holds reversed bases 32 (w - 1) .. 32 w - 1,
-    // i.e. bases L - 32 w .. L - 32 (w - 1) - 1 in reverse order
-    auto stage_rev = [&](uint64_t *dst, const uint64_t *src, uint64_t p0, int L) {
+    // reversed copy of a staged array: word w holds bases L - 1 - 32 w down to
+    // L - 32 (w + 1) of the array whose base 0 sits at LDS base position fb
+    auto stage_rev = [&](uint64_t *dst, uint32_t fb, int L) {
         const int nw = (L >> 5) + 3;
         for (int w = rl; w < nw; w += RW) {
-            const int64_t gp = (int64_t)p0 + L - 32 * (int64_t)w;
-            dst[w] = (w && gp >= -64) ? rev2(win_s(src, gp)) : 0ull;
+            const int fp = L - 32 * (w + 1);
+            dst[w] = fp > -32 ? rev2(win3(S, (uint32_t)((int)fb + fp))) : 0ull;
         }
     };
 
@@ -926,142 +972,119 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
         // ---------------- transitions ----------------
         while (act < A_DONE) {
             if (act == A_FETCH) {
-                if (chunk && li >= lend) {
-                    unsigned long long b = 0;
-                    if (rl == 0) b = atomicAdd(P.work, (unsigned long long)chunk);
-                    b = (unsigned long long)__shfl((long long)b, RW * row);
-                    li = b < P.n_cand ? (uint32_t)b : (uint32_t)P.n_cand;
-                    lend = li + (uint32_t)chunk;
-                }
-                if (li >= P.n_cand) {
+                if (lnx >= ncand) {
                     act = A_DONE;
                     continue;
                 }
-                while (shard + 1 < NSHARD && sprefix[shard + 1] <= li) shard++;
-                const uint64_t ci = (uint64_t)shard * P.cand_cap + (li - sprefix[shard]);
-                const Cand cd = P.cands[ci];
-                const TxInfo qt = db.tx[cd.q_gtx], st = db.tx[cd.s_gtx];
-                const int Lq = (int)qt.len, Lt = (int)st.len;
-                if (Lq + SPAD > smax || Lt + SPAD > smax) {
-                    if (rl == 0) {
-                        const unsigned long long di = atomicAdd(P.defer_count, 1ull);
-                        P.defer[di] = (uint32_t)ci;
-                    }
-                    li += chunk ? 1u : nrows;
-                    continue;
-                }
-                const uint64_t q0 = cd.strand ? total - qt.start - (uint64_t)Lq : qt.start;
-                const uint64_t *QA = cd.strand ? db.RC : db.F;
-                stage_fwd(stg, QA, q0, Lq);
-                stage_fwd(stg + sw, db.F, st.start, Lt);
-                stage_rev(stg + 2 * sw, QA, q0, Lq);
-                stage_rev(stg + 3 * sw, db.F, st.start, Lt);
-                if (AMB) {
-                    const uint64_t *QM = cd.strand ? db.ARC : db.AF;
-                    stage_fwd(stg + 4 * sw, QM, q0, Lq);
-                    stage_fwd(stg + 5 * sw, db.AF, st.start, Lt);
-                    stage_rev(stg + 6 * sw, QM, q0, Lq);
-                    stage_rev(stg + 7 * sw, db.AF, st.start, Lt);
-                }
+                const uint64_t ci = slot(lnx, RS_SHARD);
+                if (rl < CAND_DWORDS) meta[RM_REC + rl] = recv;
                 if (rl == 0) {
                     meta[RM_CLO] = (int)(uint32_t)ci;
                     meta[RM_CHI] = (int)(uint32_t)(ci >> 32);
-                    meta[RM_QTX] = (int)cd.q_gtx;
-                    meta[RM_STX] = (int)cd.s_gtx;
-                    meta[RM_LQ] = Lq;
-                    meta[RM_LT] = Lt;
-                    meta[RM_STRAND] = cd.strand;
-                    meta[RM_SOFF] = (int)cd.seed_off;
+                }
+                // prefetch the next record
+                if (++lnx >= (uint32_t)RL.st[RS_LEND]) grab();
+                recv = load_rec(lnx);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                const int Lq = meta[RM_REC + RC_LQ], Lt = meta[RM_REC + RC_LT];
+                const uint64_t q0 = (uint64_t)(uint32_t)meta[RM_REC + RC_Q0] |
+                                    ((uint64_t)(uint32_t)meta[RM_REC + RC_Q0 + 1] << 32);
+                const uint64_t s0 = (uint64_t)(uint32_t)meta[RM_REC + RC_S0] |
+                                    ((uint64_t)(uint32_t)meta[RM_REC + RC_S0 + 1] << 32);
+                const int strand = (meta[RM_REC + RC_CNT_STRAND] >> 16) & 1;
+                const int nwq = (int)(((q0 & 31) + (uint64_t)Lq) >> 5) + 3;
+                const int nwt = (int)(((s0 & 31) + (uint64_t)Lt) >> 5) + 3;
+                if (nwq > sw || nwt > sw || (Lq >> 5) + 3 > sw || (Lt >> 5) + 3 > sw) {
+                    if (rl == 0) {
+                        const unsigned long long di = atomicAdd(P.defer_count, 1ull);
+                        P.defer[di] = (uint32_t)ci;
+                        P.cand_box[ci * BOX_REC + BOX_NH] = -1;
+                    }
+                    continue;
+                }
+                const int ns = meta[RM_REC + RC_CNT_STRAND] & 0xFFFF;
+                // raw words of query and subject, and the first seed chunk
+                const uint64_t *QA = strand ? db.RC : db.F;
+                const uint64_t *qw = QA + (q0 >> 5), *tw = db.F + (s0 >> 5);
+                {
+                    // every load in flight before the first LDS write: one round trip
+                    GSeed g0 = {0, 0, 0};
+                    if (rl < ns) g0 = P.seeds[(uint32_t)meta[RM_REC + RC_SOFF] + (uint32_t)rl];
+                    const uint64_t a0 = rl < nwq ? qw[rl] : 0ull, a1 = rl + RW < nwq ? qw[rl + RW] : 0ull;
+                    const uint64_t b0 = rl < nwt ? tw[rl] : 0ull, b1 = rl + RW < nwt ? tw[rl + RW] : 0ull;
+                    if (rl < nwq) stg[rl] = a0;
+                    if (rl + RW < nwq) stg[rl + RW] = a1;
+                    if (rl < nwt) stg[sw + rl] = b0;
+                    if (rl + RW < nwt) stg[sw + rl + RW] = b1;
+                    sxa[rl] = (int)g0.x;
+                    sya[rl] = (int)g0.y;
+                    sla[rl] = (int)g0.len;
+                }
+                for (int w = rl + 2 * RW; w < nwq; w += RW) stg[w] = qw[w];
+                for (int w = rl + 2 * RW; w < nwt; w += RW) stg[sw + w] = tw[w];
+                if (AMB) {
+                    const uint64_t *qm = (strand ? db.ARC : db.AF) + (q0 >> 5), *tm = db.AF + (s0 >> 5);
+                    for (int w = rl; w < nwq; w += RW) stg[4 * sw + w] = qm[w];
+                    for (int w = rl; w < nwt; w += RW) stg[5 * sw + w] = tm[w];
+                }
+                const uint32_t qb = base0 + (uint32_t)(q0 & 31), tb = base0 + 32u * (uint32_t)sw + (uint32_t)(s0 & 31);
+                if (rl == 0) {
+                    meta[RM_QB] = (int)qb;
+                    meta[RM_TB] = (int)tb;
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
-                ns = cd.seed_cnt;
-                nh = 0;
-                si = 0;
-                cb = -1;
-                if (rl == 0) atomicAdd(&rcnt[1], 1u);
+                stage_rev(stg + 2 * sw, qb, Lq);
+                stage_rev(stg + 3 * sw, tb, Lt);
+                if (AMB) {
+                    stage_rev(stg + 6 * sw, qb + moff, Lq);
+                    stage_rev(stg + 7 * sw, tb + moff, Lt);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                if (rl == 0) {
+                    RL.st[RS_NH] = 0;
+                    RL.st[RS_SI] = 0;
+                    RL.st[RS_CB] = 0;
+                    atomicAdd(&rcnt[1], 1u);
+                }
                 act = A_SEED;
             } else if (act == A_SEED) {
+                const int ns = meta[RM_REC + RC_CNT_STRAND] & 0xFFFF;
+                const int nh = RL.st[RS_NH], si = RL.st[RS_SI];
                 if (nh >= MAX_HSP || si >= ns) {
-                    // ---- candidate done: purge, e-value cut, output ----
+                    // ---- candidate done: its boxes go out; ext_finish_kernel
+                    // purges, applies the e-value cuts and writes the HSPs ----
                     const uint64_t ci = (uint64_t)(uint32_t)meta[RM_CLO] | ((uint64_t)(uint32_t)meta[RM_CHI] << 32);
-                    const int Lq = meta[RM_LQ], Lt = meta[RM_LT], strand = meta[RM_STRAND];
-                    const uint32_t q_gtx = (uint32_t)meta[RM_QTX], s_gtx = (uint32_t)meta[RM_STX];
-                    const bool mine = rl < nh;
-                    const int *hb = rbox[rs][mine ? rl : 0];
-                    const int bqa = hb[HB_QA], bqb = hb[HB_QB], bsa = hb[HB_SA], bsb = hb[HB_SB];
-                    const int bsc = hb[HB_SC];
-                    bool kept = mine && rl == 0;
-                    if (nh > 1) {
-                        int rank = 0;
-                        for (int j = 0; j < nh; j++) {
-                            const int sj = rbox[rs][j][HB_SC];
-                            if (mine && (sj > bsc || (sj == bsc && j < rl))) rank++;
-                        }
-                        kept = false;
-                        for (int rr = 0; rr < nh; rr++) {
-                            const uint32_t m = rw_mask<RW>(__ballot(mine && rank == rr), row);
-                            const int i = __builtin_ctz(m);
-                            const int *hi = rbox[rs][i];
-                            const bool conflict = kept && mine && ((bqa == hi[HB_QA] && bsa == hi[HB_SA]) ||
-                                                                   (bqb == hi[HB_QB] && bsb == hi[HB_SB]));
-                            if (!rw_mask<RW>(__ballot(conflict), row) && rl == i) kept = true;
-                        }
-                    }
-                    const int qs = db.tx[q_gtx].sample, ss = db.tx[s_gtx].sample;
-                    const int thr_f = P.thr[(size_t)ss * (size_t)(P.max_len + 1) + (size_t)Lq];
-                    const int thr_r = P.thr[(size_t)qs * (size_t)(P.max_len + 1) + (size_t)Lt];
-                    const bool pf = bsc >= thr_f, pr = bsc >= thr_r;
-                    const bool out = kept && (pf || pr);
-                    const uint32_t om = rw_mask<RW>(__ballot(out), row);
-                    const int nout = __popc(om);
+                    const int *flat = &rbox_row[0][0];
+                    int *cbx = P.cand_box + ci * BOX_REC;
+                    if (rl < HB_N) cbx[rl] = flat[rl];
                     uint32_t obase = 0;
-                    if (nout > 1 && rl == 0) {
-                        const unsigned long long b = atomicAdd(P.ovf_count, (unsigned long long)(nout - 1));
-                        if (b + (nout - 1) > P.ovf_cap) atomicOr(P.status, 1u);
-                        obase = (uint32_t)b;
-                    }
-                    obase = __shfl(obase, RW * row);
-                    if (out) {
-                        const int rk = __popc(om & ((1u << rl) - 1u));
-                        DHsp h;
-                        h.q_tx = q_gtx;
-                        h.s_tx = s_gtx;
-                        if (!strand) {
-                            h.qstart = bqa + 1; h.qend = bqb; h.sstart = bsa + 1; h.send = bsb;
-                        } else {
-                            h.qstart = Lq - bqb + 1; h.qend = Lq - bqa; h.sstart = bsb; h.send = bsa + 1;
+                    if (nh > 1) {
+                        if (rl == 0) {
+                            const unsigned long long b = atomicAdd(P.box_ovf_count, (unsigned long long)(nh - 1));
+                            if (b + (nh - 1) > P.box_ovf_cap) atomicOr(P.status, 1u);
+                            obase = (uint32_t)b;
                         }
-                        const int bd = hb[HB_D], bg = hb[HB_G], bni = hb[HB_NI];
-                        h.gaps = bg;
-                        h.gapopen = hb[HB_O];
-                        h.mismatch = bd - bg;
-                        h.nident = bni;
-                        h.length = bni + (bd - bg) + bg;
-                        h.score_half = bsc;
-                        h.bits10 = P.bits10[bsc];
-                        h.strand = strand | (pf ? HSP_FWD : 0) | (pr ? HSP_REV : 0) | (rl << HSP_IDX_SHIFT);
-                        if (rk == 0) P.cand_hsp[ci] = h;
-                        else if ((uint64_t)obase + (rk - 1) < P.ovf_cap) P.ovf[obase + rk - 1] = h;
+                        obase = __shfl(obase, RW * row);
+                        if ((uint64_t)obase + (nh - 1) <= P.box_ovf_cap)
+                            for (int f = rl; f < (nh - 1) * HB_N; f += RW) P.box_ovf[(size_t)obase * HB_N + f] = flat[HB_N + f];
                     }
                     if (rl == 0) {
-                        P.cand_nh[ci] = (uint8_t)nout;
-                        P.cand_ovf[ci] = obase;
+                        cbx[BOX_NH] = nh;
+                        cbx[BOX_OVF] = (int)obase;
                     }
-                    li += chunk ? 1u : nrows;
                     act = A_FETCH;
                     continue;
                 }
                 // next seed not inside a kept box, searched RW at a time
                 const int c0 = si & ~(RW - 1);
+                int cb = RL.st[RS_CB];
                 if (c0 != cb) {
                     cb = c0;
-                    if (cb + rl < ns) {
-                        const GSeed g = P.seeds[(uint32_t)meta[RM_SOFF] + (uint32_t)(cb + rl)];
-                        sxa[rl] = (int)g.x;
-                        sya[rl] = (int)g.y;
-                        sla[rl] = (int)g.len;
-                    }
+                    if (rl == 0) RL.st[RS_CB] = cb;
+                    seed_chunk(cb, ns);
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                 }
@@ -1069,26 +1092,27 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                 const int sx = sxa[rl], sy = sya[rl], sl = sla[rl];
                 bool contained = false;
                 for (int j = 0; j < nh; j++) {
-                    const int *hj = rbox[rs][j];
+                    const int *hj = rbox_row[j];
                     contained |= hj[HB_QA] <= sx && sx + sl <= hj[HB_QB] && hj[HB_SA] <= sy && sy + sl <= hj[HB_SB];
                 }
                 const uint32_t m = rw_mask<RW>(__ballot(idx >= si && idx < ns && !contained), row);
                 if (!m) {
-                    si = cb + RW;
+                    __builtin_amdgcn_wave_barrier();
+                    if (rl == 0) RL.st[RS_SI] = cb + RW;
                     continue;
                 }
                 const int f = __builtin_ctz(m);
                 const int x = sxa[f], y = sya[f], len = sla[f];
-                si = cb + f + 1;
                 if (rl == 0) {
+                    RL.st[RS_SI] = cb + f + 1;
                     meta[RM_X] = x;
                     meta[RM_Y] = y;
                     meta[RM_LEN] = len;
                 }
-                const int Lq = meta[RM_LQ], Lt = meta[RM_LT];
-                pa = bq + (uint32_t)(x + len);
+                const int Lq = meta[RM_REC + RC_LQ], Lt = meta[RM_REC + RC_LT];
+                pa = (uint32_t)meta[RM_QB] + (uint32_t)(x + len);
                 alen = Lq - (x + len);
-                pb = bt + (uint32_t)(y + len);
+                pb = (uint32_t)meta[RM_TB] + (uint32_t)(y + len);
                 blen = Lt - (y + len);
                 ext_init(A_RDONE);
             } else if (act == A_RDONE || act == A_LDONE) {
@@ -1106,7 +1130,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                     }
                     // left extension: forward from reversed position L - x
                     // (= base x - 1) of the reversed copies
-                    const int Lq = meta[RM_LQ], Lt = meta[RM_LT];
+                    const int Lq = meta[RM_REC + RC_LQ], Lt = meta[RM_REC + RC_LT];
                     pa = bqr + (uint32_t)(Lq - x);
                     alen = x;
                     pb = btr + (uint32_t)(Lt - y);
@@ -1117,8 +1141,9 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                     const int rgo = meta[RM_RGO];
                     const int lg = ego & GMASK, lo = (ego >> OBIT) & GMASK;
                     const int rg = rgo & GMASK, ro = (rgo >> OBIT) & GMASK;
+                    const int nh = RL.st[RS_NH];
                     if (rl == 0) {
-                        int *hb = rbox[rs][nh];
+                        int *hb = rbox_row[nh];
                         hb[HB_QA] = x - ei;
                         hb[HB_QB] = x + len + ri;
                         hb[HB_SA] = y - ej;
@@ -1128,19 +1153,20 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                         hb[HB_G] = lg + rg;
                         hb[HB_O] = lo + ro;
                         hb[HB_NI] = len + (ei + ej - 2 * ed + lg) / 2 + (ri + rj - 2 * rd + rg) / 2;
+                        RL.st[RS_NH] = nh + 1;
                     }
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
-                    nh++;
                     act = A_SEED;
                 }
             } else {   // A_ABORT: the sub-band overflowed; extend_kernel redoes the candidate
                 if (rl == 0) {
+                    const uint64_t ci = (uint64_t)(uint32_t)meta[RM_CLO] | ((uint64_t)(uint32_t)meta[RM_CHI] << 32);
                     const unsigned long long di = atomicAdd(P.defer_count, 1ull);
-                    P.defer[di] = (uint32_t)meta[RM_CLO];
+                    P.defer[di] = (uint32_t)ci;
+                    P.cand_box[ci * BOX_REC + BOX_NH] = -1;
+                    atomicAdd(&rcnt[2], 1u);
                 }
-                if (rl == 0) atomicAdd(&rcnt[2], 1u);
-                li += chunk ? 1u : nrows;
                 act = A_FETCH;
             }
         }
@@ -1213,6 +1239,95 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
     if (lane == 0 && P.counters) atomicAdd(&P.counters[0], steps);
     __syncthreads();
     if (threadIdx.x < 3 && P.counters) atomicAdd(&P.counters[1 + threadIdx.x], (unsigned long long)rcnt[threadIdx.x]);
+}
+
+
+// Purge, e-value cuts and HSP records of the candidates extend_rows_kernel
+// finished (its boxes; deferred candidates, BOX_NH < 0, were written by
+// extend_kernel): one thread per candidate, same rules as extend_kernel.
+__global__ __launch_bounds__(256) void ext_finish_kernel(ExtParams P)
+{
+    for (uint64_t li = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; li < P.n_cand;
+         li += (uint64_t)gridDim.x * blockDim.x) {
+        int lo = 0, hi = NSHARD;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (P.shard_prefix[mid] <= li) lo = mid; else hi = mid;
+        }
+        const uint64_t ci = (uint64_t)lo * P.cand_cap + (li - P.shard_prefix[lo]);
+        const int *cbx = P.cand_box + ci * BOX_REC;
+        const int nh = cbx[BOX_NH];
+        if (nh < 0) continue;
+        const int *ovb = P.box_ovf + (size_t)(uint32_t)cbx[BOX_OVF] * HB_N;
+        auto box = [&](int i) -> const int * { return i ? ovb + (size_t)(i - 1) * HB_N : cbx; };
+        // keep unless a start or end point is shared with a better (score
+        // desc, index asc) kept box
+        uint32_t kept = 0;
+        for (int rr = 0; rr < nh; rr++) {
+            int bi = -1, bs = INT_MIN;
+            for (int i = 0; i < nh; i++) {   // rr-th in (score desc, index asc)
+                const int sc = box(i)[HB_SC];
+                int rank = 0;
+                for (int j = 0; j < nh; j++) {
+                    const int sj = box(j)[HB_SC];
+                    rank += (sj > sc || (sj == sc && j < i)) ? 1 : 0;
+                }
+                if (rank == rr) {
+                    bi = i;
+                    bs = sc;
+                }
+            }
+            (void)bs;
+            const int *b = box(bi);
+            bool ok = true;
+            for (int j = 0; j < nh && ok; j++) {
+                if (!((kept >> j) & 1u)) continue;
+                const int *c = box(j);
+                if ((b[HB_QA] == c[HB_QA] && b[HB_SA] == c[HB_SA]) || (b[HB_QB] == c[HB_QB] && b[HB_SB] == c[HB_SB]))
+                    ok = false;
+            }
+            if (ok) kept |= 1u << bi;
+        }
+        const Cand cd = P.cands[ci];
+        const int thr_f = P.thr[(size_t)cd.ssam * (size_t)(P.max_len + 1) + (size_t)cd.Lq];
+        const int thr_r = P.thr[(size_t)cd.qsam * (size_t)(P.max_len + 1) + (size_t)cd.Lt];
+        int nout = 0;
+        for (int i = 0; i < nh; i++)
+            if (((kept >> i) & 1u) && (box(i)[HB_SC] >= thr_f || box(i)[HB_SC] >= thr_r)) nout++;
+        uint32_t obase = 0;
+        if (nout > 1) {
+            const unsigned long long b = atomicAdd(P.ovf_count, (unsigned long long)(nout - 1));
+            if (b + (nout - 1) > P.ovf_cap) atomicOr(P.status, 1u);
+            obase = (uint32_t)b;
+        }
+        int rk = 0;
+        for (int i = 0; i < nh; i++) {
+            const int *b = box(i);
+            const bool pf = b[HB_SC] >= thr_f, pr = b[HB_SC] >= thr_r;
+            if (!((kept >> i) & 1u) || !(pf || pr)) continue;
+            DHsp h;
+            h.q_tx = cd.q_gtx;
+            h.s_tx = cd.s_gtx;
+            if (!cd.strand) {
+                h.qstart = b[HB_QA] + 1; h.qend = b[HB_QB]; h.sstart = b[HB_SA] + 1; h.send = b[HB_SB];
+            } else {
+                h.qstart = cd.Lq - b[HB_QB] + 1; h.qend = cd.Lq - b[HB_QA]; h.sstart = b[HB_SB]; h.send = b[HB_SA] + 1;
+            }
+            h.gaps = b[HB_G];
+            h.gapopen = b[HB_O];
+            h.mismatch = b[HB_D] - b[HB_G];
+            h.nident = b[HB_NI];
+            h.length = b[HB_NI] + b[HB_D];
+            h.score_half = b[HB_SC];
+            h.bits10 = P.bits10[b[HB_SC]];
+            h.strand = cd.strand | (pf ? HSP_FWD : 0) | (pr ? HSP_REV : 0) | (i << HSP_IDX_SHIFT);
+            if (rk == 0) P.cand_hsp[ci] = h;
+            else if ((uint64_t)obase + (rk - 1) < P.ovf_cap) P.ovf[obase + rk - 1] = h;
+            rk++;
+        }
+        P.cand_nh[ci] = (uint8_t)nout;
+        P.cand_ovf[ci] = obase;
+    }
 }
 
 // ------------------------------------------------------------------------
@@ -1396,7 +1511,7 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
     if (P.n_cand == 0) return;
     ExtParams W = P;
     const int rw = row_width == 16 ? 16 : 32;
-    const size_t lds = (size_t)(EBLOCK / rw) * (amb ? 8 : 4) * (size_t)P.dsw * 8;
+    const size_t lds = ((size_t)(EBLOCK / rw) * (amb ? 8 : 4) * (size_t)P.dsw + 2) * 8;
 #define RC_LAUNCH_ROWS(A, RWV, MW)                                                                        \
     do {                                                                                                  \
         auto kern = extend_rows_kernel<A, RWV, MW>;                                                       \
@@ -1419,6 +1534,9 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
         auto kern = extend_kernel<false>;
         hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W);
     }
+    uint64_t g = (P.n_cand + 255) / 256;
+    if (g > 65536) g = 65536;
+    hipLaunchKernelGGL(ext_finish_kernel, dim3((unsigned)g), dim3(256), 0, st, W);
 }
 
 void launch_group(const GroupParams &P, int pass, hipStream_t st)

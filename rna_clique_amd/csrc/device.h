@@ -87,12 +87,19 @@ struct GSeed {
 };
 
 // Candidate = (query transcript, strand, subject transcript) with >= 1 seed.
+// Self-contained (48 B): the extension reads one record, no transcript table.
 struct Cand {
     uint32_t seed_off;     // absolute index of its first seed (sorted by (x, y))
     uint32_t q_gtx, s_gtx;
     uint16_t seed_cnt;
     uint8_t strand, pad;
+    uint64_t q0;           // first base of the oriented query: in F (strand 0) or RC (strand 1)
+    uint64_t s0;           // first base of the subject in F
+    int32_t Lq, Lt;        // transcript lengths
+    int32_t qsam, ssam;    // samples of query and subject
 };
+constexpr int CAND_DWORDS = (int)(sizeof(Cand) / 4);
+static_assert(sizeof(Cand) == 48, "Cand is read as 12 dwords");
 
 // seed_kernel: per query gene, lookups -> canonical seeds -> candidates.
 struct SeedParams {
@@ -133,6 +140,10 @@ struct ExtParams {
     // two-candidate kernel: staging slot (u64 words per sequence) and the
     // candidates it defers to the one-wave kernel (transcripts past the slot)
     int32_t dsw;
+    int32_t *cand_box;            // row kernel: first HSP box of each candidate + count + overflow offset
+    int32_t *box_ovf;             // boxes 2..nh (9 ints each)
+    uint64_t box_ovf_cap;
+    unsigned long long *box_ovf_count;
     int32_t chunk;                // row kernel: candidates per work grab (0: static round robin)
     unsigned long long *work;     // row kernel: work counter
     uint32_t *defer;
@@ -143,6 +154,9 @@ struct ExtParams {
 // freshly extended HSP (bit 1: passes the query->subject e-value cut, bit 2:
 // passes the mirrored direction's) and its index in the candidate (bits 3-5).
 constexpr int HSP_FWD = 2, HSP_REV = 4, HSP_IDX_SHIFT = 3;
+
+// cand_box record (ints): box fields 0..8, count (-1: deferred to extend_kernel), overflow offset
+constexpr int BOX_NH = 9, BOX_OVF = 10, BOX_REC = 12;
 
 constexpr int DSTAGE_MAX = 4096;   // longest transcript the two-candidate extension stages
 

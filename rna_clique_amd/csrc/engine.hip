@@ -239,11 +239,12 @@ struct rc_engine {
     DBuf<Cand> d_cands;
     DBuf<DHsp> d_cand_hsp, d_ovf;
     DBuf<uint8_t> d_cand_nh;
+    DBuf<int32_t> d_cand_box, d_box_ovf;
     DBuf<uint32_t> d_cand_ovf, d_gc_off, d_gc_cnt, d_gcount, d_defer;
     DBuf<uint64_t> d_gscan, d_mscan, d_mkey, d_tmask;
     DBuf<uint32_t> d_mcnt, d_mcur, d_tx_pos;
     DBuf<unsigned long long> d_shard_cnt, d_shard_prefix;
-    uint64_t seed_cap = 0, cand_cap = 0, ovf_cap = 0;   // per-shard / total capacities
+    uint64_t seed_cap = 0, cand_cap = 0, ovf_cap = 0, box_ovf_cap = 0;   // per-shard / total capacities
     DBuf<uint32_t> d_grp_off, d_grp_cnt;
     DBuf<unsigned long long> d_count;
     DBuf<unsigned int> d_status;
@@ -808,10 +809,13 @@ static int do_align(rc_engine *e)
     CHK(e->d_cand_hsp.ensure(slots));
     CHK(e->d_cand_nh.ensure(slots));
     CHK(e->d_cand_ovf.ensure(slots));
+    CHK(e->d_cand_box.ensure(slots * BOX_REC));
     CHK(e->d_defer.ensure(std::max<uint64_t>(n_cand, 1)));
+    if (!e->box_ovf_cap) e->box_ovf_cap = n_cand / 8 + 1024;
     for (int attempt = 0;; attempt++) {
         if (attempt == 4) return fail(RC_E_NOMEM, "HSP overflow buffer kept overflowing");
         CHK(e->d_ovf.ensure(e->ovf_cap));
+        CHK(e->d_box_ovf.ensure(e->box_ovf_cap * 9));
         HIPCHK(hipMemsetAsync(e->d_count.p, 0, 16 * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
         ExtParams X;
@@ -832,13 +836,17 @@ static int do_align(rc_engine *e)
         X.ovf_count = e->d_count.p;
         X.status = e->d_status.p;
         X.counters = e->d_count.p + 1;
-        X.dsw = ((std::min(e->max_len, DSTAGE_MAX) + 32 + 31) >> 5) + 4;   // row staging slot (u64 words)
+        X.dsw = ((std::min(e->max_len, DSTAGE_MAX) + 31) >> 5) + 3;   // row staging slot (u64 words)
         X.defer = e->d_defer.p;
         X.defer_count = e->d_count.p + 6;
         X.work = e->d_count.p + 7;
+        X.cand_box = e->d_cand_box.p;
+        X.box_ovf = e->d_box_ovf.p;
+        X.box_ovf_cap = e->box_ovf_cap;
+        X.box_ovf_count = e->d_count.p + 12;
         {
             const char *cv = getenv("RC_ROW_CHUNK");
-            X.chunk = cv ? atoi(cv) : 4;
+            X.chunk = cv ? atoi(cv) : 8;
         }
         HIPCHK(hipEventRecord(e->ev[10], e->st));
         {
@@ -862,7 +870,10 @@ static int do_align(rc_engine *e)
         if (ctr[8] || ctr[9])   // row kernel built with RC_ROW_TIMING: wave cycles in transitions / steps
             fprintf(stderr, "row kernel wave-cycles: transitions %.4g steps %.4g\n", (double)ctr[8], (double)ctr[9]);
         if (!(status & 1u)) break;
-        e->ovf_cap = ovn * 5 / 4 + 1024;
+        unsigned long long bovn = 0;
+        HIPCHK(hipMemcpy(&bovn, e->d_count.p + 12, sizeof bovn, hipMemcpyDeviceToHost));
+        e->ovf_cap = std::max<uint64_t>(e->ovf_cap, ovn * 5 / 4 + 1024);
+        e->box_ovf_cap = std::max<uint64_t>(e->box_ovf_cap, bovn * 5 / 4 + 1024);
     }
     // --- groups: (query gene, subject sample) -> contiguous HSPs ---
     // Direct groups (query sample < subject sample) come first in d_hsp, in
