@@ -20,7 +20,8 @@
 namespace rcg {
 
 constexpr int SBLOCK = 256;
-constexpr int SEED_CAP = 1024;
+constexpr int SEED_CAP = 768;
+constexpr int HBATCH = 4;                          // hits per lane per batch of the seed kernel
 constexpr int MAX_SAMPLES = 256;
 
 constexpr int EBLOCK = 256;
@@ -88,6 +89,17 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *wsum, uin
     return before + x - v;
 }
 
+// last k with pre[k] <= h over an SBLOCK + 1 prefix table (the word a hit belongs to)
+__device__ __forceinline__ int run_of(const uint32_t *pre, uint32_t h)
+{
+    int lo = 0, hi = SBLOCK;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (pre[mid] <= h) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
 template <bool AMB>
 __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParams P)
 {
@@ -98,7 +110,10 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
     __shared__ LSeed seeds[SEED_CAP];
     __shared__ uint16_t seg_begin[SEED_CAP + 1];
     __shared__ uint32_t it_lo[SBLOCK], it_cnt[SBLOCK], it_pre[SBLOCK + 1], it_info[SBLOCK];
-    __shared__ uint32_t sh_carry_lo, sh_carry_cnt;
+    __shared__ uint32_t it_key[SBLOCK];
+    __shared__ uint32_t hq_pos[SBLOCK / 64][64 * HBATCH];   // per-wave queue of hits for the full test
+    __shared__ uint8_t hq_k[SBLOCK / 64][64 * HBATCH];
+    __shared__ uint64_t it_qlw[SBLOCK], it_qlm[AMB ? SBLOCK : 1];
     __shared__ uint64_t iso_start[MAX_ISO];
     __shared__ uint32_t iso_len[MAX_ISO], iso_gtx[MAX_ISO], iso_pre[MAX_ISO + 1];
     __shared__ uint32_t tcnt[MAX_SAMPLES], tpre[MAX_SAMPLES + 1];
@@ -137,6 +152,18 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
     }
     __syncthreads();
     const uint32_t n_items = iso_pre[niso];
+#ifdef RC_ROW_TIMING
+    unsigned long long tph[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long tc = __builtin_readcyclecounter();
+    auto tick = [&](int i) {
+        const unsigned long long t = __builtin_readcyclecounter();
+        tph[i] += t - tc;
+        tc = t;
+    };
+#define SEED_TICK(i) tick(i)
+#else
+#define SEED_TICK(i) ((void)0)
+#endif
     const uint32_t gl = g - P.gene_begin;
 
     // subject samples of this shard: higher-numbered samples only (symmetric
@@ -149,15 +176,17 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
             sh_flags = 0;
         }
         __syncthreads();
-        // words p of the oriented query at stride s, one per thread; each
-        // word's index run narrowed to the bases of subject samples [T0, T1)
-        // (runs hold ascending global positions; samples are contiguous)
+        // words p of the oriented query at stride s, one per thread; hits are
+        // the entries of the word's bucket with its key and a position in the
+        // subject samples [T0, T1) (samples are contiguous in position)
         const uint32_t pb0 = (uint32_t)db.sample_pos_begin[T0], pb1 = (uint32_t)db.sample_pos_begin[T1];
-        const bool join = stride <= W16;   // canonical test through the previous word's run
-        if (tid == 0) sh_carry_cnt = 0;
+        // canonical pre-test by sequence: a hit whose s bases before it match
+        // (inside both transcripts) extends left past p - s: not canonical
+        const bool fast = stride <= 32;
         for (uint32_t ib = 0; ib < n_items; ib += SBLOCK) {
             const uint32_t it = ib + tid;
-            uint32_t lo = 0, cnt = 0, info = 0;
+            uint32_t lo = 0, cnt = 0, info = 0, key = 0;
+            uint64_t qlw = 0, qlm = 0;
             if (it < n_items) {
                 uint32_t ii = 0;
                 while (ii + 1 < niso && iso_pre[ii + 1] <= it) ii++;
@@ -175,103 +204,120 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
                     ok = (win(QM, qp) & 0xFFFFFFFFull) == 0;
                 }
                 if (ok) {
-                    const uint32_t key = (uint32_t)win(QA, qp);
+                    key = (uint32_t)win(QA, qp);
+                    // the whole bucket of the key's top bits (one round trip, no
+                    // search): the hit loop filters by key and subject range
                     const uint32_t b = key >> (32 - ix.bits);
-                    // entries of the k-mer with position in [pb0, pb1): lower
-                    // bounds of (key, pb0) and (key, pb1) inside the bucket
-                    const uint64_t k0 = ((uint64_t)key << 32) | pb0, k1 = ((uint64_t)key << 32) | pb1;
-                    uint32_t l0 = ix.bucket[b], h0 = ix.bucket[b + 1];
-                    uint32_t h1 = h0;
-                    while (l0 < h0) {
-                        const uint32_t m = (l0 + h0) >> 1;
-                        const uint64_t v = ix.ent[m];
-                        if (v < k0) l0 = m + 1; else h0 = m;
-                        if (v >= k1) h1 = min(h1, m);
+                    lo = ix.bucket[b];
+                    cnt = ix.bucket[b + 1] - lo;
+                    // the 32 query bases before p (canonical pre-test)
+                    if (fast && p >= stride) {
+                        qlw = win_s(QA, (int64_t)qp - 32);
+                        if (AMB) qlm = win_s(strand ? db.ARC : db.AF, (int64_t)qp - 32);
                     }
-                    uint32_t l1 = l0;
-                    while (l1 < h1) {
-                        const uint32_t m = (l1 + h1) >> 1;
-                        if (ix.ent[m] < k1) l1 = m + 1; else h1 = m;
-                    }
-                    lo = l0;
-                    cnt = l1 - l0;
                 }
             }
             it_lo[tid] = lo;
             it_cnt[tid] = cnt;
             it_info[tid] = info;
+            it_key[tid] = key;
+            it_qlw[tid] = qlw;
+            if (AMB) it_qlm[tid] = qlm;
             uint32_t tot;
+            SEED_TICK(0);
             it_pre[tid] = block_exscan(cnt, wsum, tot);
             if (tid == 0) it_pre[SBLOCK] = tot;
             __syncthreads();
+            SEED_TICK(1);
             const uint32_t nh = it_pre[SBLOCK];
-            const uint32_t carry_lo = sh_carry_lo, carry_cnt = sh_carry_cnt;
-            for (uint32_t h = tid; h < nh; h += SBLOCK) {
-                int lo2 = 0, hi2 = SBLOCK;   // last k with it_pre[k] <= h
-                while (hi2 - lo2 > 1) {
-                    const int mid = (lo2 + hi2) >> 1;
-                    if (it_pre[mid] <= h) lo2 = mid; else hi2 = mid;
+            const int lane = tid & 63, wid = tid >> 6;
+            uint32_t *wqp = hq_pos[wid];
+            uint8_t *wqk = hq_k[wid];
+            for (uint32_t hb0 = 0; hb0 < nh; hb0 += SBLOCK * HBATCH) {
+                // pass A: HBATCH hits per lane with their loads in flight
+                // together; drop other keys, other samples and hits the
+                // sequence pre-test proves non-canonical (the s bases before
+                // them equal and unambiguous, no transcript start in
+                // (pos - s, pos]: the full test below would reject them)
+                uint32_t hk[HBATCH];
+                uint64_t hev[HBATCH], hsw[HBATCH], hsm[HBATCH], hbw[HBATCH];
+                bool live[HBATCH];
+#pragma unroll
+                for (int j = 0; j < HBATCH; j++) {
+                    const uint32_t h = hb0 + (uint32_t)j * SBLOCK + (uint32_t)tid;
+                    live[j] = h < nh;
+                    hk[j] = live[j] ? (uint32_t)run_of(it_pre, h) : 0u;
+                    hev[j] = live[j] ? ix.ent[it_lo[hk[j]] + (h - it_pre[hk[j]])] : 0ull;
                 }
-                const int k = lo2;
-                const uint64_t ev = ix.ent[it_lo[k] + (h - it_pre[k])];
-                const uint32_t pos = (uint32_t)ev;
-                const uint32_t inf = it_info[k];
-                const int p = (int)(inf >> 8);
-                if (join && p >= stride) {
-                    // the maximal run reaches back to p - s iff the previous
-                    // word hits position pos - s (an indexed window never
-                    // crosses a transcript boundary, so then off >= s too)
-                    uint32_t plo = k ? it_lo[k - 1] : carry_lo, pcnt = k ? it_cnt[k - 1] : carry_cnt;
-                    const uint32_t tp = pos - (uint32_t)stride;
-                    while (pcnt > 0) {
-                        const uint32_t half = pcnt >> 1;
-                        if ((uint32_t)ix.ent[plo + half] < tp) {
-                            plo += half + 1;
-                            pcnt -= half + 1;
-                        } else {
-                            pcnt = half;
-                        }
+#pragma unroll
+                for (int j = 0; j < HBATCH; j++) {
+                    const uint32_t pos = (uint32_t)hev[j];
+                    live[j] = live[j] && (uint32_t)(hev[j] >> 32) == it_key[hk[j]] && pos >= pb0 && pos < pb1;
+                    hsw[j] = hsm[j] = hbw[j] = 0;
+                    if (live[j] && fast && (int)(it_info[hk[j]] >> 8) >= stride) {
+                        hsw[j] = win_s(db.F, (int64_t)pos - 32) ^ it_qlw[hk[j]];
+                        if (AMB) hsm[j] = win_s(db.AF, (int64_t)pos - 32) | it_qlm[hk[j]];
+                        hbw[j] = win_bits(db.txstart, (int64_t)pos - 63);
+                    } else {
+                        hsw[j] = ~0ull;
                     }
-                    const uint32_t pend = k ? it_lo[k - 1] + it_cnt[k - 1] : carry_lo + carry_cnt;
-                    if (plo < pend && (uint32_t)ix.ent[plo] == tp) continue;
                 }
-                TxInfo st;
-                const uint32_t stx = tx_of_pos(db, ix, pos, st);
-                if (!((tm[st.sample >> 6] >> (st.sample & 63)) & 1)) continue;
-                const int off = (int)(pos - (uint32_t)st.start);
-                const uint32_t ii = inf & 127;
-                const int strand = (inf >> 7) & 1;
-                QGeo qg = {iso_start[ii], (int)iso_len[ii]};
-                const int maxl = min(min(p, off), stride);
-                const uint64_t *QL = strand ? db.F : db.RC;
-                const uint64_t *QLM = strand ? db.AF : db.ARC;
-                const int l = lcp<AMB>(QL, QLM, qrev_pos(qg, strand, total, p), db.RC, db.ARC,
-                                       total - st.start - (uint64_t)off, maxl);
-                if (l >= stride) continue;   // not canonical
-                const uint64_t *QR = strand ? db.RC : db.F;
-                const uint64_t *QRM = strand ? db.ARC : db.AF;
-                const int maxr = min(qg.Lq - p - W16, (int)st.len - off - W16);
-                const int r = lcp<AMB>(QR, QRM, qfwd_pos(qg, strand, total, p + W16), db.F, db.AF,
-                                       st.start + (uint64_t)off + W16, maxr);
-                const int len = l + W16 + r;
-                if (len < P.word) continue;
-                const uint32_t slot = atomicAdd(&sh_nseed, 1u);
-                if (slot < (uint32_t)SEED_CAP) {
-                    LSeed sd;
-                    sd.k1 = ((uint64_t)ii << 57) | ((uint64_t)strand << 56) | ((uint64_t)stx << 24) |
-                            (uint64_t)(uint32_t)(p - l);
-                    sd.y = (uint32_t)(off - l);
-                    sd.len = (uint32_t)len;
-                    seeds[slot] = sd;
-                } else {
-                    atomicOr(&sh_flags, 1u);
+                uint32_t qn = 0;
+#pragma unroll
+                for (int j = 0; j < HBATCH; j++) {
+                    if (live[j] && (((hsw[j] | hsm[j]) >> (64 - 2 * stride)) == 0) && ((hbw[j] >> (64 - stride)) == 0))
+                        live[j] = false;
+                    const uint64_t m = __ballot(live[j]);
+                    if (live[j]) {
+                        const uint32_t q = qn + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                        wqp[q] = (uint32_t)hev[j];
+                        wqk[q] = (uint8_t)hk[j];
+                    }
+                    qn += (uint32_t)__popcll(m);
                 }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                // pass B: the full canonical test and the seed of each queued hit
+                for (uint32_t q = (uint32_t)lane; q < qn; q += 64) {
+                    const uint32_t pos = wqp[q];
+                    const int k = wqk[q];
+                    const uint32_t inf = it_info[k];
+                    const int p = (int)(inf >> 8);
+                    TxInfo st;
+                    const uint32_t stx = tx_of_pos(db, ix, pos, st);
+                    if (!((tm[st.sample >> 6] >> (st.sample & 63)) & 1)) continue;
+                    const int off = (int)(pos - (uint32_t)st.start);
+                    const uint32_t ii = inf & 127;
+                    const int strand = (inf >> 7) & 1;
+                    QGeo qg = {iso_start[ii], (int)iso_len[ii]};
+                    const int maxl = min(min(p, off), stride);
+                    const uint64_t *QL = strand ? db.F : db.RC;
+                    const uint64_t *QLM = strand ? db.AF : db.ARC;
+                    const int l = lcp<AMB>(QL, QLM, qrev_pos(qg, strand, total, p), db.RC, db.ARC,
+                                           total - st.start - (uint64_t)off, maxl);
+                    if (l >= stride) continue;   // not canonical
+                    const uint64_t *QR = strand ? db.RC : db.F;
+                    const uint64_t *QRM = strand ? db.ARC : db.AF;
+                    const int maxr = min(qg.Lq - p - W16, (int)st.len - off - W16);
+                    const int r = lcp<AMB>(QR, QRM, qfwd_pos(qg, strand, total, p + W16), db.F, db.AF,
+                                           st.start + (uint64_t)off + W16, maxr);
+                    const int len = l + W16 + r;
+                    if (len < P.word) continue;
+                    const uint32_t slot = atomicAdd(&sh_nseed, 1u);
+                    if (slot < (uint32_t)SEED_CAP) {
+                        LSeed sd;
+                        sd.k1 = ((uint64_t)ii << 57) | ((uint64_t)strand << 56) | ((uint64_t)stx << 24) |
+                                (uint64_t)(uint32_t)(p - l);
+                        sd.y = (uint32_t)(off - l);
+                        sd.len = (uint32_t)len;
+                        seeds[slot] = sd;
+                    } else {
+                        atomicOr(&sh_flags, 1u);
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
             }
             __syncthreads();
-            if (tid == SBLOCK - 1) {
-                sh_carry_lo = lo;
-                sh_carry_cnt = cnt;
-            }
         }
         if (sh_flags & 1u) {   // too many seeds: fewer subject samples per pass
             if (T1 - T0 == 1) {
@@ -282,6 +328,7 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
             __syncthreads();
             continue;
         }
+        SEED_TICK(2);
         const uint32_t nseed = sh_nseed;
         // bitonic sort by (k1, y)
         uint32_t np2 = 1;
@@ -308,6 +355,7 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
                 __syncthreads();
             }
         }
+        SEED_TICK(3);
         // candidates (segments of equal (iso, strand, gtx)), block-parallel
         uint32_t nseg = 0;
         for (uint32_t c0 = 0; c0 < nseed; c0 += SBLOCK) {
@@ -384,7 +432,13 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
         T0 = T1;
         T1 = N;
         __syncthreads();
+        SEED_TICK(4);
     }
+#ifdef RC_ROW_TIMING
+    if (tid == 0 && P.prof)
+        for (int i = 0; i < 5; i++) atomicAdd(&P.prof[i], tph[i]);
+#endif
+#undef SEED_TICK
 }
 
 // ------------------------------------------------------------------------
@@ -828,15 +882,6 @@ __device__ __forceinline__ int slide_fwd(const uint32_t *S, uint32_t pa, uint32_
     return maxn > 0 ? maxn : 0;
 }
 
-// 32 bases at a signed base position of a packed global array (the arrays
-// carry two zero words in front, so p >= -64 stays in bounds)
-__device__ __forceinline__ uint64_t win_s(const uint64_t *__restrict__ a, int64_t p)
-{
-    const int64_t w = p >> 5;
-    const unsigned sh = (unsigned)(p & 31) * 2u;
-    const uint64_t lo = a[w], hi = a[w + 1];
-    return (lo >> sh) | ((hi << 1) << (63u - sh));
-}
 
 // per-row bookkeeping in LDS: the candidate record (CAND_DWORDS dwords) and state
 enum { RM_REC = 0, RM_CLO = CAND_DWORDS, RM_CHI, RM_QB, RM_TB, RM_X, RM_Y, RM_LEN,

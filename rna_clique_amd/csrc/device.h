@@ -56,6 +56,7 @@ struct Db {
     const uint32_t *sample_gene_begin;       // n_samples + 1
     const uint32_t *sample_tx_begin;         // n_samples + 1
     const uint64_t *sample_pos_begin;        // n_samples + 1: first base of each sample
+    const uint64_t *txstart;                 // bit per base: 1 where a transcript starts (+1 guard word)
     int32_t n_samples;
 };
 
@@ -115,6 +116,7 @@ struct SeedParams {
     uint32_t *gc_off, *gc_cnt;    // [(g - gene_begin) * N + T] candidates of (gene, sample)
     const uint64_t *tmask;        // [n_samples][4] subject samples (> query sample) of this shard
     unsigned int *status;         // bit 0 overflow, bit 1 gene limit
+    unsigned long long *prof;     // RC_ROW_TIMING builds: block cycles per phase
 };
 
 // extend_kernel: one wave per candidate, greedy X-drop, purge, e-value cut.
@@ -244,6 +246,25 @@ __device__ __forceinline__ int lcp(const uint64_t *__restrict__ A, const uint64_
         return n < maxn ? n : maxn;
     }
     return maxn > 0 ? maxn : 0;
+}
+
+// 32 bases at a signed base position (arrays carry two zero words in front,
+// so p >= -64 stays in bounds)
+__device__ __forceinline__ uint64_t win_s(const uint64_t *__restrict__ a, int64_t p)
+{
+    const int64_t w = p >> 5;
+    const unsigned sh = (unsigned)(p & 31) * 2u;
+    const uint64_t lo = a[w], hi = a[w + 1];
+    return (lo >> sh) | ((hi << 1) << (63u - sh));
+}
+
+// 64 bits of a bit array starting at signed bit b (b >= -64: one guard word in front)
+__device__ __forceinline__ uint64_t win_bits(const uint64_t *__restrict__ a, int64_t b)
+{
+    const int64_t w = b >> 6;
+    const unsigned sh = (unsigned)(b & 63);
+    const uint64_t lo = a[w], hi = a[w + 1];
+    return (lo >> sh) | ((hi << 1) << (63u - sh));
 }
 
 __device__ __forceinline__ uint64_t rev2(uint64_t x)

@@ -231,7 +231,8 @@ struct rc_engine {
     DBuf<uint64_t> d_kpos_off, d_kcnt;
     DBuf<uint64_t> d_ent, d_ent2;   // (k-mer << 32 | position), unsorted / sorted
     DBuf<uint32_t> d_bucket, d_pos_tx;
-    DBuf<uint64_t> d_sample_pos;
+    DBuf<uint64_t> d_sample_pos, d_txstart;
+    DBuf<unsigned long long> d_prof;
     DBuf<uint8_t> d_tmp;
     DBuf<int32_t> d_thr, d_bits10;
     DBuf<DHsp> d_hsp;
@@ -536,6 +537,13 @@ static int upload(rc_engine *e)
         for (int si = 0; si <= N; si++) spos[si] = si < N ? e->tx_start[e->sample_tx_begin[si]] : total;
         CHK(up(e->d_sample_pos, spos));
     }
+    // transcript-start bit per base, one guard word in front and two behind
+    std::vector<uint64_t> txb((total >> 6) + 4, 0);
+    for (uint32_t t = 0; t < n_tx; t++) {
+        const uint64_t p = e->tx_start[t] + 64;
+        txb[p >> 6] |= 1ull << (p & 63);
+    }
+    CHK(up(e->d_txstart, txb));
     e->n_kpos = koff[n_tx];   // upper bound; exact count for the no-ambiguity case
     if (e->n_kpos > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "more than 2^32 seed positions on one GPU");
     // statistics tables
@@ -622,6 +630,7 @@ static Db make_db(rc_engine *e)
     db.sample_gene_begin = e->d_sample_gene_begin.p;
     db.sample_tx_begin = e->d_sample_tx_begin.p;
     db.sample_pos_begin = e->d_sample_pos.p;
+    db.txstart = e->d_txstart.p + 1;
     db.n_samples = (int32_t)e->samples.size();
     return db;
 }
@@ -778,6 +787,9 @@ static int do_align(rc_engine *e)
         S.gc_cnt = e->d_gc_cnt.p;
         S.tmask = e->d_tmask.p;
         S.status = e->d_status.p;
+        CHK(e->d_prof.ensure(8));
+        HIPCHK(hipMemsetAsync(e->d_prof.p, 0, 8 * sizeof(unsigned long long), e->st));
+        S.prof = e->d_prof.p;
         HIPCHK(hipEventRecord(e->ev[3], e->st));
         launch_seed(e->has_amb, db, ix, S, e->st);
         HIPCHK(hipGetLastError());
@@ -867,8 +879,13 @@ static int do_align(rc_engine *e)
         e->tm.ext_calls = (double)ctr[1];
         e->tm.ext_fullband = (double)ctr[3];
         e->tm.ext_deferred = (double)ctr[5];
-        if (ctr[8] || ctr[9])   // row kernel built with RC_ROW_TIMING: wave cycles in transitions / steps
+        if (ctr[8] || ctr[9]) {   // built with RC_ROW_TIMING: wave cycles in transitions / steps
             fprintf(stderr, "row kernel wave-cycles: transitions %.4g steps %.4g\n", (double)ctr[8], (double)ctr[9]);
+            unsigned long long pr[8];
+            HIPCHK(hipMemcpy(pr, e->d_prof.p, sizeof pr, hipMemcpyDeviceToHost));
+            fprintf(stderr, "seed kernel block-cycles: words %.4g scan %.4g hits %.4g sort %.4g write %.4g\n",
+                    (double)pr[0], (double)pr[1], (double)pr[2], (double)pr[3], (double)pr[4]);
+        }
         if (!(status & 1u)) break;
         unsigned long long bovn = 0;
         HIPCHK(hipMemcpy(&bovn, e->d_count.p + 12, sizeof bovn, hipMemcpyDeviceToHost));
