@@ -559,8 +559,12 @@ static int upload(rc_engine *e)
     CHK(e->d_status.ensure(4));
     CHK(e->d_count.ensure(16));
     HIPCHK(hipStreamSynchronize(e->st));
+    // bucket table over the top k-mer bits: about one bucket per indexed
+    // position, capped (RC_INDEX_BITS_MAX) so that the table stays small
+    const char *ibv = getenv("RC_INDEX_BITS_MAX");
+    const int bmax = ibv ? std::max(16, std::min(30, atoi(ibv))) : 30;
     int bits = 16;
-    while (bits < 30 && (1ull << bits) < e->n_kpos) bits++;
+    while (bits < bmax && (1ull << bits) < e->n_kpos) bits++;
     e->index_bits = bits;
     e->uploaded = true;
     return RC_OK;

@@ -213,16 +213,27 @@ __device__ __forceinline__ uint32_t desc_rank(const DHsp *h, uint32_t off, uint3
 
 __global__ void rbh_kernel(RbhParams P, int pass)
 {
-    // items [item0, item0 + n_items) of this shard; per-item arrays are local
-    for (uint64_t li = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; li < P.n_items;
-         li += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t item = P.item0 + li;
-        int lo = 0, hi = P.n_pairs;
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (P.pair_item_begin[mid] <= item) lo = mid; else hi = mid;
+    // items [item0, item0 + n_items) of this shard; per-item arrays are local.
+    // The pair of an item: one binary search per block (its first item), then
+    // a short walk (a block's 256 items span one or two pairs)
+    __shared__ int sh_pair;
+    for (uint64_t lb = blockIdx.x * (uint64_t)blockDim.x; lb < P.n_items; lb += (uint64_t)gridDim.x * blockDim.x) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint64_t item0 = P.item0 + lb;
+            int lo = 0, hi = P.n_pairs;
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (P.pair_item_begin[mid] <= item0) lo = mid; else hi = mid;
+            }
+            sh_pair = lo;
         }
-        const int pr = lo;
+        __syncthreads();
+        const uint64_t li = lb + threadIdx.x;
+        if (li >= P.n_items) continue;
+        const uint64_t item = P.item0 + li;
+        int pr = sh_pair;
+        while (pr + 1 < P.n_pairs && P.pair_item_begin[pr + 1] <= item) pr++;
         const int A = P.pair_a[pr], B = P.pair_b[pr];
         const uint32_t b = P.sample_gene_begin[B] + (uint32_t)(item - P.pair_item_begin[pr]);
         const int N = P.N;
