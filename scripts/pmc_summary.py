@@ -15,7 +15,7 @@ import sys
 
 
 def short(name):
-    for k in ("seed_kernel", "extend_kernel", "rbh_kernel", "kmer_fill", "radix_sort", "pack_fwd",
+    for k in ("seed_kernel", "extend_rows_kernel", "ext_finish_kernel", "extend_kernel", "rbh_kernel", "kmer_fill", "radix_sort", "pack_fwd",
               "pack_rc", "bucket_fill", "mirror_scatter", "mirror_sort", "group_count", "group_write",
               "cc_hook", "cc_count", "pair_sums"):
         if k in name:
@@ -33,13 +33,13 @@ def main(src, dst, commit=None):
     out = {"source": src, "commit": commit, "note": "per bench step (1 step, C3); FETCH_SIZE/WRITE_SIZE KiB",
            "kernels": {k: dict(v) for k, v in agg.items()}}
     tb = 0.0
-    for k in ("seed_kernel", "extend_kernel"):
+    for k in ("seed_kernel", "extend_rows_kernel", "extend_kernel", "ext_finish_kernel"):
         v = agg.get(k, {})
         tb += 2 * 1024 * v.get("FETCH_SIZE", 0.0) + 1024 * v.get("WRITE_SIZE", 0.0)
     out["traffic_bytes_seed_extend"] = int(tb)
     with open(dst, "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
-    print(json.dumps({k: out["kernels"].get(k) for k in ("seed_kernel", "extend_kernel")}, indent=1))
+    print(json.dumps({k: out["kernels"].get(k) for k in ("seed_kernel", "extend_rows_kernel")}, indent=1))
     print("traffic_bytes_seed_extend", out["traffic_bytes_seed_extend"])
 
 
