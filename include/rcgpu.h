@@ -167,8 +167,13 @@ int rc_pair_rows(rc_engine *eng, int32_t s1, int32_t s2, rc_row *buf, uint64_t c
 int rc_graph_stats(rc_engine *eng, rc_stats *stats);
 int rc_edges(rc_engine *eng, rc_edge *buf, uint64_t cap, uint64_t *n);
 int rc_ideal_nodes(rc_engine *eng, int32_t *sample, int32_t *gene, uint64_t cap, uint64_t *n);
-/* num/den: n_samples x n_samples row-major (sample ids), 0 on the diagonal. */
+/* num/den: n_samples x n_samples row-major (sample ids), 0 on the diagonal.
+ * rc_pair_sums: rows restricted to ideal components (SampleSimilarity,
+ * filtered_distance.py:234-247); rc_pair_sums_unfiltered: every row of the
+ * pair's gene matches table (UnfilteredSimilarity, unfiltered_distance.py:9-16,
+ * similarity_computer.py:21-42). */
 int rc_pair_sums(rc_engine *eng, int64_t *num, int64_t *den);
+int rc_pair_sums_unfiltered(rc_engine *eng, int64_t *num, int64_t *den);
 /* order[n]: sample ids in output order; out: n x n row-major distances.
  * Returns RC_E_NO_IDEAL when some pair has no ideal rows. */
 int rc_distance(rc_engine *eng, const int32_t *order, double *out);

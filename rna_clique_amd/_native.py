@@ -112,6 +112,7 @@ SIGNATURES = {
     "rc_edges": (ctypes.c_int, [VP, VP, ctypes.c_uint64, P(ctypes.c_uint64)]),
     "rc_ideal_nodes": (ctypes.c_int, [VP, VP, VP, ctypes.c_uint64, P(ctypes.c_uint64)]),
     "rc_pair_sums": (ctypes.c_int, [VP, VP, VP]),
+    "rc_pair_sums_unfiltered": (ctypes.c_int, [VP, VP, VP]),
     "rc_distance": (ctypes.c_int, [VP, VP, VP]),
     "rc_timings": (ctypes.c_int, [VP, P(RcTiming)]),
     "rc_fasta_open": (ctypes.c_int, [ctypes.c_char_p, P(VP)]),

@@ -36,7 +36,7 @@ void launch_gather_rows(const DHsp *, const DRow *, uint64_t, DHsp *, hipStream_
 void launch_cc(const DEdge *, uint64_t, uint32_t, const int32_t *, int, uint32_t *, uint32_t *, uint32_t *,
                uint32_t *, uint32_t *, uint8_t *, unsigned long long *, hipStream_t);
 void launch_pair_sums(const DEdge *, uint64_t, const uint32_t *, const uint8_t *, unsigned long long *,
-                      unsigned long long *, hipStream_t);
+                      unsigned long long *, unsigned long long *, unsigned long long *, hipStream_t);
 void launch_distance(const unsigned long long *, const unsigned long long *, const int32_t *, const int32_t *,
                      int, double *, unsigned int *, hipStream_t);
 }  // namespace rcg
@@ -259,12 +259,12 @@ struct rc_engine {
     uint64_t n_rows = 0, n_edges = 0, n_hsps = 0, n_seeds = 0, n_cands = 0;
     DBuf<uint32_t> d_parent, d_present, d_cnodes, d_cedges, d_sample_present;
     DBuf<uint8_t> d_ideal;
-    DBuf<unsigned long long> d_stats, d_num, d_den;
+    DBuf<unsigned long long> d_stats, d_num, d_den, d_num_all, d_den_all;
     DBuf<int32_t> d_order;
     DBuf<double> d_dist;
 
     // host results
-    std::vector<unsigned long long> h_num, h_den, h_stats;
+    std::vector<unsigned long long> h_num, h_den, h_num_all, h_den_all, h_stats;
     rc_timing tm{};
     hipEvent_t ev[16] = {};
 
@@ -1064,16 +1064,25 @@ static int do_graph(rc_engine *e)
     HIPCHK(hipEventRecord(e->ev[7], e->st));
     CHK(e->d_num.ensure(np));
     CHK(e->d_den.ensure(np));
+    CHK(e->d_num_all.ensure(np));
+    CHK(e->d_den_all.ensure(np));
     HIPCHK(hipMemsetAsync(e->d_num.p, 0, np * 8, e->st));
     HIPCHK(hipMemsetAsync(e->d_den.p, 0, np * 8, e->st));
-    launch_pair_sums(e->d_edges.p, e->n_edges, e->d_parent.p, e->d_ideal.p, e->d_num.p, e->d_den.p, e->st);
+    HIPCHK(hipMemsetAsync(e->d_num_all.p, 0, np * 8, e->st));
+    HIPCHK(hipMemsetAsync(e->d_den_all.p, 0, np * 8, e->st));
+    launch_pair_sums(e->d_edges.p, e->n_edges, e->d_parent.p, e->d_ideal.p, e->d_num.p, e->d_den.p,
+                     e->d_num_all.p, e->d_den_all.p, e->st);
     HIPCHK(hipGetLastError());
     e->h_num.assign(np, 0);
     e->h_den.assign(np, 0);
+    e->h_num_all.assign(np, 0);
+    e->h_den_all.assign(np, 0);
     e->h_stats.assign(8, 0);
     if (np) {
         HIPCHK(hipMemcpyAsync(e->h_num.data(), e->d_num.p, np * 8, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipMemcpyAsync(e->h_den.data(), e->d_den.p, np * 8, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipMemcpyAsync(e->h_num_all.data(), e->d_num_all.p, np * 8, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipMemcpyAsync(e->h_den_all.data(), e->d_den_all.p, np * 8, hipMemcpyDeviceToHost, e->st));
     }
     HIPCHK(hipMemcpyAsync(e->h_stats.data(), e->d_stats.p, 8 * 8, hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipEventRecord(e->ev[8], e->st));
@@ -1300,6 +1309,27 @@ int rc_pair_sums(rc_engine *e, int64_t *num, int64_t *den)
             const int p = e->pair_index[a * N + b];
             num[a * N + b] = (int64_t)e->h_num[p];
             den[a * N + b] = (int64_t)e->h_den[p];
+        }
+    return RC_OK;
+}
+
+// Unfiltered sums: every gene matches table row of the pair
+// (UnfilteredSimilarity, unfiltered_distance.py:9-16 over similarities_from_dfs,
+// similarity_computer.py:21-42).
+int rc_pair_sums_unfiltered(rc_engine *e, int64_t *num, int64_t *den)
+{
+    if (!e || !num || !den) return fail(RC_E_ARG, "null argument");
+    if (!e->finished) return fail(RC_E_STATE, "no results yet");
+    const int N = (int)e->samples.size();
+    for (int a = 0; a < N; a++)
+        for (int b = 0; b < N; b++) {
+            if (a == b) {
+                num[a * N + b] = den[a * N + b] = 0;
+                continue;
+            }
+            const int p = e->pair_index[a * N + b];
+            num[a * N + b] = (int64_t)e->h_num_all[p];
+            den[a * N + b] = (int64_t)e->h_den_all[p];
         }
     return RC_OK;
 }

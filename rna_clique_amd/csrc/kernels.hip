@@ -563,23 +563,29 @@ __global__ void cc_ideal_kernel(const uint32_t *parent, const uint32_t *present,
 
 // restricted sums per pair (filtered_distance.py:66-124 + similarity_computer.py:37-41)
 __global__ void pair_sums_kernel(const DEdge *edges, uint64_t n_edges, const uint32_t *parent,
-                                 const uint8_t *ideal, unsigned long long *num, unsigned long long *den)
+                                 const uint8_t *ideal, unsigned long long *num, unsigned long long *den,
+                                 unsigned long long *num_all, unsigned long long *den_all)
 {
-    // Edges are stored pair-major, so a wave usually sees one pair: reduce in
-    // registers and issue one atomic per wave; mixed waves fall back to lanes.
+    // Restricted sums (edges inside ideal components: SampleSimilarity,
+    // filtered_distance.py:234-247) and unfiltered sums (every edge:
+    // UnfilteredSimilarity, unfiltered_distance.py:9-16). Edges are stored
+    // pair-major, so a wave usually sees one pair: reduce in registers and
+    // issue one atomic per sum per wave; mixed waves fall back to lanes.
     const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t start = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     const uint64_t iters = (n_edges + nt - 1) / nt;
     for (uint64_t it = 0; it < iters; it++) {
         const uint64_t e = start + it * nt;
         uint32_t pair = 0xFFFFFFFFu;
-        unsigned long long a = 0, b = 0;
+        unsigned long long a = 0, b = 0, ua = 0, ub = 0;
         if (e < n_edges) {
             const DEdge ed = edges[e];
             pair = ed.pair;
+            ua = (unsigned long long)ed.nident;
+            ub = (unsigned long long)ed.den;
             if (ideal[parent[ed.a]]) {
-                a = (unsigned long long)ed.nident;
-                b = (unsigned long long)ed.den;
+                a = ua;
+                b = ub;
             }
         }
         const uint32_t p0 = __shfl(pair, 0);
@@ -588,14 +594,28 @@ __global__ void pair_sums_kernel(const DEdge *edges, uint64_t n_edges, const uin
             for (int off = 32; off > 0; off >>= 1) {
                 a += __shfl_xor(a, off);
                 b += __shfl_xor(b, off);
+                ua += __shfl_xor(ua, off);
+                ub += __shfl_xor(ub, off);
             }
-            if ((threadIdx.x & 63) == 0 && p0 != 0xFFFFFFFFu && (a || b)) {
-                atomicAdd(&num[p0], a);
-                atomicAdd(&den[p0], b);
+            if ((threadIdx.x & 63) == 0 && p0 != 0xFFFFFFFFu) {
+                if (a || b) {
+                    atomicAdd(&num[p0], a);
+                    atomicAdd(&den[p0], b);
+                }
+                if (ua || ub) {
+                    atomicAdd(&num_all[p0], ua);
+                    atomicAdd(&den_all[p0], ub);
+                }
             }
-        } else if (pair != 0xFFFFFFFFu && (a || b)) {
-            atomicAdd(&num[pair], a);
-            atomicAdd(&den[pair], b);
+        } else if (pair != 0xFFFFFFFFu) {
+            if (a || b) {
+                atomicAdd(&num[pair], a);
+                atomicAdd(&den[pair], b);
+            }
+            if (ua || ub) {
+                atomicAdd(&num_all[pair], ua);
+                atomicAdd(&den_all[pair], ub);
+            }
         }
     }
 }
@@ -691,11 +711,12 @@ void launch_cc(const DEdge *edges, uint64_t n_edges, uint32_t n_nodes, const int
 }
 
 void launch_pair_sums(const DEdge *edges, uint64_t n_edges, const uint32_t *parent, const uint8_t *ideal,
-                      unsigned long long *num, unsigned long long *den, hipStream_t st)
+                      unsigned long long *num, unsigned long long *den, unsigned long long *num_all,
+                      unsigned long long *den_all, hipStream_t st)
 {
     if (!n_edges) return;
     hipLaunchKernelGGL(pair_sums_kernel, dim3(grid_for(n_edges, 256)), dim3(256), 0, st, edges, n_edges, parent,
-                       ideal, num, den);
+                       ideal, num, den, num_all, den_all);
 }
 
 void launch_distance(const unsigned long long *num, const unsigned long long *den, const int32_t *pair_index,

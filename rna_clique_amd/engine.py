@@ -172,12 +172,15 @@ class Engine:
         nat.check(nat.lib().rc_graph_stats(self._h, ctypes.byref(st)))
         return {k: getattr(st, k) for k, _ in nat.RcStats._fields_ if k != "pad"}
 
-    def pair_sums(self):
+    def pair_sums(self, unfiltered=False):
+        """(num, den) int64 N x N: sums of nident and of length - gaps over the
+        rows of each pair's gene matches table inside ideal components, or
+        over all of them (unfiltered=True)."""
         n = len(self.labels)
         num = np.zeros((n, n), dtype=np.int64)
         den = np.zeros((n, n), dtype=np.int64)
-        nat.check(nat.lib().rc_pair_sums(self._h, num.ctypes.data_as(ctypes.c_void_p),
-                                         den.ctypes.data_as(ctypes.c_void_p)))
+        fn = nat.lib().rc_pair_sums_unfiltered if unfiltered else nat.lib().rc_pair_sums
+        nat.check(fn(self._h, num.ctypes.data_as(ctypes.c_void_p), den.ctypes.data_as(ctypes.c_void_p)))
         return num, den
 
     def distance(self, order=None):

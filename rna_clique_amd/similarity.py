@@ -194,3 +194,121 @@ class SampleSimilarity:
 
     def get_dissimilarity_df(self) -> pd.DataFrame:
         return self._matrix_to_df(self.get_dissimilarity_matrix())
+
+
+def _table_sums(df: pd.DataFrame):
+    """(sum nident, sum length - sum gaps) of one gene matches table, as exact
+    ints (similarities_from_dfs, similarity_computer.py:21-42)."""
+    return int(df["nident"].sum()), int(df["length"].sum() - df["gaps"].sum())
+
+
+class UnfilteredSimilarity:
+    """Similarities from whole gene matches tables, without the ideal-clique
+    filter (unfiltered_distance.py:9-16 over ComparisonSimilarityComputer,
+    similarity_computer.py:44-375).
+
+    Built on a finished engine (the sums come from the GPU's per-pair
+    reduction over every table row, rc_pair_sums_unfiltered) or on tables
+    (`from_dfs` / `from_filenames`: the sums of the given DataFrames). As in
+    the reference, a pair whose table is empty makes `similarities` raise
+    ZeroDivisionError (Fraction(x, 0))."""
+
+    def __init__(self, engine=None, comparison_dfs=None, sample_count=None):
+        if (engine is None) == (comparison_dfs is None):
+            raise ValueError("give an engine or comparison_dfs")
+        self.engine = engine
+        self._comparison_dfs = comparison_dfs
+        self._sample_count = sample_count
+        self._samples = None
+
+    @classmethod
+    def from_dfs(cls, comparison_dfs, sample_count=None):
+        """comparison_dfs: iterable of (pair of sample names, table), or a
+        mapping with such items (the reference's comparison_dfs forms)."""
+        items = comparison_dfs.items() if hasattr(comparison_dfs, "items") else comparison_dfs
+        return cls(comparison_dfs=[(tuple(k), df) for k, df in items], sample_count=sample_count)
+
+    @classmethod
+    def mapping_from_dfs(cls, dfs):
+        """(pair, table) from each table's own qsample/ssample columns
+        (similarity_computer.py:90-115; the first row rather than label 0,
+        see SURVEY.md Q1)."""
+        for df in dfs:
+            yield (str(df["qsample"].iloc[0]), str(df["ssample"].iloc[0])), df
+
+    @classmethod
+    def from_filenames(cls, paths):
+        """Tables written by tables.write_table (this package's own files)."""
+        from .tables import read_table
+        return cls.from_dfs(list(cls.mapping_from_dfs(read_table(p) for p in paths)))
+
+    # ------------------------------------------------------------ numbers
+    def _pair_sums(self):
+        """{(a, b): (num, den)} over unordered sample pairs."""
+        out = PairDict()
+        if self.engine is not None:
+            labels = list(self.engine.labels)
+            num, den = self.engine.pair_sums(unfiltered=True)
+            for a, b in itertools.combinations(range(len(labels)), 2):
+                out[(labels[a], labels[b])] = (int(num[a, b]), int(den[a, b]))
+        else:
+            for (a, b), df in self._comparison_dfs:
+                n, d = _table_sums(df)
+                if (a, b) in out:
+                    n0, d0 = out[(a, b)]
+                    n, d = n0 + n, d0 + d
+                out[(a, b)] = (n, d)
+        return out
+
+    @property
+    def sample_count(self):
+        if self._sample_count is None:
+            self._sample_count = len(self._pair_sums().key_elements())
+        return self._sample_count
+
+    @cached_property
+    def similarities(self) -> PairDict:
+        res = PairDict()
+        for k, (n, d) in self._pair_sums().items():
+            res[k] = Fraction(n, d)   # ZeroDivisionError on an empty table, as the reference
+        self._samples = sorted(res.key_elements())
+        for s in self._samples:
+            res[(s, s)] = 1
+        return res
+
+    similarity_to_dissimilarity = SampleSimilarity.similarity_to_dissimilarity
+
+    def get_similarities(self) -> PairDict:
+        return self.similarities
+
+    def get_dissimilarities(self) -> PairDict:
+        return PairDict({k: self.similarity_to_dissimilarity(v) for k, v in self.similarities.items()})
+
+    @property
+    def samples(self):
+        if self._samples is None:
+            self.similarities
+        return self._samples
+
+    def _pair_dict_to_matrix(self, d) -> np.ndarray:
+        s = self.samples
+        out = np.zeros((len(s), len(s)))
+        for i, a in enumerate(s):
+            for j, b in enumerate(s):
+                out[i, j] = float(d[(a, b)])   # float(Fraction): correctly rounded
+        return out
+
+    def get_similarity_matrix(self) -> np.ndarray:
+        return self._pair_dict_to_matrix(self.similarities)
+
+    def get_dissimilarity_matrix(self) -> np.ndarray:
+        return self._pair_dict_to_matrix(self.get_dissimilarities())
+
+    def _matrix_to_df(self, mat):
+        return pd.DataFrame(mat).set_axis(self.samples, axis=1).set_axis(self.samples, axis=0)
+
+    def get_similarity_df(self) -> pd.DataFrame:
+        return self._matrix_to_df(self.get_similarity_matrix())
+
+    def get_dissimilarity_df(self) -> pd.DataFrame:
+        return self._matrix_to_df(self.get_dissimilarity_matrix())

@@ -89,6 +89,17 @@ def write_table(df: pd.DataFrame, path: Path):
         raise ValueError(f"Could not determine file type for extension {path.suffix}.")
 
 
+def read_table(path: Path) -> pd.DataFrame:
+    """gene_matches_tables.py read_table: a table write_table wrote (.pkl is
+    this package's own pickle output; .h5 needs PyTables)."""
+    path = Path(path)
+    if path.suffix == ".pkl":
+        return pd.read_pickle(path)
+    if path.suffix == ".h5":
+        return pd.read_hdf(path, key="gene_matches")   # needs PyTables
+    raise ValueError(f"Could not determine file type for extension {path.suffix}.")
+
+
 def build_graph(tables):
     """build_graph.py:40-68 over (ssample, qsample, rows) triples or DataFrames:
     per table, the s-nodes, then the q-nodes, then the edges, in row order."""

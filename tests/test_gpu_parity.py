@@ -149,9 +149,56 @@ def test_golden_reference_tables(native):
             labels, mat = eng.distance()
             assert labels == exp["matrix"]["labels"]
             assert np.array_equal(mat, np.array(exp["matrix"]["values"]))
+        # UnfilteredSimilarity (unfiltered_distance.py:9-16) from the GPU sums,
+        # against the reduction restated over the reference's golden tables
+        from rna_clique_amd.similarity import UnfilteredSimilarity
+        from test_oracle_golden import unfiltered_expected
+        usim = UnfilteredSimilarity(eng)
+        want = unfiltered_expected(exp)
+        if want is None:
+            with pytest.raises(ZeroDivisionError):
+                usim.get_dissimilarity_df()
+        else:
+            udf = usim.get_dissimilarity_df()
+            assert [str(x) for x in udf.index] == want["labels"]
+            assert np.array_equal(udf.values, np.array(want["values"]))
         eng.close()
         checked += 1
     assert checked >= 15
+
+
+def test_homolog_finder_single_pair(native, tmp_path):
+    """find_homologs' HomologFinder.get_match_table on two top-genes FASTA
+    files equals the pair's table from a full run (same engine path), and
+    the CLI's Fraction equals the unfiltered sums of that pair."""
+    from fractions import Fraction
+    from rna_clique_amd.find_homologs import HomologFinder, match_table_similarity
+    from rna_clique_amd.simulate import simulate
+    from rna_clique_amd.similarity import UnfilteredSimilarity
+    from rna_clique_amd.tables import pair_table
+    from rna_clique_amd.transcripts import TranscriptID, default_gene_re
+    samples, _ = simulate(2, 90, seed=31, p_iso2=0.2, indel_rate=0.002)
+    paths = []
+    for s in samples:
+        p = tmp_path / f"{s.name}_top.fasta"
+        s.write_fasta(p)
+        paths.append(p)
+    hf = HomologFinder(TranscriptID.parser_from_re(default_gene_re), 1, 1e-99, True)
+    table = hf.get_match_table(paths[0], paths[1])
+    assert list(table.columns[-5:]) == ["qgene", "qiso", "sgene", "siso", "reverse"]
+    assert len(table) > 0
+    eng = _run_sim(samples)
+    full = pair_table(eng, 0, 1)
+    cols = list(table.columns)
+    assert table.index.tolist() == full.index.tolist()
+    assert table[cols].astype(str).values.tolist() == full[cols].astype(str).values.tolist()
+    num, den = eng.pair_sums(unfiltered=True)
+    assert match_table_similarity(table) == Fraction(int(num[0, 1]), int(den[0, 1]))
+    sims = UnfilteredSimilarity(eng).get_similarities()
+    assert sims[(samples[0].name, samples[1].name)] == Fraction(int(num[0, 1]), int(den[0, 1]))
+    dedup = HomologFinder.without_duplicates(table)
+    assert list(dedup.columns) == ["qgene", "sgene"] and len(dedup) <= len(table)
+    eng.close()
 
 
 def test_repeat_runs_identical(native):

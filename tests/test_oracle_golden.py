@@ -2,6 +2,7 @@
 golden fixtures captured by tests/golden/make_golden.py."""
 import json
 import os
+from fractions import Fraction
 
 import pytest
 
@@ -46,6 +47,54 @@ def test_oracle_matches_reference(fx):
         labels, mat = po.distance_matrix(fx["samples"], res["sums"])
         assert labels == exp["matrix"]["labels"]
         assert mat == exp["matrix"]["values"]
+
+
+def unfiltered_expected(exp):
+    """The unfiltered matrix restated from the reference's own golden tables:
+    similarities_from_dfs (similarity_computer.py:21-42) over whole tables,
+    dissimilarity float(1 - Fraction) in sorted label order
+    (similarity_computer.py:216-345). None when a table is empty (the
+    reference's Fraction(x, 0) raises ZeroDivisionError). The reduction is a
+    restatement: the golden file holds the reference's tables and filtered
+    matrix, not its unfiltered one."""
+    sums = {}
+    for key, rows in exp["tables"].items():
+        t1, t2 = key.split("|")
+        n = sum(r[COLS.index("nident")] for r in rows)
+        d = sum(r[COLS.index("length")] for r in rows) - sum(r[COLS.index("gaps")] for r in rows)
+        sums[frozenset((t1, t2))] = (n, d)
+    if any(d == 0 for _, d in sums.values()):
+        return None
+    labels = sorted(set().union(*sums.keys()))
+    vals = [[0.0 if a == b else float(1 - Fraction(*sums[frozenset((a, b))])) for b in labels]
+            for a in labels]
+    return {"labels": labels, "values": vals}
+
+
+@pytest.mark.parametrize("fx", FIX, ids=[f"s{f['seed']}-n{f['top_matches']}-{f['keep_all']}" for f in FIX])
+def test_unfiltered_similarity_on_reference_tables(fx):
+    """UnfilteredSimilarity (unfiltered_distance.py:9-16) over the reference's
+    own tables."""
+    import numpy as np
+    import pandas as pd
+    from rna_clique_amd.similarity import UnfilteredSimilarity
+    exp = fx["expected"]
+    if any(k != "matrix" for k in exp["errors"]):
+        pytest.skip("reference raised: " + ", ".join(exp["errors"].values()))
+    dfs = []
+    for key, rows in exp["tables"].items():
+        t1, t2 = key.split("|")
+        df = pd.DataFrame([r[1:] for r in rows], columns=COLS[1:])
+        dfs.append(((t2, t1), df))
+    usim = UnfilteredSimilarity.from_dfs(dfs)
+    want = unfiltered_expected(exp)
+    if want is None:
+        with pytest.raises(ZeroDivisionError):
+            usim.get_dissimilarity_df()
+    else:
+        df = usim.get_dissimilarity_df()
+        assert [str(x) for x in df.index] == want["labels"]
+        assert np.array_equal(df.values, np.array(want["values"]))
 
 
 def test_reference_quirks_recorded():
