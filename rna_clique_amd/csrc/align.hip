@@ -283,24 +283,50 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
                     const int k = wqk[q];
                     const uint32_t inf = it_info[k];
                     const int p = (int)(inf >> 8);
-                    TxInfo st;
-                    const uint32_t stx = tx_of_pos(db, ix, pos, st);
-                    if (!((tm[st.sample >> 6] >> (st.sample & 63)) & 1)) continue;
-                    const int off = (int)(pos - (uint32_t)st.start);
                     const uint32_t ii = inf & 127;
                     const int strand = (inf >> 7) & 1;
                     QGeo qg = {iso_start[ii], (int)iso_len[ii]};
+                    const uint64_t *QA = strand ? db.RC : db.F;
+                    const uint64_t *QAM = strand ? db.ARC : db.AF;
+                    const uint64_t qp = qfwd_pos(qg, strand, total, p);
+                    // the transcript lookup and the 32-base windows on both sides
+                    // of the word (query and subject) are independent: all their
+                    // loads go out together, the bounds are applied afterwards
+                    TxInfo st;
+                    const uint32_t stx = tx_of_pos(db, ix, pos, st);
+                    uint64_t xl = 0, xr = 0;
+                    if (fast) {
+                        xl = win_s(QA, (int64_t)qp - 32) ^ win_s(db.F, (int64_t)pos - 32);
+                        xr = win(QA, qp + W16) ^ win(db.F, (uint64_t)pos + W16);
+                        if (AMB) {
+                            xl |= win_s(QAM, (int64_t)qp - 32) | win_s(db.AF, (int64_t)pos - 32);
+                            xr |= win(QAM, qp + W16) | win(db.AF, (uint64_t)pos + W16);
+                        }
+                    }
+                    if (!((tm[st.sample >> 6] >> (st.sample & 63)) & 1)) continue;
+                    const int off = (int)(pos - (uint32_t)st.start);
                     const int maxl = min(min(p, off), stride);
-                    const uint64_t *QL = strand ? db.F : db.RC;
-                    const uint64_t *QLM = strand ? db.AF : db.ARC;
-                    const int l = lcp<AMB>(QL, QLM, qrev_pos(qg, strand, total, p), db.RC, db.ARC,
-                                           total - st.start - (uint64_t)off, maxl);
+                    int l;
+                    if (fast) {
+                        // matching bases leftwards from (p - 1, pos - 1): the
+                        // highest differing base of the windows ending there
+                        l = min(xl ? (int)(__builtin_clzll(xl) >> 1) : 32, maxl);
+                    } else {
+                        const uint64_t *QL = strand ? db.F : db.RC;
+                        const uint64_t *QLM = strand ? db.AF : db.ARC;
+                        l = lcp<AMB>(QL, QLM, qrev_pos(qg, strand, total, p), db.RC, db.ARC,
+                                     total - st.start - (uint64_t)off, maxl);
+                    }
                     if (l >= stride) continue;   // not canonical
-                    const uint64_t *QR = strand ? db.RC : db.F;
-                    const uint64_t *QRM = strand ? db.ARC : db.AF;
                     const int maxr = min(qg.Lq - p - W16, (int)st.len - off - W16);
-                    const int r = lcp<AMB>(QR, QRM, qfwd_pos(qg, strand, total, p + W16), db.F, db.AF,
-                                           st.start + (uint64_t)off + W16, maxr);
+                    int r;
+                    if (fast && xr) {
+                        r = min((int)(__builtin_ctzll(xr) >> 1), max(maxr, 0));
+                    } else {
+                        const int r0 = fast ? min(32, max(maxr, 0)) : 0;
+                        r = r0 + lcp<AMB>(QA, QAM, qp + (uint64_t)(W16 + r0), db.F, db.AF,
+                                          st.start + (uint64_t)(off + W16 + r0), maxr - r0);
+                    }
                     const int len = l + W16 + r;
                     if (len < P.word) continue;
                     const uint32_t slot = atomicAdd(&sh_nseed, 1u);
