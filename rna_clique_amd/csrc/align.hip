@@ -169,8 +169,17 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
     // subject samples of this shard: higher-numbered samples only (symmetric
     // spec: the pair's other direction is the mirror image)
     const uint64_t tm[4] = {P.tmask[4 * Q], P.tmask[4 * Q + 1], P.tmask[4 * Q + 2], P.tmask[4 * Q + 3]};
-    int T0 = Q + 1, T1 = N;
-    while (T0 < N) {
+    // the shard's subjects of this query sample: a contiguous sample range
+    // (pairs are numbered subject-major), so hits are filtered by position
+    int Thi = 0, T0 = N;
+    for (int w = 0; w < 4; w++)
+        if (tm[w]) {
+            T0 = min(T0, 64 * w + __builtin_ctzll(tm[w]));
+            Thi = max(Thi, 64 * w + 64 - __builtin_clzll(tm[w]));
+        }
+    T0 = max(T0, Q + 1);
+    int T1 = Thi;
+    while (T0 < Thi) {
         if (tid == 0) {
             sh_nseed = 0;
             sh_flags = 0;
@@ -456,7 +465,7 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
             P.gc_cnt[gi] = tcnt[T];
         }
         T0 = T1;
-        T1 = N;
+        T1 = Thi;
         __syncthreads();
         SEED_TICK(4);
     }

@@ -209,7 +209,8 @@ struct rc_engine {
     int32_t max_len = 0;
     uint64_t n_items = 0;
     int index_bits = 16;
-    uint64_t n_kpos = 0;
+    uint64_t n_kpos = 0, n_index = 0;   // k-mer slots of all samples / entries of this shard's index
+    std::vector<uint64_t> h_koff;       // closed-form k-mer slot prefix per transcript
 
     // external HSPs
     bool external = false;
@@ -231,7 +232,7 @@ struct rc_engine {
     DBuf<uint64_t> d_kpos_off, d_kcnt;
     DBuf<uint64_t> d_ent, d_ent2;   // (k-mer << 32 | position), unsorted / sorted
     DBuf<uint32_t> d_bucket, d_pos_tx;
-    DBuf<uint64_t> d_sample_pos, d_txstart;
+    DBuf<uint64_t> d_sample_pos, d_txstart, d_kpos_rel;
     DBuf<unsigned long long> d_prof;
     DBuf<uint8_t> d_tmp;
     DBuf<int32_t> d_thr, d_bits10;
@@ -450,14 +451,17 @@ static int upload(rc_engine *e)
     for (uint32_t g = 0; g < n_genes; g++)
         if (e->gene_tx_off[g + 1] - e->gene_tx_off[g] > (uint32_t)MAX_ISO)
             return fail(RC_E_LIMIT, "gene " + std::to_string(e->gene_id[g]) + " has more than 127 transcripts");
-    // pairs in itertools.combinations order; items = (pair, gene of the second sample)
+    // pairs (a < b) numbered subject-major -- (0,1), (0,2), (1,2), (0,3), ... --
+    // so that a contiguous range of pairs (a shard) has a contiguous range of
+    // second samples b, whose index is all the shard builds; items = (pair,
+    // gene of b). (Outputs are per pair and do not depend on this numbering.)
     e->pair_a.clear();
     e->pair_b.clear();
     e->pair_item_begin.assign(1, 0);
     e->pair_index.assign((size_t)N * N, -1);
     uint64_t items = 0;
-    for (int a = 0; a < N; a++)
-        for (int b = a + 1; b < N; b++) {
+    for (int b = 0; b < N; b++)
+        for (int a = 0; a < b; a++) {
             e->pair_index[a * N + b] = e->pair_index[b * N + a] = (int32_t)e->pair_a.size();
             e->pair_a.push_back(a);
             e->pair_b.push_back(b);
@@ -521,6 +525,7 @@ static int upload(rc_engine *e)
         koff[t + 1] = koff[t] + (uint64_t)(L >= W16 ? L - W16 + 1 : 0);
     }
     CHK(up(e->d_kpos_off, koff));
+    e->h_koff = koff;
     // base position -> transcript, per 2^POS_TX_SHIFT-base block; first base of each sample
     if (total >= (1ull << 32)) return fail(RC_E_LIMIT, "more than 2^32 bases on one GPU: shard the samples");
     // (host vectors outlive the async copies: the stream is synchronized below)
@@ -580,28 +585,43 @@ static double ev_ms(rc_engine *e, int a, int b)
     return ms;
 }
 
+// The seed index of this shard: every 16-mer position of the samples that are
+// second samples (subjects) of its pairs -- a contiguous sample range, so a
+// contiguous range of transcripts and of k-mer position slots.
 static int build_index(rc_engine *e)
 {
-    const uint32_t n_tx = (uint32_t)e->tx_sample.size();
     const bool amb = e->has_amb;
-    uint64_t npos = e->n_kpos;
+    int slo = (int)e->samples.size(), shi = -1;
+    for (uint64_t p = e->pair0; p < e->pair1; p++) {
+        slo = std::min(slo, (int)e->pair_b[p]);
+        shi = std::max(shi, (int)e->pair_b[p]);
+    }
+    const uint32_t t0 = shi < 0 ? 0 : e->sample_tx_begin[slo];
+    const uint32_t t1 = shi < 0 ? 0 : e->sample_tx_begin[shi + 1];
+    const uint32_t n_tx = t1 - t0;
+    uint64_t npos = e->h_koff[t1] - e->h_koff[t0];
+    uint64_t *ent_base = e->d_ent.p;
+    const uint64_t *offs = e->d_kpos_off.p + t0;   // closed-form slots (no ambiguous bases)
     if (amb) {
         CHK(e->d_kcnt.ensure(n_tx + 1));
         HIPCHK(hipMemsetAsync(e->d_kcnt.p, 0, (n_tx + 1) * sizeof(uint64_t), e->st));
-        if (n_tx) launch_kmer_count(e->d_tx.p, n_tx, e->d_AF.p + FRONT_PAD, e->d_kcnt.p, e->st);
+        if (n_tx) launch_kmer_count(e->d_tx.p + t0, n_tx, e->d_AF.p + FRONT_PAD, e->d_kcnt.p, e->st);
         size_t tmp = 0;
-        HIPCHK(rocprim::exclusive_scan(nullptr, tmp, e->d_kcnt.p, e->d_kpos_off.p, (uint64_t)0, (size_t)n_tx + 1,
+        CHK(e->d_kpos_rel.ensure(n_tx + 1));
+        HIPCHK(rocprim::exclusive_scan(nullptr, tmp, e->d_kcnt.p, e->d_kpos_rel.p, (uint64_t)0, (size_t)n_tx + 1,
                                        rocprim::plus<uint64_t>(), e->st));
         CHK(e->d_tmp.ensure(tmp));
-        HIPCHK(rocprim::exclusive_scan(e->d_tmp.p, tmp, e->d_kcnt.p, e->d_kpos_off.p, (uint64_t)0,
+        HIPCHK(rocprim::exclusive_scan(e->d_tmp.p, tmp, e->d_kcnt.p, e->d_kpos_rel.p, (uint64_t)0,
                                        (size_t)n_tx + 1, rocprim::plus<uint64_t>(), e->st));
-        HIPCHK(hipMemcpyAsync(&npos, e->d_kpos_off.p + n_tx, sizeof(uint64_t), hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipMemcpyAsync(&npos, e->d_kpos_rel.p + n_tx, sizeof(uint64_t), hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipStreamSynchronize(e->st));
+        offs = e->d_kpos_rel.p;
     }
-    CHK(e->d_ent.ensure(npos));
-    CHK(e->d_ent2.ensure(npos));
-    if (n_tx) launch_kmer_fill(amb, e->d_tx.p, n_tx, e->d_F.p + FRONT_PAD, amb ? e->d_AF.p + FRONT_PAD : nullptr,
-                               e->d_kpos_off.p, e->d_ent.p, e->st);
+    CHK(e->d_ent.ensure(std::max<uint64_t>(npos, 1)));
+    CHK(e->d_ent2.ensure(std::max<uint64_t>(npos, 1)));
+    ent_base = amb ? e->d_ent.p : e->d_ent.p - e->h_koff[t0];   // the kernel writes at absolute slots
+    if (n_tx) launch_kmer_fill(amb, e->d_tx.p + t0, n_tx, e->d_F.p + FRONT_PAD, amb ? e->d_AF.p + FRONT_PAD : nullptr,
+                               offs, ent_base, e->st);
     // sort on the k-mer (bits 32..63); the fill order is position order and the
     // onesweep radix sort is stable, so positions stay ascending per k-mer.
     // rocPRIM sorts up to 2^20 items with a merge sort that did not keep that
@@ -614,7 +634,7 @@ static int build_index(rc_engine *e)
     HIPCHK(rocprim::radix_sort_keys(e->d_tmp.p, tmp, e->d_ent.p, e->d_ent2.p, (size_t)npos, bb, 64u, e->st));
     CHK(e->d_bucket.ensure((1ull << e->index_bits) + 1));
     launch_bucket_fill(e->d_ent2.p, npos, e->index_bits, e->d_bucket.p, e->st);
-    e->n_kpos = npos;
+    e->n_index = npos;
     return RC_OK;
 }
 
@@ -1401,17 +1421,19 @@ int rc_import_edges(rc_engine *e, const void *buf, uint64_t n, int on_device)
     return do_graph(e);
 }
 
-// The sample pairs in itertools.combinations order, cut into shard_count
-// contiguous ranges of about equal sequence length (L_a + L_b per pair, the
-// byte model of SURVEY.md §8d): pair p goes to the shard whose share of the
-// total holds the midpoint of p's cost interval.
+// The sample pairs in the engine's subject-major order ((0,1), (0,2), (1,2),
+// (0,3), ...), cut into shard_count contiguous ranges of about equal sequence
+// length (L_a + L_b per pair, the byte model of SURVEY.md §8d): pair p goes to
+// the shard whose share of the total holds the midpoint of p's cost interval.
+// A shard's second samples are then a contiguous sample range, and its seed
+// index covers only those samples.
 int rc_plan_shards(const int64_t *sample_bases, int32_t n_samples, int32_t shard_count, int64_t *pair_first)
 {
     if (!pair_first || shard_count < 1 || n_samples < 0 || (n_samples && !sample_bases))
         return fail(RC_E_ARG, "bad argument");
     std::vector<double> cum(1, 0.0);
-    for (int a = 0; a < n_samples; a++)
-        for (int b = a + 1; b < n_samples; b++)
+    for (int b = 0; b < n_samples; b++)
+        for (int a = 0; a < b; a++)
             cum.push_back(cum.back() + (double)(sample_bases[a] + sample_bases[b]));
     const int64_t np = (int64_t)cum.size() - 1;
     const double tot = cum.back();

@@ -1,10 +1,12 @@
 """Multi-GPU: one engine per GPU, sample pairs sharded, one edge exchange.
 
 SURVEY.md §8e. Every rank loads the same samples. rc_plan_shards cuts the
-C(N,2) pairs (combinations order) into contiguous ranges of equal sequence
-length; each rank aligns its pairs (seed + extend, both directions at once)
-and runs top-N / reciprocal best hits for them, which yields its share of the
-gene matches tables and graph edges. The ideal-clique filter needs the whole
+C(N,2) pairs, numbered subject-major ((0,1), (0,2), (1,2), (0,3), ...), into
+contiguous ranges of equal sequence length, so each rank's second samples are
+a contiguous sample range and its seed index covers only those; each rank
+aligns its pairs (seed + extend, both directions at once) and runs top-N /
+reciprocal best hits for them, which yields its share of the gene matches
+tables and graph edges. The ideal-clique filter needs the whole
 graph, so the edge records (20 B each: two node ids, the pair, and the edge's
 nident and length - gaps sums) are all-gathered once -- over RCCL on GPUs,
 gloo on CPU -- and every rank runs connected components, the ideal filter and

@@ -34,6 +34,7 @@ class Engine:
         self._h = h
         self.labels = []
         self.n_tx = []
+        self.shard_count = int(shard_count)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -89,8 +90,19 @@ class Engine:
     def finish(self):
         nat.check(nat.lib().rc_finish(self._h))
 
+    @staticmethod
+    def pair_order(n):
+        """The engine's pair numbering: (a, b), a < b, subject-major."""
+        return [(a, b) for b in range(n) for a in range(b)]
+
+    def owned_pairs(self):
+        """(a, b) pairs whose tables this shard holds."""
+        first, last = self.shard_pairs()
+        return self.pair_order(len(self.labels))[first:last]
+
     def shard_pairs(self):
-        """[first, last) of this shard's sample pairs in combinations order."""
+        """[first, last) of this shard's sample pairs, numbered subject-major
+        ((0,1), (0,2), (1,2), (0,3), ...; see pair_order)."""
         a, b = ctypes.c_int64(), ctypes.c_int64()
         nat.check(nat.lib().rc_shard_pairs(self._h, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value

@@ -96,10 +96,14 @@ def rna_clique(
     sim = SampleSimilarity(eng, store_dfs=store_dfs)
     from . import distributed
     writer = distributed.world(process_group)[1] == 0
-    if writer and out_dir_2 is not None and table_format != "none":
+    if out_dir_2 is not None and table_format != "none":
+        # every rank writes the tables of the pairs it owns (all of them on one GPU)
         out_dir_2 = Path(out_dir_2)
         out_dir_2.mkdir(parents=True, exist_ok=True)
+        own = set(eng.owned_pairs())
         for a, b in itertools.combinations(range(len(samples)), 2):
+            if (a, b) not in own:
+                continue
             t = pair_table(eng, a, b)
             write_table(t, out_dir_2 / f"{samples[a].name}--{samples[b].name}.{table_format}")
     if writer and output_graph is not None:

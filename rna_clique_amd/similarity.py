@@ -90,7 +90,20 @@ class SampleSimilarity:
 
     @cached_property
     def graph(self):
-        """The gene matches graph (networkx), as build_graph.py:40-68 makes it."""
+        """The gene matches graph (networkx), as build_graph.py:40-68 makes it.
+        A sharded engine holds only its own pairs' tables, but every shard has
+        all graph edges after the exchange: the graph is built from those
+        (same nodes and edges; insertion order by pair, then edge)."""
+        if getattr(self.engine, "shard_count", 1) > 1:
+            import networkx as nx
+            e = self.engine.edges()
+            g = nx.Graph()
+            for r in e.tolist():
+                d = dict(zip(e.dtype.names, r))
+                g.add_edge((self.labels[d["sample_a"]], int(d["gene_a"])),
+                           (self.labels[d["sample_b"]], int(d["gene_b"])))
+            return g
+
         def rows():
             for a, b in self._pairs():
                 yield self.labels[a], self.labels[b], self.engine.pair_rows(a, b)

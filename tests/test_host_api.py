@@ -280,8 +280,14 @@ def test_plan_shards_partitions_pairs(native, n, shards):
     n_pairs = n * (n - 1) // 2
     assert first[0] == 0 and first[-1] == n_pairs
     assert (np.diff(first) >= 0).all()
-    cost = np.array([bases[a] + bases[b] for a, b in itertools.combinations(range(n), 2)])
+    # pairs in the engine's subject-major order: (0,1), (0,2), (1,2), (0,3), ...
+    pairs = [(a, b) for b in range(n) for a in range(b)]
+    cost = np.array([bases[a] + bases[b] for a, b in pairs])
     loads = [cost[first[r]:first[r + 1]].sum() for r in range(shards)]
+    # each shard's second samples form a contiguous range (its index covers only them)
+    for r in range(shards):
+        bs = sorted({pairs[p][1] for p in range(first[r], first[r + 1])})
+        assert bs == list(range(bs[0], bs[-1] + 1)) if bs else True
     if n_pairs >= 4 * shards:
         # contiguous cut at cost midpoints: no shard above its share + one pair
         assert max(loads) <= cost.sum() / shards + cost.max()
