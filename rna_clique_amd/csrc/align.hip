@@ -925,11 +925,19 @@ enum { RM_REC = 0, RM_CLO = CAND_DWORDS, RM_CHI, RM_QB, RM_TB, RM_X, RM_Y, RM_LE
 enum { RC_SOFF = 0, RC_QTX = 1, RC_STX = 2, RC_CNT_STRAND = 3, RC_Q0 = 4, RC_S0 = 6, RC_LQ = 8, RC_LT = 9,
        RC_QSAM = 10, RC_SSAM = 11 };
 enum { HB_QA, HB_QB, HB_SA, HB_SB, HB_SC, HB_D, HB_G, HB_O, HB_NI, HB_N };
-// candidate progress and work cursors of a row
-enum { RS_NH, RS_SI, RS_CB, RS_LEND, RS_SHARD, RS_SHN, RS_N };
+// work cursors of a row
+enum { RS_LEND, RS_SHARD, RS_SHN, RS_N };
 // row actions (transition actions < A_DONE; extending: A_STEP_R / A_STEP_L = their done action + 4)
-enum { A_FETCH, A_SEED, A_RDONE, A_LDONE, A_ABORT, A_DONE, A_STEP_R, A_STEP_L };
+enum { A_FETCH, A_UNUSED, A_RDONE, A_LDONE, A_ABORT, A_DONE, A_STEP_R, A_STEP_L };
+// cand_box record of a first-seed extension: status (0 done, -1 deferred),
+// right (score, i, j, d, gap state), left (same)
+enum { FX_STATUS = 0, FX_R = 1, FX_L = 6 };
 
+// Extension of every candidate's FIRST seed (its smallest (x, y): always
+// extended, RC-megablast spec 3) to the right and to the left. Anything
+// further -- the other seeds' containment, more HSPs, purge, e-values -- is
+// first_finish_kernel's; a candidate that needs more than its first seed goes
+// to extend_kernel whole, as does one whose frontier reaches the sub-band edge.
 template <bool AMB, int RW, int MINW>
 __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtParams P)
 {
@@ -937,16 +945,12 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
     constexpr int RC0 = RW / 2;          // row lane of diagonal 0
     constexpr int NA = AMB ? 8 : 4;      // staged arrays per row: Q, T (raw words), Qrev, Trev (+ masks)
     constexpr int EBIT = 26, OBIT = 13;
-    constexpr int GMASK = 8191;
     extern __shared__ uint64_t rstg[];                    // [RROWS][NA][sw]
     __shared__ unsigned long long sprefix[NSHARD + 1];
-    // per-row state that only transitions touch lives in LDS, one struct per
-    // row addressed off one base register
+    // per-row state that only transitions touch lives in LDS
     struct RowLds {
         int meta[RM_N];
-        int st[RS_N];                    // candidate progress, work cursors
-        int box[MAX_HSP][HB_N];          // kept HSP boxes of the candidate
-        int seed[3][RW];                 // seed chunk: x, y, len
+        int st[RS_N];
     };
     __shared__ RowLds rows_lds[RROWS];
     __shared__ unsigned int rcnt[4];                      // extensions, candidates, overflows
@@ -966,8 +970,6 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
     const uint32_t moff = 128u * (uint32_t)sw;
     RowLds &RL = rows_lds[rs];
     int *meta = RL.meta;
-    int *sxa = RL.seed[0], *sya = RL.seed[1], *sla = RL.seed[2];
-    int (*rbox_row)[HB_N] = RL.box;
     const int X = P.xdrop;
     // candidates come in chunks from a global counter (P.chunk >= 1); the
     // record of the next one is prefetched (one dword per lane) while the
@@ -992,6 +994,13 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
     auto load_rec = [&](uint32_t l) -> int {
         if (l >= ncand || rl >= CAND_DWORDS) return 0;
         return reinterpret_cast<const int *>(P.cands + slot(l, RS_SHN))[rl];
+    };
+    auto defer = [&](uint64_t ci) {   // row-uniform; extend_kernel takes the candidate whole
+        if (rl == 0) {
+            const unsigned long long di = atomicAdd(P.defer_count, 1ull);
+            P.defer[di] = (uint32_t)ci;
+            P.cand_box[ci * BOX_REC + FX_STATUS] = -1;
+        }
     };
     if (rl == 0) {
         RL.st[RS_SHARD] = 0;
@@ -1023,14 +1032,6 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
         d6 = 0;
         if (rl == 0) atomicAdd(&rcnt[0], 1u);
         act = (min(alen, blen) - r0 <= 0) ? done_act : done_act + (A_STEP_R - A_RDONE);
-    };
-    auto seed_chunk = [&](int c0, int ns) {
-        if (c0 + rl < ns) {
-            const GSeed g = P.seeds[(uint32_t)meta[RM_REC + RC_SOFF] + (uint32_t)(c0 + rl)];
-            sxa[rl] = (int)g.x;
-            sya[rl] = (int)g.y;
-            sla[rl] = (int)g.len;
-        }
     };
     // reversed copy of a staged array: word w holds bases L - 1 - 32 w down to
     // L - 32 (w + 1) of the array whose base 0 sits at LDS base position fb
@@ -1076,30 +1077,25 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                 const int nwq = (int)(((q0 & 31) + (uint64_t)Lq) >> 5) + 3;
                 const int nwt = (int)(((s0 & 31) + (uint64_t)Lt) >> 5) + 3;
                 if (nwq > sw || nwt > sw || (Lq >> 5) + 3 > sw || (Lt >> 5) + 3 > sw) {
-                    if (rl == 0) {
-                        const unsigned long long di = atomicAdd(P.defer_count, 1ull);
-                        P.defer[di] = (uint32_t)ci;
-                        P.cand_box[ci * BOX_REC + BOX_NH] = -1;
-                    }
+                    defer(ci);
                     continue;
                 }
-                const int ns = meta[RM_REC + RC_CNT_STRAND] & 0xFFFF;
-                // raw words of query and subject, and the first seed chunk
+                // raw words of query and subject, and the first seed: one round trip
                 const uint64_t *QA = strand ? db.RC : db.F;
                 const uint64_t *qw = QA + (q0 >> 5), *tw = db.F + (s0 >> 5);
                 {
-                    // every load in flight before the first LDS write: one round trip
-                    GSeed g0 = {0, 0, 0};
-                    if (rl < ns) g0 = P.seeds[(uint32_t)meta[RM_REC + RC_SOFF] + (uint32_t)rl];
+                    const GSeed g0 = P.seeds[(uint32_t)meta[RM_REC + RC_SOFF]];
                     const uint64_t a0 = rl < nwq ? qw[rl] : 0ull, a1 = rl + RW < nwq ? qw[rl + RW] : 0ull;
                     const uint64_t b0 = rl < nwt ? tw[rl] : 0ull, b1 = rl + RW < nwt ? tw[rl + RW] : 0ull;
                     if (rl < nwq) stg[rl] = a0;
                     if (rl + RW < nwq) stg[rl + RW] = a1;
                     if (rl < nwt) stg[sw + rl] = b0;
                     if (rl + RW < nwt) stg[sw + rl + RW] = b1;
-                    sxa[rl] = (int)g0.x;
-                    sya[rl] = (int)g0.y;
-                    sla[rl] = (int)g0.len;
+                    if (rl == 0) {
+                        meta[RM_X] = (int)g0.x;
+                        meta[RM_Y] = (int)g0.y;
+                        meta[RM_LEN] = (int)g0.len;
+                    }
                 }
                 for (int w = rl + 2 * RW; w < nwq; w += RW) stg[w] = qw[w];
                 for (int w = rl + 2 * RW; w < nwt; w += RW) stg[sw + w] = tw[w];
@@ -1123,83 +1119,18 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
-                if (rl == 0) {
-                    RL.st[RS_NH] = 0;
-                    RL.st[RS_SI] = 0;
-                    RL.st[RS_CB] = 0;
-                    atomicAdd(&rcnt[1], 1u);
-                }
-                act = A_SEED;
-            } else if (act == A_SEED) {
-                const int ns = meta[RM_REC + RC_CNT_STRAND] & 0xFFFF;
-                const int nh = RL.st[RS_NH], si = RL.st[RS_SI];
-                if (nh >= MAX_HSP || si >= ns) {
-                    // ---- candidate done: its boxes go out; ext_finish_kernel
-                    // purges, applies the e-value cuts and writes the HSPs ----
-                    const uint64_t ci = (uint64_t)(uint32_t)meta[RM_CLO] | ((uint64_t)(uint32_t)meta[RM_CHI] << 32);
-                    const int *flat = &rbox_row[0][0];
-                    int *cbx = P.cand_box + ci * BOX_REC;
-                    if (rl < HB_N) cbx[rl] = flat[rl];
-                    uint32_t obase = 0;
-                    if (nh > 1) {
-                        if (rl == 0) {
-                            const unsigned long long b = atomicAdd(P.box_ovf_count, (unsigned long long)(nh - 1));
-                            if (b + (nh - 1) > P.box_ovf_cap) atomicOr(P.status, 1u);
-                            obase = (uint32_t)b;
-                        }
-                        obase = __shfl(obase, RW * row);
-                        if ((uint64_t)obase + (nh - 1) <= P.box_ovf_cap)
-                            for (int f = rl; f < (nh - 1) * HB_N; f += RW) P.box_ovf[(size_t)obase * HB_N + f] = flat[HB_N + f];
-                    }
-                    if (rl == 0) {
-                        cbx[BOX_NH] = nh;
-                        cbx[BOX_OVF] = (int)obase;
-                    }
-                    act = A_FETCH;
-                    continue;
-                }
-                // next seed not inside a kept box, searched RW at a time
-                const int c0 = si & ~(RW - 1);
-                int cb = RL.st[RS_CB];
-                if (c0 != cb) {
-                    cb = c0;
-                    if (rl == 0) RL.st[RS_CB] = cb;
-                    seed_chunk(cb, ns);
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                }
-                const int idx = cb + rl;
-                const int sx = sxa[rl], sy = sya[rl], sl = sla[rl];
-                bool contained = false;
-                for (int j = 0; j < nh; j++) {
-                    const int *hj = rbox_row[j];
-                    contained |= hj[HB_QA] <= sx && sx + sl <= hj[HB_QB] && hj[HB_SA] <= sy && sy + sl <= hj[HB_SB];
-                }
-                const uint32_t m = rw_mask<RW>(__ballot(idx >= si && idx < ns && !contained), row);
-                if (!m) {
-                    __builtin_amdgcn_wave_barrier();
-                    if (rl == 0) RL.st[RS_SI] = cb + RW;
-                    continue;
-                }
-                const int f = __builtin_ctz(m);
-                const int x = sxa[f], y = sya[f], len = sla[f];
-                if (rl == 0) {
-                    RL.st[RS_SI] = cb + f + 1;
-                    meta[RM_X] = x;
-                    meta[RM_Y] = y;
-                    meta[RM_LEN] = len;
-                }
-                const int Lq = meta[RM_REC + RC_LQ], Lt = meta[RM_REC + RC_LT];
-                pa = (uint32_t)meta[RM_QB] + (uint32_t)(x + len);
+                if (rl == 0) atomicAdd(&rcnt[1], 1u);
+                // right extension from the seed's end
+                const int x = meta[RM_X], y = meta[RM_Y], len = meta[RM_LEN];
+                pa = qb + (uint32_t)(x + len);
                 alen = Lq - (x + len);
-                pb = (uint32_t)meta[RM_TB] + (uint32_t)(y + len);
+                pb = tb + (uint32_t)(y + len);
                 blen = Lt - (y + len);
                 ext_init(A_RDONE);
             } else if (act == A_RDONE || act == A_LDONE) {
                 const int src = RW * row + bl;
                 const int ei = __shfl(wi, src), ed = __shfl(wd, src) / 6, ego = __shfl(wg, src);
                 const int ej = ei - (bl - RC0);
-                const int x = meta[RM_X], y = meta[RM_Y], len = meta[RM_LEN];
                 if (act == A_RDONE) {
                     if (rl == 0) {
                         meta[RM_RSC] = best;
@@ -1210,6 +1141,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                     }
                     // left extension: forward from reversed position L - x
                     // (= base x - 1) of the reversed copies
+                    const int x = meta[RM_X], y = meta[RM_Y];
                     const int Lq = meta[RM_REC + RC_LQ], Lt = meta[RM_REC + RC_LT];
                     pa = bqr + (uint32_t)(Lq - x);
                     alen = x;
@@ -1217,36 +1149,22 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                     blen = y;
                     ext_init(A_LDONE);
                 } else {
-                    const int rsc = meta[RM_RSC], ri = meta[RM_RI], rj = meta[RM_RJ], rd = meta[RM_RD];
-                    const int rgo = meta[RM_RGO];
-                    const int lg = ego & GMASK, lo = (ego >> OBIT) & GMASK;
-                    const int rg = rgo & GMASK, ro = (rgo >> OBIT) & GMASK;
-                    const int nh = RL.st[RS_NH];
-                    if (rl == 0) {
-                        int *hb = rbox_row[nh];
-                        hb[HB_QA] = x - ei;
-                        hb[HB_QB] = x + len + ri;
-                        hb[HB_SA] = y - ej;
-                        hb[HB_SB] = y + len + rj;
-                        hb[HB_SC] = best + 2 * len + rsc;
-                        hb[HB_D] = ed + rd;
-                        hb[HB_G] = lg + rg;
-                        hb[HB_O] = lo + ro;
-                        hb[HB_NI] = len + (ei + ej - 2 * ed + lg) / 2 + (ri + rj - 2 * rd + rg) / 2;
-                        RL.st[RS_NH] = nh + 1;
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    act = A_SEED;
-                }
-            } else {   // A_ABORT: the sub-band overflowed; extend_kernel redoes the candidate
-                if (rl == 0) {
+                    // both results of the first seed: first_finish_kernel builds the box
                     const uint64_t ci = (uint64_t)(uint32_t)meta[RM_CLO] | ((uint64_t)(uint32_t)meta[RM_CHI] << 32);
-                    const unsigned long long di = atomicAdd(P.defer_count, 1ull);
-                    P.defer[di] = (uint32_t)ci;
-                    P.cand_box[ci * BOX_REC + BOX_NH] = -1;
-                    atomicAdd(&rcnt[2], 1u);
+                    int v = 0;
+                    if (rl >= FX_R && rl < FX_R + 5) v = meta[RM_RSC + (rl - FX_R)];
+                    if (rl == FX_L) v = best;
+                    if (rl == FX_L + 1) v = ei;
+                    if (rl == FX_L + 2) v = ej;
+                    if (rl == FX_L + 3) v = ed;
+                    if (rl == FX_L + 4) v = ego;
+                    if (rl < BOX_REC) P.cand_box[ci * BOX_REC + rl] = v;
+                    act = A_FETCH;
                 }
+            } else {   // A_ABORT: the sub-band overflowed
+                const uint64_t ci = (uint64_t)(uint32_t)meta[RM_CLO] | ((uint64_t)(uint32_t)meta[RM_CHI] << 32);
+                defer(ci);
+                if (rl == 0) atomicAdd(&rcnt[2], 1u);
                 act = A_FETCH;
             }
         }
@@ -1321,12 +1239,14 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
     if (threadIdx.x < 3 && P.counters) atomicAdd(&P.counters[1 + threadIdx.x], (unsigned long long)rcnt[threadIdx.x]);
 }
 
-
-// Purge, e-value cuts and HSP records of the candidates extend_rows_kernel
-// finished (its boxes; deferred candidates, BOX_NH < 0, were written by
-// extend_kernel): one thread per candidate, same rules as extend_kernel.
-__global__ __launch_bounds__(256) void ext_finish_kernel(ExtParams P)
+// The candidates' first-seed extensions -> box; the other seeds of the
+// candidate are checked against it (spec 3: a seed inside a found HSP box is
+// not extended). All inside: the candidate has this one HSP -- e-value cuts of
+// both directions, HSP record. Otherwise extend_kernel redoes the candidate
+// whole (the defer list it runs next). One thread per candidate.
+__global__ __launch_bounds__(256) void first_finish_kernel(ExtParams P)
 {
+    constexpr int OBIT = 13, GMASK = 8191;
     for (uint64_t li = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; li < P.n_cand;
          li += (uint64_t)gridDim.x * blockDim.x) {
         int lo = 0, hi = NSHARD;
@@ -1335,78 +1255,51 @@ __global__ __launch_bounds__(256) void ext_finish_kernel(ExtParams P)
             if (P.shard_prefix[mid] <= li) lo = mid; else hi = mid;
         }
         const uint64_t ci = (uint64_t)lo * P.cand_cap + (li - P.shard_prefix[lo]);
-        const int *cbx = P.cand_box + ci * BOX_REC;
-        const int nh = cbx[BOX_NH];
-        if (nh < 0) continue;
-        const int *ovb = P.box_ovf + (size_t)(uint32_t)cbx[BOX_OVF] * HB_N;
-        auto box = [&](int i) -> const int * { return i ? ovb + (size_t)(i - 1) * HB_N : cbx; };
-        // keep unless a start or end point is shared with a better (score
-        // desc, index asc) kept box
-        uint32_t kept = 0;
-        for (int rr = 0; rr < nh; rr++) {
-            int bi = -1, bs = INT_MIN;
-            for (int i = 0; i < nh; i++) {   // rr-th in (score desc, index asc)
-                const int sc = box(i)[HB_SC];
-                int rank = 0;
-                for (int j = 0; j < nh; j++) {
-                    const int sj = box(j)[HB_SC];
-                    rank += (sj > sc || (sj == sc && j < i)) ? 1 : 0;
-                }
-                if (rank == rr) {
-                    bi = i;
-                    bs = sc;
-                }
-            }
-            (void)bs;
-            const int *b = box(bi);
-            bool ok = true;
-            for (int j = 0; j < nh && ok; j++) {
-                if (!((kept >> j) & 1u)) continue;
-                const int *c = box(j);
-                if ((b[HB_QA] == c[HB_QA] && b[HB_SA] == c[HB_SA]) || (b[HB_QB] == c[HB_QB] && b[HB_SB] == c[HB_SB]))
-                    ok = false;
-            }
-            if (ok) kept |= 1u << bi;
-        }
+        const int *fx = P.cand_box + ci * BOX_REC;
+        if (fx[FX_STATUS] < 0) continue;   // deferred by the row kernel
         const Cand cd = P.cands[ci];
+        const GSeed s0 = P.seeds[cd.seed_off];
+        const int x = (int)s0.x, y = (int)s0.y, len = (int)s0.len;
+        const int rsc = fx[FX_R], ri = fx[FX_R + 1], rj = fx[FX_R + 2], rd = fx[FX_R + 3], rgo = fx[FX_R + 4];
+        const int lsc = fx[FX_L], lI = fx[FX_L + 1], lJ = fx[FX_L + 2], ld = fx[FX_L + 3], lgo = fx[FX_L + 4];
+        const int lg = lgo & GMASK, lo2 = (lgo >> OBIT) & GMASK, rg = rgo & GMASK, ro = (rgo >> OBIT) & GMASK;
+        const int bqa = x - lI, bqb = x + len + ri, bsa = y - lJ, bsb = y + len + rj;
+        bool all_in = true;
+        for (uint32_t i = 1; i < cd.seed_cnt && all_in; i++) {
+            const GSeed s = P.seeds[cd.seed_off + i];
+            all_in = bqa <= (int)s.x && (int)(s.x + s.len) <= bqb && bsa <= (int)s.y && (int)(s.y + s.len) <= bsb;
+        }
+        if (!all_in) {
+            const unsigned long long di = atomicAdd(P.defer_count, 1ull);
+            P.defer[di] = (uint32_t)ci;
+            continue;
+        }
+        const int bsc = lsc + 2 * len + rsc, bd = ld + rd, bg = lg + rg, bo = lo2 + ro;
+        const int bni = len + (lI + lJ - 2 * ld + lg) / 2 + (ri + rj - 2 * rd + rg) / 2;
         const int thr_f = P.thr[(size_t)cd.ssam * (size_t)(P.max_len + 1) + (size_t)cd.Lq];
         const int thr_r = P.thr[(size_t)cd.qsam * (size_t)(P.max_len + 1) + (size_t)cd.Lt];
-        int nout = 0;
-        for (int i = 0; i < nh; i++)
-            if (((kept >> i) & 1u) && (box(i)[HB_SC] >= thr_f || box(i)[HB_SC] >= thr_r)) nout++;
-        uint32_t obase = 0;
-        if (nout > 1) {
-            const unsigned long long b = atomicAdd(P.ovf_count, (unsigned long long)(nout - 1));
-            if (b + (nout - 1) > P.ovf_cap) atomicOr(P.status, 1u);
-            obase = (uint32_t)b;
-        }
-        int rk = 0;
-        for (int i = 0; i < nh; i++) {
-            const int *b = box(i);
-            const bool pf = b[HB_SC] >= thr_f, pr = b[HB_SC] >= thr_r;
-            if (!((kept >> i) & 1u) || !(pf || pr)) continue;
+        const bool pf = bsc >= thr_f, pr = bsc >= thr_r;
+        if (pf || pr) {
             DHsp h;
             h.q_tx = cd.q_gtx;
             h.s_tx = cd.s_gtx;
             if (!cd.strand) {
-                h.qstart = b[HB_QA] + 1; h.qend = b[HB_QB]; h.sstart = b[HB_SA] + 1; h.send = b[HB_SB];
+                h.qstart = bqa + 1; h.qend = bqb; h.sstart = bsa + 1; h.send = bsb;
             } else {
-                h.qstart = cd.Lq - b[HB_QB] + 1; h.qend = cd.Lq - b[HB_QA]; h.sstart = b[HB_SB]; h.send = b[HB_SA] + 1;
+                h.qstart = cd.Lq - bqb + 1; h.qend = cd.Lq - bqa; h.sstart = bsb; h.send = bsa + 1;
             }
-            h.gaps = b[HB_G];
-            h.gapopen = b[HB_O];
-            h.mismatch = b[HB_D] - b[HB_G];
-            h.nident = b[HB_NI];
-            h.length = b[HB_NI] + b[HB_D];
-            h.score_half = b[HB_SC];
-            h.bits10 = P.bits10[b[HB_SC]];
-            h.strand = cd.strand | (pf ? HSP_FWD : 0) | (pr ? HSP_REV : 0) | (i << HSP_IDX_SHIFT);
-            if (rk == 0) P.cand_hsp[ci] = h;
-            else if ((uint64_t)obase + (rk - 1) < P.ovf_cap) P.ovf[obase + rk - 1] = h;
-            rk++;
+            h.gaps = bg;
+            h.gapopen = bo;
+            h.mismatch = bd - bg;
+            h.nident = bni;
+            h.length = bni + bd;
+            h.score_half = bsc;
+            h.bits10 = P.bits10[bsc];
+            h.strand = cd.strand | (pf ? HSP_FWD : 0) | (pr ? HSP_REV : 0);
+            P.cand_hsp[ci] = h;
         }
-        P.cand_nh[ci] = (uint8_t)nout;
-        P.cand_ovf[ci] = obase;
+        P.cand_nh[ci] = (uint8_t)((pf || pr) ? 1 : 0);
+        P.cand_ovf[ci] = 0;
     }
 }
 
@@ -1583,9 +1476,10 @@ static unsigned resident_blocks(K kernel, size_t lds)
     return (unsigned)(cus * per_cu);
 }
 
-// Row kernel over all candidates, then extend_kernel over the ones it deferred
-// (sub-band overflow, or transcripts longer than the row staging slot). The
-// deferred count stays on the device: the list launch reads it.
+// Row kernel (first seeds) over all candidates, first_finish_kernel, then
+// extend_kernel over the candidates either deferred (sub-band overflow,
+// transcripts longer than the row staging slot, seeds outside the first box).
+// The deferred count stays on the device: the list launch reads it.
 void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_width, hipStream_t st)
 {
     if (P.n_cand == 0) return;
@@ -1607,6 +1501,9 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
         if (amb) RC_LAUNCH_ROWS(true, 32, ROW_MIN_WAVES); else RC_LAUNCH_ROWS(false, 32, ROW_MIN_WAVES);
     }
 #undef RC_LAUNCH_ROWS
+    uint64_t g = (P.n_cand + 255) / 256;
+    if (g > 65536) g = 65536;
+    hipLaunchKernelGGL(first_finish_kernel, dim3((unsigned)g), dim3(256), 0, st, W);
     if (amb) {
         auto kern = extend_kernel<true>;
         hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W);
@@ -1614,9 +1511,6 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
         auto kern = extend_kernel<false>;
         hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W);
     }
-    uint64_t g = (P.n_cand + 255) / 256;
-    if (g > 65536) g = 65536;
-    hipLaunchKernelGGL(ext_finish_kernel, dim3((unsigned)g), dim3(256), 0, st, W);
 }
 
 void launch_group(const GroupParams &P, int pass, hipStream_t st)
