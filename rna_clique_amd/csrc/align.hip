@@ -219,6 +219,24 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
                     const uint32_t b = key >> (32 - ix.bits);
                     lo = ix.bucket[b];
                     cnt = ix.bucket[b + 1] - lo;
+                    // entries are ascending (k-mer, position) and the subject
+                    // samples a contiguous position range: two lower bounds in
+                    // the bucket (searched together) leave exactly the key's
+                    // entries in [pb0, pb1)
+                    const uint64_t K0 = ((uint64_t)key << 32) | pb0, K1 = ((uint64_t)key << 32) | pb1;
+                    uint32_t b0 = lo, n0 = cnt, b1 = lo, n1 = cnt;
+                    while (n0 | n1) {
+                        const uint32_t h0 = n0 >> 1, h1 = n1 >> 1;
+                        const uint64_t e0 = n0 ? ix.ent[b0 + h0] : 0ull, e1 = n1 ? ix.ent[b1 + h1] : 0ull;
+                        if (n0) {
+                            if (e0 < K0) { b0 += h0 + 1; n0 -= h0 + 1; } else n0 = h0;
+                        }
+                        if (n1) {
+                            if (e1 < K1) { b1 += h1 + 1; n1 -= h1 + 1; } else n1 = h1;
+                        }
+                    }
+                    lo = b0;
+                    cnt = b1 - b0;
                     // the 32 query bases before p (canonical pre-test)
                     if (fast && p >= stride) {
                         qlw = win_s(QA, (int64_t)qp - 32);
@@ -365,14 +383,44 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
         }
         SEED_TICK(2);
         const uint32_t nseed = sh_nseed;
-        // bitonic sort by (k1, y)
+        // sort by (k1, y). Up to SBLOCK seeds: one per thread, bitonic in
+        // registers -- partners within the wave by lane exchange, the few
+        // stages across waves through LDS; beyond: bitonic in LDS
         uint32_t np2 = 1;
         while (np2 < nseed) np2 <<= 1;
+        if (np2 <= SBLOCK) {
+            LSeed v = {~0ull, 0xFFFFFFFFu, 0u};
+            if ((uint32_t)tid < nseed) v = seeds[tid];
+            for (uint32_t kk = 2; kk <= np2; kk <<= 1) {
+                for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+                    LSeed o;
+                    if (j >= 64) {
+                        __syncthreads();
+                        seeds[tid] = v;
+                        __syncthreads();
+                        o = seeds[tid ^ j];
+                    } else {
+                        const int jj = (int)j;
+                        o.k1 = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(v.k1 >> 32), jj) << 32) |
+                               (uint32_t)__shfl_xor((int)(uint32_t)v.k1, jj);
+                        o.y = (uint32_t)__shfl_xor((int)v.y, jj);
+                        o.len = (uint32_t)__shfl_xor((int)v.len, jj);
+                    }
+                    const bool gt = (v.k1 > o.k1) || (v.k1 == o.k1 && v.y > o.y);
+                    const bool want_min = ((tid & j) == 0) == ((tid & kk) == 0);
+                    if (gt == want_min) v = o;
+                }
+            }
+            __syncthreads();
+            if ((uint32_t)tid < nseed) seeds[tid] = v;
+            __syncthreads();
+            np2 = 1;   // sorted
+        }
         for (uint32_t i = nseed + tid; i < np2; i += SBLOCK) {
             seeds[i].k1 = ~0ull;
             seeds[i].y = 0xFFFFFFFFu;
         }
-        __syncthreads();
+        if (np2 > 1) __syncthreads();
         for (uint32_t kk = 2; kk <= np2; kk <<= 1) {
             for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
                 for (uint32_t i = tid; i < np2; i += SBLOCK) {
