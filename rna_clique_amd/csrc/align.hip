@@ -972,7 +972,6 @@ enum { RM_REC = 0, RM_CLO = CAND_DWORDS, RM_CHI, RM_QB, RM_TB, RM_X, RM_Y, RM_LE
 // fields of the record (dword offsets, layout of Cand)
 enum { RC_SOFF = 0, RC_QTX = 1, RC_STX = 2, RC_CNT_STRAND = 3, RC_Q0 = 4, RC_S0 = 6, RC_LQ = 8, RC_LT = 9,
        RC_QSAM = 10, RC_SSAM = 11 };
-enum { HB_QA, HB_QB, HB_SA, HB_SB, HB_SC, HB_D, HB_G, HB_O, HB_NI, HB_N };
 // work cursors of a row
 enum { RS_LEND, RS_SHARD, RS_SHN, RS_N };
 // row actions (transition actions < A_DONE; extending: A_STEP_R / A_STEP_L = their done action + 4)

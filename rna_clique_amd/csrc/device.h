@@ -142,10 +142,7 @@ struct ExtParams {
     // two-candidate kernel: staging slot (u64 words per sequence) and the
     // candidates it defers to the one-wave kernel (transcripts past the slot)
     int32_t dsw;
-    int32_t *cand_box;            // row kernel: first HSP box of each candidate + count + overflow offset
-    int32_t *box_ovf;             // boxes 2..nh (9 ints each)
-    uint64_t box_ovf_cap;
-    unsigned long long *box_ovf_count;
+    int32_t *cand_box;            // row kernel: status + right/left results of each candidate's first seed
     int32_t chunk;                // row kernel: candidates per work grab (0: static round robin)
     unsigned long long *work;     // row kernel: work counter
     uint32_t *defer;
@@ -157,8 +154,8 @@ struct ExtParams {
 // passes the mirrored direction's) and its index in the candidate (bits 3-5).
 constexpr int HSP_FWD = 2, HSP_REV = 4, HSP_IDX_SHIFT = 3;
 
-// cand_box record (ints): box fields 0..8, count (-1: deferred to extend_kernel), overflow offset
-constexpr int BOX_NH = 9, BOX_OVF = 10, BOX_REC = 12;
+// cand_box record: BOX_REC ints per candidate (align.hip FX_*)
+constexpr int BOX_REC = 12;
 
 constexpr int DSTAGE_MAX = 4096;   // longest transcript the two-candidate extension stages
 

@@ -241,12 +241,12 @@ struct rc_engine {
     DBuf<Cand> d_cands;
     DBuf<DHsp> d_cand_hsp, d_ovf;
     DBuf<uint8_t> d_cand_nh;
-    DBuf<int32_t> d_cand_box, d_box_ovf;
+    DBuf<int32_t> d_cand_box;
     DBuf<uint32_t> d_cand_ovf, d_gc_off, d_gc_cnt, d_gcount, d_defer;
     DBuf<uint64_t> d_gscan, d_mscan, d_mkey, d_tmask;
     DBuf<uint32_t> d_mcnt, d_mcur, d_tx_pos;
     DBuf<unsigned long long> d_shard_cnt, d_shard_prefix;
-    uint64_t seed_cap = 0, cand_cap = 0, ovf_cap = 0, box_ovf_cap = 0;   // per-shard / total capacities
+    uint64_t seed_cap = 0, cand_cap = 0, ovf_cap = 0;   // per-shard / total capacities
     DBuf<uint32_t> d_grp_off, d_grp_cnt;
     DBuf<unsigned long long> d_count;
     DBuf<unsigned int> d_status;
@@ -847,11 +847,9 @@ static int do_align(rc_engine *e)
     CHK(e->d_cand_ovf.ensure(slots));
     CHK(e->d_cand_box.ensure(slots * BOX_REC));
     CHK(e->d_defer.ensure(std::max<uint64_t>(n_cand, 1)));
-    if (!e->box_ovf_cap) e->box_ovf_cap = n_cand / 8 + 1024;
     for (int attempt = 0;; attempt++) {
         if (attempt == 4) return fail(RC_E_NOMEM, "HSP overflow buffer kept overflowing");
         CHK(e->d_ovf.ensure(e->ovf_cap));
-        CHK(e->d_box_ovf.ensure(e->box_ovf_cap * 9));
         HIPCHK(hipMemsetAsync(e->d_count.p, 0, 16 * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
         ExtParams X;
@@ -877,9 +875,6 @@ static int do_align(rc_engine *e)
         X.defer_count = e->d_count.p + 6;
         X.work = e->d_count.p + 7;
         X.cand_box = e->d_cand_box.p;
-        X.box_ovf = e->d_box_ovf.p;
-        X.box_ovf_cap = e->box_ovf_cap;
-        X.box_ovf_count = e->d_count.p + 12;
         {
             const char *cv = getenv("RC_ROW_CHUNK");
             X.chunk = cv ? atoi(cv) : 8;
@@ -911,10 +906,7 @@ static int do_align(rc_engine *e)
                     (double)pr[0], (double)pr[1], (double)pr[2], (double)pr[3], (double)pr[4]);
         }
         if (!(status & 1u)) break;
-        unsigned long long bovn = 0;
-        HIPCHK(hipMemcpy(&bovn, e->d_count.p + 12, sizeof bovn, hipMemcpyDeviceToHost));
         e->ovf_cap = std::max<uint64_t>(e->ovf_cap, ovn * 5 / 4 + 1024);
-        e->box_ovf_cap = std::max<uint64_t>(e->box_ovf_cap, bovn * 5 / 4 + 1024);
     }
     // --- groups: (query gene, subject sample) -> contiguous HSPs ---
     // Direct groups (query sample < subject sample) come first in d_hsp, in

@@ -15,7 +15,7 @@ import sys
 
 
 def short(name):
-    for k in ("seed_kernel", "extend_rows_kernel", "ext_finish_kernel", "extend_kernel", "rbh_kernel", "kmer_fill", "radix_sort", "pack_fwd",
+    for k in ("seed_kernel", "extend_rows_kernel", "ext_finish_kernel", "first_finish_kernel", "extend_kernel", "rbh_kernel", "kmer_fill", "radix_sort", "pack_fwd",
               "pack_rc", "bucket_fill", "mirror_scatter", "mirror_sort", "group_count", "group_write",
               "cc_hook", "cc_count", "pair_sums"):
         if k in name:
