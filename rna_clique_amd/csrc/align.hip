@@ -1544,6 +1544,10 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
         if (amb) RC_LAUNCH_ROWS(true, 16, ROW_MIN_WAVES); else RC_LAUNCH_ROWS(false, 16, ROW_MIN_WAVES);
     } else if (mw == 5) {
         if (amb) RC_LAUNCH_ROWS(true, 32, 5); else RC_LAUNCH_ROWS(false, 32, 5);
+    } else if (mw == 7) {
+        if (amb) RC_LAUNCH_ROWS(true, 32, 7); else RC_LAUNCH_ROWS(false, 32, 7);
+    } else if (mw == 8) {
+        if (amb) RC_LAUNCH_ROWS(true, 32, 8); else RC_LAUNCH_ROWS(false, 32, 8);
     } else {
         if (amb) RC_LAUNCH_ROWS(true, 32, ROW_MIN_WAVES); else RC_LAUNCH_ROWS(false, 32, ROW_MIN_WAVES);
     }

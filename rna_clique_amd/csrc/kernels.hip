@@ -152,18 +152,39 @@ __global__ __launch_bounds__(256) void kmer_fill_kernel(const TxInfo *__restrict
 }
 
 // bucket[b] = first sorted index whose key >> (32 - bits) >= b, b in [0, 2^bits].
-__global__ void bucket_fill_kernel(const uint64_t *__restrict__ ent, uint64_t n, int bits,
-                                   uint32_t *__restrict__ bucket)
+// bucket[x] = first entry whose top `bits` k-mer bits are >= x (x = 0 .. 2^bits).
+// Each thread owns BF_PER consecutive entries: one wide load of its own
+// entries (plus the one before) with every load in flight at once, then the
+// bucket slots from the previous entry's bucket (exclusive) to each entry's.
+constexpr int BF_PER = 4;
+__global__ __launch_bounds__(256) void bucket_fill_kernel(const uint64_t *__restrict__ ent, uint64_t n, int bits,
+                                                          uint32_t *__restrict__ bucket)
 {
     const unsigned sh = 64u - (unsigned)bits;
     const uint64_t nb = 1ull << bits;
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i <= n;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t b = (i < n) ? (ent[i] >> sh) : nb + 1;
-        const uint64_t pb = (i > 0) ? (ent[i - 1] >> sh) : 0;
-        const uint64_t lo = (i > 0) ? pb + 1 : 0;
-        const uint64_t hi = (i < n) ? b : nb;
-        for (uint64_t x = lo; x <= hi && x <= nb; x++) bucket[x] = (uint32_t)i;
+    const uint64_t i0 = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) * BF_PER;
+    if (i0 > n) return;
+    uint64_t e[BF_PER + 1];
+    e[0] = i0 > 0 ? ent[i0 - 1] : 0ull;
+    if (i0 + BF_PER <= n) {
+        const ulonglong2 *v = reinterpret_cast<const ulonglong2 *>(ent + i0);
+#pragma unroll
+        for (int j = 0; j < BF_PER / 2; j++) {
+            const ulonglong2 w = v[j];
+            e[1 + 2 * j] = w.x;
+            e[2 + 2 * j] = w.y;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < BF_PER; j++) e[1 + j] = i0 + j < n ? ent[i0 + j] : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < BF_PER; j++) {
+        const uint64_t i = i0 + j;
+        if (i > n) break;
+        const uint64_t lo = i > 0 ? (e[j] >> sh) + 1 : 0;
+        const uint64_t hi = i < n ? (e[j + 1] >> sh) : nb;
+        for (uint64_t x = lo; x <= hi; x++) bucket[x] = (uint32_t)i;
     }
 }
 
@@ -687,7 +708,8 @@ void launch_kmer_fill(bool amb, const TxInfo *tx, uint32_t n_tx, const uint64_t 
 
 void launch_bucket_fill(const uint64_t *ent, uint64_t n, int bits, uint32_t *bucket, hipStream_t st)
 {
-    hipLaunchKernelGGL(bucket_fill_kernel, dim3(grid_for(n + 1, 256)), dim3(256), 0, st, ent, n, bits, bucket);
+    const uint64_t threads = n / BF_PER + 1;   // entries 0 .. n (entry n closes the table)
+    hipLaunchKernelGGL(bucket_fill_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, ent, n, bits, bucket);
 }
 
 void launch_rbh(const RbhParams &P, int pass, hipStream_t st)
