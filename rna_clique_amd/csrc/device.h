@@ -205,7 +205,13 @@ struct RbhParams {
     const uint64_t *row_off, *fsel_off, *rsel_off, *edge_off;
     DRow *rows;
     DEdge *edges;
+    // pass 2 (counts + rows and edges in fixed per-item slots, labels local to
+    // the item; rbh_place_kernel moves them once the offsets are scanned)
+    DRow *rows_tmp;               // RBH_RMAX per item
+    DEdge *edges_tmp;             // RBH_EMAX per item
+    unsigned int *ovf;            // set when an item needs more slots (pass 1 then runs)
 };
+constexpr int RBH_RMAX = 2, RBH_EMAX = 1;
 
 // ------------------------------------------------------------------------
 // 2-bit windows

@@ -32,6 +32,7 @@ void launch_extend_rows(bool, const Db &, const ExtParams &, int, hipStream_t);
 void launch_group(const GroupParams &, int, hipStream_t);
 
 void launch_rbh(const RbhParams &, int, hipStream_t);
+void launch_rbh_place(const RbhParams &, hipStream_t);
 void launch_gather_rows(const DHsp *, const DRow *, uint64_t, DHsp *, hipStream_t);
 void launch_cc(const DEdge *, uint64_t, uint32_t, const int32_t *, int, uint32_t *, uint32_t *, uint32_t *,
                uint32_t *, uint32_t *, uint8_t *, unsigned long long *, hipStream_t);
@@ -242,6 +243,8 @@ struct rc_engine {
     DBuf<DHsp> d_cand_hsp, d_ovf;
     DBuf<uint8_t> d_cand_nh;
     DBuf<int32_t> d_cand_box;
+    DBuf<DRow> d_rows_tmp;
+    DBuf<DEdge> d_edges_tmp;
     DBuf<uint32_t> d_cand_ovf, d_gc_off, d_gc_cnt, d_gcount, d_defer;
     DBuf<uint64_t> d_gscan, d_mscan, d_mkey, d_tmask;
     DBuf<uint32_t> d_mcnt, d_mcur, d_tx_pos;
@@ -1015,7 +1018,14 @@ static int do_rbh(rc_engine *e)
     R.n_fsel = e->d_cnt4.p + (ni + 1);
     R.n_rsel = e->d_cnt4.p + 2 * (ni + 1);
     R.n_edges = e->d_cnt4.p + 3 * (ni + 1);
-    launch_rbh(R, 0, e->st);
+    // one pass over the groups: counts, and rows/edges in per-item slots
+    CHK(e->d_rows_tmp.ensure(std::max<uint64_t>(ni, 1) * RBH_RMAX));
+    CHK(e->d_edges_tmp.ensure(std::max<uint64_t>(ni, 1) * RBH_EMAX));
+    HIPCHK(hipMemsetAsync(e->d_status.p + 1, 0, sizeof(unsigned int), e->st));
+    R.rows_tmp = e->d_rows_tmp.p;
+    R.edges_tmp = e->d_edges_tmp.p;
+    R.ovf = e->d_status.p + 1;
+    launch_rbh(R, 2, e->st);
     HIPCHK(hipGetLastError());
     for (int k = 0; k < 4; k++) {
         size_t tmp = 0;
@@ -1030,6 +1040,8 @@ static int do_rbh(rc_engine *e)
     uint64_t tot[4] = {0, 0, 0, 0};
     for (int k = 0; k < 4; k++)
         HIPCHK(hipMemcpyAsync(&tot[k], e->d_off4.p + k * (ni + 1) + ni, 8, hipMemcpyDeviceToHost, e->st));
+    unsigned int slot_ovf = 0;
+    HIPCHK(hipMemcpyAsync(&slot_ovf, e->d_status.p + 1, sizeof slot_ovf, hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
     e->n_rows = tot[0];
     e->n_edges = tot[3];
@@ -1042,7 +1054,10 @@ static int do_rbh(rc_engine *e)
     R.edge_off = e->d_off4.p + 3 * (ni + 1);
     R.rows = e->d_rows.p;
     R.edges = e->d_edges.p;
-    launch_rbh(R, 1, e->st);
+    if (slot_ovf || getenv("RC_RBH_TWO_PASS"))
+        launch_rbh(R, 1, e->st);   // an item had more rows or edges than its slots: full second pass
+    else
+        launch_rbh_place(R, e->st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e->ev[6], e->st));
     HIPCHK(hipEventSynchronize(e->ev[6]));

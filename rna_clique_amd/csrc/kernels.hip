@@ -232,8 +232,12 @@ __device__ __forceinline__ uint32_t desc_rank(const DHsp *h, uint32_t off, uint3
     return r;
 }
 
+// pass 0: per-item counts; pass 1: rows and edges at the scanned offsets;
+// pass 2: counts plus rows and edges in per-item slots with item-local labels
+// (rbh_place_kernel finishes them) -- one pass over the groups instead of two.
 __global__ void rbh_kernel(RbhParams P, int pass)
 {
+    const bool tmp = pass == 2;
     // items [item0, item0 + n_items) of this shard; per-item arrays are local.
     // The pair of an item: one binary search per block (its first item), then
     // a short walk (a block's 256 items span one or two pairs)
@@ -306,11 +310,18 @@ __global__ void rbh_kernel(RbhParams P, int pass)
         // (keep "first": only the first such row)
         uint32_t prev_a = 0;
         bool have_prev = false, done = false;
-        uint64_t row_w = pass ? P.row_off[li] : 0, edge_w = pass ? P.edge_off[li] : 0;
-        const uint64_t fsel_base = pass ? P.fsel_off[li] - P.fsel_off[P.pair_item_begin[pr] - P.item0] : 0;
+        const bool fin = pass == 1;
+        uint64_t row_w = fin ? P.row_off[li] : 0, edge_w = fin ? P.edge_off[li] : 0;
+        const uint64_t fsel_base = fin ? P.fsel_off[li] - P.fsel_off[P.pair_item_begin[pr] - P.item0] : 0;
         const uint64_t fsel_pair_total =
-            pass ? P.fsel_off[P.pair_item_begin[pr + 1] - P.item0] - P.fsel_off[P.pair_item_begin[pr] - P.item0] : 0;
-        const uint64_t rsel_base = pass ? P.rsel_off[li] - P.rsel_off[P.pair_item_begin[pr] - P.item0] : 0;
+            fin ? P.fsel_off[P.pair_item_begin[pr + 1] - P.item0] - P.fsel_off[P.pair_item_begin[pr] - P.item0] : 0;
+        const uint64_t rsel_base = fin ? P.rsel_off[li] - P.rsel_off[P.pair_item_begin[pr] - P.item0] : 0;
+        auto put_row = [&](const DRow &row) {
+            if (!tmp) P.rows[row_w] = row;
+            else if (row_w < (uint64_t)RBH_RMAX) P.rows_tmp[li * RBH_RMAX + row_w] = row;
+            else atomicOr(P.ovf, 1u);
+            row_w++;
+        };
         while (fsel && !done) {
             // next smallest a among selected F rows
             bool found = false;
@@ -362,7 +373,7 @@ __global__ void rbh_kernel(RbhParams P, int pass)
                     row.reverse = 0;
                     row.label = (int32_t)(fsel_base + rk);
                     row.pad = 0;
-                    P.rows[row_w++] = row;
+                    put_row(row);
                 }
                 en += f.nident;
                 ed += f.length - f.gaps;
@@ -420,7 +431,7 @@ __global__ void rbh_kernel(RbhParams P, int pass)
                     row.reverse = 1;
                     row.label = (int32_t)(fsel_pair_total + rsel_base + before + rk);
                     row.pad = 0;
-                    P.rows[row_w++] = row;
+                    put_row(row);
                 }
                 en += r.nident;
                 ed += r.length - r.gaps;
@@ -436,12 +447,15 @@ __global__ void rbh_kernel(RbhParams P, int pass)
                     e.pair = (uint32_t)pr;
                     e.nident = en;
                     e.den = ed;
-                    P.edges[edge_w++] = e;
+                    if (!tmp) P.edges[edge_w] = e;
+                    else if (edge_w < (uint64_t)RBH_EMAX) P.edges_tmp[li * RBH_EMAX + edge_w] = e;
+                    else atomicOr(P.ovf, 1u);
+                    edge_w++;
                 }
                 nedges++;
             }
         }
-        if (!pass) {
+        if (pass != 1) {
             P.n_rows[li] = nrows;
             P.n_fsel[li] = fsel;
             P.n_rsel[li] = rsel;
@@ -710,6 +724,52 @@ void launch_bucket_fill(const uint64_t *ent, uint64_t n, int bits, uint32_t *buc
 {
     const uint64_t threads = n / BF_PER + 1;   // entries 0 .. n (entry n closes the table)
     hipLaunchKernelGGL(bucket_fill_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, ent, n, bits, bucket);
+}
+
+// After pass 2 and the scans: each item's rows and edges from its slots to
+// their offsets, labels made pair-global (F rows: + the item's F_sel base; R
+// rows: + the pair's F_sel total + the item's R_sel base).
+__global__ void rbh_place_kernel(RbhParams P)
+{
+    __shared__ int sh_pair;
+    for (uint64_t lb = blockIdx.x * (uint64_t)blockDim.x; lb < P.n_items; lb += (uint64_t)gridDim.x * blockDim.x) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint64_t item0 = P.item0 + lb;
+            int lo = 0, hi = P.n_pairs;
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (P.pair_item_begin[mid] <= item0) lo = mid; else hi = mid;
+            }
+            sh_pair = lo;
+        }
+        __syncthreads();
+        const uint64_t li = lb + threadIdx.x;
+        if (li >= P.n_items) continue;
+        const uint64_t item = P.item0 + li;
+        int pr = sh_pair;
+        while (pr + 1 < P.n_pairs && P.pair_item_begin[pr + 1] <= item) pr++;
+        const uint64_t pb = P.pair_item_begin[pr] - P.item0, pe = P.pair_item_begin[pr + 1] - P.item0;
+        const uint32_t nr = P.n_rows[li], ne = P.n_edges[li];
+        if (nr) {
+            const int32_t fb = (int32_t)(P.fsel_off[li] - P.fsel_off[pb]);
+            const int32_t rb = (int32_t)(P.fsel_off[pe] - P.fsel_off[pb] + P.rsel_off[li] - P.rsel_off[pb]);
+            const uint64_t o = P.row_off[li];
+            for (uint32_t k = 0; k < nr && k < (uint32_t)RBH_RMAX; k++) {
+                DRow r = P.rows_tmp[li * RBH_RMAX + k];
+                r.label += r.reverse ? rb : fb;
+                P.rows[o + k] = r;
+            }
+        }
+        const uint64_t eo = P.edge_off[li];
+        for (uint32_t k = 0; k < ne && k < (uint32_t)RBH_EMAX; k++) P.edges[eo + k] = P.edges_tmp[li * RBH_EMAX + k];
+    }
+}
+
+void launch_rbh_place(const RbhParams &P, hipStream_t st)
+{
+    if (P.n_items == 0) return;
+    hipLaunchKernelGGL(rbh_place_kernel, dim3(grid_for(P.n_items, 256)), dim3(256), 0, st, P);
 }
 
 void launch_rbh(const RbhParams &P, int pass, hipStream_t st)

@@ -58,8 +58,13 @@ def test_simulated_parity_long_and_gappy(native, lens, indel):
     assert summary["hsps"] > 0
 
 
-@pytest.mark.parametrize("top_matches,keep_all", [(1, True), (1, False), (2, True)])
-def test_simulated_parity_options(native, top_matches, keep_all):
+@pytest.mark.parametrize("top_matches,keep_all,two_pass", [(1, True, False), (1, False, False), (2, True, False),
+                                                            (2, True, True), (1, False, True)])
+def test_simulated_parity_options(native, monkeypatch, top_matches, keep_all, two_pass):
+    """two_pass: the RBH step's fallback (a second pass over the groups, used
+    when an item has more rows or edges than its slots) forced by RC_RBH_TWO_PASS."""
+    if two_pass:
+        monkeypatch.setenv("RC_RBH_TWO_PASS", "1")
     from rna_clique_amd.simulate import simulate
     samples, _ = simulate(4, 100, seed=11, p_iso2=0.3, indel_rate=0.003)
     eng = _run_sim(samples, top_matches=top_matches, keep_all=keep_all)
