@@ -22,38 +22,56 @@ namespace rcg {
 // pack
 // ------------------------------------------------------------------------
 
-__device__ __forceinline__ void code_of(uint8_t c, uint64_t &code, uint64_t &amb)
-{
-    const uint8_t l = c | 0x20;
-    code = (l == 'c') ? 1 : (l == 'g') ? 2 : (l == 't') ? 3 : 0;
-    amb = (l == 'a' || l == 'c' || l == 'g' || l == 't') ? 0 : 3;
-}
-
-// One thread per 64-bit word (32 bases): 32 input bytes as two 16-B loads.
+// One thread per 64-bit word (32 bases): 32 input bytes as two 16-B loads,
+// coded four bytes at a time in registers. The 2-bit code of A/C/G/T (either
+// case) is ((c >> 1) ^ (c >> 2)) & 3 (A 0, C 1, G 2, T 3); any other byte is
+// ambiguous (mask 3, code 0).
 __global__ void pack_fwd_kernel(const uint8_t *__restrict__ ascii, uint64_t total, uint64_t nwords,
                                 uint64_t *__restrict__ F, uint64_t *__restrict__ AF)
 {
     for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < nwords;
          w += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t p0 = w * 32;
-        uint8_t b[32];
+        uint32_t d[8];
         if (p0 + 32 <= total) {
             const uint4 *v = reinterpret_cast<const uint4 *>(ascii + p0);
-            uint4 x0 = v[0], x1 = v[1];
-            *reinterpret_cast<uint4 *>(b) = x0;
-            *reinterpret_cast<uint4 *>(b + 16) = x1;
+            const uint4 x0 = v[0], x1 = v[1];
+            d[0] = x0.x; d[1] = x0.y; d[2] = x0.z; d[3] = x0.w;
+            d[4] = x1.x; d[5] = x1.y; d[6] = x1.z; d[7] = x1.w;
         } else {
 #pragma unroll
-            for (int i = 0; i < 32; i++) b[i] = (p0 + i < total) ? ascii[p0 + i] : 'A';
+            for (int j = 0; j < 8; j++) {
+                uint32_t x = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint64_t p = p0 + 4 * j + k;
+                    x |= (uint32_t)(p < total ? ascii[p] : (uint8_t)'A') << (8 * k);
+                }
+                d[j] = x;
+            }
         }
         uint64_t word = 0, amb = 0;
 #pragma unroll
-        for (int i = 0; i < 32; i++) {
-            uint64_t c, a;
-            code_of(b[i], c, a);
-            if (p0 + i >= total) c = 0, a = 0;
-            word |= c << (2 * i);
-            amb |= a << (2 * i);
+        for (int j = 0; j < 8; j++) {
+            const uint32_t t = (d[j] >> 1) ^ (d[j] >> 2);
+#pragma unroll
+            for (int k = 0; k < 4; k++) word |= (uint64_t)((t >> (8 * k)) & 3u) << (8 * j + 2 * k);
+        }
+        if (AF) {
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t l = ((d[j] >> (8 * k)) & 0xFFu) | 0x20u;
+                    const bool ok = l == 'a' || l == 'c' || l == 'g' || l == 't';
+                    amb |= (uint64_t)(ok ? 0u : 3u) << (8 * j + 2 * k);
+                }
+            word &= ~amb;   // ambiguous bases code as 0
+        }
+        if (p0 + 32 > total) {
+            const uint64_t keep = (1ull << (2 * (total - p0))) - 1ull;   // total - p0 < 32
+            word &= keep;
+            amb &= keep;
         }
         F[w] = word;
         if (AF) AF[w] = amb;
