@@ -45,6 +45,28 @@ def test_simulated_parity(native, seed, taxa, genes, iso, indel):
     assert summary["hsps"] > 0 and summary["ideal_nodes"] > 0
 
 
+@pytest.mark.parametrize("amb_rate", [0.002, 0.02])
+def test_simulated_parity_ambiguous(native, amb_rate):
+    """Non-ACGT bytes (N, IUPAC codes, either case) and lowercase bases: the
+    ambiguity-mask kernels (seed and extension) against the oracle, where a
+    non-ACGT base never matches and no index window contains one."""
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(4, 100, seed=31, p_iso2=0.2, indel_rate=0.002)
+    rng = np.random.default_rng(5)
+    junk = np.frombuffer(b"NnRYKMSWryx-", dtype=np.uint8)
+    for s in samples:
+        seq = s.seq.copy()
+        low = rng.random(seq.size) < 0.05
+        seq[low] |= 0x20
+        pos = np.flatnonzero(rng.random(seq.size) < amb_rate)
+        seq[pos] = junk[rng.integers(0, junk.size, pos.size)]
+        s.seq = seq
+    eng = _run_sim(samples)
+    msgs, summary = full_check(eng, samples)
+    assert not msgs, "\n".join(msgs[:10])
+    assert summary["hsps"] > 0
+
+
 @pytest.mark.parametrize("lens,indel", [((200, 9000), 0.002), (None, 0.03)])
 def test_simulated_parity_long_and_gappy(native, lens, indel):
     """Long transcripts (past the LDS staging limit, global-memory path) and
