@@ -45,6 +45,18 @@ def test_simulated_parity(native, seed, taxa, genes, iso, indel):
     assert summary["hsps"] > 0 and summary["ideal_nodes"] > 0
 
 
+def test_simulated_parity_large_index(native):
+    """More than 2^20 indexed positions: the onesweep-sorted index (smaller
+    ones take rocPRIM's merge-sort path, sorted on all 64 bits)."""
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(3, 500, seed=41, p_iso2=0.1)
+    assert sum(s.seq.size for s in samples) > 2 * (1 << 20)
+    eng = _run_sim(samples)
+    msgs, summary = full_check(eng, samples)
+    assert not msgs, "\n".join(msgs[:10])
+    assert summary["hsps"] > 0
+
+
 @pytest.mark.parametrize("amb_rate", [0.002, 0.02])
 def test_simulated_parity_ambiguous(native, amb_rate):
     """Non-ACGT bytes (N, IUPAC codes, either case) and lowercase bases: the
