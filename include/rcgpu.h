@@ -192,6 +192,11 @@ int rc_fasta_info(const rc_fasta *f, uint64_t *n_records, uint64_t *n_bases, uin
 /* titles concatenated into buf (title_bytes), offsets[n_records + 1];
  * seq_lens[n_records] (may be NULL) */
 int rc_fasta_titles(const rc_fasta *f, char *buf, uint64_t *offsets, uint64_t *seq_lens);
+/* (coverage, gene, isoform) of every record under the default rnaSPAdes id
+ * pattern (transcripts.py:8 of the reference, matched as re.search does);
+ * records it cannot decide (non-ASCII title, no match, > 18 digits) count in
+ * n_undecided -- the caller then parses the ids with the regex itself */
+int rc_fasta_parse_rnaspades(const rc_fasta *f, double *cov, int64_t *gene, int64_t *iso, uint64_t *n_undecided);
 /* selected sequences concatenated into seq; tx_offsets[n_selected + 1] */
 int rc_fasta_select(const rc_fasta *f, const uint8_t *keep, uint8_t *seq, uint64_t *tx_offsets);
 /* selected records as Bio.SeqIO.write(..., "fasta") writes them (width 60) */

@@ -119,6 +119,7 @@ SIGNATURES = {
     "rc_fasta_close": (ctypes.c_int, [VP]),
     "rc_fasta_info": (ctypes.c_int, [VP, P(ctypes.c_uint64), P(ctypes.c_uint64), P(ctypes.c_uint64)]),
     "rc_fasta_titles": (ctypes.c_int, [VP, VP, VP, VP]),
+    "rc_fasta_parse_rnaspades": (ctypes.c_int, [VP, VP, VP, VP, VP]),
     "rc_fasta_select": (ctypes.c_int, [VP, VP, VP, VP]),
     "rc_fasta_write": (ctypes.c_int, [VP, VP, ctypes.c_char_p, ctypes.c_int32]),
 }

@@ -35,6 +35,8 @@ struct rc_fasta {
     std::vector<uint32_t> title_len;   // [n]
     std::vector<uint64_t> body_off;    // [n + 1] body byte range in data
     std::vector<uint64_t> seq_len;     // [n] cleaned sequence length
+    std::vector<char> clean;           // every record's cleaned sequence, back to back
+    std::vector<uint64_t> seq_off;     // [n + 1] record i's sequence in clean
 };
 
 namespace {
@@ -60,6 +62,13 @@ void body_runs(const char *b, const char *e, F &&f)
         const char *nl = static_cast<const char *>(memchr(b, '\n', (size_t)(e - b)));
         const char *le = nl ? nl : e;
         const char *re = rstrip(b, le);
+        const size_t n = (size_t)(re - b);
+        // the usual line holds neither ' ' nor '\r': one run
+        if (n && !memchr(b, ' ', n) && !memchr(b, '\r', n)) {
+            f(b, n);
+            b = nl ? nl + 1 : e;
+            continue;
+        }
         const char *p = b;
         while (p < re) {
             const char *q = p;
@@ -120,12 +129,22 @@ int rc_fasta_open(const char *path, rc_fasta **out)
     }
     const size_t n = f->title_off.size();
     f->body_off.push_back((uint64_t)f->size);
+    // clean every sequence once; select and write copy from here
     f->seq_len.assign(n, 0);
+    f->seq_off.assign(n + 1, 0);
+    f->clean.resize(f->size);
+    char *c = f->clean.data();
+    uint64_t w = 0;
     for (size_t i = 0; i < n; i++) {
-        uint64_t L = 0;
-        body_runs(d + f->body_off[i], d + body_end(f, i), [&](const char *, size_t k) { L += k; });
-        f->seq_len[i] = L;
+        f->seq_off[i] = w;
+        body_runs(d + f->body_off[i], d + body_end(f, i), [&](const char *q, size_t k) {
+            memcpy(c + w, q, k);
+            w += k;
+        });
+        f->seq_len[i] = w - f->seq_off[i];
     }
+    f->seq_off[n] = w;
+    f->clean.resize(w);
     *out = f;
     return RC_OK;
 }
@@ -167,17 +186,84 @@ int rc_fasta_titles(const rc_fasta *f, char *buf, uint64_t *offsets, uint64_t *s
     return RC_OK;
 }
 
+// rnaSPAdes ids under the default pattern of transcripts.py (the reference's
+// default_gene_re, transcripts.py:8): re.search(r"^.*cov_([0-9]+(?:\.[0-9]+))
+// _g([0-9]+)_i([0-9]+)", id) on the record id (the title's first whitespace
+// token). The greedy ".*" makes the match the LAST position where the tail
+// pattern matches; its digit runs are maximal (each is followed by a fixed
+// non-digit or, for the isoform, by nothing). Coverage goes through strtod
+// (correctly rounded, as Python's float()). A record this cannot decide --
+// a non-ASCII title (Python splits ids on Unicode whitespace too), no match,
+// a gene or isoform beyond 18 digits -- counts in *n_undecided and gets
+// zeros; the caller then parses every id with the regex instead.
+int rc_fasta_parse_rnaspades(const rc_fasta *f, double *cov, int64_t *gene, int64_t *iso, uint64_t *n_undecided)
+{
+    if (!f || !cov || !gene || !iso || !n_undecided) return rcg_fail(RC_E_ARG, "null argument");
+    const size_t n = f->seq_len.size();
+    uint64_t bad = 0;
+    auto digits = [](const char *p, const char *e) {
+        const char *q = p;
+        while (q < e && *q >= '0' && *q <= '9') q++;
+        return q;
+    };
+    for (size_t i = 0; i < n; i++) {
+        const char *t = f->data + f->title_off[i];
+        const char *const te = t + f->title_len[i];
+        bool ascii = true;
+        for (const char *p = t; p < te; p++)
+            if ((unsigned char)*p >= 0x80) ascii = false;
+        auto split_ws = [](char c) { return is_ws(c) || (c >= '\x1c' && c <= '\x1f'); };
+        while (t < te && split_ws(*t)) t++;   // str.split() drops leading whitespace
+        const char *e = t;
+        while (e < te && !split_ws(*e)) e++;
+        cov[i] = 0;
+        gene[i] = iso[i] = 0;
+        bool ok = false;
+        if (ascii) {
+            for (ptrdiff_t jo = (e - t) - 4; jo >= 0 && !ok; jo--) {
+                const char *j = t + jo;
+                if (memcmp(j, "cov_", 4) != 0) continue;
+                const char *c0 = j + 4, *c1 = digits(c0, e);
+                if (c1 == c0 || c1 >= e || *c1 != '.') continue;
+                const char *c2 = digits(c1 + 1, e);
+                if (c2 == c1 + 1 || e - c2 < 2 || c2[0] != '_' || c2[1] != 'g') continue;
+                const char *g0 = c2 + 2, *g1 = digits(g0, e);
+                if (g1 == g0 || e - g1 < 2 || g1[0] != '_' || g1[1] != 'i') continue;
+                const char *i0 = g1 + 2, *i1 = digits(i0, e);
+                if (i1 == i0) continue;
+                if (g1 - g0 > 18 || i1 - i0 > 18) break;   // undecided
+                const std::string cs(c0, c2);
+                cov[i] = strtod(cs.c_str(), nullptr);
+                int64_t gv = 0, iv = 0;
+                for (const char *p = g0; p < g1; p++) gv = gv * 10 + (*p - '0');
+                for (const char *p = i0; p < i1; p++) iv = iv * 10 + (*p - '0');
+                gene[i] = gv;
+                iso[i] = iv;
+                ok = true;
+            }
+        }
+        if (!ok) bad++;
+    }
+    *n_undecided = bad;
+    return RC_OK;
+}
+
 int rc_fasta_select(const rc_fasta *f, const uint8_t *keep, uint8_t *seq, uint64_t *tx_offsets)
 {
     if (!f || !seq || !tx_offsets) return rcg_fail(RC_E_ARG, "null argument");
+    const size_t n = f->seq_len.size();
+    const char *c = f->clean.data();
+    if (!keep) {
+        if (n) memcpy(seq, c, f->seq_off[n]);
+        for (size_t i = 0; i <= n; i++) tx_offsets[i] = f->seq_off[i];
+        return RC_OK;
+    }
     uint64_t w = 0, k = 0;
-    for (size_t i = 0; i < f->seq_len.size(); i++) {
-        if (keep && !keep[i]) continue;
+    for (size_t i = 0; i < n; i++) {
+        if (!keep[i]) continue;
         tx_offsets[k++] = w;
-        body_runs(f->data + f->body_off[i], f->data + body_end(f, i), [&](const char *p, size_t m) {
-            memcpy(seq + w, p, m);
-            w += m;
-        });
+        memcpy(seq + w, c + f->seq_off[i], f->seq_len[i]);
+        w += f->seq_len[i];
     }
     tx_offsets[k] = w;
     return RC_OK;
@@ -187,33 +273,37 @@ int rc_fasta_write(const rc_fasta *f, const uint8_t *keep, const char *path, int
 {
     if (!f || !path) return rcg_fail(RC_E_ARG, "null argument");
     if (width <= 0) return rcg_fail(RC_E_ARG, "line width must be positive");
-    FILE *o = fopen(path, "wb");
-    if (!o) return rcg_fail(RC_E_ARG, std::string("cannot create ") + path);
-    std::vector<char> buf(1 << 20);
-    setvbuf(o, buf.data(), _IOFBF, buf.size());
-    bool ok = true;
-    for (size_t i = 0; i < f->seq_len.size() && ok; i++) {
+    // the whole file in one buffer, one write
+    const size_t n = f->seq_len.size();
+    uint64_t bytes = 0;
+    for (size_t i = 0; i < n; i++) {
         if (keep && !keep[i]) continue;
-        ok &= fputc('>', o) != EOF;
-        ok &= fwrite(f->data + f->title_off[i], 1, f->title_len[i], o) == f->title_len[i];
-        ok &= fputc('\n', o) != EOF;
-        int col = 0;
-        body_runs(f->data + f->body_off[i], f->data + body_end(f, i), [&](const char *p, size_t m) {
-            while (m) {
-                const size_t take = std::min<size_t>(m, (size_t)(width - col));
-                ok &= fwrite(p, 1, take, o) == take;
-                p += take;
-                m -= take;
-                col += (int)take;
-                if (col == width) {
-                    ok &= fputc('\n', o) != EOF;
-                    col = 0;
-                }
-            }
-        });
-        if (col) ok &= fputc('\n', o) != EOF;
+        const uint64_t L = f->seq_len[i];
+        bytes += 2 + f->title_len[i] + L + (L + (uint64_t)width - 1) / (uint64_t)width;
     }
-    ok &= fclose(o) == 0;
+    std::vector<char> out(bytes);
+    char *o = out.data();
+    const char *c = f->clean.data();
+    for (size_t i = 0; i < n; i++) {
+        if (keep && !keep[i]) continue;
+        *o++ = '>';
+        memcpy(o, f->data + f->title_off[i], f->title_len[i]);
+        o += f->title_len[i];
+        *o++ = '\n';
+        const char *p = c + f->seq_off[i];
+        for (uint64_t L = f->seq_len[i]; L;) {
+            const uint64_t take = std::min<uint64_t>(L, (uint64_t)width);
+            memcpy(o, p, take);
+            o += take;
+            *o++ = '\n';
+            p += take;
+            L -= take;
+        }
+    }
+    FILE *fo = fopen(path, "wb");
+    if (!fo) return rcg_fail(RC_E_ARG, std::string("cannot create ") + path);
+    bool ok = fwrite(out.data(), 1, (size_t)(o - out.data()), fo) == (size_t)(o - out.data());
+    ok &= fclose(fo) == 0;
     if (!ok) return rcg_fail(RC_E_ARG, std::string("write failed: ") + path);
     return RC_OK;
 }

@@ -8,12 +8,16 @@ from __future__ import annotations
 
 import ctypes
 import os
+import re
 from typing import NamedTuple
 
 import numpy as np
 
 from . import _native as nat
 from .transcripts import fasta_id
+
+# whitespace str.split() splits on, other than the newline separator
+_WS = re.compile(r"[ \t\r\x0b\x0c\x1c-\x1f\x85\xa0\u1680\u2000-\u200a\u2028\u2029\u202f\u205f\u3000]")
 
 
 class Record(NamedTuple):
@@ -41,11 +45,46 @@ class FastaFile:
         nat.check(nat.lib().rc_fasta_titles(h, buf.ctypes.data_as(ctypes.c_void_p),
                                             offs.ctypes.data_as(ctypes.c_void_p),
                                             self.lengths.ctypes.data_as(ctypes.c_void_p)))
-        raw = buf[:tb.value].tobytes()
-        o = offs.tolist()
-        self.titles = [raw[o[i]:o[i + 1]].decode("utf-8", errors="replace")
-                       for i in range(n.value)]
-        self.ids = [fasta_id(t) for t in self.titles]
+        self._tbuf, self._toffs = buf[:tb.value], offs
+        self._titles = self._ids = None
+
+    @property
+    def titles(self):
+        """Header lines (decoded on first use: one decode of the titles joined
+        by newlines -- a title never holds one, and an ASCII newline ends any
+        broken UTF-8 sequence exactly where a per-title decode would)."""
+        if self._titles is None:
+            if self.n_records:
+                joined = np.insert(self._tbuf, self._toffs[1:-1].astype(np.int64), ord("\n"))
+                self._titles = joined.tobytes().decode("utf-8", errors="replace").split("\n")
+            else:
+                self._titles = []
+        return self._titles
+
+    @property
+    def ids(self):
+        """Record ids: each title's first whitespace-separated token."""
+        if self._ids is None:
+            t = self.titles
+            if _WS.search("\n".join(t)) is None:
+                self._ids = list(t)   # no whitespace: the id is the whole title
+            else:
+                self._ids = [fasta_id(x) for x in t]
+        return self._ids
+
+    def parse_rnaspades(self):
+        """(coverage float64, gene int64, isoform int64) per record under the
+        default rnaSPAdes id pattern, parsed natively; None when some record is
+        undecided there (the caller parses with the regex instead)."""
+        n = self.n_records
+        cov = np.zeros(n, dtype=np.float64)
+        gene = np.zeros(n, dtype=np.int64)
+        iso = np.zeros(n, dtype=np.int64)
+        bad = ctypes.c_uint64()
+        nat.check(nat.lib().rc_fasta_parse_rnaspades(
+            self._h, cov.ctypes.data_as(ctypes.c_void_p), gene.ctypes.data_as(ctypes.c_void_p),
+            iso.ctypes.data_as(ctypes.c_void_p), ctypes.byref(bad)))
+        return None if bad.value else (cov, gene, iso)
 
     def close(self):
         if getattr(self, "_h", None):

@@ -90,9 +90,13 @@ def rna_clique(
     module docstring for what differs from the reference underneath).
 
     Returns (SampleSimilarity, {top-genes FASTA path: sample name})."""
+    import time
+    t0 = time.perf_counter()
     samples = select_all(dirs, out_dir_1, transcripts, top_genes, id_parser, max(1, jobs))
+    t1 = time.perf_counter()
     pts = {s.path: s.name for s in samples}
     eng = run_engine(samples, top_matches, evalue, keep_all, device, process_group)
+    t2 = time.perf_counter()
     sim = SampleSimilarity(eng, store_dfs=store_dfs)
     from . import distributed
     writer = distributed.world(process_group)[1] == 0
@@ -113,4 +117,11 @@ def rna_clique(
         os.replace(tmp, output_graph)
     if writer and output_matrix is not None:
         write_matrix(sim.get_dissimilarity_df(), output_matrix)
+    last_timings.clear()
+    last_timings.update(select_s=t1 - t0, engine_s=t2 - t1, outputs_s=time.perf_counter() - t2)
     return sim, pts
+
+
+# wall-clock phases of the last rna_clique() call in this process (seconds):
+# top-gene selection, engine (load + GPU path), outputs (tables, graph, matrix)
+last_timings: dict = {}

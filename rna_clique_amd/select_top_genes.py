@@ -12,6 +12,7 @@ from __future__ import annotations
 import dataclasses
 import heapq
 import os
+import re
 from collections import defaultdict
 from pathlib import Path
 from typing import Callable, Iterable, Iterator
@@ -22,8 +23,59 @@ from .fasta import FastaFile, Record
 from .transcripts import TranscriptID, default_parser
 
 
+def _is_default(parse_transcript_id):
+    """The parser is the default rnaSPAdes regex parser (transcripts.py)."""
+    from .transcripts import RegexIDParser, default_gene_re
+    return (isinstance(parse_transcript_id, RegexIDParser) and parse_transcript_id.cls is TranscriptID
+            and parse_transcript_id.expr.pattern == default_gene_re.pattern
+            and parse_transcript_id.expr.flags == default_gene_re.flags)
+
+
+def _fast_default_ids(ids, parse_transcript_id):
+    """(coverage float64, gene int64, isoform int64) arrays for the default
+    rnaSPAdes pattern in one regex pass over all ids, or None when the parser
+    is anything else or some id does not match (the per-id path then raises
+    TranscriptIDParseError exactly as the reference does)."""
+    from .transcripts import default_gene_re
+    if not _is_default(parse_transcript_id):
+        return None
+    ids = list(ids)
+    if any("\n" in i for i in ids):
+        return None
+    # `^` per line, `.*` never crosses a newline: line i's match is exactly
+    # expr.search(ids[i]) (greedy, so the last cov_/_g/_i group of the id)
+    rx = re.compile(default_gene_re.pattern, default_gene_re.flags | re.MULTILINE)
+    found = rx.findall("\n".join(ids))
+    if len(found) != len(ids):
+        return None
+    if not found:
+        return np.zeros(0), np.zeros(0, np.int64), np.zeros(0, np.int64)
+    cov_s, gene_s, iso_s = zip(*found)
+    cov = np.array([float(c) for c in cov_s], dtype=np.float64)
+    return cov, np.array(gene_s, dtype=np.int64), np.array(iso_s, dtype=np.int64)
+
+
+def _top_from_arrays(cov, genes, isos, top):
+    """top_gene_ids on parsed arrays: per gene the max coverage, then
+    nlargest(top, (cov, gene)) -- descending by coverage, ties to the larger
+    gene id."""
+    if top <= 0 or len(genes) == 0:
+        return [], genes, isos
+    o = np.lexsort((-cov, genes))
+    g_sorted = genes[o]
+    first = np.ones(len(o), dtype=bool)
+    first[1:] = g_sorted[1:] != g_sorted[:-1]
+    ug, ucov = g_sorted[first], cov[o][first]
+    sel = np.lexsort((-ug, -ucov))[:top]
+    return ug[sel].tolist(), genes, isos
+
+
 def top_gene_ids(ids: Iterable[str], top: int, parse_transcript_id=default_parser):
     """(top gene ids in nlargest order, per-record (gene, isoform) arrays)."""
+    ids = list(ids)
+    fast = _fast_default_ids(ids, parse_transcript_id)
+    if fast is not None:
+        return _top_from_arrays(*fast, top)
     best = defaultdict(float)
     genes, isos = [], []
     for id_ in ids:
@@ -81,7 +133,13 @@ class TopSample:
     tx_offsets: np.ndarray   # uint64, n_tx + 1
     gene: np.ndarray         # int32
     iso: np.ndarray          # int32
-    ids: list
+    ids_src: object          # the ids (list), or a callable making them on first use
+
+    @property
+    def ids(self) -> list:
+        if callable(self.ids_src):
+            self.ids_src = self.ids_src()
+        return self.ids_src
 
     @property
     def n_tx(self):
@@ -104,15 +162,20 @@ def select_top_sample(out_dir, transcripts: str, x, top: int,
     x = Path(x)
     out = Path(out_dir) / (x.stem + "_top.fasta")
     with FastaFile(x / transcripts) as f:
-        top_ids, genes, isos = top_gene_ids(f.ids, top, parse_transcript_id)
+        parsed = f.parse_rnaspades() if _is_default(parse_transcript_id) else None
+        if parsed is not None:
+            top_ids, genes, isos = _top_from_arrays(*parsed, top)
+        else:
+            top_ids, genes, isos = top_gene_ids(f.ids, top, parse_transcript_id)
         keep = np.isin(genes, np.asarray(top_ids, dtype=np.int64)).astype(np.uint8)
         if write:
             f.write(out, keep)
         seq, offs = f.select(keep)
         sel = keep.astype(bool)
-        ids = [i for i, k in zip(f.ids, sel) if k]
+    # the kept ids are only decoded when someone asks (titles stay in f)
     return TopSample(out, x.stem, seq, offs, _int32(genes[sel], "gene"),
-                     _int32(isos[sel], "isoform"), ids)
+                     _int32(isos[sel], "isoform"),
+                     lambda: [i for i, k in zip(f.ids, sel) if k])
 
 
 def select_top_and_save(out_dir, transcripts: str, x, *args):

@@ -48,13 +48,19 @@ class Sample:
     def transcript(self, t):
         return self.seq[self.tx_offsets[t]:self.tx_offsets[t + 1]].tobytes().decode()
 
-    def write_fasta(self, path):
-        with open(path, "w") as f:
-            for t, name in enumerate(self.ids()):
-                f.write(f">{name}\n")
-                s = self.transcript(t)
-                for k in range(0, len(s), 80):
-                    f.write(s[k:k + 80] + "\n")
+    def write_fasta(self, path, width=80):
+        """FASTA with `width`-column sequence lines (bytes-level, no per-base
+        Python work)."""
+        seq = self.seq.tobytes()
+        offs = self.tx_offsets
+        parts = []
+        for t, name in enumerate(self.ids()):
+            a, b = int(offs[t]), int(offs[t + 1])
+            parts.append(b">" + name.encode() + b"\n")
+            parts.append(b"\n".join(seq[k:min(k + width, b)] for k in range(a, b, width)))
+            parts.append(b"\n")
+        with open(path, "wb") as f:
+            f.write(b"".join(parts))
 
 
 def birth_death_tree(taxa, rng, birth=1.0, death=0.5):

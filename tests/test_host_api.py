@@ -291,3 +291,47 @@ def test_plan_shards_partitions_pairs(native, n, shards):
     if n_pairs >= 4 * shards:
         # contiguous cut at cost midpoints: no shard above its share + one pair
         assert max(loads) <= cost.sum() / shards + cost.max()
+
+
+def test_native_rnaspades_ids_match_regex(native, tmp_path):
+    """rc_fasta_parse_rnaspades == re.search(default_gene_re, id) on every
+    record, and the selection built on it == the per-id regex path."""
+    import random
+    from rna_clique_amd.fasta import FastaFile
+    from rna_clique_amd.select_top_genes import top_gene_ids, _top_from_arrays
+    from rna_clique_amd.transcripts import default_parser
+    rng = random.Random(11)
+    titles = []
+    for k in range(3000):
+        g, i = rng.randint(0, 400), rng.randint(0, 3)
+        cov = rng.choice([f"{rng.random() * 1e4:.{rng.randint(1, 8)}f}", "5.0", "0.1", "12.000001",
+                          "1" * 25 + ".5"])
+        pre = rng.choice(["NODE_%d_length_9_" % k, "", "cov_1.0_g7_i7_", "xcov_", "cov_9_g1_i1_",
+                          "  ", "\t"])
+        post = rng.choice(["", " desc words", "_x", "\tmore", "z"])
+        titles.append(f"{pre}cov_{cov}_g{g}_i{i}{post}")
+    p = tmp_path / "t.fasta"
+    p.write_text("".join(f">{t}\nACGT\n" for t in titles))
+    with FastaFile(p) as f:
+        cov, gene, iso = f.parse_rnaspades()
+        for k, id_ in enumerate(f.ids):
+            c, g, i = default_parser(id_)
+            assert (cov[k], gene[k], iso[k]) == (c, g, i), id_
+        a = _top_from_arrays(cov, gene, iso, 150)
+        b = top_gene_ids(f.ids, 150)
+        assert a[0] == b[0]
+    # an id the pattern does not match: undecided natively (the regex path raises)
+    p.write_text(">NODE_cov_1_g2_i3\nAC\n>NODE_cov_1.5_g2_i3\nAC\n")
+    with FastaFile(p) as f:
+        assert f.parse_rnaspades() is None
+    # non-ASCII title: undecided natively; select_top_sample falls back to the regex
+    from rna_clique_amd.select_top_genes import select_top_sample
+    d = tmp_path / "S"
+    d.mkdir()
+    (d / "transcripts.fasta").write_text(">NODE_\u00e9_cov_1.5_g2_i3\nAC\n>NODE_cov_2.5_g4_i0\nGT\n",
+                                         encoding="utf-8")
+    with FastaFile(d / "transcripts.fasta") as f:
+        assert f.parse_rnaspades() is None
+    (tmp_path / "od1").mkdir()
+    s = select_top_sample(tmp_path / "od1", "transcripts.fasta", d, 1)
+    assert s.gene.tolist() == [4] and s.ids == ["NODE_cov_2.5_g4_i0"]
