@@ -154,11 +154,20 @@ int rc_finish(rc_engine *eng);
 uint64_t rc_edge_record_size(void);
 int rc_export_edges(rc_engine *eng, void *buf, uint64_t cap, uint64_t *n, int on_device);
 int rc_import_edges(rc_engine *eng, const void *buf, uint64_t n, int on_device);
-/* This shard's sample-pair range [first, last) in combinations order. */
+/* This shard's sample-pair range [first, last) in the engine's pair order
+ * (rc_pair_order). */
 int rc_shard_pairs(rc_engine *eng, int64_t *first, int64_t *last);
-/* The split itself (no device needed): pair_first[shard_count + 1], shard r
- * owns pairs [pair_first[r], pair_first[r + 1]). sample_bases = total bases
- * of each sample's transcripts. */
+/* The engine's pair numbering: pair p is (pair_a[p], pair_b[p]), a < b;
+ * C(N,2) entries each. */
+int rc_pair_order(rc_engine *eng, int32_t *pair_a, int32_t *pair_b);
+/* The split itself (no device needed). Each shard takes one rectangle of the
+ * (query a, subject b) pair triangle; pairs are numbered shard by shard,
+ * subject-major inside a shard (one shard: (0,1), (0,2), (1,2), (0,3), ...).
+ * pair_first[shard_count + 1]: shard r owns pairs [pair_first[r],
+ * pair_first[r + 1]); pair_a/pair_b (C(N,2) entries, may be NULL) the order.
+ * sample_bases = total bases of each sample's transcripts. */
+int rc_plan_pairs(const int64_t *sample_bases, int32_t n_samples, int32_t shard_count, int32_t *pair_a,
+                  int32_t *pair_b, int64_t *pair_first);
 int rc_plan_shards(const int64_t *sample_bases, int32_t n_samples, int32_t shard_count, int64_t *pair_first);
 
 /* Results (after rc_run / rc_finish). */

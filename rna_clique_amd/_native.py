@@ -104,6 +104,8 @@ SIGNATURES = {
     "rc_import_edges": (ctypes.c_int, [VP, VP, ctypes.c_uint64, ctypes.c_int]),
     "rc_shard_pairs": (ctypes.c_int, [VP, P(ctypes.c_int64), P(ctypes.c_int64)]),
     "rc_plan_shards": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.c_int32, VP]),
+    "rc_plan_pairs": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.c_int32, VP, VP, VP]),
+    "rc_pair_order": (ctypes.c_int, [VP, VP, VP]),
     "rc_hsps": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.c_int32, VP, ctypes.c_uint64,
                                P(ctypes.c_uint64)]),
     "rc_pair_rows": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.c_int32, VP, ctypes.c_uint64,

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <array>
 #include <map>
 #include <numeric>
 #include <string>
@@ -97,6 +98,22 @@ struct DBuf {
         cap = 0;
     }
 };
+
+// every byte is A/C/G/T in either case (a branch-free inner loop the compiler
+// vectorises; the scan stops at the first 64 KiB block holding another byte)
+static bool all_acgt(const char *s, uint64_t n)
+{
+    for (uint64_t i0 = 0; i0 < n; i0 += 65536) {
+        const uint64_t i1 = std::min<uint64_t>(n, i0 + 65536);
+        unsigned bad = 0;
+        for (uint64_t i = i0; i < i1; i++) {
+            const unsigned char c = (unsigned char)s[i] | 0x20;
+            bad |= (unsigned)((c != 'a') & (c != 'c') & (c != 'g') & (c != 't'));
+        }
+        if (bad) return false;
+    }
+    return true;
+}
 
 // ------------------------------------------------------------------------
 // Karlin-Altschul statistics (BLAST restated; same spec as the oracle)
@@ -196,7 +213,7 @@ struct rc_engine {
     rc_opts o{};
     hipStream_t st = nullptr;
     std::vector<SampleRec> samples;
-    std::vector<char> seq;
+    uint64_t total_bases = 0;   // input bases added so far (they go straight to d_ascii)
     std::vector<uint64_t> tx_start{0};
     std::vector<int32_t> tx_sample, tx_gene_id, tx_iso;
     bool has_amb = false;
@@ -206,6 +223,7 @@ struct rc_engine {
     std::vector<int32_t> gene_sample, gene_id;
     std::vector<int64_t> db_len, db_n;
     std::vector<int32_t> pair_a, pair_b, pair_index;
+    std::vector<int64_t> shard_first;   // shard r owns pairs [shard_first[r], shard_first[r + 1])
     std::vector<uint32_t> pair_item_begin;
     int32_t max_len = 0;
     uint64_t n_items = 0;
@@ -353,19 +371,33 @@ int rc_add_sample(rc_engine *e, const char *label, const char *seq, const uint64
     if (nb && !seq) return fail(RC_E_ARG, "null sequence");
     SampleRec s;
     s.label = label;
-    s.base = e->seq.size();
+    s.base = e->total_bases;
     s.nbases = nb;
     s.tx_begin = (uint32_t)e->tx_sample.size();
     s.n_tx = n_tx;
-    e->seq.insert(e->seq.end(), seq, seq + nb);
-    if (!e->has_amb) {
-        for (uint64_t i = 0; i < nb; i++) {
-            const char c = (char)(seq[i] | 0x20);
-            if (c != 'a' && c != 'c' && c != 'g' && c != 't') {
-                e->has_amb = true;
-                break;
+    // the bases go straight to HBM (the ASCII array the pack kernels read);
+    // the device array grows geometrically, old contents moved device-side
+    if (nb) {
+        CHK(set_device(e));
+        const uint64_t need = e->total_bases + nb + 64;
+        if (need > e->d_ascii.cap) {
+            const size_t cap = std::max<size_t>({(size_t)need, 2 * e->d_ascii.cap, (size_t)1 << 28});
+            uint8_t *np = nullptr;
+            if (hipMalloc((void **)&np, cap) != hipSuccess) {
+                (void)hipGetLastError();
+                return fail(RC_E_NOMEM, "hipMalloc of " + std::to_string(cap) + " bytes failed");
             }
+            if (e->total_bases)
+                HIPCHK(hipMemcpyAsync(np, e->d_ascii.p, e->total_bases, hipMemcpyDeviceToDevice, e->st));
+            HIPCHK(hipStreamSynchronize(e->st));
+            e->d_ascii.release();
+            e->d_ascii.p = np;
+            e->d_ascii.cap = cap;
         }
+        HIPCHK(hipMemcpyAsync(e->d_ascii.p + e->total_bases, seq, nb, hipMemcpyHostToDevice, e->st));
+        if (!e->has_amb) e->has_amb = !all_acgt(seq, nb);
+        HIPCHK(hipStreamSynchronize(e->st));   // the caller's buffer is not retained
+        e->total_bases += nb;
     }
     const int32_t sid = (int32_t)e->samples.size();
     for (uint32_t t = 0; t < n_tx; t++) {
@@ -399,7 +431,109 @@ int rc_add_hsps(rc_engine *e, int32_t q, int32_t s, const rc_hsp *h, uint64_t n)
 // Build gene numbering, tables and upload everything that does not change
 // between runs. Inputs are then resident in HBM; rc_run repacks from them.
 static void shard_pairs(rc_engine *e);
-extern "C" int rc_plan_shards(const int64_t *, int32_t, int32_t, int64_t *);
+
+// Shard plan. The C(N,2) sample pairs (a < b) are the cells
+// of the (query a, subject b) triangle; shard_count shards each take one
+// rectangle [a0, a1) x [b0, b1) of it, found by recursive bisection that
+// minimises the largest shard's modelled time:
+//   pair work    1 x (L_a + L_b) per pair (seed hits, extension, RBH)
+//   query scan   5 x L_a per query sample of the shard (seed-kernel word lookups)
+//   index       11 x L_b per subject sample (the shard's 16-mer index)
+// (coefficients from C3 per-shard timings, scripts/shard_time.py). A
+// rectangle keeps both the shard's subjects (its index) and its queries
+// (its seed-kernel gene range) contiguous sample ranges and small. Pairs are
+// numbered shard by shard, subject-major inside a shard; one shard gives the
+// plain subject-major order (0,1), (0,2), (1,2), (0,3), ...
+namespace plan {
+struct Rect {
+    int a0, a1, b0, b1;
+};
+struct Planner {
+    int N;
+    std::vector<double> SL;   // prefix sums of sample bases
+    std::map<std::array<int, 5>, std::pair<double, std::vector<Rect>>> memo;
+    double S(int i, int j) const { return j > i ? SL[j] - SL[i] : 0.0; }
+    static Rect norm(Rect r)
+    {
+        r.a1 = std::min(r.a1, r.b1 - 1);
+        r.b0 = std::max(r.b0, r.a0 + 1);
+        if (r.a1 <= r.a0 || r.b1 <= r.b0) r = Rect{0, 0, 0, 0};
+        return r;
+    }
+    static bool empty(const Rect &r) { return r.a1 <= r.a0 || r.b1 <= r.b0; }
+    double leaf(const Rect &r) const
+    {
+        if (empty(r)) return 0.0;
+        double pw = 0.0;
+        for (int b = r.b0; b < r.b1; b++) {
+            const int ae = std::min(r.a1, b);
+            if (ae > r.a0) pw += S(r.a0, ae) + (double)(ae - r.a0) * (SL[b + 1] - SL[b]);
+        }
+        return pw + 5.0 * S(r.a0, r.a1) + 11.0 * S(r.b0, r.b1);
+    }
+    std::pair<double, std::vector<Rect>> best(Rect r, int k)
+    {
+        r = norm(r);
+        const std::array<int, 5> key{r.a0, r.a1, r.b0, r.b1, k};
+        auto it = memo.find(key);
+        if (it != memo.end()) return it->second;
+        std::pair<double, std::vector<Rect>> res{leaf(r), std::vector<Rect>(k, Rect{0, 0, 0, 0})};
+        res.second[0] = r;
+        if (k > 1 && !empty(r)) {
+            const int k1 = k / 2;
+            auto consider = [&](Rect x, Rect y) {
+                for (int sw = 0; sw < (k1 == k - k1 ? 1 : 2); sw++) {
+                    const int kx = sw ? k - k1 : k1;
+                    const auto X = best(x, kx);
+                    if (X.first >= res.first) continue;
+                    const auto Y = best(y, k - kx);
+                    const double c = std::max(X.first, Y.first);
+                    if (c < res.first) {
+                        res.first = c;
+                        res.second = X.second;
+                        res.second.insert(res.second.end(), Y.second.begin(), Y.second.end());
+                    }
+                }
+            };
+            const int nc = N > 128 ? 12 : 32;   // cut candidates per axis
+            const int sa = std::max(1, (r.a1 - r.a0) / nc), sb = std::max(1, (r.b1 - r.b0) / nc);
+            for (int c = r.a0 + sa; c < r.a1; c += sa) consider({r.a0, c, r.b0, r.b1}, {c, r.a1, r.b0, r.b1});
+            for (int c = r.b0 + sb; c < r.b1; c += sb) consider({r.a0, r.a1, r.b0, c}, {r.a0, r.a1, c, r.b1});
+        }
+        memo.emplace(key, res);
+        return res;
+    }
+};
+
+// pair order (pair_a, pair_b) and shard cuts pair_first[shard_count + 1]
+static void plan_pairs(const int64_t *bases, int N, int shards, std::vector<int32_t> &pa, std::vector<int32_t> &pb,
+                       std::vector<int64_t> &first)
+{
+    pa.clear();
+    pb.clear();
+    first.assign((size_t)shards + 1, 0);
+    std::vector<Rect> rects;
+    if (shards == 1) {
+        rects.push_back(Planner::norm({0, N, 0, N}));
+    } else {
+        Planner P;
+        P.N = N;
+        P.SL.assign((size_t)N + 1, 0.0);
+        for (int i = 0; i < N; i++) P.SL[i + 1] = P.SL[i] + (double)std::max<int64_t>(bases[i], 1);
+        rects = P.best({0, N, 0, N}, shards).second;
+    }
+    for (int r = 0; r < shards; r++) {
+        first[r] = (int64_t)pa.size();
+        const Rect q = rects[r];
+        for (int b = q.b0; b < q.b1; b++)
+            for (int a = q.a0; a < std::min(q.a1, b); a++) {
+                pa.push_back(a);
+                pb.push_back(b);
+            }
+    }
+    first[shards] = (int64_t)pa.size();
+}
+}  // namespace plan
 
 static int upload(rc_engine *e)
 {
@@ -454,33 +588,33 @@ static int upload(rc_engine *e)
     for (uint32_t g = 0; g < n_genes; g++)
         if (e->gene_tx_off[g + 1] - e->gene_tx_off[g] > (uint32_t)MAX_ISO)
             return fail(RC_E_LIMIT, "gene " + std::to_string(e->gene_id[g]) + " has more than 127 transcripts");
-    // pairs (a < b) numbered subject-major -- (0,1), (0,2), (1,2), (0,3), ... --
-    // so that a contiguous range of pairs (a shard) has a contiguous range of
-    // second samples b, whose index is all the shard builds; items = (pair,
-    // gene of b). (Outputs are per pair and do not depend on this numbering.)
-    e->pair_a.clear();
-    e->pair_b.clear();
+    // pairs (a < b) in the shard plan's order (plan::plan_pairs): every
+    // shard a contiguous pair range whose subjects b -- the samples its
+    // index covers -- and queries a are contiguous sample ranges; items =
+    // (pair, gene of b). (Outputs are per pair and do not depend on this.)
+    {
+        std::vector<int64_t> bases(N);
+        for (int i = 0; i < N; i++) bases[i] = e->db_len[i];
+        plan::plan_pairs(bases.data(), N, e->o.shard_count, e->pair_a, e->pair_b, e->shard_first);
+    }
     e->pair_item_begin.assign(1, 0);
     e->pair_index.assign((size_t)N * N, -1);
     uint64_t items = 0;
-    for (int b = 0; b < N; b++)
-        for (int a = 0; a < b; a++) {
-            e->pair_index[a * N + b] = e->pair_index[b * N + a] = (int32_t)e->pair_a.size();
-            e->pair_a.push_back(a);
-            e->pair_b.push_back(b);
-            items += e->samples[b].n_genes;
-            if (items > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "too many (pair, gene) items");
-            e->pair_item_begin.push_back((uint32_t)items);
-        }
+    for (size_t p = 0; p < e->pair_a.size(); p++) {
+        const int a = e->pair_a[p], b = e->pair_b[p];
+        e->pair_index[a * N + b] = e->pair_index[b * N + a] = (int32_t)p;
+        items += e->samples[b].n_genes;
+        if (items > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "too many (pair, gene) items");
+        e->pair_item_begin.push_back((uint32_t)items);
+    }
     e->n_items = items;
     if (N > 256) return fail(RC_E_LIMIT, "more than 256 samples per engine");
     shard_pairs(e);
 
     // device copies
-    const uint64_t total = e->seq.size();
+    const uint64_t total = e->total_bases;
     const uint64_t nwords = (total + 31) / 32 + 4;
-    CHK(e->d_ascii.ensure(total + 64));
-    HIPCHK(hipMemcpyAsync(e->d_ascii.p, e->seq.data(), total, hipMemcpyHostToDevice, e->st));
+    CHK(e->d_ascii.ensure(total + 64));   // (already holds the bases when total > 0)
     // packed arrays carry FRONT_PAD zero words in front (backward windows of
     // the first transcript read them); the kernels see p + FRONT_PAD
     CHK(e->d_F.ensure(nwords + FRONT_PAD));
@@ -567,13 +701,7 @@ static int upload(rc_engine *e)
     CHK(e->d_status.ensure(4));
     CHK(e->d_count.ensure(16));
     HIPCHK(hipStreamSynchronize(e->st));
-    // bucket table over the top k-mer bits: about one bucket per indexed
-    // position, capped (RC_INDEX_BITS_MAX) so that the table stays small
-    const char *ibv = getenv("RC_INDEX_BITS_MAX");
-    const int bmax = ibv ? std::max(16, std::min(30, atoi(ibv))) : 30;
-    int bits = 16;
-    while (bits < bmax && (1ull << bits) < e->n_kpos) bits++;
-    e->index_bits = bits;
+
     e->uploaded = true;
     return RC_OK;
 }
@@ -635,6 +763,14 @@ static int build_index(rc_engine *e)
     HIPCHK(rocprim::radix_sort_keys(nullptr, tmp, e->d_ent.p, e->d_ent2.p, (size_t)npos, bb, 64u, e->st));
     CHK(e->d_tmp.ensure(tmp));
     HIPCHK(rocprim::radix_sort_keys(e->d_tmp.p, tmp, e->d_ent.p, e->d_ent2.p, (size_t)npos, bb, 64u, e->st));
+    // bucket table over the top k-mer bits: about one bucket per indexed
+    // position of this shard, at most 2^28 (RC_INDEX_BITS_MAX; 28 measured
+    // best at C3 -- a 1 GiB table instead of 4 GiB, same seed-kernel time)
+    const char *ibv = getenv("RC_INDEX_BITS_MAX");
+    const int bmax = ibv ? std::max(16, std::min(30, atoi(ibv))) : 28;
+    int bits = 16;
+    while (bits < bmax && (1ull << bits) < npos) bits++;
+    e->index_bits = bits;
     CHK(e->d_bucket.ensure((1ull << e->index_bits) + 1));
     launch_bucket_fill(e->d_ent2.p, npos, e->index_bits, e->d_bucket.p, e->st);
     e->n_index = npos;
@@ -648,7 +784,7 @@ static Db make_db(rc_engine *e)
     db.RC = e->d_RC.p + FRONT_PAD;
     db.AF = e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr;
     db.ARC = e->has_amb ? e->d_ARC.p + FRONT_PAD : nullptr;
-    db.total = e->seq.size();
+    db.total = e->total_bases;
     db.tx = e->d_tx.p;
     db.tx_gene = e->d_tx_gene.p;
     db.gene_tx_off = e->d_gene_tx_off.p;
@@ -664,12 +800,8 @@ static Db make_db(rc_engine *e)
 
 static void shard_pairs(rc_engine *e)
 {
-    const int N = (int)e->samples.size();
-    std::vector<int64_t> bases(N), first(e->o.shard_count + 1);
-    for (int i = 0; i < N; i++) bases[i] = e->db_len[i];
-    rc_plan_shards(bases.data(), N, e->o.shard_count, first.data());
-    e->pair0 = (uint64_t)first[e->o.shard_rank];
-    e->pair1 = (uint64_t)first[e->o.shard_rank + 1];
+    e->pair0 = (uint64_t)e->shard_first[e->o.shard_rank];
+    e->pair1 = (uint64_t)e->shard_first[e->o.shard_rank + 1];
     e->item0 = e->pair_item_begin[e->pair0];
     e->item1 = e->pair_item_begin[e->pair1];
 }
@@ -747,7 +879,7 @@ static int do_align(rc_engine *e)
         e->aligned = true;
         return RC_OK;
     }
-    const uint64_t total = e->seq.size();
+    const uint64_t total = e->total_bases;
     const uint64_t nwords = (total + 31) / 32 + 2;
     HIPCHK(hipEventRecord(e->ev[0], e->st));
     launch_pack(e->d_ascii.p, total, nwords, e->d_F.p + FRONT_PAD, e->d_RC.p + FRONT_PAD,
@@ -1436,25 +1568,30 @@ int rc_import_edges(rc_engine *e, const void *buf, uint64_t n, int on_device)
 // index covers only those samples.
 int rc_plan_shards(const int64_t *sample_bases, int32_t n_samples, int32_t shard_count, int64_t *pair_first)
 {
+    return rc_plan_pairs(sample_bases, n_samples, shard_count, nullptr, nullptr, pair_first);
+}
+
+int rc_plan_pairs(const int64_t *sample_bases, int32_t n_samples, int32_t shard_count, int32_t *pair_a,
+                  int32_t *pair_b, int64_t *pair_first)
+{
     if (!pair_first || shard_count < 1 || n_samples < 0 || (n_samples && !sample_bases))
         return fail(RC_E_ARG, "bad argument");
-    std::vector<double> cum(1, 0.0);
-    for (int b = 0; b < n_samples; b++)
-        for (int a = 0; a < b; a++)
-            cum.push_back(cum.back() + (double)(sample_bases[a] + sample_bases[b]));
-    const int64_t np = (int64_t)cum.size() - 1;
-    const double tot = cum.back();
-    int64_t p = 0;
-    for (int r = 0; r < shard_count; r++) {
-        pair_first[r] = p;
-        while (p < np) {
-            const int owner = tot > 0 ? std::min(shard_count - 1, (int)(0.5 * (cum[p] + cum[p + 1]) / tot * shard_count))
-                                      : (int)((p * shard_count) / np);
-            if (owner > r) break;
-            p++;
-        }
-    }
-    pair_first[shard_count] = np;
+    if (n_samples > 256) return fail(RC_E_LIMIT, "more than 256 samples");
+    std::vector<int32_t> pa, pb;
+    std::vector<int64_t> first;
+    plan::plan_pairs(sample_bases, n_samples, shard_count, pa, pb, first);
+    std::copy(first.begin(), first.end(), pair_first);
+    if (pair_a) std::copy(pa.begin(), pa.end(), pair_a);
+    if (pair_b) std::copy(pb.begin(), pb.end(), pair_b);
+    return RC_OK;
+}
+
+int rc_pair_order(rc_engine *e, int32_t *pair_a, int32_t *pair_b)
+{
+    if (!e || !pair_a || !pair_b) return fail(RC_E_ARG, "null argument");
+    CHK(upload(e));
+    std::copy(e->pair_a.begin(), e->pair_a.end(), pair_a);
+    std::copy(e->pair_b.begin(), e->pair_b.end(), pair_b);
     return RC_OK;
 }
 

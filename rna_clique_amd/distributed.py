@@ -1,9 +1,10 @@
 """Multi-GPU: one engine per GPU, sample pairs sharded, one edge exchange.
 
-SURVEY.md §8e. Every rank loads the same samples. rc_plan_shards cuts the
-C(N,2) pairs, numbered subject-major ((0,1), (0,2), (1,2), (0,3), ...), into
-contiguous ranges of equal sequence length, so each rank's second samples are
-a contiguous sample range and its seed index covers only those; each rank
+SURVEY.md §8e. Every rank loads the same samples. rc_plan_pairs gives every
+rank one rectangle [a0, a1) x [b0, b1) of the (query a, subject b) pair
+triangle, chosen by recursive bisection against a cost model of pair work,
+query-word lookups and index build, so each rank's subjects (its seed index)
+and its queries are short contiguous sample ranges; each rank
 aligns its pairs (seed + extend, both directions at once) and runs top-N /
 reciprocal best hits for them, which yields its share of the gene matches
 tables and graph edges. The ideal-clique filter needs the whole
@@ -34,11 +35,21 @@ def world(process_group=None):
 
 def plan_shards(sample_bases, shard_count):
     """pair_first[shard_count + 1] from rc_plan_shards (no device needed)."""
+    return plan_pairs(sample_bases, shard_count)[1]
+
+
+def plan_pairs(sample_bases, shard_count):
+    """([(a, b), ...] the pair order, pair_first[shard_count + 1]) from
+    rc_plan_pairs (no device needed)."""
     b = np.ascontiguousarray(sample_bases, dtype=np.int64)
+    n = len(b)
+    m = n * (n - 1) // 2
+    pa, pb = np.zeros(max(m, 1), dtype=np.int32), np.zeros(max(m, 1), dtype=np.int32)
     out = np.zeros(shard_count + 1, dtype=np.int64)
-    nat.check(nat.lib().rc_plan_shards(b.ctypes.data_as(ctypes.c_void_p), len(b), int(shard_count),
-                                       out.ctypes.data_as(ctypes.c_void_p)))
-    return out
+    nat.check(nat.lib().rc_plan_pairs(b.ctypes.data_as(ctypes.c_void_p), n, int(shard_count),
+                                      pa.ctypes.data_as(ctypes.c_void_p), pb.ctypes.data_as(ctypes.c_void_p),
+                                      out.ctypes.data_as(ctypes.c_void_p)))
+    return list(zip(pa[:m].tolist(), pb[:m].tolist())), out
 
 
 def all_gather_records(local, record_size, process_group=None, device=None):

@@ -90,19 +90,24 @@ class Engine:
     def finish(self):
         nat.check(nat.lib().rc_finish(self._h))
 
-    @staticmethod
-    def pair_order(n):
-        """The engine's pair numbering: (a, b), a < b, subject-major."""
-        return [(a, b) for b in range(n) for a in range(b)]
+    def pair_order(self):
+        """The engine's pair numbering [(a, b), ...], a < b: shard by shard,
+        subject-major inside a shard (rc_pair_order; one shard: (0,1), (0,2),
+        (1,2), (0,3), ...)."""
+        n = len(self.labels)
+        m = n * (n - 1) // 2
+        pa, pb = np.zeros(max(m, 1), dtype=np.int32), np.zeros(max(m, 1), dtype=np.int32)
+        nat.check(nat.lib().rc_pair_order(self._h, pa.ctypes.data_as(ctypes.c_void_p),
+                                          pb.ctypes.data_as(ctypes.c_void_p)))
+        return list(zip(pa[:m].tolist(), pb[:m].tolist()))
 
     def owned_pairs(self):
         """(a, b) pairs whose tables this shard holds."""
         first, last = self.shard_pairs()
-        return self.pair_order(len(self.labels))[first:last]
+        return self.pair_order()[first:last]
 
     def shard_pairs(self):
-        """[first, last) of this shard's sample pairs, numbered subject-major
-        ((0,1), (0,2), (1,2), (0,3), ...; see pair_order)."""
+        """[first, last) of this shard's sample pairs in pair_order()."""
         a, b = ctypes.c_int64(), ctypes.c_int64()
         nat.check(nat.lib().rc_shard_pairs(self._h, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value

@@ -271,67 +271,37 @@ def test_matrix_h5_reads_back_with_libhdf5(tmp_path):
 # ---------------------------------------------------------------- shard planning
 
 
-@pytest.mark.parametrize("n,shards", [(4, 1), (4, 2), (5, 8), (32, 8), (13, 3), (2, 4)])
+@pytest.mark.parametrize("n,shards", [(4, 1), (4, 2), (5, 8), (32, 8), (13, 3), (2, 4), (64, 8), (32, 5)])
 def test_plan_shards_partitions_pairs(native, n, shards):
-    from rna_clique_amd.distributed import plan_shards
+    from rna_clique_amd.distributed import plan_pairs, plan_shards
     rng = np.random.default_rng(n * 7 + shards)
     bases = rng.integers(1_000, 1_000_000, n)
-    first = plan_shards(bases, shards)
+    pairs, first = plan_pairs(bases, shards)
+    assert np.array_equal(first, plan_shards(bases, shards))
     n_pairs = n * (n - 1) // 2
     assert first[0] == 0 and first[-1] == n_pairs
     assert (np.diff(first) >= 0).all()
-    # pairs in the engine's subject-major order: (0,1), (0,2), (1,2), (0,3), ...
-    pairs = [(a, b) for b in range(n) for a in range(b)]
-    cost = np.array([bases[a] + bases[b] for a, b in pairs])
-    loads = [cost[first[r]:first[r + 1]].sum() for r in range(shards)]
-    # each shard's second samples form a contiguous range (its index covers only them)
+    # every pair exactly once, a < b
+    assert sorted(pairs, key=lambda p: (p[1], p[0])) == [(a, b) for b in range(n) for a in range(b)]
+    if shards == 1:   # one shard: plain subject-major order
+        assert pairs == [(a, b) for b in range(n) for a in range(b)]
     for r in range(shards):
-        bs = sorted({pairs[p][1] for p in range(first[r], first[r + 1])})
-        assert bs == list(range(bs[0], bs[-1] + 1)) if bs else True
+        own = pairs[first[r]:first[r + 1]]
+        if not own:
+            continue
+        # one rectangle: the shard's subjects (its index) and queries are
+        # contiguous sample ranges, and it holds every pair inside them
+        bs, as_ = sorted({b for _, b in own}), sorted({a for a, _ in own})
+        assert bs == list(range(bs[0], bs[-1] + 1))
+        assert as_ == list(range(as_[0], as_[-1] + 1))
+        want = {(a, b) for b in bs for a in as_ if a < b}
+        assert set(own) == want
+        # subject-major inside the shard
+        assert own == sorted(own, key=lambda p: (p[1], p[0]))
     if n_pairs >= 4 * shards:
-        # contiguous cut at cost midpoints: no shard above its share + one pair
-        assert max(loads) <= cost.sum() / shards + cost.max()
-
-
-def test_native_rnaspades_ids_match_regex(native, tmp_path):
-    """rc_fasta_parse_rnaspades == re.search(default_gene_re, id) on every
-    record, and the selection built on it == the per-id regex path."""
-    import random
-    from rna_clique_amd.fasta import FastaFile
-    from rna_clique_amd.select_top_genes import top_gene_ids, _top_from_arrays
-    from rna_clique_amd.transcripts import default_parser
-    rng = random.Random(11)
-    titles = []
-    for k in range(3000):
-        g, i = rng.randint(0, 400), rng.randint(0, 3)
-        cov = rng.choice([f"{rng.random() * 1e4:.{rng.randint(1, 8)}f}", "5.0", "0.1", "12.000001",
-                          "1" * 25 + ".5"])
-        pre = rng.choice(["NODE_%d_length_9_" % k, "", "cov_1.0_g7_i7_", "xcov_", "cov_9_g1_i1_",
-                          "  ", "\t"])
-        post = rng.choice(["", " desc words", "_x", "\tmore", "z"])
-        titles.append(f"{pre}cov_{cov}_g{g}_i{i}{post}")
-    p = tmp_path / "t.fasta"
-    p.write_text("".join(f">{t}\nACGT\n" for t in titles))
-    with FastaFile(p) as f:
-        cov, gene, iso = f.parse_rnaspades()
-        for k, id_ in enumerate(f.ids):
-            c, g, i = default_parser(id_)
-            assert (cov[k], gene[k], iso[k]) == (c, g, i), id_
-        a = _top_from_arrays(cov, gene, iso, 150)
-        b = top_gene_ids(f.ids, 150)
-        assert a[0] == b[0]
-    # an id the pattern does not match: undecided natively (the regex path raises)
-    p.write_text(">NODE_cov_1_g2_i3\nAC\n>NODE_cov_1.5_g2_i3\nAC\n")
-    with FastaFile(p) as f:
-        assert f.parse_rnaspades() is None
-    # non-ASCII title: undecided natively; select_top_sample falls back to the regex
-    from rna_clique_amd.select_top_genes import select_top_sample
-    d = tmp_path / "S"
-    d.mkdir()
-    (d / "transcripts.fasta").write_text(">NODE_\u00e9_cov_1.5_g2_i3\nAC\n>NODE_cov_2.5_g4_i0\nGT\n",
-                                         encoding="utf-8")
-    with FastaFile(d / "transcripts.fasta") as f:
-        assert f.parse_rnaspades() is None
-    (tmp_path / "od1").mkdir()
-    s = select_top_sample(tmp_path / "od1", "transcripts.fasta", d, 1)
-    assert s.gene.tolist() == [4] and s.ids == ["NODE_cov_2.5_g4_i0"]
+        # the modelled load of the largest shard is within 2x of the even split
+        cost = lambda own: (sum(bases[a] + bases[b] for a, b in own)  # noqa: E731
+                            + 5 * sum(bases[a] for a in {a for a, _ in own})
+                            + 11 * sum(bases[b] for b in {b for _, b in own}))
+        loads = [cost(pairs[first[r]:first[r + 1]]) for r in range(shards)]
+        assert max(loads) <= 2 * sum(bases[a] + bases[b] for a, b in pairs) / shards + 16 * max(bases) * n
