@@ -1356,9 +1356,12 @@ __global__ __launch_bounds__(256) void first_finish_kernel(ExtParams P)
 
 __global__ void group_count_kernel(GroupParams P)
 {
-    const uint64_t n = (uint64_t)(P.gene_end - P.gene_begin) * (uint64_t)P.N;
+    const uint64_t sg = (uint64_t)(P.gene_end - P.gene_begin), n = sg * (uint64_t)P.N;
+    // gi: the seed kernel's gene-major (query gene, subject sample) index, read
+    // in order; si: sample-major, the order direct groups are placed in
     for (uint64_t gi = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; gi < n;
          gi += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t si = (gi % (uint64_t)P.N) * sg + gi / (uint64_t)P.N;
         const uint32_t o = P.gc_off[gi], c = P.gc_cnt[gi];
         uint32_t s = 0;
         for (uint32_t i = 0; i < c; i++) {
@@ -1368,21 +1371,22 @@ __global__ void group_count_kernel(GroupParams P)
             const uint32_t ov = P.cand_ovf[o + i];
             for (uint32_t k = 1; k < nh; k++) s += (P.ovf[ov + k - 1].strand & HSP_FWD) ? 1u : 0u;
         }
-        P.cnt[gi] = s;
+        P.cnt[si] = s;
     }
 }
 
 __global__ void group_write_kernel(GroupParams P)
 {
-    const uint64_t n = (uint64_t)(P.gene_end - P.gene_begin) * (uint64_t)P.N;
+    const uint64_t sg = (uint64_t)(P.gene_end - P.gene_begin), n = sg * (uint64_t)P.N;
     for (uint64_t gi = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; gi < n;
          gi += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t si = (gi % (uint64_t)P.N) * sg + gi / (uint64_t)P.N;
         const uint32_t o = P.gc_off[gi], c = P.gc_cnt[gi];
-        uint64_t w = P.scan[gi];
-        const uint64_t gg = (uint64_t)P.gene_begin * P.N + gi;
-        if (P.cnt[gi]) {
+        uint64_t w = P.scan[si];
+        const uint64_t gg = grp_index(P.gene_begin + (uint32_t)(si % sg), (int)(si / sg), P.n_genes);
+        if (P.cnt[si]) {
             P.grp_off[gg] = (uint32_t)w;
-            P.grp_cnt[gg] = P.cnt[gi];
+            P.grp_cnt[gg] = P.cnt[si];
         }
         for (uint32_t i = 0; i < c; i++) {
             const uint32_t nh = P.cand_nh[o + i];
@@ -1434,7 +1438,7 @@ __global__ void mirror_scatter_kernel(GroupParams P, int pass)
         for (uint32_t k = 0; k < nh; k++) {
             const DHsp &h = k ? P.ovf[ov + k - 1] : P.cand_hsp[ci];
             if (!(h.strand & HSP_REV)) continue;
-            const uint64_t gi = (uint64_t)P.tx_gene[h.s_tx] * P.N + (uint64_t)P.tx[h.q_tx].sample;
+            const uint64_t gi = grp_index(P.tx_gene[h.s_tx], P.tx[h.q_tx].sample, P.n_genes);
             if (pass == 0) {
                 atomicAdd(&P.mcnt[gi], 1u);
             } else {

@@ -20,6 +20,15 @@ struct TxInfo {
 };
 
 // HSP of a directed search (56 B), BLAST tabular coordinates.
+// HSP group table index of (query gene, subject sample): sample-major, so the
+// groups of consecutive genes against one sample are adjacent (the RBH items
+// of a sample pair walk them in gene order; gene-major put every item on its
+// own cache line of the table)
+__host__ __device__ __forceinline__ size_t grp_index(uint32_t gene, int sample, uint32_t n_genes)
+{
+    return (size_t)sample * n_genes + gene;
+}
+
 struct DHsp {
     uint32_t q_tx, s_tx;   // global transcript ids
     int32_t qstart, qend, sstart, send;
@@ -191,13 +200,14 @@ struct GroupParams {
 // Parameters of the two reciprocal-best-hit passes.
 struct RbhParams {
     const DHsp *hsp;
-    const uint32_t *grp_off, *grp_cnt;   // [gene * N + T], full gene range
+    const uint32_t *grp_off, *grp_cnt;   // [grp_index(gene, T)], full gene range
     const uint32_t *tx_gene;
     const TxInfo *tx;
     const uint32_t *sample_gene_begin;
     const uint32_t *pair_item_begin;     // n_pairs + 1
     const int32_t *pair_a, *pair_b;
     int32_t n_pairs, N, top_n, keep_all;
+    uint32_t n_genes;
     uint64_t item0, n_items;             // this shard's items [item0, item0 + n_items)
     // pass 0 outputs (per item)
     uint32_t *n_rows, *n_fsel, *n_rsel, *n_edges;

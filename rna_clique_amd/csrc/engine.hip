@@ -843,7 +843,7 @@ static int load_external(rc_engine *e)
             d.qstart = h.qstart; d.qend = h.qend; d.sstart = h.sstart; d.send = h.send;
             d.length = h.length; d.nident = h.nident; d.mismatch = h.mismatch; d.gaps = h.gaps;
             d.gapopen = h.gapopen; d.score_half = h.score_half; d.bits10 = h.bits10; d.strand = h.strand;
-            grp[(size_t)e->tx_gene[d.q_tx] * N + s].push_back(d);
+            grp[grp_index(e->tx_gene[d.q_tx], s, n_genes)].push_back(d);
         }
     }
     std::vector<DHsp> all;
@@ -1134,6 +1134,7 @@ static int do_rbh(rc_engine *e)
     R.hsp = e->d_hsp.p;
     R.grp_off = e->d_grp_off.p;
     R.grp_cnt = e->d_grp_cnt.p;
+    R.n_genes = (uint32_t)e->gene_sample.size();
     R.tx_gene = e->d_tx_gene.p;
     R.tx = e->d_tx.p;
     R.sample_gene_begin = e->d_sample_gene_begin.p;
@@ -1326,18 +1327,19 @@ int rc_hsps(rc_engine *e, int32_t q, int32_t s, rc_hsp *buf, uint64_t cap, uint6
     std::vector<uint32_t> off, cnt;
     CHK(copy_groups(e, off, cnt));
     const SampleRec &Q = e->samples[q];
+    const uint32_t ng = (uint32_t)e->gene_sample.size();
     uint64_t tot = 0;
-    for (uint32_t g = Q.gene_begin; g < Q.gene_begin + Q.n_genes; g++) tot += cnt[(size_t)g * N + s];
+    for (uint32_t g = Q.gene_begin; g < Q.gene_begin + Q.n_genes; g++) tot += cnt[grp_index(g, s, ng)];
     *n = tot;
     if (!buf) return RC_OK;
     if (cap < tot) return fail(RC_E_CAPACITY, "buffer too small");
     uint64_t w = 0;
     std::vector<DHsp> tmp;
     for (uint32_t g = Q.gene_begin; g < Q.gene_begin + Q.n_genes; g++) {
-        const uint32_t c = cnt[(size_t)g * N + s];
+        const uint32_t c = cnt[grp_index(g, s, ng)];
         if (!c) continue;
         tmp.resize(c);
-        HIPCHK(hipMemcpy(tmp.data(), e->d_hsp.p + off[(size_t)g * N + s], c * sizeof(DHsp), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(tmp.data(), e->d_hsp.p + off[grp_index(g, s, ng)], c * sizeof(DHsp), hipMemcpyDeviceToHost));
         for (uint32_t i = 0; i < c; i++) buf[w++] = to_rc_hsp(e, tmp[i], q, s);
     }
     return RC_OK;

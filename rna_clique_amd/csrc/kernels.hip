@@ -280,7 +280,7 @@ __global__ void rbh_kernel(RbhParams P, int pass)
         const int A = P.pair_a[pr], B = P.pair_b[pr];
         const uint32_t b = P.sample_gene_begin[B] + (uint32_t)(item - P.pair_item_begin[pr]);
         const int N = P.N;
-        const size_t fgi = (size_t)b * N + A;
+        const size_t fgi = grp_index(b, A, P.n_genes);
         const uint32_t foff = P.grp_off[fgi], fcnt = P.grp_cnt[fgi];
         const DHsp *H = P.hsp;
         const int fthr = group_thr(H, foff, fcnt, P.top_n);
@@ -292,7 +292,7 @@ __global__ void rbh_kernel(RbhParams P, int pass)
             const DHsp &f = H[foff + i];
             if (f.bits10 < fthr) continue;
             const uint32_t a = P.tx_gene[f.s_tx];
-            const size_t rgi = (size_t)a * N + B;
+            const size_t rgi = grp_index(a, B, P.n_genes);
             const uint32_t roff = P.grp_off[rgi], rcnt = P.grp_cnt[rgi];
             const int rthr = group_thr(H, roff, rcnt, P.top_n);
             bool inP = false;
@@ -354,7 +354,7 @@ __global__ void rbh_kernel(RbhParams P, int pass)
             if (!found) break;
             prev_a = a;
             have_prev = true;
-            const size_t rgi = (size_t)a * N + B;
+            const size_t rgi = grp_index(a, B, P.n_genes);
             const uint32_t roff = P.grp_off[rgi], rcnt = P.grp_cnt[rgi];
             const int rthr = group_thr(H, roff, rcnt, P.top_n);
             auto r_sel = [&](uint32_t j) {
@@ -379,7 +379,7 @@ __global__ void rbh_kernel(RbhParams P, int pass)
                         const DHsp &f2 = H[foff + j];
                         if (f2.bits10 < fthr) return false;
                         const uint32_t a2 = P.tx_gene[f2.s_tx];
-                        const size_t g2 = (size_t)a2 * N + B;
+                        const size_t g2 = grp_index(a2, B, P.n_genes);
                         const uint32_t o2 = P.grp_off[g2], c2 = P.grp_cnt[g2];
                         const int t2 = group_thr(H, o2, c2, P.top_n);
                         for (uint32_t k2 = 0; k2 < c2; k2++)
@@ -437,7 +437,7 @@ __global__ void rbh_kernel(RbhParams P, int pass)
                             if (rk2 < rk) firstrow = false;
                         }
                         if (!firstrow || rk > myfirst) continue;
-                        const size_t g2 = (size_t)a2 * N + B;
+                        const size_t g2 = grp_index(a2, B, P.n_genes);
                         const uint32_t o2 = P.grp_off[g2], c2 = P.grp_cnt[g2];
                         const int t2 = group_thr(H, o2, c2, P.top_n);
                         for (uint32_t k2 = 0; k2 < c2; k2++)

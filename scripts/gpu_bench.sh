@@ -9,6 +9,6 @@ timeout -k 10 900 python bench.py --config "$CFG" --steps "$STEPS" --warmup 1 > 
 rc=$?; echo "bench rc=$rc"; tail -c 3000 gpurun_out/bench_$CFG.json
 [ $rc -eq 0 ] || exit $rc
 export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$CFG -o run -- python bench.py --config "$CFG" --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/prof_$CFG.log 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$CFG -o run -- python bench.py --config "$CFG" --steps 1 --warmup 0 --no-cpu-baseline --no-e2e > gpurun_out/prof_$CFG.log 2>&1
 rc=$?; echo "rocprof rc=$rc"
 exit $rc

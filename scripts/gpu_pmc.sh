@@ -13,7 +13,7 @@ fi
 i=0
 for grp in "$@"; do
   i=$((i+1))
-  timeout -k 10 600 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d gpurun_out/pmc_$CFG/p$i -o run -- python bench.py --config "$CFG" --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/pmc_${CFG}_p$i.log 2>&1
+  timeout -k 10 600 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d gpurun_out/pmc_$CFG/p$i -o run -- python bench.py --config "$CFG" --steps 1 --warmup 0 --no-cpu-baseline --no-e2e > gpurun_out/pmc_${CFG}_p$i.log 2>&1
   rc=$?; echo "pass $i ($grp) rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 done
