@@ -192,6 +192,7 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
         // canonical pre-test by sequence: a hit whose s bases before it match
         // (inside both transcripts) extends left past p - s: not canonical
         const bool fast = stride <= 32;
+        const bool lpre = !AMB && P.pre_mode == 1 && stride >= 1 && stride < W16;
         for (uint32_t ib = 0; ib < n_items; ib += SBLOCK) {
             const uint32_t it = ib + tid;
             uint32_t lo = 0, cnt = 0, info = 0, key = 0;
@@ -276,12 +277,52 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
                     hk[j] = live[j] ? (uint32_t)run_of(it_pre, h) : 0u;
                     hev[j] = live[j] ? ix.ent[it_lo[hk[j]] + (h - it_pre[hk[j]])] : 0ull;
                 }
+                // Hit-list pre-test (stride < 16, no ambiguity codes): item k-1
+                // is the word at p - s of the same isoform and strand, and its
+                // hit list is exactly its k-mer's entries in [pb0, pb1), in
+                // position order. The s bases before a hit at pos match (same
+                // transcript, no start in (pos - s, pos]) iff pos - s is in that
+                // list: the entry's 16-mer covers them and the base at pos.
+                // The chunk's positions go to LDS (the queue's space) and each
+                // hit binary-searches its previous word's list there; hits whose
+                // previous list is not wholly in this chunk take the sequence
+                // pre-test.
+                constexpr uint32_t HCHUNK = SBLOCK * HBATCH;
+                uint32_t *chk = &hq_pos[0][0];
+                if (lpre) {
+                    __syncthreads();   // the previous chunk's queue is consumed
+#pragma unroll
+                    for (int j = 0; j < HBATCH; j++)
+                        if (live[j]) chk[(uint32_t)j * SBLOCK + (uint32_t)tid] = (uint32_t)hev[j];
+                    __syncthreads();
+                }
 #pragma unroll
                 for (int j = 0; j < HBATCH; j++) {
                     const uint32_t pos = (uint32_t)hev[j];
                     live[j] = live[j] && (uint32_t)(hev[j] >> 32) == it_key[hk[j]] && pos >= pb0 && pos < pb1;
                     hsw[j] = hsm[j] = hbw[j] = 0;
-                    if (live[j] && fast && (int)(it_info[hk[j]] >> 8) >= stride) {
+                    bool decided = false;
+                    if (lpre && live[j] && hk[j] > 0 && (int)(it_info[hk[j]] >> 8) >= stride) {
+                        const uint32_t a = it_pre[hk[j] - 1], b = it_pre[hk[j]];
+                        if (a >= hb0 && b <= hb0 + HCHUNK) {
+                            const uint32_t tgt = pos - (uint32_t)stride;
+                            uint32_t lo = a - hb0, n = b - a;
+                            while (n) {
+                                const uint32_t half = n >> 1;
+                                if (chk[lo + half] < tgt) {
+                                    lo += half + 1;
+                                    n -= half + 1;
+                                } else {
+                                    n = half;
+                                }
+                            }
+                            const bool found = pos >= (uint32_t)stride && lo < b - hb0 && chk[lo] == tgt;
+                            hsw[j] = found ? 0ull : ~0ull;
+                            decided = true;
+                        }
+                    }
+                    if (decided) {
+                    } else if (live[j] && fast && (int)(it_info[hk[j]] >> 8) >= stride) {
                         hsw[j] = win_s(db.F, (int64_t)pos - 32) ^ it_qlw[hk[j]];
                         if (AMB) hsm[j] = win_s(db.AF, (int64_t)pos - 32) | it_qlm[hk[j]];
                         hbw[j] = win_bits(db.txstart, (int64_t)pos - 63);
@@ -289,6 +330,7 @@ __global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParam
                         hsw[j] = ~0ull;
                     }
                 }
+                if (lpre) __syncthreads();   // every wave is done with chk before the queue reuses it
                 uint32_t qn = 0;
 #pragma unroll
                 for (int j = 0; j < HBATCH; j++) {

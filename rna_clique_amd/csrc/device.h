@@ -115,6 +115,7 @@ static_assert(sizeof(Cand) == 48, "Cand is read as 12 dwords");
 struct SeedParams {
     int32_t word;                 // W
     int32_t stride;               // W - 16 + 1
+    int32_t pre_mode;             // canonical pre-test: 1 = previous word's hits (LDS), 0 = sequence windows
     uint32_t gene_begin, gene_end;   // shard
     GSeed *seeds;
     uint64_t seed_cap;            // per allocation shard

@@ -934,6 +934,10 @@ static int do_align(rc_engine *e)
         SeedParams S;
         S.word = e->o.word_size;
         S.stride = e->o.word_size - W16 + 1;
+        {
+            const char *pm = getenv("RC_SEED_PRE");   // A/B knob; 1 = hit-list pre-test
+            S.pre_mode = pm ? atoi(pm) : 1;
+        }
         S.gene_begin = g0;
         S.gene_end = g1;
         S.seeds = e->d_seeds.p;
