@@ -20,7 +20,13 @@
 namespace rcg {
 
 constexpr int SBLOCK = 256;
-constexpr int SEED_CAP = 768;
+#ifndef RC_SEED_CAP
+#define RC_SEED_CAP 768
+#endif
+#ifndef RC_SEED_WAVES
+#define RC_SEED_WAVES 1
+#endif
+constexpr int SEED_CAP = RC_SEED_CAP;
 constexpr int HBATCH = 4;                          // hits per lane per batch of the seed kernel
 constexpr int MAX_SAMPLES = 256;
 
@@ -101,7 +107,7 @@ __device__ __forceinline__ int run_of(const uint32_t *pre, uint32_t h)
 }
 
 template <bool AMB>
-__global__ __launch_bounds__(SBLOCK) void seed_kernel(Db db, Index ix, SeedParams P)
+__global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Index ix, SeedParams P)
 {
     const uint32_t g = P.gene_begin + blockIdx.x;
     if (g >= P.gene_end) return;
