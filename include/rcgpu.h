@@ -52,6 +52,14 @@ typedef struct rc_opts {
     int32_t device;        /* HIP device ordinal */
     int32_t shard_rank;    /* rc_align() processes query genes of this shard */
     int32_t shard_count;   /* number of shards (1 = everything) */
+    int32_t symmetric;     /* 0 (default): both directed searches of a pair run
+                              independently, as BLAST runs them (find_homologs.py:
+                              235-246); 1: spec 5b -- each pair extended once, the
+                              higher sample's search reported as mirror images */
+    int32_t dust_level;    /* symmetric DUST on the query words (blastn default
+                              -dust 20 64 1); 0 = off */
+    int32_t dust_window;
+    int32_t dust_linker;
 } rc_opts;
 
 /* One HSP of a directed search, BLAST tabular semantics (1-based, inclusive;
@@ -105,6 +113,7 @@ typedef struct rc_timing {
     double ext_calls;         /* greedy extensions (left + right per HSP attempt) */
     double ext_fullband;      /* extensions recomputed with the full 64-diagonal band */
     double ext_deferred;      /* candidates past the two-candidate staging slot */
+    double big_passes;        /* (query gene, subject sample) seed passes run from global memory */
 } rc_timing;
 
 void rc_default_opts(rc_opts *opts);
@@ -187,6 +196,10 @@ int rc_pair_sums_unfiltered(rc_engine *eng, int64_t *num, int64_t *den);
  * Returns RC_E_NO_IDEAL when some pair has no ideal rows. */
 int rc_distance(rc_engine *eng, const int32_t *order, double *out);
 int rc_timings(rc_engine *eng, rc_timing *t);
+/* The DUST mask of sample `s` after rc_run / rc_align: one byte per base of
+ * its concatenated transcripts (1 = masked query base, spec 1b of the oracle);
+ * all zero when DUST is off. buf == NULL queries the size. */
+int rc_dust_mask(rc_engine *eng, int32_t s, uint8_t *buf, uint64_t cap, uint64_t *n);
 
 /* ---- FASTA input (host only; fasta.cpp) ----------------------------------
  * Replaces the Bio.SeqIO passes of TopGeneSelector (select_top_genes.py:108-127)

@@ -25,7 +25,15 @@ class OrcHsp(ctypes.Structure):
 
 class OrcParams(ctypes.Structure):
     _fields_ = [("word_size", ctypes.c_int32), ("xdrop_half", ctypes.c_int32),
-                ("evalue", ctypes.c_double)]
+                ("evalue", ctypes.c_double), ("symmetric", ctypes.c_int32),
+                ("dust_level", ctypes.c_int32), ("dust_window", ctypes.c_int32),
+                ("dust_linker", ctypes.c_int32)]
+
+
+# base codes of the oracle: A C G T (either case) -> 0..3, anything else 4
+CODE_LUT = np.full(256, 4, dtype=np.uint8)
+for _i, _c in enumerate(b"ACGT"):
+    CODE_LUT[_c] = CODE_LUT[_c | 0x20] = _i
 
 
 HSP_DTYPE = np.dtype([(n, np.uint32) for n in ("q_tx", "s_tx")] +
@@ -52,7 +60,11 @@ def lib():
             P(ctypes.c_int32), ctypes.c_int32, ctypes.c_int32, P(OrcParams),
             P(P(OrcHsp)), P(ctypes.c_uint64)]
         L.orc_align.restype = ctypes.c_int
+        L.orc_align_codes.argtypes = [ctypes.c_void_p] + L.orc_align.argtypes[2:]
+        L.orc_align_codes.restype = ctypes.c_int
         L.orc_free.argtypes = [ctypes.c_void_p]
+        L.orc_dust.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                               ctypes.c_int32, ctypes.c_void_p]
         L.orc_bits10.argtypes = [ctypes.c_int32]
         L.orc_bits10.restype = ctypes.c_int32
         L.orc_threshold.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
@@ -83,7 +95,7 @@ class OracleDB:
             starts.extend((offs[1:] + base).tolist())
             base += int(offs[-1])
             tx_sample.extend([si] * s.n_tx)
-        self.seq = np.concatenate(seqs).tobytes() if seqs else b""
+        self.codes = CODE_LUT[np.concatenate(seqs)] if seqs else np.zeros(1, np.uint8)
         self.tx_start = np.array(starts, dtype=np.uint64)
         self.tx_sample = np.array(tx_sample, dtype=np.int32)
         gene_tx_off, gene_tx, gene_sample, gene_id = [0], [], [], []
@@ -102,14 +114,21 @@ class OracleDB:
         self.gene_sample = np.array(gene_sample, dtype=np.int32)
         self.gene_id = np.array(gene_id, dtype=np.int64)
 
-    def align(self, qsample, tsample, word_size=28, xdrop_half=108, evalue=1e-99):
+    def align(self, qsample, tsample, word_size=28, xdrop_half=108, evalue=1e-99,
+              symmetric=False, dust=None):
+        """One directed search (query sample qsample, subject tsample).
+        symmetric: spec 5b (the pair extended once, the higher-numbered
+        sample's search reported as mirror images); default: the search run
+        on its own, as BLAST runs each direction. dust: (level, window,
+        linker) of symmetric DUST on the query, or None."""
         L = lib()
         P = ctypes.POINTER
         out = P(OrcHsp)()
         n = ctypes.c_uint64()
-        prm = OrcParams(word_size, xdrop_half, evalue)
-        rc = L.orc_align(
-            self.seq, len(self.seq),
+        dl, dw, dk = dust if dust else (0, 64, 1)
+        prm = OrcParams(word_size, xdrop_half, evalue, 1 if symmetric else 0, dl, dw, dk)
+        rc = L.orc_align_codes(
+            self.codes.ctypes.data_as(ctypes.c_void_p),
             self.tx_start.ctypes.data_as(P(ctypes.c_uint64)),
             self.tx_sample.ctypes.data_as(P(ctypes.c_int32)),
             len(self.tx_sample),
@@ -128,6 +147,20 @@ class OracleDB:
         L.orc_free(out)
         del buf
         return res
+
+    def dust_mask(self, sample, level=20, window=64, linker=1):
+        """The oracle's DUST mask (spec 1b) of one sample's transcripts,
+        concatenated (uint8 per base)."""
+        L = lib()
+        out = []
+        for t in range(self.tx_base[sample], self.tx_base[sample] + self.samples[sample].n_tx):
+            a, b = int(self.tx_start[t]), int(self.tx_start[t + 1])
+            c = np.ascontiguousarray(self.codes[a:b])
+            m = np.zeros(max(1, b - a), dtype=np.uint8)
+            L.orc_dust(c.ctypes.data_as(ctypes.c_void_p), b - a, level, window, linker,
+                       m.ctypes.data_as(ctypes.c_void_p))
+            out.append(m[:b - a])
+        return np.concatenate(out) if out else np.zeros(0, np.uint8)
 
     def hsp_rows(self, hsps):
         """Oracle HSPs -> BLAST-tabular-like dicts (for oracle.post_oracle)."""

@@ -18,11 +18,25 @@
  *  1. Words. w = 16 (index word), W = word_size (28 = megablast default),
  *     stride s = W - w + 1. Query positions p with p % s == 0 on the oriented
  *     query (plus strand = q, minus strand = revcomp(q)); subject positions at
- *     every offset. Windows containing a non-ACGT base are skipped.
+ *     every offset. A query word is usable unless its window holds a non-ACGT
+ *     base or a DUST-masked base (1b).
+ * 1b. DUST (blastn's default query filter, -dust 20 64 1, applied as a soft
+ *     mask: it removes query words, extension runs through masked bases).
+ *     Symmetric DUST (Morgulis et al. 2006) on the forward transcript, each
+ *     maximal ACGT run on its own: an interval x of 3..window bases with
+ *     n >= 3 triplets, r(x) = sum over the 64 triplets of c(c-1)/2, is
+ *     *perfect* iff 10 r(x) > level (n - 1) and r(x)/(n-1) >= r(y)/(n_y-1)
+ *     for every perfect interval y inside x. Masked bases = the union of the
+ *     perfect intervals, plus gaps shorter than `linker` between them. The
+ *     minus strand uses the same bases, reversed. (dust_run below evaluates
+ *     this with the windowed bookkeeping of the published algorithm.)
  *  2. Seeds. A word hit (p, subject tx t, offset o) lies on a maximal exact run
- *     [x, e) of its diagonal (non-ACGT never matches). It is canonical iff
- *     p - x < s; a canonical hit with e - x >= W is a seed (x, y = x + o - p,
- *     len = e - x). Every exact match of length >= W yields exactly one seed.
+ *     [x, e) of its diagonal (non-ACGT never matches). It is canonical iff no
+ *     usable query word p' with x <= p' < p exists, i.e. p - x < D(p), D(p) =
+ *     distance to the previous usable word (s when that word is usable; with
+ *     no DUST always s, since a run never covers a non-ACGT base); a canonical
+ *     hit with e - x >= W is a seed (x, y = x + o - p, len = e - x). Every exact
+ *     match of length >= W holding a usable word yields exactly one seed.
  *  3. Per (query tx, strand, subject tx) seeds are sorted by (x, y). Each seed
  *     not contained in an HSP found so far (box containment) is extended left
  *     and right with the greedy X-drop algorithm below (at most 8 HSPs).
@@ -40,6 +54,7 @@
  *     independently; this is where the restatement departs from it.)
  *  6. Bitscore as BLAST prints it (integer-truncated above 99.9) in tenths.
  */
+#include <limits.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -63,6 +78,10 @@ typedef struct {
     int32_t word_size;
     int32_t xdrop_half;
     double evalue;
+    int32_t symmetric;     /* 1: spec 5b (mirror), 0: two independent directed searches */
+    int32_t dust_level;    /* symmetric DUST on the query (spec 1b); 0 = off */
+    int32_t dust_window;
+    int32_t dust_linker;
 } orc_params;
 
 /* Karlin-Altschul parameters for reward 1 / penalty -2, linear gaps
@@ -175,6 +194,111 @@ static inline uint8_t qbase(const uint8_t *codes, uint64_t start, int32_t len, i
     if (!strand) return codes[start + u];
     uint8_t b = codes[start + (uint64_t)(len - 1 - u)];
     return b < 4 ? (uint8_t)(3 - b) : 4;
+}
+
+/* ---------------- DUST (spec 1b) ---------------- */
+
+/* One maximal ACGT run s[0, n): mask[u] = 1 for every base of a perfect
+ * interval. Window bookkeeping of the published symmetric DUST: the last
+ * `window` bases as a queue of triplets with counts cw (rw = r of the whole
+ * window) and, for the longest suffix whose triplet counts all stay <= 2
+ * level / 10, counts cv (rv, L triplets; no interval inside that suffix can
+ * be perfect). Ending at each base, the suffixes longer than L are tried from
+ * shortest to longest against the best ratio of the perfect intervals they
+ * contain. Perfect intervals are kept per start (best ratio, furthest end):
+ * that is all the containment test and the union need. */
+static void dust_run(const uint8_t *s, int32_t n, int T, int W, uint8_t *mask)
+{
+    int cw[64], cv[64], c[64];
+    int q[256], qh = 0, qn = 0;                    /* triplet queue (ring), oldest at qh */
+    int sr[256], sl[256], sf[256];                 /* per start (mod W): best ratio r/l, furthest end */
+    int rw = 0, rv = 0, L = 0;
+    memset(cw, 0, sizeof cw);
+    memset(cv, 0, sizeof cv);
+    for (int k = 0; k < W; k++) sf[k] = -1;
+    for (int32_t i = 2; i <= n; i++) {
+        const int32_t wstart = (i < n) ? (i + 1 - W > 0 ? i + 1 - W : 0) : n;
+        /* perfect intervals whose start left the window are final: one start
+         * leaves per base (wstart - 1), at the end of the run all of them */
+        for (int32_t st = wstart - 1; st >= 0 && st >= (i < n ? wstart - 1 : wstart - W); st--) {
+            const int k = st % W;
+            if (sf[k] < 0) continue;
+            for (int32_t u = st; u < sf[k]; u++) mask[u] = 1;
+            sf[k] = -1;
+        }
+        if (i == n) break;
+        const int t = s[i - 2] * 16 + s[i - 1] * 4 + s[i];
+        if (qn == W - 2) {   /* drop the oldest triplet */
+            const int o = q[qh];
+            qh = (qh + 1) % 256;
+            qn--;
+            rw -= --cw[o];
+            if (L > qn) { L--; rv -= --cv[o]; }
+        }
+        q[(qh + qn) % 256] = t;
+        qn++;
+        L++;
+        rw += cw[t]++;
+        rv += cv[t]++;
+        if (cv[t] * 10 > 2 * T) {   /* shrink the suffix past the previous copy of t */
+            int o;
+            do {
+                o = q[(qh + qn - L) % 256];
+                rv -= --cv[o];
+                L--;
+            } while (o != t);
+        }
+        if (rw * 10 <= L * T) continue;
+        /* suffixes longer than L, shortest first: triplet index j .. qn-1,
+         * bases [wstart + j, i + 1) */
+        memcpy(c, cv, sizeof c);
+        int r = rv, mr = 0, ml = 0;
+        for (int32_t st = wstart + qn - L; st <= i; st++) {   /* perfect intervals inside the L-suffix */
+            const int k = st % W;
+            if (st < n && sf[k] >= 0 && (mr == 0 || sr[k] * ml > mr * sl[k])) { mr = sr[k]; ml = sl[k]; }
+        }
+        for (int j = qn - L - 1; j >= 0; j--) {
+            const int tt = q[(qh + j) % 256];
+            r += c[tt]++;
+            const int l = qn - j - 1;
+            const int32_t st = wstart + j;
+            const int k = st % W;
+            if (sf[k] >= 0 && (mr == 0 || sr[k] * ml > mr * sl[k])) { mr = sr[k]; ml = sl[k]; }
+            if (r * 10 > T * l && (mr == 0 || r * ml >= mr * l)) {
+                if (sf[k] < 0 || r * sl[k] > sr[k] * l) { sr[k] = r; sl[k] = l; }
+                if (sf[k] < i + 1) sf[k] = i + 1;
+                mr = r;
+                ml = l;
+            }
+        }
+    }
+}
+
+/* mask[0, L) of one transcript (codes c): DUST on every ACGT run, then gaps
+ * shorter than `linker` between masked bases filled */
+static void dust_tx(const uint8_t *c, int32_t L, int T, int W, int linker, uint8_t *mask)
+{
+    memset(mask, 0, (size_t)(L > 0 ? L : 1));
+    for (int32_t i = 0; i < L;) {
+        while (i < L && c[i] > 3) i++;
+        const int32_t a = i;
+        while (i < L && c[i] <= 3) i++;
+        if (i - a >= 3) dust_run(c + a, i - a, T, W, mask + a);
+    }
+    int32_t last = -1;   /* end of the last masked base run */
+    for (int32_t u = 0; u < L; u++) {
+        if (!mask[u]) continue;
+        if (last >= 0 && u > last && u - last < linker)
+            for (int32_t v = last; v < u; v++) mask[v] = 1;
+        while (u < L && mask[u]) u++;
+        last = u;
+    }
+}
+
+/* exported for tests: the DUST mask of one code sequence */
+void orc_dust(const uint8_t *codes, int32_t L, int32_t level, int32_t window, int32_t linker, uint8_t *mask)
+{
+    dust_tx(codes, L, level, window, linker, mask);
 }
 
 /* ---------------- index of one subject sample ---------------- */
@@ -469,14 +593,24 @@ static void core_search(const uint8_t *codes, const uint64_t *tx_start, const in
     const int32_t s = P->word_size - W16 + 1;
     seed *sd = NULL;
     uint64_t sdcap = 0;
+    uint8_t *mask = NULL;
+    int32_t mcap = 0;
     for (uint32_t g = 0; g < n_genes; g++) {
         if (gene_sample[g] != qsample) continue;
         for (uint32_t ii = gene_tx_off[g]; ii < gene_tx_off[g + 1]; ii++) {
             uint32_t q = gene_tx[ii];
             uint64_t qs = tx_start[q];
             int32_t Lq = (int32_t)(tx_start[q + 1] - qs);
+            if (P->dust_level > 0) {
+                if (Lq + 1 > mcap) {
+                    mcap = 2 * Lq + 1;
+                    mask = (uint8_t *)realloc(mask, (size_t)mcap);
+                }
+                dust_tx(codes + qs, Lq, P->dust_level, P->dust_window, P->dust_linker, mask);
+            }
             for (int strand = 0; strand < 2; strand++) {
                 uint64_t nsd = 0;
+                int32_t prev_usable = INT32_MIN / 2;   /* previous usable word (spec 2: D(p)) */
                 for (int32_t p = 0; p + W16 <= Lq; p += s) {
                     uint32_t key = 0;
                     int ok = 1;
@@ -485,7 +619,12 @@ static void core_search(const uint8_t *codes, const uint64_t *tx_start, const in
                         if (c > 3) { ok = 0; break; }
                         key |= (uint32_t)c << (2 * k);
                     }
+                    if (ok && P->dust_level > 0)   /* forward bases of the oriented window */
+                        for (int k = 0; k < W16 && ok; k++)
+                            if (mask[strand ? Lq - 1 - (p + k) : p + k]) ok = 0;
                     if (!ok) continue;
+                    const int32_t D = p - prev_usable;
+                    prev_usable = p;
                     for (uint64_t e = lower_key(&ix, key); e < ix.n && ix.e[e].key == key; e++) {
                         uint32_t t = ix.e[e].tx;
                         int32_t o = (int32_t)ix.e[e].off;
@@ -497,7 +636,7 @@ static void core_search(const uint8_t *codes, const uint64_t *tx_start, const in
                             if (a > 3 || b > 3 || a != b) break;
                             x--, y--;
                         }
-                        if (p - x >= s) continue;  /* not canonical */
+                        if (p - x >= D) continue;  /* not canonical */
                         int32_t e2 = p + W16, f2 = o + W16;
                         while (e2 < Lq && f2 < Lt) {
                             uint8_t a = qbase(codes, qs, Lq, strand, e2), b = codes[ts + f2];
@@ -524,6 +663,7 @@ static void core_search(const uint8_t *codes, const uint64_t *tx_start, const in
         }
     }
     free(sd);
+    free(mask);
     free(ix.e);
 }
 
@@ -544,19 +684,17 @@ static int keyed_cmp(const void *pa, const void *pb)
  * sample as query; the other direction's HSPs are their mirror images. Each
  * direction applies its own e-value cut (its query length and subject DB).
  * Output order: (query gene, isoform, strand, subject tx, HSP index). */
-int orc_align(const char *seq, uint64_t total_len, const uint64_t *tx_start,
-              const int32_t *tx_sample, uint32_t n_tx,
-              const uint32_t *gene_tx_off, const uint32_t *gene_tx, uint32_t n_genes,
-              const int32_t *gene_sample, int32_t qsample, int32_t tsample,
-              const orc_params *P, orc_hsp **out, uint64_t *n_out)
+int orc_align_codes(const uint8_t *codes, const uint64_t *tx_start,
+                    const int32_t *tx_sample, uint32_t n_tx,
+                    const uint32_t *gene_tx_off, const uint32_t *gene_tx, uint32_t n_genes,
+                    const int32_t *gene_sample, int32_t qsample, int32_t tsample,
+                    const orc_params *P, orc_hsp **out, uint64_t *n_out)
 {
     if (P->word_size < W16 || P->word_size > 64 || qsample == tsample) return -1;
-    uint8_t *codes = (uint8_t *)malloc(total_len ? total_len : 1);
-    for (uint64_t i = 0; i < total_len; i++) codes[i] = code_of(seq[i]);
     int64_t dblen = 0, dbn = 0;   /* subject sample of this direction */
     for (uint32_t t = 0; t < n_tx; t++)
         if (tx_sample[t] == tsample) { dblen += (int64_t)(tx_start[t + 1] - tx_start[t]); dbn++; }
-    const int mirror = qsample > tsample;
+    const int mirror = P->symmetric && qsample > tsample;
     core_vec cv = {0, 0, 0};
     core_search(codes, tx_start, tx_sample, n_tx, gene_tx_off, gene_tx, n_genes, gene_sample,
                 mirror ? tsample : qsample, mirror ? qsample : tsample, P, &cv);
@@ -598,10 +736,24 @@ int orc_align(const char *seq, uint64_t total_len, const uint64_t *tx_start,
         free(tx_pos);
     }
     free(cv.v);
-    free(codes);
     *out = hv.v;
     *n_out = hv.n;
     return 0;
+}
+
+/* ASCII entry point: the whole concatenation converted to codes first. */
+int orc_align(const char *seq, uint64_t total_len, const uint64_t *tx_start,
+              const int32_t *tx_sample, uint32_t n_tx,
+              const uint32_t *gene_tx_off, const uint32_t *gene_tx, uint32_t n_genes,
+              const int32_t *gene_sample, int32_t qsample, int32_t tsample,
+              const orc_params *P, orc_hsp **out, uint64_t *n_out)
+{
+    uint8_t *codes = (uint8_t *)malloc(total_len ? total_len : 1);
+    for (uint64_t i = 0; i < total_len; i++) codes[i] = code_of(seq[i]);
+    int rc = orc_align_codes(codes, tx_start, tx_sample, n_tx, gene_tx_off, gene_tx, n_genes, gene_sample,
+                             qsample, tsample, P, out, n_out);
+    free(codes);
+    return rc;
 }
 
 void orc_free(void *p) { free(p); }

@@ -22,10 +22,25 @@ ROW_COMPARE = ["label", "qgene", "qiso", "sgene", "siso", "reverse", "bitscore",
 
 
 def oracle_all_hsps(db: OracleDB, n_samples, word_size=28, xdrop_half=108,
-                    evalue=1e-99):
-    """Every directed search (q, s), q != s, with the C oracle."""
-    return {(q, s): db.align(q, s, word_size, xdrop_half, evalue)
-            for q, s in itertools.permutations(range(n_samples), 2)}
+                    evalue=1e-99, symmetric=False, dust=None, threads=None):
+    """Every directed search (q, s), q != s, with the C oracle -- run on a
+    thread pool (ctypes releases the GIL; the oracle keeps no global state)."""
+    from concurrent.futures import ThreadPoolExecutor
+    perms = list(itertools.permutations(range(n_samples), 2))
+    run = lambda qs: db.align(qs[0], qs[1], word_size, xdrop_half, evalue, symmetric, dust)  # noqa: E731
+    with ThreadPoolExecutor(threads or oracle_threads()) as ex:
+        return dict(zip(perms, ex.map(run, perms)))
+
+
+def oracle_threads():
+    """Worker threads for the oracle: the cores this process may use, at most
+    16 (the GPU box's CPU share; os.cpu_count() there shows the whole host)."""
+    import os
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
 
 
 def diff_hsps(eng, ora, db: OracleDB, q, s):
@@ -97,11 +112,13 @@ def diff_rows(eng_rows, ora_rows, tag=""):
 
 def full_check(engine, samples, word_size=28, xdrop_half=108, evalue=1e-99,
                top_matches=1, keep_all=True, check_hsps=True):
-    """Engine (already run) vs oracles on the same samples. Returns messages
-    (empty = bit-exact parity) and a small summary dict."""
+    """Engine (already run) vs oracles on the same samples, in the engine's
+    alignment mode (independent directed searches or spec 5b; DUST or not).
+    Returns messages (empty = bit-exact parity) and a small summary dict."""
     db = OracleDB(samples)
     N = len(samples)
-    ora = oracle_all_hsps(db, N, word_size, xdrop_half, evalue)
+    ora = oracle_all_hsps(db, N, word_size, xdrop_half, evalue,
+                          getattr(engine, "symmetric", False), getattr(engine, "dust", None))
     msgs = []
     if check_hsps:
         for (q, s), arr in ora.items():

@@ -29,7 +29,9 @@ class RcOpts(ctypes.Structure):
     _fields_ = [("top_matches", ctypes.c_int32), ("keep_all", ctypes.c_int32),
                 ("evalue", ctypes.c_double), ("word_size", ctypes.c_int32),
                 ("xdrop_half", ctypes.c_int32), ("device", ctypes.c_int32),
-                ("shard_rank", ctypes.c_int32), ("shard_count", ctypes.c_int32)]
+                ("shard_rank", ctypes.c_int32), ("shard_count", ctypes.c_int32),
+                ("symmetric", ctypes.c_int32), ("dust_level", ctypes.c_int32),
+                ("dust_window", ctypes.c_int32), ("dust_linker", ctypes.c_int32)]
 
 
 HSP_FIELDS = ["q_tx", "s_tx", "qstart", "qend", "sstart", "send", "length",
@@ -76,7 +78,7 @@ class RcTiming(ctypes.Structure):
     _fields_ = [(n, ctypes.c_double) for n in (
         "pack_ms", "index_ms", "align_ms", "topn_ms", "rbh_ms", "graph_ms",
         "reduce_ms", "total_ms", "seed_kernel_ms", "align_kernel_ms", "ext_steps",
-        "ext_calls", "ext_fullband", "ext_deferred")]
+        "ext_calls", "ext_fullband", "ext_deferred", "big_passes")]
 
 
 assert HSP_DTYPE.itemsize == ctypes.sizeof(RcHsp)
@@ -117,6 +119,7 @@ SIGNATURES = {
     "rc_pair_sums_unfiltered": (ctypes.c_int, [VP, VP, VP]),
     "rc_distance": (ctypes.c_int, [VP, VP, VP]),
     "rc_timings": (ctypes.c_int, [VP, P(RcTiming)]),
+    "rc_dust_mask": (ctypes.c_int, [VP, ctypes.c_int32, VP, ctypes.c_uint64, P(ctypes.c_uint64)]),
     "rc_fasta_open": (ctypes.c_int, [ctypes.c_char_p, P(VP)]),
     "rc_fasta_close": (ctypes.c_int, [VP]),
     "rc_fasta_info": (ctypes.c_int, [VP, P(ctypes.c_uint64), P(ctypes.c_uint64), P(ctypes.c_uint64)]),

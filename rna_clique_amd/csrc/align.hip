@@ -16,17 +16,19 @@
 
 #include <climits>
 #include <cstdlib>
+#include <type_traits>
 
 namespace rcg {
 
 constexpr int SBLOCK = 256;
 #ifndef RC_SEED_CAP
-#define RC_SEED_CAP 768
+#define RC_SEED_CAP 1024
 #endif
 #ifndef RC_SEED_WAVES
 #define RC_SEED_WAVES 1
 #endif
-constexpr int SEED_CAP = RC_SEED_CAP;
+constexpr int SEED_CAP = RC_SEED_CAP;   // seeds of one pass in LDS (a power of two: the bitonic sort pads to one)
+static_assert((SEED_CAP & (SEED_CAP - 1)) == 0, "RC_SEED_CAP must be a power of two");
 constexpr int HBATCH = 4;                          // hits per lane per batch of the seed kernel
 constexpr int MAX_SAMPLES = 256;
 
@@ -46,10 +48,6 @@ __device__ __forceinline__ uint64_t rfl(uint64_t v)
     return ((uint64_t)rfl((uint32_t)(v >> 32)) << 32) | rfl((uint32_t)v);
 }
 
-struct LSeed {
-    uint64_t k1;    // iso:7 | strand:1 | gtx:32 | x:24
-    uint32_t y, len;
-};
 
 // Oriented query geometry. strand 0: q; strand 1: revcomp(q).
 struct QGeo {
@@ -106,24 +104,54 @@ __device__ __forceinline__ int run_of(const uint32_t *pre, uint32_t h)
     return lo;
 }
 
+// Query word at oriented position p of a transcript (forward start qs,
+// length Lq): usable for seeding unless its 16 bases hold an ambiguous base or
+// a DUST-masked one (spec 1, 1b; the mask is over forward positions)
 template <bool AMB>
+__device__ __forceinline__ bool word_usable(const Db &db, uint64_t qs, int Lq, int strand, int p, uint64_t total)
+{
+    if (AMB) {
+        const QGeo qg = {qs, Lq};
+        const uint64_t *QM = strand ? db.ARC : db.AF;
+        if (win(QM, qfwd_pos(qg, strand, total, p)) & 0xFFFFFFFFull) return false;
+    }
+    if (db.dmask) {
+        const int64_t f = (int64_t)qs + (strand ? (int64_t)(Lq - p - W16) : (int64_t)p);
+        if (win_bits(db.dmask, f) & 0xFFFFull) return false;
+    }
+    return true;
+}
+
+// BIG = false: one workgroup per query gene, the seeds of a pass in LDS; a
+// (gene, subject sample) pass that alone overflows LDS is put on P.big_list.
+// BIG = true: one workgroup per big_list entry, that single pass with its
+// seeds in global scratch (P.big_cap per workgroup); an entry that overflows
+// even that goes to P.big_retry (the host doubles big_cap).
+template <bool AMB, bool BIG>
 __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Index ix, SeedParams P)
 {
-    const uint32_t g = P.gene_begin + blockIdx.x;
+    const uint64_t big_e = BIG ? P.big_list[blockIdx.x] : 0ull;
+    const uint32_t g = BIG ? P.gene_begin + (uint32_t)(big_e >> 8) : P.gene_begin + blockIdx.x;
     if (g >= P.gene_end) return;
     const int tid = threadIdx.x;
 
-    __shared__ LSeed seeds[SEED_CAP];
-    __shared__ uint16_t seg_begin[SEED_CAP + 1];
+    using SegIdx = typename std::conditional<BIG, uint32_t, uint16_t>::type;
+    __shared__ LSeed seeds_lds[BIG ? 1 : SEED_CAP];
+    __shared__ SegIdx seg_lds[BIG ? 1 : SEED_CAP + 1];
+    __shared__ uint8_t segT_lds[BIG ? 1 : SEED_CAP];
+    const uint32_t cap = BIG ? P.big_cap : (uint32_t)SEED_CAP;
+    LSeed *const seeds = BIG ? P.big_seeds + (size_t)blockIdx.x * cap : seeds_lds;
+    SegIdx *const seg_begin = BIG ? reinterpret_cast<SegIdx *>(P.big_seg + (size_t)blockIdx.x * (cap + 1)) : seg_lds;
+    uint8_t *const seg_T = BIG ? P.big_segT + (size_t)blockIdx.x * cap : segT_lds;
     __shared__ uint32_t it_lo[SBLOCK], it_cnt[SBLOCK], it_pre[SBLOCK + 1], it_info[SBLOCK];
     __shared__ uint32_t it_key[SBLOCK];
+    __shared__ uint32_t it_d[SBLOCK];   // D(p): distance to the previous usable query word (spec 2)
     __shared__ uint32_t hq_pos[SBLOCK / 64][64 * HBATCH];   // per-wave queue of hits for the full test
     __shared__ uint8_t hq_k[SBLOCK / 64][64 * HBATCH];
     __shared__ uint64_t it_qlw[SBLOCK], it_qlm[AMB ? SBLOCK : 1];
     __shared__ uint64_t iso_start[MAX_ISO];
     __shared__ uint32_t iso_len[MAX_ISO], iso_gtx[MAX_ISO], iso_pre[MAX_ISO + 1];
     __shared__ uint32_t tcnt[MAX_SAMPLES], tpre[MAX_SAMPLES + 1];
-    __shared__ uint8_t seg_T[SEED_CAP];
     __shared__ uint32_t wsum[SBLOCK / 64];
     __shared__ uint32_t sh_nseed, sh_flags;
     __shared__ unsigned long long sh_sbase, sh_cbase;
@@ -172,20 +200,29 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
 #endif
     const uint32_t gl = g - P.gene_begin;
 
-    // subject samples of this shard: higher-numbered samples only (symmetric
-    // spec: the pair's other direction is the mirror image)
+    // subject samples of this query sample in this shard (spec 5b: the
+    // higher-numbered ones only, the pair's other direction is the mirror image)
     const uint64_t tm[4] = {P.tmask[4 * Q], P.tmask[4 * Q + 1], P.tmask[4 * Q + 2], P.tmask[4 * Q + 3]};
-    // the shard's subjects of this query sample: a contiguous sample range
-    // (pairs are numbered subject-major), so hits are filtered by position
-    int Thi = 0, T0 = N;
-    for (int w = 0; w < 4; w++)
-        if (tm[w]) {
-            T0 = min(T0, 64 * w + __builtin_ctzll(tm[w]));
-            Thi = max(Thi, 64 * w + 64 - __builtin_clzll(tm[w]));
-        }
-    T0 = max(T0, Q + 1);
-    int T1 = Thi;
-    while (T0 < Thi) {
+    // passes run over the span [T0, Tr) of the subject samples (a contiguous
+    // position range, so hits are filtered by position; the query's own
+    // sample, inside the span when both directions are searched, is filtered
+    // out by position too), halved [T0, T1) while their seeds overflow the
+    // pass capacity; the seed test drops any other sample outside the mask
+    int T0 = N, Tr = 0;
+    if (BIG) {
+        T0 = (int)(big_e & 0xFFu);
+        Tr = T0 + 1;
+    } else {
+        for (int w = 0; w < 4; w++)
+            if (tm[w]) {
+                T0 = min(T0, 64 * w + __builtin_ctzll(tm[w]));
+                Tr = max(Tr, 64 * w + 64 - __builtin_clzll(tm[w]));
+            }
+        if (P.sym) T0 = max(T0, Q + 1);
+    }
+    int T1 = Tr;
+    const uint32_t qpb0 = (uint32_t)db.sample_pos_begin[Q], qpb1 = (uint32_t)db.sample_pos_begin[Q + 1];
+    while (T0 < Tr) {
         if (tid == 0) {
             sh_nseed = 0;
             sh_flags = 0;
@@ -203,22 +240,40 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
             const uint32_t it = ib + tid;
             uint32_t lo = 0, cnt = 0, info = 0, key = 0;
             uint64_t qlw = 0, qlm = 0;
+            bool ok = false;
+            int p = 0, strand = 0;
+            uint32_t ii = 0;
             if (it < n_items) {
-                uint32_t ii = 0;
                 while (ii + 1 < niso && iso_pre[ii + 1] <= it) ii++;
                 const uint32_t rem = it - iso_pre[ii];
                 const uint32_t ns = (iso_pre[ii + 1] - iso_pre[ii]) >> 1;
-                const int strand = rem >= ns ? 1 : 0;
-                const int p = (int)(rem - (strand ? ns : 0)) * stride;
+                strand = rem >= ns ? 1 : 0;
+                p = (int)(rem - (strand ? ns : 0)) * stride;
                 info = ii | ((uint32_t)strand << 7) | ((uint32_t)p << 8);
+                ok = word_usable<AMB>(db, iso_start[ii], (int)iso_len[ii], strand, p, total);
+            }
+            // D(p): the previous usable word of the same isoform and strand is
+            // item it - k (p - k s), in this batch's LDS or looked up again
+            it_d[tid] = ok ? 1u : 0u;
+            __syncthreads();
+            uint32_t D = (uint32_t)p + 1u;   // none: every hit is canonical
+            if (ok) {
+                for (int k = 1; p - k * stride >= 0; k++) {
+                    const bool u = tid - k >= 0 ? it_d[tid - k] != 0
+                                                : word_usable<AMB>(db, iso_start[ii], (int)iso_len[ii], strand,
+                                                                   p - k * stride, total);
+                    if (u) {
+                        D = (uint32_t)(k * stride);
+                        break;
+                    }
+                }
+            }
+            __syncthreads();
+            it_d[tid] = D;
+            if (it < n_items) {
                 QGeo qg = {iso_start[ii], (int)iso_len[ii]};
                 const uint64_t qp = qfwd_pos(qg, strand, total, p);
                 const uint64_t *QA = strand ? db.RC : db.F;
-                bool ok = true;
-                if (AMB) {
-                    const uint64_t *QM = strand ? db.ARC : db.AF;
-                    ok = (win(QM, qp) & 0xFFFFFFFFull) == 0;
-                }
                 if (ok) {
                     key = (uint32_t)win(QA, qp);
                     // the whole bucket of the key's top bits (one round trip, no
@@ -305,10 +360,12 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
 #pragma unroll
                 for (int j = 0; j < HBATCH; j++) {
                     const uint32_t pos = (uint32_t)hev[j];
-                    live[j] = live[j] && (uint32_t)(hev[j] >> 32) == it_key[hk[j]] && pos >= pb0 && pos < pb1;
+                    live[j] = live[j] && (uint32_t)(hev[j] >> 32) == it_key[hk[j]] && pos >= pb0 && pos < pb1 &&
+                              (pos < qpb0 || pos >= qpb1);
                     hsw[j] = hsm[j] = hbw[j] = 0;
                     bool decided = false;
-                    if (lpre && live[j] && hk[j] > 0 && (int)(it_info[hk[j]] >> 8) >= stride) {
+                    if (lpre && live[j] && hk[j] > 0 && it_d[hk[j]] == (uint32_t)stride &&
+                        (int)(it_info[hk[j]] >> 8) >= stride) {
                         const uint32_t a = it_pre[hk[j] - 1], b = it_pre[hk[j]];
                         if (a >= hb0 && b <= hb0 + HCHUNK) {
                             const uint32_t tgt = pos - (uint32_t)stride;
@@ -328,7 +385,8 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                         }
                     }
                     if (decided) {
-                    } else if (live[j] && fast && (int)(it_info[hk[j]] >> 8) >= stride) {
+                    } else if (live[j] && fast && it_d[hk[j]] == (uint32_t)stride &&
+                               (int)(it_info[hk[j]] >> 8) >= stride) {
                         hsw[j] = win_s(db.F, (int64_t)pos - 32) ^ it_qlw[hk[j]];
                         if (AMB) hsm[j] = win_s(db.AF, (int64_t)pos - 32) | it_qlm[hk[j]];
                         hbw[j] = win_bits(db.txstart, (int64_t)pos - 63);
@@ -380,9 +438,10 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     }
                     if (!((tm[st.sample >> 6] >> (st.sample & 63)) & 1)) continue;
                     const int off = (int)(pos - (uint32_t)st.start);
-                    const int maxl = min(min(p, off), stride);
+                    const int Dp = (int)it_d[k];
+                    const int maxl = min(min(p, off), Dp);
                     int l;
-                    if (fast) {
+                    if (fast && (xl || maxl <= 32)) {
                         // matching bases leftwards from (p - 1, pos - 1): the
                         // highest differing base of the windows ending there
                         l = min(xl ? (int)(__builtin_clzll(xl) >> 1) : 32, maxl);
@@ -392,7 +451,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                         l = lcp<AMB>(QL, QLM, qrev_pos(qg, strand, total, p), db.RC, db.ARC,
                                      total - st.start - (uint64_t)off, maxl);
                     }
-                    if (l >= stride) continue;   // not canonical
+                    if (l >= Dp) continue;   // not canonical: a usable word lies in [x, p)
                     const int maxr = min(qg.Lq - p - W16, (int)st.len - off - W16);
                     int r;
                     if (fast && xr) {
@@ -405,7 +464,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     const int len = l + W16 + r;
                     if (len < P.word) continue;
                     const uint32_t slot = atomicAdd(&sh_nseed, 1u);
-                    if (slot < (uint32_t)SEED_CAP) {
+                    if (slot < cap) {
                         LSeed sd;
                         sd.k1 = ((uint64_t)ii << 57) | ((uint64_t)strand << 56) | ((uint64_t)stx << 24) |
                                 (uint64_t)(uint32_t)(p - l);
@@ -422,8 +481,18 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
         }
         if (sh_flags & 1u) {   // too many seeds: fewer subject samples per pass
             if (T1 - T0 == 1) {
-                if (tid == 0) atomicOr(P.status, 2u);
-                return;
+                // one subject sample alone overflows: the global-memory pass
+                // takes (gene, T0); its groups stay empty here
+                if (tid == 0) {
+                    const uint64_t e = ((uint64_t)gl << 8) | (uint64_t)T0;
+                    const unsigned long long k = atomicAdd(BIG ? P.big_retry_n : P.big_n, 1ull);
+                    if (k < P.big_list_cap) (BIG ? P.big_retry : P.big_out)[k] = e;
+                    else atomicOr(P.status, 8u);
+                }
+                T0 = T1;
+                T1 = Tr;
+                __syncthreads();
+                continue;
             }
             T1 = T0 + (T1 - T0) / 2;
             __syncthreads();
@@ -494,10 +563,10 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
             const uint32_t f = (i < nseed && (i == 0 || (seeds[i].k1 >> 24) != (seeds[i - 1].k1 >> 24))) ? 1u : 0u;
             uint32_t tot;
             const uint32_t pos = nseg + block_exscan(f, wsum, tot);
-            if (f) seg_begin[pos] = (uint16_t)i;
+            if (f) seg_begin[pos] = (SegIdx)i;
             nseg += tot;
         }
-        if (tid == 0) seg_begin[nseg] = (uint16_t)nseed;
+        if (tid == 0) seg_begin[nseg] = (SegIdx)nseed;
         for (int T = tid; T < N; T += SBLOCK) tcnt[T] = 0;
         __syncthreads();
         for (uint32_t sg = tid; sg < nseg; sg += SBLOCK) {
@@ -536,7 +605,11 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                 const uint32_t gtx = (uint32_t)(k1 >> 24);
                 const int T = seg_T[sg];
                 uint32_t rk = 0;   // rank among earlier candidates of the same sample
-                for (uint32_t s2 = 0; s2 < sg; s2++) rk += seg_T[s2] == T;
+                if (T1 - T0 == 1)
+                    rk = sg;
+                else
+                    for (uint32_t s2 = 0; s2 < sg; s2++) rk += seg_T[s2] == T;
+                if (b1 - b0 > 0xFFFFu) atomicOr(P.status, 16u);   // seed_cnt is 16 bits
                 Cand c;
                 c.seed_off = (uint32_t)(sbase + b0);
                 c.q_gtx = iso_gtx[(uint32_t)(k1 >> 57)];
@@ -561,7 +634,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
             P.gc_cnt[gi] = tcnt[T];
         }
         T0 = T1;
-        T1 = Thi;
+        T1 = Tr;
         __syncthreads();
         SEED_TICK(4);
     }
@@ -845,7 +918,7 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
         // DB) and the mirrored one (subject length, query sample's DB)
         const int thr_f = P.thr[(size_t)st.sample * (size_t)(P.max_len + 1) + (size_t)Lq];
         const int thr_r = P.thr[(size_t)qt.sample * (size_t)(P.max_len + 1) + (size_t)Lt];
-        const bool pf = bsc >= thr_f, pr = bsc >= thr_r;
+        const bool pf = bsc >= thr_f, pr = P.sym && bsc >= thr_r;
         const bool out = kept && (pf || pr);
         const uint64_t om = __ballot(out);
         const int nout = __popcll(om);
@@ -1373,7 +1446,7 @@ __global__ __launch_bounds__(256) void first_finish_kernel(ExtParams P)
         const int bni = len + (lI + lJ - 2 * ld + lg) / 2 + (ri + rj - 2 * rd + rg) / 2;
         const int thr_f = P.thr[(size_t)cd.ssam * (size_t)(P.max_len + 1) + (size_t)cd.Lq];
         const int thr_r = P.thr[(size_t)cd.qsam * (size_t)(P.max_len + 1) + (size_t)cd.Lt];
-        const bool pf = bsc >= thr_f, pr = bsc >= thr_r;
+        const bool pf = bsc >= thr_f, pr = P.sym && bsc >= thr_r;
         if (pf || pr) {
             DHsp h;
             h.q_tx = cd.q_gtx;
@@ -1541,9 +1614,19 @@ void launch_seed(bool amb, const Db &db, const Index &ix, const SeedParams &P, h
     const uint32_t n = P.gene_end - P.gene_begin;
     if (n == 0) return;
     if (amb)
-        hipLaunchKernelGGL(seed_kernel<true>, dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
+        hipLaunchKernelGGL((seed_kernel<true, false>), dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
     else
-        hipLaunchKernelGGL(seed_kernel<false>, dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
+        hipLaunchKernelGGL((seed_kernel<false, false>), dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
+}
+
+// the global-memory passes of the (gene, sample) entries P.big_list[0, n)
+void launch_seed_big(bool amb, const Db &db, const Index &ix, const SeedParams &P, uint32_t n, hipStream_t st)
+{
+    if (n == 0) return;
+    if (amb)
+        hipLaunchKernelGGL((seed_kernel<true, true>), dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
+    else
+        hipLaunchKernelGGL((seed_kernel<false, true>), dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
 }
 
 void launch_extend(bool amb, const Db &db, const ExtParams &P, hipStream_t st)

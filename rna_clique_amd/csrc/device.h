@@ -66,6 +66,7 @@ struct Db {
     const uint32_t *sample_tx_begin;         // n_samples + 1
     const uint64_t *sample_pos_begin;        // n_samples + 1: first base of each sample
     const uint64_t *txstart;                 // bit per base: 1 where a transcript starts (+1 guard word)
+    const uint64_t *dmask;                   // bit per base: DUST-masked query bases (+1 guard word), or null
     int32_t n_samples;
 };
 
@@ -111,11 +112,18 @@ struct Cand {
 constexpr int CAND_DWORDS = (int)(sizeof(Cand) / 4);
 static_assert(sizeof(Cand) == 48, "Cand is read as 12 dwords");
 
+// A seed of the seed kernel before sorting: k1 = iso:7 | strand:1 | gtx:32 | x:24
+struct LSeed {
+    uint64_t k1;
+    uint32_t y, len;
+};
+
 // seed_kernel: per query gene, lookups -> canonical seeds -> candidates.
 struct SeedParams {
     int32_t word;                 // W
     int32_t stride;               // W - 16 + 1
     int32_t pre_mode;             // canonical pre-test: 1 = previous word's hits (LDS), 0 = sequence windows
+    int32_t sym;                  // spec 5b: subjects are higher-numbered samples only
     uint32_t gene_begin, gene_end;   // shard
     GSeed *seeds;
     uint64_t seed_cap;            // per allocation shard
@@ -125,13 +133,25 @@ struct SeedParams {
     unsigned long long *cand_count;  // [NSHARD]
     uint32_t *gc_off, *gc_cnt;    // [(g - gene_begin) * N + T] candidates of (gene, sample)
     const uint64_t *tmask;        // [n_samples][4] subject samples (> query sample) of this shard
-    unsigned int *status;         // bit 0 overflow, bit 1 gene limit
+    unsigned int *status;         // bit 0 overflow, bit 1 gene limit, bit 3 big list full, bit 4 seed_cnt > 16 bits
     unsigned long long *prof;     // RC_ROW_TIMING builds: block cycles per phase
+    // (gene, sample) passes whose seeds overflow LDS: ((gene - gene_begin) << 8) | sample
+    uint64_t *big_out;            // the LDS kernel appends here
+    unsigned long long *big_n;
+    const uint64_t *big_list;     // the global-memory kernel's entries (one workgroup each)
+    uint64_t *big_retry;          // entries that overflowed big_cap too
+    unsigned long long *big_retry_n;
+    uint64_t big_list_cap;
+    uint32_t big_cap;             // seeds per workgroup in global scratch (power of two)
+    LSeed *big_seeds;
+    uint32_t *big_seg;            // big_cap + 1 per workgroup
+    uint8_t *big_segT;            // big_cap per workgroup
 };
 
 // extend_kernel: one wave per candidate, greedy X-drop, purge, e-value cut.
 struct ExtParams {
     int32_t xdrop;
+    int32_t sym;                  // spec 5b: also apply the mirrored direction's e-value cut
     int32_t max_len;
     const int32_t *thr;           // [n_samples][max_len + 1] min score_half
     const int32_t *bits10;        // [2 * max_len + 2]

@@ -28,6 +28,10 @@ void launch_kmer_fill(bool, const TxInfo *, uint32_t, const uint64_t *, const ui
                       uint64_t *, hipStream_t);
 void launch_bucket_fill(const uint64_t *, uint64_t, int, uint32_t *, hipStream_t);
 void launch_seed(bool, const Db &, const Index &, const SeedParams &, hipStream_t);
+void launch_seed_big(bool, const Db &, const Index &, const SeedParams &, uint32_t, hipStream_t);
+void launch_dust(bool, uint64_t, const uint64_t *, const uint64_t *, const uint64_t *, const TxInfo *, uint32_t, int,
+                 int, int, uint32_t *, uint32_t, uint64_t *, hipStream_t);
+uint32_t dust_scratch_words(uint32_t);
 void launch_extend(bool, const Db &, const ExtParams &, hipStream_t);
 void launch_extend_rows(bool, const Db &, const ExtParams &, int, hipStream_t);
 void launch_group(const GroupParams &, int, hipStream_t);
@@ -251,7 +255,8 @@ struct rc_engine {
     DBuf<uint64_t> d_kpos_off, d_kcnt;
     DBuf<uint64_t> d_ent, d_ent2;   // (k-mer << 32 | position), unsorted / sorted
     DBuf<uint32_t> d_bucket, d_pos_tx;
-    DBuf<uint64_t> d_sample_pos, d_txstart, d_kpos_rel;
+    DBuf<uint64_t> d_sample_pos, d_txstart, d_kpos_rel, d_dmask;
+    DBuf<uint32_t> d_dust_scratch;
     DBuf<unsigned long long> d_prof;
     DBuf<uint8_t> d_tmp;
     DBuf<int32_t> d_thr, d_bits10;
@@ -268,6 +273,14 @@ struct rc_engine {
     DBuf<uint32_t> d_mcnt, d_mcur, d_tx_pos;
     DBuf<unsigned long long> d_shard_cnt, d_shard_prefix;
     uint64_t seed_cap = 0, cand_cap = 0, ovf_cap = 0;   // per-shard / total capacities
+    // (gene, sample) seed passes too big for LDS, and their global scratch
+    DBuf<uint64_t> d_big_out, d_big_list, d_big_retry;
+    DBuf<LSeed> d_big_seeds;
+    DBuf<uint32_t> d_big_seg;
+    DBuf<uint8_t> d_big_segT;
+    uint64_t big_list_cap = 1 << 16;
+    uint32_t big_cap = 1 << 13;
+    uint64_t n_big = 0;   // entries of the last run (rc_timing)
     DBuf<uint32_t> d_grp_off, d_grp_cnt;
     DBuf<unsigned long long> d_count;
     DBuf<unsigned int> d_status;
@@ -312,6 +325,10 @@ void rc_default_opts(rc_opts *o)
     o->device = 0;
     o->shard_rank = 0;
     o->shard_count = 1;
+    o->symmetric = 0;
+    o->dust_level = 20;
+    o->dust_window = 64;
+    o->dust_linker = 1;
 }
 
 const char *rc_last_error(void) { return g_err.c_str(); }
@@ -324,6 +341,11 @@ int rc_create(const rc_opts *opts, rc_engine **out)
     if (opts->top_matches < 1) return fail(RC_E_ARG, "top_matches must be >= 1");
     if (opts->word_size < W16 || opts->word_size > 64) return fail(RC_E_ARG, "word_size must be in [16, 64]");
     if (opts->xdrop_half < 0) return fail(RC_E_ARG, "xdrop_half must be >= 0");
+    if (opts->dust_level < 0 || (opts->dust_level > 0 && (opts->dust_window < 8 || opts->dust_window > 64 ||
+                                                          opts->dust_linker < 0)))
+        return fail(RC_E_ARG, "bad DUST parameters");
+    if (opts->dust_level > 0 && opts->symmetric)
+        return fail(RC_E_ARG, "DUST masks each direction's query: it needs symmetric = 0");
     if (opts->shard_count < 1 || opts->shard_rank < 0 || opts->shard_rank >= opts->shard_count)
         return fail(RC_E_ARG, "bad shard");
     int ndev = 0;
@@ -726,6 +748,10 @@ static int build_index(rc_engine *e)
     for (uint64_t p = e->pair0; p < e->pair1; p++) {
         slo = std::min(slo, (int)e->pair_b[p]);
         shi = std::max(shi, (int)e->pair_b[p]);
+        if (!e->o.symmetric) {   // both samples of a pair are subjects
+            slo = std::min(slo, (int)e->pair_a[p]);
+            shi = std::max(shi, (int)e->pair_a[p]);
+        }
     }
     const uint32_t t0 = shi < 0 ? 0 : e->sample_tx_begin[slo];
     const uint32_t t1 = shi < 0 ? 0 : e->sample_tx_begin[shi + 1];
@@ -794,6 +820,7 @@ static Db make_db(rc_engine *e)
     db.sample_tx_begin = e->d_sample_tx_begin.p;
     db.sample_pos_begin = e->d_sample_pos.p;
     db.txstart = e->d_txstart.p + 1;
+    db.dmask = e->o.dust_level > 0 ? e->d_dmask.p + 1 : nullptr;
     db.n_samples = (int32_t)e->samples.size();
     return db;
 }
@@ -819,6 +846,11 @@ static void shard_plan(rc_engine *e, uint32_t &g0, uint32_t &g1, std::vector<uin
         tmask[4 * qa + (sb >> 6)] |= 1ull << (sb & 63);
         smin = std::min(smin, qa);
         smax = std::max(smax, qa);
+        if (!e->o.symmetric) {   // the pair's second directed search: query b, subject a
+            tmask[4 * sb + (qa >> 6)] |= 1ull << (qa & 63);
+            smin = std::min(smin, sb);
+            smax = std::max(smax, sb);
+        }
     }
     if (smax < 0) {
         g0 = g1 = 0;
@@ -885,6 +917,18 @@ static int do_align(rc_engine *e)
     launch_pack(e->d_ascii.p, total, nwords, e->d_F.p + FRONT_PAD, e->d_RC.p + FRONT_PAD,
                 e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr, e->has_amb ? e->d_ARC.p + FRONT_PAD : nullptr, e->st);
     HIPCHK(hipGetLastError());
+    if (e->o.dust_level > 0) {
+        // DUST masks of the query transcripts (every transcript), bit per base
+        const size_t mw = (total >> 6) + 4;
+        CHK(e->d_dmask.ensure(mw));
+        HIPCHK(hipMemsetAsync(e->d_dmask.p, 0, mw * 8, e->st));
+        const uint32_t dblocks = 256 * 16;   // resident lanes of the chunk kernel (their slot scratch)
+        CHK(e->d_dust_scratch.ensure(dust_scratch_words(dblocks)));
+        launch_dust(e->has_amb, total, e->d_F.p + FRONT_PAD, e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr,
+                    e->d_txstart.p + 1, e->d_tx.p, (uint32_t)e->tx_sample.size(), e->o.dust_level,
+                    e->o.dust_window, e->o.dust_linker, e->d_dust_scratch.p, dblocks, e->d_dmask.p + 1, e->st);
+        HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipEventRecord(e->ev[1], e->st));
     CHK(build_index(e));
     HIPCHK(hipGetLastError());
@@ -922,22 +966,28 @@ static int do_align(rc_engine *e)
     ix.bits = e->index_bits;
     // --- seeds ---
     std::vector<unsigned long long> shard_cnt(2 * NSHARD);
+    CHK(e->d_count.ensure(16));
+    unsigned long long *big_n = e->d_count.p + 12, *big_retry_n = e->d_count.p + 13;
+    e->n_big = 0;
     for (int attempt = 0;; attempt++) {
-        if (attempt == 4) return fail(RC_E_NOMEM, "seed/candidate buffers kept overflowing");
+        if (attempt == 6) return fail(RC_E_NOMEM, "seed/candidate buffers kept overflowing");
         if (e->seed_cap * NSHARD > 0xFFFFFFFFull || e->cand_cap * NSHARD > 0xFFFFFFFFull)
             return fail(RC_E_LIMIT, "more than 2^32 seeds or candidates on one GPU: use more shards");
         CHK(e->d_seeds.ensure(e->seed_cap * NSHARD));
         CHK(e->d_cands.ensure(e->cand_cap * NSHARD));
+        CHK(e->d_big_out.ensure(e->big_list_cap));
         HIPCHK(hipMemsetAsync(e->d_shard_cnt.p, 0, 2 * NSHARD * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
+        HIPCHK(hipMemsetAsync(big_n, 0, 2 * sizeof(unsigned long long), e->st));
         if (nsgrp) HIPCHK(hipMemsetAsync(e->d_gc_cnt.p, 0, nsgrp * 4, e->st));
-        SeedParams S;
+        SeedParams S{};
         S.word = e->o.word_size;
         S.stride = e->o.word_size - W16 + 1;
         {
             const char *pm = getenv("RC_SEED_PRE");   // A/B knob; 1 = hit-list pre-test
             S.pre_mode = pm ? atoi(pm) : 1;
         }
+        S.sym = e->o.symmetric;
         S.gene_begin = g0;
         S.gene_end = g1;
         S.seeds = e->d_seeds.p;
@@ -950,20 +1000,73 @@ static int do_align(rc_engine *e)
         S.gc_cnt = e->d_gc_cnt.p;
         S.tmask = e->d_tmask.p;
         S.status = e->d_status.p;
+        S.big_out = e->d_big_out.p;
+        S.big_n = big_n;
+        S.big_retry_n = big_retry_n;
+        S.big_list_cap = e->big_list_cap;
         CHK(e->d_prof.ensure(8));
         HIPCHK(hipMemsetAsync(e->d_prof.p, 0, 8 * sizeof(unsigned long long), e->st));
         S.prof = e->d_prof.p;
         HIPCHK(hipEventRecord(e->ev[3], e->st));
         launch_seed(e->has_amb, db, ix, S, e->st);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(e->ev[9], e->st));
         unsigned int status = 0;
-        HIPCHK(hipMemcpyAsync(shard_cnt.data(), e->d_shard_cnt.p, 2 * NSHARD * 8, hipMemcpyDeviceToHost, e->st));
+        unsigned long long nb = 0;   // (big_n: d_count[12], next to the extension's counters [0, 8))
         HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipMemcpyAsync(&nb, big_n, sizeof nb, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipStreamSynchronize(e->st));
-        if (status & 2u)
-            return fail(RC_E_LIMIT, "a query gene has too many seeds against a single sample (or > 127 isoforms)");
-        if (!(status & 1u)) break;
+        if (status & 2u) return fail(RC_E_LIMIT, "a query gene has more than 127 isoforms");
+        if (status & 8u) {   // the big-pass list itself overflowed
+            e->big_list_cap = std::max<uint64_t>(4 * e->big_list_cap, nb + 1024);
+            continue;
+        }
+        bool again = (status & 1u) != 0;
+        // (gene, sample) passes whose seeds overflow LDS: global-memory passes,
+        // at most BIG_CHUNK workgroups per launch; entries that overflow big_cap
+        // too are collected and rerun with twice the scratch
+        const uint64_t BIG_CHUNK = 2048;
+        uint64_t *list = e->d_big_out.p;
+        e->n_big = nb;
+        while (!again && nb) {
+            if ((uint64_t)e->big_cap > (1ull << 22)) return fail(RC_E_LIMIT, "a (query gene, subject sample) pass has more than 2^22 seeds");
+            const uint64_t chunk = std::min<uint64_t>(nb, BIG_CHUNK);
+            CHK(e->d_big_list.ensure(nb));
+            CHK(e->d_big_retry.ensure(nb));
+            CHK(e->d_big_seeds.ensure(chunk * e->big_cap));
+            CHK(e->d_big_seg.ensure(chunk * (e->big_cap + 1)));
+            CHK(e->d_big_segT.ensure(chunk * e->big_cap));
+            if (list != e->d_big_list.p)
+                HIPCHK(hipMemcpyAsync(e->d_big_list.p, list, nb * 8, hipMemcpyDeviceToDevice, e->st));
+            HIPCHK(hipMemsetAsync(big_retry_n, 0, sizeof(unsigned long long), e->st));
+            SeedParams B = S;
+            B.big_retry = e->d_big_retry.p;
+            B.big_list_cap = nb;
+            B.big_cap = e->big_cap;
+            B.big_seeds = e->d_big_seeds.p;
+            B.big_seg = e->d_big_seg.p;
+            B.big_segT = e->d_big_segT.p;
+            for (uint64_t c0 = 0; c0 < nb; c0 += chunk) {
+                B.big_list = e->d_big_list.p + c0;
+                launch_seed_big(e->has_amb, db, ix, B, (uint32_t)std::min<uint64_t>(chunk, nb - c0), e->st);
+                HIPCHK(hipGetLastError());
+            }
+            unsigned long long nr = 0;
+            HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
+            HIPCHK(hipMemcpyAsync(&nr, big_retry_n, sizeof nr, hipMemcpyDeviceToHost, e->st));
+            HIPCHK(hipStreamSynchronize(e->st));
+            if (status & 16u) return fail(RC_E_LIMIT, "a candidate has more than 65535 seeds");
+            again = (status & 1u) != 0;
+            nb = nr;
+            // the retry entries become the next list (buffers swapped, not copied)
+            std::swap(e->d_big_list.p, e->d_big_retry.p);
+            std::swap(e->d_big_list.cap, e->d_big_retry.cap);
+            list = e->d_big_list.p;
+            if (nb) e->big_cap *= 2;
+        }
+        HIPCHK(hipEventRecord(e->ev[9], e->st));
+        HIPCHK(hipMemcpyAsync(shard_cnt.data(), e->d_shard_cnt.p, 2 * NSHARD * 8, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipStreamSynchronize(e->st));
+        if (!again) break;
         uint64_t ms = 0, mc = 0;
         for (int i = 0; i < NSHARD; i++) {
             ms = std::max<uint64_t>(ms, shard_cnt[i]);
@@ -972,6 +1075,7 @@ static int do_align(rc_engine *e)
         e->seed_cap = std::max<uint64_t>(e->seed_cap, ms * 5 / 4 + 4096);
         e->cand_cap = std::max<uint64_t>(e->cand_cap, mc * 5 / 4 + 1024);
     }
+    e->tm.big_passes = (double)e->n_big;
     std::vector<unsigned long long> prefix(NSHARD + 1, 0);
     for (int i = 0; i < NSHARD; i++) prefix[i + 1] = prefix[i] + shard_cnt[NSHARD + i];
     const uint64_t n_cand = prefix[NSHARD];
@@ -993,6 +1097,7 @@ static int do_align(rc_engine *e)
         HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
         ExtParams X;
         X.xdrop = e->o.xdrop_half;
+        X.sym = e->o.symmetric;
         X.max_len = e->max_len;
         X.thr = e->d_thr.p;
         X.bits10 = e->d_bits10.p;
@@ -1080,7 +1185,7 @@ static int do_align(rc_engine *e)
     HIPCHK(hipMemsetAsync(e->d_mcnt.p, 0, (ngrp + 1) * 4, e->st));
     HIPCHK(hipMemsetAsync(e->d_mcur.p, 0, ngrp * 4, e->st));
     launch_group(G, 0, e->st);
-    launch_group(G, 2, e->st);
+    if (e->o.symmetric) launch_group(G, 2, e->st);   // mirrored groups (spec 5b)
     auto exscan = [&](const uint32_t *in, uint64_t *out, size_t n) -> int {
         size_t tmp = 0;
         HIPCHK(rocprim::exclusive_scan(nullptr, tmp, in, out, (uint64_t)0, n, rocprim::plus<uint64_t>(), e->st));
@@ -1106,8 +1211,10 @@ static int do_align(rc_engine *e)
     G.mbase = nd;
     G.mkey = e->d_mkey.p;
     launch_group(G, 1, e->st);
-    launch_group(G, 3, e->st);
-    launch_group(G, 4, e->st);
+    if (e->o.symmetric) {
+        launch_group(G, 3, e->st);
+        launch_group(G, 4, e->st);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e->ev[4], e->st));
     HIPCHK(hipEventSynchronize(e->ev[4]));
@@ -1521,6 +1628,31 @@ int rc_distance(rc_engine *e, const int32_t *order, double *out)
     HIPCHK(hipMemcpyAsync(&status, e->d_status.p, 4, hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
     if (status & 4u) return fail(RC_E_NO_IDEAL, "No ideal components found. Cannot report distances!");
+    return RC_OK;
+}
+
+int rc_dust_mask(rc_engine *e, int32_t s, uint8_t *buf, uint64_t cap, uint64_t *n)
+{
+    if (!e || !n) return fail(RC_E_ARG, "null argument");
+    if (!e->aligned) return fail(RC_E_STATE, "no alignment yet");
+    if (s < 0 || s >= (int)e->samples.size()) return fail(RC_E_ARG, "bad sample");
+    const SampleRec &S = e->samples[s];
+    *n = S.nbases;
+    if (!buf) return RC_OK;
+    if (cap < S.nbases) return fail(RC_E_CAPACITY, "buffer too small");
+    if (!S.nbases) return RC_OK;
+    if (e->o.dust_level <= 0 || e->external) {
+        std::memset(buf, 0, S.nbases);
+        return RC_OK;
+    }
+    CHK(set_device(e));
+    const uint64_t w0 = S.base >> 6, w1 = (S.base + S.nbases + 63) >> 6;
+    std::vector<uint64_t> words(w1 - w0);
+    HIPCHK(hipMemcpy(words.data(), e->d_dmask.p + 1 + w0, words.size() * 8, hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < S.nbases; i++) {
+        const uint64_t p = S.base + i;
+        buf[i] = (uint8_t)((words[(p >> 6) - w0] >> (p & 63)) & 1);
+    }
     return RC_OK;
 }
 

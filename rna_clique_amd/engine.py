@@ -17,7 +17,10 @@ class Engine:
     added (the reference's `inputs` order)."""
 
     def __init__(self, top_matches=1, keep_all=True, evalue=1e-99, word_size=28,
-                 xdrop_half=108, device=0, shard_rank=0, shard_count=1):
+                 xdrop_half=108, device=0, shard_rank=0, shard_count=1, symmetric=False,
+                 dust=None):
+        """dust: None = the default (rc_default_opts), False = off, or
+        (level, window, linker)."""
         L = nat.lib()
         o = nat.RcOpts()
         L.rc_default_opts(ctypes.byref(o))
@@ -29,6 +32,13 @@ class Engine:
         o.device = int(device)
         o.shard_rank = int(shard_rank)
         o.shard_count = int(shard_count)
+        o.symmetric = 1 if symmetric else 0
+        if dust is False:
+            o.dust_level = 0
+        elif dust is not None:
+            o.dust_level, o.dust_window, o.dust_linker = (int(v) for v in dust)
+        self.symmetric = bool(symmetric)
+        self.dust = (o.dust_level, o.dust_window, o.dust_linker) if o.dust_level else None
         h = ctypes.c_void_p()
         nat.check(L.rc_create(ctypes.byref(o), ctypes.byref(h)))
         self._h = h
@@ -212,6 +222,10 @@ class Engine:
         nat.check(nat.lib().rc_distance(self._h, order.ctypes.data_as(ctypes.c_void_p),
                                         out.ctypes.data_as(ctypes.c_void_p)))
         return [self.labels[i] for i in order], out
+
+    def dust_mask(self, s):
+        """DUST mask of sample s (uint8 per base, 1 = masked query base)."""
+        return self._sized(nat.lib().rc_dust_mask, np.uint8, int(s))
 
     def timings(self):
         t = nat.RcTiming()

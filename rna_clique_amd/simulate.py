@@ -13,8 +13,17 @@ follows the configuration the reference's install test feeds it
   transcript-ID regex (transcripts.py:8) parses it, distinct per gene;
 * ids "NODE_cov_{cov}_g{gene}_i{iso}".
 
-Extras for correctness runs: a fraction of genes gets a second isoform with a
-skipped internal segment (alternative splicing), and short indels can be added.
+Extras for correctness runs (all off by default):
+* p_iso2: a fraction of genes gets a second isoform with a skipped internal
+  segment (alternative splicing); rich_genes x rich_iso: genes with many
+  isoforms (different skipped segments, every taxon);
+* indel_rate: short insertions/deletions;
+* p_revcomp: per taxon, genes whose transcripts are reported on the other
+  strand (assemblers orient transcripts arbitrarily: minus-strand hits);
+* p_paralog: genes duplicated in one random taxon (a recent copy with 0-0.5 %
+  divergence: reciprocal-best-hit ties and non-ideal components);
+* polya = (fraction, lo, hi): poly-A tails of lo..hi bases on a fraction of
+  transcripts (low-complexity sequence shared by unrelated transcripts).
 Gene ids are permuted per taxon so nothing can rely on ortholog ids matching.
 """
 from __future__ import annotations
@@ -132,9 +141,14 @@ def _indels(gene_seqs, rate, rng):
     return out
 
 
+def _revcomp(codes):
+    return (3 - codes[::-1]).astype(np.uint8)
+
+
 def simulate(taxa, genes, seed=487, len_loc=1950, len_n=1000, len_p=0.1,
              len_uniform=None, mutation_rate=0.01, p_iso2=0.0, indel_rate=0.0,
-             permute_genes=True, prefix="T"):
+             permute_genes=True, prefix="T", p_revcomp=0.0, p_paralog=0.0,
+             rich_genes=0, rich_iso=1, polya=None):
     """Simulate `taxa` transcriptomes with `genes` orthologous genes each.
 
     len_uniform=(lo, hi) draws lengths uniformly instead of loc + Binomial.
@@ -169,6 +183,17 @@ def simulate(taxa, genes, seed=487, len_loc=1950, len_n=1000, len_p=0.1,
             seqs[c] = _hky85_mutate(s, mutation_rate * blen[c], rng)
             stack.append(c)
     iso2 = rng.random(genes) < p_iso2
+    rich = set(rng.choice(genes, size=min(rich_genes, genes), replace=False).tolist()) if rich_genes else set()
+    # skipped segments of the isoform-rich genes, shared by every taxon
+    rich_cuts = {g: [(int(a), int(a) + int(w)) for a, w in zip(
+        rng.integers(50, max(51, lengths[g] - 200), size=rich_iso - 1),
+        rng.integers(30, 120, size=rich_iso - 1))] for g in sorted(rich)}
+    # (draws only for enabled extras: the default data stay those of earlier rounds)
+    paralog_taxon = np.full(genes, -1)
+    paralog_div = np.zeros(genes)
+    if p_paralog > 0:
+        paralog_taxon = np.where(rng.random(genes) < p_paralog, rng.integers(0, taxa, size=genes), -1)
+        paralog_div = rng.choice([0.0, 0.002, 0.005], size=genes)
     cov = rng.uniform(0, 10000, size=genes)
     samples = []
     for li, leaf in enumerate(leaves):
@@ -176,18 +201,32 @@ def simulate(taxa, genes, seed=487, len_loc=1950, len_n=1000, len_p=0.1,
         gseqs = [s[offs[g]:offs[g + 1]] for g in range(genes)]
         if indel_rate > 0:
             gseqs = _indels(gseqs, indel_rate, rng)
-        gid = (rng.permutation(genes) if permute_genes else np.arange(genes)) + 1
+        n_par = int((paralog_taxon == li).sum())
+        gid = (rng.permutation(genes + n_par) if permute_genes else np.arange(genes + n_par)) + 1
+        flip = rng.random(genes + n_par) < p_revcomp if p_revcomp > 0 else np.zeros(genes + n_par, bool)
         parts, gene_l, iso_l, cov_l = [], [], [], []
         # per-taxon coverage jitter keeps top-n selection meaningful but distinct
         tcov = cov * rng.uniform(0.9, 1.1, size=genes)
+        extra = genes
         for g in range(genes):
-            parts.append(gseqs[g])
-            gene_l.append(gid[g]); iso_l.append(1); cov_l.append(tcov[g])
-            if iso2[g] and gseqs[g].size > 400:
-                a = int(rng.integers(100, gseqs[g].size // 2))
-                b = a + int(rng.integers(60, 160))
-                parts.append(np.concatenate([gseqs[g][:a], gseqs[g][b:]]))
-                gene_l.append(gid[g]); iso_l.append(2); cov_l.append(tcov[g] * 0.5)
+            copies = [(g, gseqs[g], tcov[g])]
+            if paralog_taxon[g] == li:
+                dup = _hky85_mutate(gseqs[g], paralog_div[g], rng) if paralog_div[g] > 0 else gseqs[g]
+                copies.append((extra, dup, tcov[g] * 0.77))
+                extra += 1
+            for k, gs, cv in copies:
+                isos = [gs]
+                if g in rich:
+                    isos += [np.concatenate([gs[:a], gs[b:]]) for a, b in rich_cuts[g] if b < gs.size]
+                elif iso2[g] and gs.size > 400:
+                    a = int(rng.integers(100, gs.size // 2))
+                    b = a + int(rng.integers(60, 160))
+                    isos.append(np.concatenate([gs[:a], gs[b:]]))
+                for i, t in enumerate(isos):
+                    if polya is not None and rng.random() < polya[0]:
+                        t = np.concatenate([t, np.zeros(int(rng.integers(polya[1], polya[2] + 1)), np.uint8)])
+                    parts.append(_revcomp(t) if flip[k] else t)
+                    gene_l.append(gid[k]); iso_l.append(i + 1); cov_l.append(cv * (0.5 ** i))
         lens = np.array([p.size for p in parts], dtype=np.uint64)
         txo = np.zeros(len(parts) + 1, dtype=np.uint64)
         txo[1:] = np.cumsum(lens)

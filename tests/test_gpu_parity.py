@@ -1,9 +1,12 @@
 """GPU parity: the HIP path against the CPU oracles, bit for bit.
 
 Alignment: oracle/align_oracle.c (restated megablast; parity vs BLAST itself is
-unpinned). Post-alignment: oracle/post_oracle.py, itself pinned
-to the reference by tests/golden/post_alignment.json -- and the engine is also
-run directly on those golden HSP tables (external-alignment mode).
+unpinned), in the engine's mode: by default both directed
+searches of a pair run independently with DUST on the query (blastn's
+defaults); spec 5b (symmetric) and DUST off are options, tested too.
+Post-alignment: oracle/post_oracle.py, itself pinned to the reference by
+tests/golden/post_alignment.json -- and the engine is also run directly on
+those golden HSP tables (external-alignment mode).
 """
 import json
 import os
@@ -43,6 +46,86 @@ def test_simulated_parity(native, seed, taxa, genes, iso, indel):
     msgs, summary = full_check(eng, samples)
     assert not msgs, "\n".join(msgs[:10])
     assert summary["hsps"] > 0 and summary["ideal_nodes"] > 0
+
+
+@pytest.mark.parametrize("symmetric,dust", [(True, False), (False, False), (False, (20, 64, 1)),
+                                           (False, (12, 48, 3))])
+def test_alignment_modes(native, symmetric, dust):
+    """Both alignment modes (independent directed searches / spec 5b) and
+    DUST on, off, or with other parameters, on isoforms, indels, minus-strand
+    transcripts and poly-A tails."""
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(4, 120, seed=12, p_iso2=0.2, indel_rate=0.003, p_revcomp=0.5,
+                          polya=(0.3, 10, 40))
+    eng = _run_sim(samples, symmetric=symmetric, dust=dust)
+    msgs, summary = full_check(eng, samples)
+    assert not msgs, "\n".join(msgs[:10])
+    assert summary["hsps"] > 0 and summary["ideal_nodes"] > 0
+
+
+def test_dust_mask_parity(native):
+    """The GPU DUST masks (rc_dust_mask) equal the oracle's, base for base, on
+    transcripts with poly-A tails, dinucleotide and triplet repeats, ambiguous
+    bases inside low-complexity runs, and plain random sequence."""
+    from oracle.align import OracleDB
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(3, 150, seed=13, polya=(0.5, 5, 120))
+    rng = np.random.default_rng(3)
+    motifs = [b"AC", b"CAG", b"T", b"GATA", b"ACGTTGCA", b"AAAAAAAAAAAAAAAAAAAAAAANAAAAAAAA"]
+    for s in samples:
+        seq = s.seq.copy()
+        offs = s.tx_offsets.astype(np.int64)
+        for t in rng.choice(s.n_tx, size=s.n_tx // 3, replace=False):
+            a, b = int(offs[t]), int(offs[t + 1])
+            m = motifs[int(rng.integers(len(motifs)))]
+            ln = int(rng.integers(8, 150))
+            rep = np.frombuffer((m * (ln // len(m) + 1))[:ln], dtype=np.uint8)
+            if b - a > ln + 10:
+                p = int(rng.integers(a, b - ln))
+                seq[p:p + ln] = rep
+        s.seq = seq
+    eng = _run_sim(samples)
+    db = OracleDB(samples)
+    masked = 0
+    for i in range(len(samples)):
+        got = eng.dust_mask(i)
+        want = db.dust_mask(i, *eng.dust)
+        assert got.shape == want.shape
+        bad = np.flatnonzero(got != want)
+        assert bad.size == 0, f"sample {i}: {bad.size} bases differ, first at {bad[:5]}"
+        masked += int(want.sum())
+    assert masked > 1000
+    msgs, _ = full_check(eng, samples)
+    assert not msgs, "\n".join(msgs[:10])
+
+
+def test_isoform_rich_genes_and_repeats(native):
+    """Genes with 30 isoforms in every sample plus shared poly-A tails: one
+    (query gene, subject sample) pass holds thousands of seeds, more than the
+    seed kernel's LDS, so the global-memory passes (and their retry with a
+    larger scratch) run. Parity with DUST on and off."""
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(3, 60, seed=14, len_loc=1200, len_n=400, len_p=0.5, rich_genes=3,
+                          rich_iso=30, p_iso2=0.1, polya=(0.6, 20, 60))
+    for dust in (None, False):
+        eng = _run_sim(samples, dust=dust)
+        msgs, summary = full_check(eng, samples)
+        assert not msgs, "\n".join(msgs[:10])
+        assert eng.timings()["big_passes"] > 0
+        eng.close()
+
+
+def test_simulated_parity_variants(native):
+    """Minus-strand transcripts, recent paralogs (reciprocal-best-hit ties,
+    non-ideal components), isoforms and indels together."""
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(5, 200, seed=15, p_iso2=0.15, indel_rate=0.002, p_revcomp=0.5,
+                          p_paralog=0.08, polya=(0.2, 15, 40))
+    eng = _run_sim(samples)
+    msgs, summary = full_check(eng, samples)
+    assert not msgs, "\n".join(msgs[:10])
+    st = eng.stats()
+    assert st["components"] > st["ideal_components"] > 0
 
 
 def test_simulated_parity_large_index(native):
