@@ -163,6 +163,24 @@ int rc_finish(rc_engine *eng);
 uint64_t rc_edge_record_size(void);
 int rc_export_edges(rc_engine *eng, void *buf, uint64_t cap, uint64_t *n, int on_device);
 int rc_import_edges(rc_engine *eng, const void *buf, uint64_t n, int on_device);
+/* Graph-only mode (SampleSimilarity(graph, comparison_dfs), filtered_distance.py:
+ * 162-169, and its from_filenames resume path :291-317): on a fresh engine
+ * whose samples carry one zero-length transcript per gene (seq may be NULL),
+ * rc_import_edges takes host records built by the caller -- rc_edge_record
+ * below -- and runs components, the ideal filter, the sums and distances on
+ * the GPU. Gene numbering: per sample in ascending gene id, sample-major. */
+typedef struct rc_edge_record {
+    uint32_t a, b;         /* global gene indices (a == b for an isolated node) */
+    uint32_t pair;         /* pair index (rc_pair_order), | RC_EDGE_SUM_ONLY for table
+                              rows whose edge is not in the graph, or RC_NODE_ONLY */
+    int32_t nident;        /* sum of nident over the edge's table rows */
+    int32_t den;           /* sum of length - gaps over them */
+} rc_edge_record;
+#define RC_EDGE_SUM_ONLY 0x80000000u
+#define RC_NODE_ONLY 0x7FFFFFFFu
+/* sample_count of the ideal-component test (0: distinct samples among the
+ * graph's nodes, filtered_distance.py:171-182) */
+int rc_set_sample_count(rc_engine *eng, int32_t sample_count);
 /* This shard's sample-pair range [first, last) in the engine's pair order
  * (rc_pair_order). */
 int rc_shard_pairs(rc_engine *eng, int64_t *first, int64_t *last);

@@ -59,9 +59,15 @@ def diff_hsps(eng, ora, db: OracleDB, q, s):
     return msgs
 
 
-def hits_for_post(samples, db: OracleDB, hsps_by_search):
-    """Oracle HSP arrays -> BLAST-tabular dicts keyed by sample labels."""
-    ids = [s.ids() for s in samples]
+def _ids(s):
+    return s.ids() if callable(s.ids) else s.ids
+
+
+def hits_for_post(samples, db: OracleDB, hsps_by_search, names=None):
+    """Oracle HSP arrays -> BLAST-tabular dicts keyed by sample labels
+    (`names`, default each sample's .name)."""
+    names = names or [s.name for s in samples]
+    ids = [_ids(s) for s in samples]
     out = {}
     for (q, s), arr in hsps_by_search.items():
         rows = []
@@ -77,7 +83,7 @@ def hits_for_post(samples, db: OracleDB, hsps_by_search):
                 "evalue": float(h["evalue"]), "bitscore": int(h["bits10"]) / 10.0,
                 "gaps": int(h["gaps"]), "nident": int(h["nident"]),
                 "sstrand": "minus" if int(h["strand"]) else "plus"})
-        out[(samples[q].name, samples[s].name)] = rows
+        out[(names[q], names[s])] = rows
     return out
 
 
@@ -123,8 +129,8 @@ def full_check(engine, samples, word_size=28, xdrop_half=108, evalue=1e-99,
     if check_hsps:
         for (q, s), arr in ora.items():
             msgs += diff_hsps(engine.hsps(q, s), arr, db, q, s)
-    names = [s.name for s in samples]
-    hits = hits_for_post(samples, db, ora)
+    names = list(getattr(engine, "labels", None) or [s.name for s in samples])
+    hits = hits_for_post(samples, db, ora, names)
     res = post_oracle.run_pipeline(names, hits, post_oracle.default_parse_id,
                                    top_matches, keep_all)
     for a in range(N):
@@ -167,3 +173,37 @@ def full_check(engine, samples, word_size=28, xdrop_half=108, evalue=1e-99,
                "edges": len(ora_edges), "ideal_nodes": len(res["valid"]),
                "stats": st, "matrix": ok_matrix}
     return msgs, summary
+
+
+def check_pairs(engine, samples, pairs, word_size=28, xdrop_half=108, evalue=1e-99,
+                top_matches=1, keep_all=True, threads=None):
+    """Bit-exact check of selected sample pairs of a (large) engine run: for
+    each pair (a, b), both directed searches with the oracle on the two samples
+    alone (a pair's HSPs and gene matches table depend on nothing else), then
+    the pair's table through the pinned post-alignment oracle, and the pair's
+    unfiltered sums. Returns messages (empty = parity)."""
+    from concurrent.futures import ThreadPoolExecutor
+    names = list(engine.labels)
+    sym, dust = getattr(engine, "symmetric", False), getattr(engine, "dust", None)
+    dbs = {(a, b): OracleDB([samples[a], samples[b]]) for a, b in pairs}
+    jobs = [(a, b, q, s) for a, b in pairs for q, s in ((0, 1), (1, 0))]
+    run = lambda j: dbs[j[:2]].align(j[2], j[3], word_size, xdrop_half, evalue, sym, dust)  # noqa: E731
+    with ThreadPoolExecutor(threads or oracle_threads()) as ex:
+        res = dict(zip(jobs, ex.map(run, jobs)))
+    num, den = engine.pair_sums(unfiltered=True)
+    msgs = []
+    for a, b in pairs:
+        db = dbs[(a, b)]
+        ora = {(0, 1): res[(a, b, 0, 1)], (1, 0): res[(a, b, 1, 0)]}
+        for (q, s), arr in ora.items():
+            got = engine.hsps((a, b)[q], (a, b)[s])
+            msgs += [f"pair {a},{b}: {m}" for m in diff_hsps(got, arr, db, q, s)]
+        pn = [names[a], names[b]]
+        hits = hits_for_post([samples[a], samples[b]], db, ora, pn)
+        out = post_oracle.run_pipeline(pn, hits, post_oracle.default_parse_id, top_matches, keep_all)
+        table = out["tables"][(pn[0], pn[1])]
+        msgs += diff_rows(engine.pair_rows(a, b), table, f"pair {a},{b}")
+        want = (sum(r["nident"] for r in table), sum(r["length"] - r["gaps"] for r in table))
+        if (int(num[a, b]), int(den[a, b])) != want:
+            msgs.append(f"pair {a},{b}: unfiltered sums {(int(num[a, b]), int(den[a, b]))} vs {want}")
+    return msgs

@@ -73,6 +73,12 @@ class RcStats(ctypes.Structure):
 EDGE_DTYPE = np.dtype([("sample_a", np.int32), ("gene_a", np.int32),
                        ("sample_b", np.int32), ("gene_b", np.int32)])
 
+# rc_edge_record (rc_import_edges' host records, graph-only mode)
+EDGE_RECORD_DTYPE = np.dtype([("a", np.uint32), ("b", np.uint32), ("pair", np.uint32),
+                              ("nident", np.int32), ("den", np.int32)])
+RC_EDGE_SUM_ONLY = 0x80000000
+RC_NODE_ONLY = 0x7FFFFFFF
+
 
 class RcTiming(ctypes.Structure):
     _fields_ = [(n, ctypes.c_double) for n in (
@@ -104,6 +110,7 @@ SIGNATURES = {
     "rc_edge_record_size": (ctypes.c_uint64, []),
     "rc_export_edges": (ctypes.c_int, [VP, VP, ctypes.c_uint64, P(ctypes.c_uint64), ctypes.c_int]),
     "rc_import_edges": (ctypes.c_int, [VP, VP, ctypes.c_uint64, ctypes.c_int]),
+    "rc_set_sample_count": (ctypes.c_int, [VP, ctypes.c_int32]),
     "rc_shard_pairs": (ctypes.c_int, [VP, P(ctypes.c_int64), P(ctypes.c_int64)]),
     "rc_plan_shards": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.c_int32, VP]),
     "rc_plan_pairs": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.c_int32, VP, VP, VP]),

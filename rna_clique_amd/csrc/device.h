@@ -45,6 +45,11 @@ struct DEdge {
     int32_t den;           // sum of (length - gaps) over the edge's table rows
 };
 
+// DEdge.pair flags of imported graphs (SampleSimilarity(graph, tables)): a
+// table row whose edge is not in the graph (sums only), and an isolated graph
+// node (a == b: it only counts as present)
+constexpr uint32_t EDGE_SUM_ONLY = 0x80000000u, NODE_REC = 0x7FFFFFFFu;
+
 // Final gene-matches-table row: index of the HSP + flags.
 struct DRow {
     uint32_t hsp;          // index into the top-hit array

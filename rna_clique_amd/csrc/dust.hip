@@ -11,22 +11,22 @@
 // c0 and run to c1 + W - 1 (or the run's end): one lane per CHUNK bases, about
 // (CHUNK + W) / CHUNK of the sequential work, and every lane busy.
 //
-// Per lane state: triplet counts in LDS laid out [triplet][lane] as dwords
-// (every lane its own bank): window (bits 0-9), L-suffix (10-19), scratch
-// (20-29). Perfect intervals by start (mod 64) in global scratch -- they are
-// rare, and a 64-bit register mask says which slots hold one. A lane stages
-// its chunk's packed bases and transcript-start bits in LDS first; the scan
-// then advances every lane of the wave to the same chunk offset each step, so
-// the register windows reload in lockstep (no divergent memory waits).
+// Per lane state in LDS, laid out [entry][lane] (every lane its own bank):
+// triplet window counts with each triplet's last start, and a ring of
+// previous-occurrence links. The L-suffix of the published algorithm (no
+// triplet more than 2 level / 10 times) then moves by following at most 4
+// links instead of a walk, and its counts -- needed only on the rare steps
+// where some suffix may pass the level -- are recounted there. Perfect
+// intervals by start (mod 64) live in global scratch (rare; a 64-bit register
+// mask says which slots hold one). Every lane of a wave is at the same chunk
+// offset each step, so the register windows of packed bases reload in
+// lockstep with the next word already in flight.
 #include "device.h"
 
 #include <algorithm>
 
 namespace rcg {
 
-#ifndef DUST_VARIANT
-#define DUST_VARIANT 0   // microbenchmark knob (scripts/micro): 1 no find-perfect, 2 no counts, 3 staging only
-#endif
 constexpr int DW = 64;          // lanes per block (one wave)
 constexpr int DCHUNK = 256;     // bases per lane
 constexpr int DWIN_MAX = 64;    // longest DUST window the kernel supports
@@ -43,8 +43,7 @@ __device__ __forceinline__ void dust_mark(uint64_t *mask, uint64_t a, uint64_t b
     }
 }
 
-constexpr int SBW = (DCHUNK + DWIN_MAX) / 32 + 2;   // packed words of a chunk's bases (+ tail)
-constexpr int STW = (DCHUNK + DWIN_MAX) / 64 + 2;   // transcript-start words of a chunk
+constexpr uint32_t DNONE = 511;   // "no earlier occurrence" in the occurrence links
 
 template <bool AMB>
 __global__ __launch_bounds__(DW) void dust_kernel(uint64_t total, uint64_t nwords, const uint64_t *__restrict__ F,
@@ -53,62 +52,75 @@ __global__ __launch_bounds__(DW) void dust_kernel(uint64_t total, uint64_t nword
                                                   uint32_t *__restrict__ scratch, uint64_t *__restrict__ mask)
 {
     // every lane owns one column of each array (no barriers: one wave)
+    //   cnt[t]:  window count (bits 0-6) | run offset of t's last start (7-15) |
+    //            count of the rare suffix pass (16-22), valid when its tag (23-30)
+    //            is the pass's
+    //   prv[p & 63]: run offset of the previous start of the triplet starting at p
+    //   qtr[p & 63]: the triplet starting at p (the window's, for the rare pass)
     __shared__ uint32_t cnt[64][DW];
-    __shared__ uint64_t sb[SBW][DW];
-    __shared__ uint64_t sa[AMB ? SBW : 1][DW];
-    __shared__ uint64_t stx[STW][DW];
+    __shared__ uint16_t prv[64][DW];
+    __shared__ uint8_t qtr[64][DW];
     const int lane = threadIdx.x;
-    const uint32_t CW = 0x3FFu, CV = 0x3FFu << 10, CS = 0x3FFu << 20;
+    constexpr uint32_t CWM = 0x7Fu, SCM = 0x7FFFu << 16;
+    uint32_t tag = 0;   // the rare pass's counts: tag, then count
+    auto scount = [&](uint32_t ce) -> int { return (ce >> 23) == tag ? (int)((ce >> 16) & 0x7Fu) : 0; };
+    auto sbump = [&](uint32_t ce) -> uint32_t {
+        return (ce & ~SCM) | (tag << 23) | ((uint32_t)(scount(ce) + 1) << 16);
+    };
     uint32_t *slot = scratch + ((size_t)blockIdx.x * DW + lane) * DWIN_MAX;   // [absolute start & 63]
     const uint64_t nchunk = (total + DCHUNK - 1) / DCHUNK;
-    auto code_at = [&](uint64_t rel) -> int {   // base at chunk offset rel (inside a run: never ambiguous)
-        return (int)((sb[rel >> 5][lane] >> (2u * (unsigned)(rel & 31))) & 3u);
-    };
+    auto word = [&](uint64_t w) -> uint64_t { return w < nwords ? F[w] : 0ull; };
+    auto aword = [&](uint64_t w) -> uint64_t { return AMB && w < nwords ? AF[w] : 0ull; };
     for (uint64_t ch = (uint64_t)blockIdx.x * DW + lane; ch < nchunk; ch += (uint64_t)gridDim.x * DW) {
         const uint64_t c0 = ch * DCHUNK, c1 = min(c0 + DCHUNK, total);
         const uint64_t lim = min(c1 + (uint64_t)W, total);   // the scan's reach
-        // stage the chunk: packed bases (c0 is a multiple of 64) and transcript-start bits
-        for (int i = 0; i < SBW; i++) {
-            const uint64_t w = (c0 >> 5) + (uint64_t)i;
-            sb[i][lane] = w < nwords ? F[w] : 0ull;
-            if (AMB) sa[i][lane] = w < nwords ? AF[w] : 0ull;
-        }
-        for (int i = 0; i < STW; i++) {
-            const uint64_t w = (c0 >> 6) + (uint64_t)i;
-            stx[i][lane] = w <= (total >> 6) + 1 ? txstart[w] : 0ull;
-        }
-        // the window scan over [c0, lim): positions advance in lockstep across
-        // the wave (every lane at chunk offset rel), runs start and end per lane
-        if (DUST_VARIANT == 3) continue;
+        // the window scan over [c0, lim): every lane of the wave at the same
+        // chunk offset rel each step, so the 32-base register windows (lead
+        // and the trailing cursor W - 2 behind) reload in lockstep, the next
+        // word already in flight
+        const uint64_t w0 = c0 >> 5;   // c0 is a multiple of 64
+        uint64_t curw = word(w0), nxtw = word(w0 + 1), cura = aword(w0), nxta = aword(w0 + 1);
+        uint64_t curt = txstart[c0 >> 6], nxtt = txstart[(c0 >> 6) + 1];
+        uint64_t curw2 = curw, nxtw2 = nxtw;
         bool in_run = false;
-        uint64_t rs = 0, set = 0, curw = 0, cura = 0, curt = 0, curw2 = 0;
-        int nb = 0, tri = 0, tri2 = 0, qn = 0, rw = 0, rv = 0, Lq = 0;
+        uint64_t rs = 0, set = 0;
+        int nb = 0, tri = 0, tri2 = 0, rw = 0, Lst = 0;
         auto finalize = [&](uint64_t a, uint32_t s) {   // interval at absolute start a
             if (a < c1) dust_mark(mask, a, a + ((s >> 20) & 0x1FFu));
         };
         auto end_run = [&]() {   // every perfect interval left is final
-            const uint64_t base = rs + (uint64_t)max(nb - W, 0);
+            const uint64_t b0 = rs + (uint64_t)max(nb - W, 0);
             while (set) {
                 const int k = __builtin_ctzll(set);
                 set &= set - 1;
-                finalize(base + (uint64_t)((k - (int)(base & 63)) & 63), slot[k]);
+                finalize(b0 + (uint64_t)((k - (int)(b0 & 63)) & 63), slot[k]);
             }
             in_run = false;
         };
         for (uint64_t rel = 0; c0 + rel < lim; rel++) {
             const uint64_t u = c0 + rel;
-            if ((rel & 31) == 0) {
-                curw = sb[rel >> 5][lane];
-                if (AMB) cura = sa[rel >> 5][lane];
+            if (rel && (rel & 31) == 0) {
+                curw = nxtw;
+                nxtw = word(w0 + (rel >> 5) + 1);
+                if (AMB) {
+                    cura = nxta;
+                    nxta = aword(w0 + (rel >> 5) + 1);
+                }
             }
-            if ((rel & 63) == 0) curt = stx[rel >> 6][lane];
+            if (rel && (rel & 63) == 0) {
+                curt = nxtt;
+                nxtt = (c0 >> 6) + (rel >> 6) + 1 <= (total >> 6) + 1 ? txstart[(c0 >> 6) + (rel >> 6) + 1] : 0ull;
+            }
             const unsigned sh = 2u * (unsigned)(rel & 31);
             const bool amb = AMB && ((cura >> sh) & 3u);
             const int b = (int)((curw >> sh) & 3u);
-            // the trailing cursor (bases W - 2 behind) feeds the triplet that drops out
+            // the trailing cursor: the triplet that leaves the window starts at u - W
             const int64_t rel2 = (int64_t)rel - W + 2;
             if (rel2 >= 0) {
-                if ((rel2 & 31) == 0) curw2 = sb[rel2 >> 5][lane];
+                if (rel2 && (rel2 & 31) == 0) {
+                    curw2 = nxtw2;
+                    nxtw2 = word(w0 + (uint64_t)(rel2 >> 5) + 1);
+                }
                 tri2 = ((tri2 << 2) | (int)((curw2 >> (2u * (unsigned)(rel2 & 31))) & 3u)) & 63;
             }
             if (in_run && (amb || ((curt >> (rel & 63)) & 1ull))) end_run();   // ambiguous base or next transcript
@@ -120,14 +132,16 @@ __global__ __launch_bounds__(DW) void dust_kernel(uint64_t total, uint64_t nword
                 if (u >= c1) break;   // runs starting past the chunk are the next lane's
                 in_run = true;
                 rs = u;
-                nb = qn = rw = rv = Lq = 0;
+                nb = rw = Lst = 0;
                 set = 0;
-                for (int k = 0; k < 64; k++) cnt[k][lane] = 0;
+                for (int k = 0; k < 64; k++) cnt[k][lane] = DNONE << 7;
+                tag = 0;
             }
             nb++;
             tri = ((tri << 2) | b) & 63;
             if (nb < 3) continue;
-            const int32_t j = nb - 1;   // run offset of u
+            const int32_t j = nb - 1;        // run offset of u
+            const int32_t pt = j - 2;        // start of the new triplet
             const int32_t wstart = max(j + 1 - W, 0);
             if (wstart > 0) {   // the start wstart - 1 left the window: final
                 const uint64_t a = rs + (uint64_t)(wstart - 1);
@@ -137,63 +151,65 @@ __global__ __launch_bounds__(DW) void dust_kernel(uint64_t total, uint64_t nword
                     set &= ~(1ull << k);
                 }
             }
+            if (j >= W) {   // the window was full: its oldest triplet (start j - W) leaves
+                const uint32_t co = cnt[tri2][lane] - 1u;
+                cnt[tri2][lane] = co;
+                rw -= (int)(co & CWM);
+            }
             const int t3 = tri;
-            if (DUST_VARIANT == 2) {
-                rw += t3 + tri2;
-                continue;
-            }
-            if (qn == W - 2) {   // drop the oldest triplet (it starts at u - W)
-                const int o = tri2;
-                qn--;
-                uint32_t co = cnt[o][lane] - 1u;
-                rw -= (int)(co & CW);
-                if (Lq > qn) {
-                    Lq--;
-                    co -= 1u << 10;
-                    rv -= (int)((co & CV) >> 10);
+            const uint32_t c = cnt[t3][lane];
+            const int cw = (int)(c & CWM);
+            rw += cw;
+            prv[pt & 63][lane] = (uint16_t)((c >> 7) & 0x1FFu);
+            qtr[pt & 63][lane] = (uint8_t)t3;
+            cnt[t3][lane] = (c & SCM) | ((uint32_t)pt << 7) | (uint32_t)(cw + 1);
+            // L-suffix: the longest suffix of the window in which no triplet
+            // occurs more than 2 level / 10 times (4 at level 20)
+            Lst = max(Lst, wstart);
+            if ((cw + 1) * 10 > 2 * T) {
+                int need = (2 * T) / 10, p = pt;   // occurrences before pt that would exceed the bound
+                bool over = true;
+                for (int k = 0; k < need; k++) {
+                    p = (int)prv[p & 63][lane];
+                    if (p == (int)DNONE || p < Lst) {
+                        over = false;
+                        break;
+                    }
                 }
-                cnt[o][lane] = co;
+                if (over) Lst = p + 1;
             }
-            qn++;
-            Lq++;
-            uint32_t ct = cnt[t3][lane];
-            rw += (int)(ct & CW);
-            rv += (int)((ct & CV) >> 10);
-            ct += 1u + (1u << 10);
-            cnt[t3][lane] = ct;
-            // window triplet q (0 = oldest) starts at run offset wstart + q
-            auto tri_at = [&](int32_t st) {
-                const uint64_t r0 = rs + (uint64_t)st - c0;
-                return code_at(r0) * 16 + code_at(r0 + 1) * 4 + code_at(r0 + 2);
-            };
-            if ((int)((ct & CV) >> 10) * 10 > 2 * T) {   // shrink the suffix past the previous copy
-                int o;
-                do {
-                    o = tri_at(wstart + qn - Lq);
-                    uint32_t co = cnt[o][lane] - (1u << 10);
-                    rv -= (int)((co & CV) >> 10);
-                    cnt[o][lane] = co;
-                    Lq--;
-                } while (o != t3);
+            const int Lq = pt - Lst + 1;
+            if (rw * 10 <= Lq * T) continue;
+            // rare: the suffixes longer than Lq that could score above the
+            // level (10 r > level (n - 1) and r <= rw), shortest first, against
+            // the best ratio of the perfect intervals inside them
+            auto tri_at = [&](int32_t st) -> int { return qtr[st & 63][lane]; };
+            if (++tag == 256) {   // tags wrapped: clear every count of the pass
+                for (int k = 0; k < 64; k++) cnt[k][lane] &= ~SCM;
+                tag = 1;
             }
-            if (rw * 10 <= Lq * T || DUST_VARIANT == 1) continue;
-            // suffixes longer than Lq, shortest first, against the best ratio of
-            // the perfect intervals inside them
-            int r = rv, mr = 0, ml = 0;
-            for (int32_t st = wstart + qn - Lq; st <= j; st++) {
+            int r = 0;
+            for (int32_t st = Lst; st <= pt; st++) {   // the L-suffix's counts
+                const int tt = tri_at(st);
+                const uint32_t ce = cnt[tt][lane];
+                r += scount(ce);
+                cnt[tt][lane] = sbump(ce);
+            }
+            int mr = 0, ml = 0;
+            for (int32_t st = Lst; st <= j; st++) {
                 const int k = (int)((rs + (uint64_t)st) & 63);
                 if (!((set >> k) & 1ull)) continue;
                 const uint32_t s = slot[k];
                 const int sr = (int)(s & 0xFFF), sl = (int)((s >> 12) & 0xFF);
                 if (mr == 0 || sr * ml > mr * sl) { mr = sr; ml = sl; }
             }
-            for (int q = qn - Lq - 1; q >= 0; q--) {
-                const int tt = tri_at(wstart + q);
+            for (int32_t st = Lst - 1; st >= wstart; st--) {
+                const int l = pt - st;
+                if (T * l >= 10 * rw) break;   // no longer suffix can pass the level
+                const int tt = tri_at(st);
                 const uint32_t ce = cnt[tt][lane];
-                r += (int)((ce & CV) >> 10) + (int)((ce & CS) >> 20);
-                cnt[tt][lane] = ce + (1u << 20);
-                const int l = qn - q - 1;
-                const int32_t st = wstart + q;
+                r += scount(ce);
+                cnt[tt][lane] = sbump(ce);
                 const int k = (int)((rs + (uint64_t)st) & 63);
                 const bool has = (set >> k) & 1ull;
                 const uint32_t s = has ? slot[k] : 0u;
@@ -210,7 +226,6 @@ __global__ __launch_bounds__(DW) void dust_kernel(uint64_t total, uint64_t nword
                     ml = l;
                 }
             }
-            for (int q = qn - Lq - 1; q >= 0; q--) cnt[tri_at(wstart + q)][lane] &= ~CS;   // scratch counts to 0
         }
         if (in_run) end_run();   // the run reaches lim
     }

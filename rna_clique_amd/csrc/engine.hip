@@ -39,7 +39,7 @@ void launch_group(const GroupParams &, int, hipStream_t);
 void launch_rbh(const RbhParams &, int, hipStream_t);
 void launch_rbh_place(const RbhParams &, hipStream_t);
 void launch_gather_rows(const DHsp *, const DRow *, uint64_t, DHsp *, hipStream_t);
-void launch_cc(const DEdge *, uint64_t, uint32_t, const int32_t *, int, uint32_t *, uint32_t *, uint32_t *,
+void launch_cc(const DEdge *, uint64_t, uint32_t, const int32_t *, int, int, uint32_t *, uint32_t *, uint32_t *,
                uint32_t *, uint32_t *, uint8_t *, unsigned long long *, hipStream_t);
 void launch_pair_sums(const DEdge *, uint64_t, const uint32_t *, const uint8_t *, unsigned long long *,
                       unsigned long long *, unsigned long long *, unsigned long long *, hipStream_t);
@@ -245,6 +245,8 @@ struct rc_engine {
     uint64_t pair0 = 0, pair1 = 0, item0 = 0, item1 = 0;
     uint64_t n_local_edges = 0;
     bool rbh_done = false;
+    bool graph_only = false;        // an imported graph + tables, no alignment (rc_import_edges on a fresh engine)
+    int32_t sample_count_given = 0; // > 0: the ideal test's sample count (rc_set_sample_count)
 
     // device buffers
     DBuf<uint8_t> d_ascii;
@@ -1329,7 +1331,8 @@ static int do_graph(rc_engine *e)
     CHK(e->d_stats.ensure(8));
     HIPCHK(hipMemsetAsync(e->d_sample_present.p, 0, N * 4, e->st));
     HIPCHK(hipMemsetAsync(e->d_stats.p, 0, 8 * 8, e->st));
-    launch_cc(e->d_edges.p, e->n_edges, n_genes, e->d_gene_sample.p, N, e->d_parent.p, e->d_present.p, e->d_cnodes.p,
+    launch_cc(e->d_edges.p, e->n_edges, n_genes, e->d_gene_sample.p, N, e->sample_count_given, e->d_parent.p,
+              e->d_present.p, e->d_cnodes.p,
               e->d_cedges.p, e->d_sample_present.p, e->d_ideal.p, e->d_stats.p, e->st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e->ev[7], e->st));
@@ -1428,6 +1431,14 @@ int rc_run(rc_engine *e)
     return do_finish(e);
 }
 
+int rc_set_sample_count(rc_engine *e, int32_t sample_count)
+{
+    if (!e) return fail(RC_E_ARG, "null engine");
+    if (sample_count < 0) return fail(RC_E_ARG, "sample_count must be >= 0");
+    e->sample_count_given = sample_count;
+    return RC_OK;
+}
+
 int rc_hsps(rc_engine *e, int32_t q, int32_t s, rc_hsp *buf, uint64_t cap, uint64_t *n)
 {
     if (!e || !n) return fail(RC_E_ARG, "null argument");
@@ -1459,7 +1470,7 @@ int rc_hsps(rc_engine *e, int32_t q, int32_t s, rc_hsp *buf, uint64_t cap, uint6
 int rc_pair_rows(rc_engine *e, int32_t s1, int32_t s2, rc_row *buf, uint64_t cap, uint64_t *n)
 {
     if (!e || !n) return fail(RC_E_ARG, "null argument");
-    if (!e->rbh_done) return fail(RC_E_STATE, "no results yet");
+    if (!e->rbh_done || e->graph_only) return fail(RC_E_STATE, "no gene matches tables on this engine");
     const int N = (int)e->samples.size();
     if (s1 < 0 || s1 >= N || s2 < 0 || s2 >= N || s1 >= s2) return fail(RC_E_ARG, "need s1 < s2 (input order)");
     CHK(set_device(e));
@@ -1672,7 +1683,8 @@ int rc_export_edges(rc_engine *e, void *buf, uint64_t cap, uint64_t *n, int on_d
     *n = tot;
     if (!buf) return RC_OK;
     if (cap < tot) return fail(RC_E_CAPACITY, "buffer too small");
-    if (e->n_edges != e->n_local_edges) return fail(RC_E_STATE, "edges already replaced by rc_import_edges");
+    if (e->n_edges != e->n_local_edges || e->graph_only)
+        return fail(RC_E_STATE, "edges already replaced by rc_import_edges");
     if (tot)
         HIPCHK(hipMemcpy(buf, e->d_edges.p, tot * sizeof(DEdge), on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost));
     return RC_OK;
@@ -1681,14 +1693,24 @@ int rc_export_edges(rc_engine *e, void *buf, uint64_t cap, uint64_t *n, int on_d
 int rc_import_edges(rc_engine *e, const void *buf, uint64_t n, int on_device)
 {
     if (!e || (n && !buf)) return fail(RC_E_ARG, "null argument");
-    if (!e->rbh_done) return fail(RC_E_STATE, "rc_import_edges before rc_finish");
+    if (!e->rbh_done) {
+        // a fresh engine (samples added, nothing aligned): graph-only mode,
+        // the records describe an imported graph and its tables
+        if (e->aligned || e->external) return fail(RC_E_STATE, "rc_import_edges before rc_finish");
+        CHK(upload(e));
+        e->graph_only = e->rbh_done = true;
+    }
     CHK(set_device(e));
     const uint32_t ng = (uint32_t)e->gene_sample.size();
     const uint64_t np = e->pair_a.size();
     if (!on_device && n) {
         const DEdge *ed = static_cast<const DEdge *>(buf);
-        for (uint64_t i = 0; i < n; i++)
-            if (ed[i].a >= ng || ed[i].b >= ng || ed[i].pair >= np) return fail(RC_E_ARG, "edge record out of range");
+        for (uint64_t i = 0; i < n; i++) {
+            const bool node = ed[i].pair == NODE_REC;
+            if (ed[i].a >= ng || ed[i].b >= ng || (!node && (ed[i].pair & ~EDGE_SUM_ONLY) >= np) ||
+                (node && ed[i].a != ed[i].b))
+                return fail(RC_E_ARG, "edge record out of range");
+        }
     }
     CHK(e->d_edges.ensure(n));
     if (n)

@@ -516,6 +516,7 @@ __global__ void cc_hook_kernel(const DEdge *edges, uint64_t n_edges, uint32_t *p
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < n_edges;
          e += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t u = edges[e].a, v = edges[e].b;
+        if (edges[e].pair & EDGE_SUM_ONLY) continue;   // a table row whose edge is not in the graph
         present[u] = 1;
         present[v] = 1;
         uint32_t ru = uf_find(parent, u), rv = uf_find(parent, v);
@@ -555,7 +556,10 @@ __global__ void cc_count_kernel(const DEdge *edges, uint64_t n_edges, const uint
 {
     const uint64_t tid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t e = tid; e < n_edges; e += nt) atomicAdd(&cedges[parent[edges[e].a]], 1u);
+    for (uint64_t e = tid; e < n_edges; e += nt) {
+        const DEdge ed = edges[e];
+        if (ed.a != ed.b && !(ed.pair & EDGE_SUM_ONLY)) atomicAdd(&cedges[parent[ed.a]], 1u);   // graph edges only
+    }
     for (uint64_t v = tid; v < n; v += nt)
         if (present[v]) {
             atomicAdd(&cnodes[parent[v]], 1u);
@@ -583,12 +587,13 @@ __device__ __forceinline__ void block_atomic_add(unsigned long long *dst, unsign
 // stats[0] components, [1] ideal components, [2] ideal nodes, [3] nodes, [4] sample_count
 __global__ void cc_ideal_kernel(const uint32_t *parent, const uint32_t *present, const uint32_t *cnodes,
                                 const uint32_t *cedges, uint32_t n, const uint32_t *sample_present, int N,
-                                uint8_t *ideal, unsigned long long *stats)
+                                int S_given, uint8_t *ideal, unsigned long long *stats)
 {
     __shared__ int S;
     if (threadIdx.x == 0) {
         int s = 0;
         for (int i = 0; i < N; i++) s += sample_present[i] ? 1 : 0;
+        if (S_given > 0) s = S_given;   // SampleSimilarity(..., sample_count=S)
         S = s;
         if (blockIdx.x == 0) stats[4] = (unsigned long long)s;
     }
@@ -631,12 +636,14 @@ __global__ void pair_sums_kernel(const DEdge *edges, uint64_t n_edges, const uin
         const uint64_t e = start + it * nt;
         uint32_t pair = 0xFFFFFFFFu;
         unsigned long long a = 0, b = 0, ua = 0, ub = 0;
-        if (e < n_edges) {
+        if (e < n_edges && edges[e].pair != NODE_REC) {
             const DEdge ed = edges[e];
-            pair = ed.pair;
+            pair = ed.pair & ~EDGE_SUM_ONLY;
             ua = (unsigned long long)ed.nident;
             ub = (unsigned long long)ed.den;
-            if (ideal[parent[ed.a]]) {
+            // both endpoints in ideal components (restrict_multi,
+            // filtered_distance.py:66-124); a graph edge's are in one
+            if (ideal[parent[ed.a]] && ideal[parent[ed.b]]) {
                 a = ua;
                 b = ub;
             }
@@ -797,7 +804,7 @@ void launch_rbh(const RbhParams &P, int pass, hipStream_t st)
 }
 
 void launch_cc(const DEdge *edges, uint64_t n_edges, uint32_t n_nodes, const int32_t *gene_sample, int N,
-               uint32_t *parent, uint32_t *present, uint32_t *cnodes, uint32_t *cedges,
+               int S_given, uint32_t *parent, uint32_t *present, uint32_t *cnodes, uint32_t *cedges,
                uint32_t *sample_present, uint8_t *ideal, unsigned long long *stats, hipStream_t st)
 {
     const unsigned gn = grid_for(n_nodes, 256), ge = grid_for(n_edges, 256);
@@ -807,7 +814,7 @@ void launch_cc(const DEdge *edges, uint64_t n_edges, uint32_t n_nodes, const int
     hipLaunchKernelGGL(cc_count_kernel, dim3(grid_for(n_edges > n_nodes ? n_edges : n_nodes, 256)), dim3(256), 0,
                        st, edges, n_edges, parent, present, gene_sample, n_nodes, cnodes, cedges, sample_present);
     hipLaunchKernelGGL(cc_ideal_kernel, dim3(gn), dim3(256), 0, st, parent, present, cnodes, cedges, n_nodes,
-                       sample_present, N, ideal, stats);
+                       sample_present, N, S_given, ideal, stats);
 }
 
 void launch_pair_sums(const DEdge *edges, uint64_t n_edges, const uint32_t *parent, const uint8_t *ideal,

@@ -151,6 +151,10 @@ class Engine:
                                         ctypes.byref(n), 0))
         return buf
 
+    def set_sample_count(self, sample_count):
+        """The ideal-component test's sample count (0: from the graph)."""
+        nat.check(nat.lib().rc_set_sample_count(self._h, int(sample_count)))
+
     def import_edges(self, buf, n=None):
         """All shards' edges (host uint8 array, or CUDA tensor + record count)
         -> graph, ideal filter, pair sums."""

@@ -11,19 +11,16 @@ What changes underneath:
   and networkx;
 * `cache_dir` (BLAST DB cache) is accepted and unused: the seed index lives in
   HBM and is rebuilt per run;
-* gene matches tables are written to `out_dir_2` as `{s1}--{s2}.pkl`
-  (write_table's pickle form, gene_matches_tables.py:42-56) when
-  `table_format="pkl"`; "none" skips them; "h5" needs PyTables;
+* gene matches tables are written to `out_dir_2` as `{s1}--{s2}.{ext}`
+  (write_table, gene_matches_tables.py:42-56): "h5" when PyTables is
+  importable, else "pkl" (`table_format` overrides; "none" skips them);
 * `output_graph` is the networkx pickle of build_graph (filtering_step.py:
   158-159); pass None to skip building it (it is the slowest host step);
 * `jobs` bounds the host threads of the top-genes step.
 """
 from __future__ import annotations
 
-import itertools
 import multiprocessing
-import os
-import pickle
 from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 from typing import Callable, Iterable, Optional
@@ -32,7 +29,6 @@ from .engine import Engine
 from .h5 import write_matrix
 from .select_top_genes import select_top_sample
 from .similarity import NoIdealComponentsError, SampleSimilarity  # noqa: F401
-from .tables import pair_table, write_table
 from .transcripts import TranscriptID, TranscriptIDParseError, default_gene_re  # noqa: F401
 
 
@@ -83,7 +79,7 @@ def rna_clique(
         jobs: int = multiprocessing.cpu_count() - 1,
         *,
         device: int = 0,
-        table_format: str = "pkl",
+        table_format: Optional[str] = None,
         process_group=None,
 ) -> tuple[SampleSimilarity, dict[Path, str]]:
     """Full RNA-clique analysis of the transcriptomes in `dirs` (see the
@@ -97,24 +93,17 @@ def rna_clique(
     pts = {s.path: s.name for s in samples}
     eng = run_engine(samples, top_matches, evalue, keep_all, device, process_group)
     t2 = time.perf_counter()
-    sim = SampleSimilarity(eng, store_dfs=store_dfs)
+    sim = SampleSimilarity.from_engine(eng, store_dfs=store_dfs)
     from . import distributed
     writer = distributed.world(process_group)[1] == 0
     if out_dir_2 is not None and table_format != "none":
         # every rank writes the tables of the pairs it owns (all of them on one GPU)
-        out_dir_2 = Path(out_dir_2)
-        out_dir_2.mkdir(parents=True, exist_ok=True)
-        own = set(eng.owned_pairs())
-        for a, b in itertools.combinations(range(len(samples)), 2):
-            if (a, b) not in own:
-                continue
-            t = pair_table(eng, a, b)
-            write_table(t, out_dir_2 / f"{samples[a].name}--{samples[b].name}.{table_format}")
+        from .find_all_pairs import table_extension, write_pair_tables
+        write_pair_tables(eng, [s.path for s in samples], out_dir_2, pts.__getitem__,
+                          table_format or table_extension())
     if writer and output_graph is not None:
-        tmp = str(output_graph) + ".tmp"
-        with open(tmp, "wb") as f:
-            pickle.dump(sim.graph, f, pickle.HIGHEST_PROTOCOL)
-        os.replace(tmp, output_graph)
+        from .filtering_step import dump_graph
+        dump_graph(sim.graph, output_graph)
     if writer and output_matrix is not None:
         write_matrix(sim.get_dissimilarity_df(), output_matrix)
     last_timings.clear()

@@ -1,10 +1,18 @@
 """SampleSimilarity over the GPU engine.
 
 Same interface as the reference's SampleSimilarity / ComparisonSimilarityComputer
-(filtered_distance.py:129-247, similarity_computer.py:44-375), but every number
+(filtered_distance.py:129-317, similarity_computer.py:44-375), but every number
 comes from librcgpu.so: the gene matches graph, its connected components and
 ideal-clique filter, the restricted sums and the distances are computed on the
-GPU. Tables and the networkx graph are only materialised on request.
+GPU. Two ways in:
+
+* `SampleSimilarity(graph, comparison_dfs, sample_count=None)` -- the
+  reference's constructor (and `from_filenames(graph_fn, table_fns)`, the
+  resume path of the filtered_distance CLI): the graph's edges and the tables'
+  rows go to a graph-only engine (rc_import_edges), which runs components, the
+  ideal filter, the restricted sums and the distances;
+* `SampleSimilarity.from_engine(engine)` -- a finished alignment run, whose
+  tables and graph stay on the GPU and are only materialised on request.
 
 Semantics kept from the reference:
 * sample_count = distinct samples among graph nodes (filtered_distance.py:171-182);
@@ -59,20 +67,70 @@ class PairDict(dict):
 
 
 class SampleSimilarity:
-    """Similarities of the samples of one finished engine run."""
+    """Similarities of samples from the gene matches graph and tables."""
 
     sample_gene_columns = [[a + b for b in ["sample", "gene"]] for a in ["s", "q"]]
     categorical_columns = ["qsample", "ssample", "sstrand"]
 
-    def __init__(self, engine, store_dfs: bool = False, sample_count=None):
+    def __init__(self, graph, comparison_dfs, sample_count=None, *, device=0):
+        """filtered_distance.py:162-169: `graph` a networkx graph of (sample,
+        gene) nodes, `comparison_dfs` the gene matches tables as an iterable
+        of (pair of samples, table) or a mapping."""
+        items = comparison_dfs.items() if hasattr(comparison_dfs, "items") else comparison_dfs
+        self._stored = PairDict()
+        for k, df in items:
+            self._stored[tuple(k) if len(k) == 2 else tuple(k) * 2] = df
+        self._graph = graph
+        self.engine = _graph_engine(graph, list(self._stored.items()), sample_count, device)
+        self.labels = list(self.engine.labels)
+        self._sample_count = self.engine.stats()["sample_count"]
+        self._samples = None
+
+    @classmethod
+    def from_engine(cls, engine, store_dfs: bool = False):
+        """The similarities of a finished engine run (rna_clique(), find_all_pairs)."""
+        self = cls.__new__(cls)
         self.engine = engine
         self.labels = list(engine.labels)
-        st = engine.stats()
-        if sample_count is not None and sample_count != st["sample_count"]:
-            raise ValueError("a sample_count other than the graph's is not supported")
-        self._sample_count = st["sample_count"]
+        self._sample_count = engine.stats()["sample_count"]
+        self._graph = None
         self._stored = PairDict(self._table_iter()) if store_dfs else None
         self._samples = None
+        return self
+
+    @classmethod
+    def mapping_from_dfs(cls, dfs):
+        """(pair, table) from each table's own qsample/ssample columns
+        (similarity_computer.py:90-115; the first row rather than label 0,
+        see SURVEY.md Q1)."""
+        for df in dfs:
+            if len(df):
+                yield frozenset((str(df["qsample"].iloc[0]), str(df["ssample"].iloc[0]))), df
+
+    @classmethod
+    def _read_table(cls, table_path, remove_seqids=True, convert_to_categorical=True):
+        """similarity_computer.py:117-164 (the reference's categorical step
+        tests `table.index` and is a no-op, Q2; this one converts)."""
+        from .tables import read_table
+        table = read_table(table_path)
+        if remove_seqids:
+            table = table.drop(columns=[c for c in ("qseqid", "sseqid") if c in table.columns])
+        if convert_to_categorical:
+            cols = [c for c in cls.categorical_columns if c in table.columns]
+            table[cols] = table[cols].astype("category")
+        return table
+
+    @classmethod
+    def from_filenames(cls, graph_fn, comparison_fns, store_dfs=True, remove_seqids=True,
+                       convert_to_categorical=True, **kwargs):
+        """filtered_distance.py:250-317: the pickled graph and the gene
+        matches tables written by a previous run (rna_clique(), the
+        find_all_pairs / filtering_step entry points)."""
+        import pickle
+        with open(graph_fn, "rb") as f:
+            graph = pickle.load(f)
+        dfs = [cls._read_table(p, remove_seqids, convert_to_categorical) for p in comparison_fns]
+        return cls(graph, list(cls.mapping_from_dfs(dfs)), **kwargs)
 
     # ------------------------------------------------------------ tables
     def _pairs(self):
@@ -84,30 +142,34 @@ class SampleSimilarity:
 
     @property
     def comparison_dfs(self):
-        """Pair -> gene matches table (a PairDict when store_dfs, else a fresh
-        generator of (pair, table))."""
+        """Pair -> gene matches table (a PairDict when stored, else a fresh
+        generator of (pair, table) from the engine)."""
         return self._stored if self._stored is not None else self._table_iter()
 
-    @cached_property
+    @property
     def graph(self):
-        """The gene matches graph (networkx), as build_graph.py:40-68 makes it.
-        A sharded engine holds only its own pairs' tables, but every shard has
-        all graph edges after the exchange: the graph is built from those
-        (same nodes and edges; insertion order by pair, then edge)."""
+        """The gene matches graph (networkx): the one given, or the one
+        build_graph.py:40-68 makes from an engine run's tables. A sharded
+        engine holds only its own pairs' tables, but every shard has all
+        graph edges after the exchange: the graph is built from those (same
+        nodes and edges; insertion order by pair, then edge)."""
+        if self._graph is not None:
+            return self._graph
         if getattr(self.engine, "shard_count", 1) > 1:
             import networkx as nx
             e = self.engine.edges()
             g = nx.Graph()
-            for r in e.tolist():
-                d = dict(zip(e.dtype.names, r))
-                g.add_edge((self.labels[d["sample_a"]], int(d["gene_a"])),
-                           (self.labels[d["sample_b"]], int(d["gene_b"])))
+            la = [self.labels[i] for i in e["sample_a"].tolist()]
+            lb = [self.labels[i] for i in e["sample_b"].tolist()]
+            g.add_edges_from(zip(zip(la, e["gene_a"].tolist()), zip(lb, e["gene_b"].tolist())))
+            self._graph = g
             return g
 
         def rows():
             for a, b in self._pairs():
                 yield self.labels[a], self.labels[b], self.engine.pair_rows(a, b)
-        return build_graph(rows())
+        self._graph = build_graph(rows())
+        return self._graph
 
     @property
     def sample_count(self):
@@ -325,3 +387,80 @@ class UnfilteredSimilarity:
 
     def get_dissimilarity_df(self) -> pd.DataFrame:
         return self._matrix_to_df(self.get_dissimilarity_matrix())
+
+
+def _graph_engine(graph, items, sample_count, device):
+    """A graph-only engine for SampleSimilarity(graph, comparison_dfs): every
+    sample with one zero-length transcript per gene (the graph's and the
+    tables' genes), then one record per graph edge carrying the sums of its
+    table rows, sums-only records for table rows whose edge is not in the
+    graph, and node records for isolated graph nodes (rc_import_edges)."""
+    from .engine import Engine
+    genes = {}
+    nodes_by_sample = {}
+    for s, g in graph.nodes:
+        genes.setdefault(str(s), set()).add(int(g))
+    tables = []
+    for (ka, kb), df in items:
+        if not len(df):
+            continue
+        ss, qs = str(df["ssample"].iloc[0]), str(df["qsample"].iloc[0])
+        sg = df["sgene"].to_numpy(dtype=np.int64)
+        qg = df["qgene"].to_numpy(dtype=np.int64)
+        genes.setdefault(ss, set()).update(np.unique(sg).tolist())
+        genes.setdefault(qs, set()).update(np.unique(qg).tolist())
+        tables.append((ss, qs, sg, qg, df["nident"].to_numpy(dtype=np.int64),
+                       (df["length"].to_numpy(dtype=np.int64) - df["gaps"].to_numpy(dtype=np.int64))))
+    for (ka, kb), _ in items:   # samples of empty tables still exist
+        genes.setdefault(str(ka), set())
+        genes.setdefault(str(kb), set())
+    labels = sorted(genes)
+    eng = Engine(device=device)
+    base, garr = {}, {}
+    off = 0
+    for lab in labels:
+        g = np.array(sorted(genes[lab]), dtype=np.int64)
+        garr[lab], base[lab] = g, off
+        off += len(g)
+        eng.add_sample(lab, np.zeros(0, np.uint8), np.zeros(len(g) + 1, np.uint64), g.astype(np.int32),
+                       np.ones(len(g), np.int32))
+    pidx = {pr: i for i, pr in enumerate(eng.pair_order())}
+    sid = {lab: i for i, lab in enumerate(labels)}
+
+    def node(lab, g):
+        return base[lab] + np.searchsorted(garr[lab], g)
+
+    def pair_of(sa, sb):
+        a, b = sid[sa], sid[sb]
+        return pidx[(min(a, b), max(a, b))]
+
+    # graph edges, keyed by their unordered node pair
+    edge_keys = {}
+    for (su, gu), (sv, gv) in graph.edges:
+        su, sv = str(su), str(sv)
+        u, v = int(node(su, int(gu))), int(node(sv, int(gv)))
+        edge_keys[(min(u, v), max(u, v))] = pair_of(su, sv) if su != sv else 0
+    recs = []
+    for ss, qs, sg, qg, ni, dn in tables:
+        a, b = node(ss, sg), node(qs, qg)
+        lo, hi = np.minimum(a, b), np.maximum(a, b)
+        key = lo.astype(np.uint64) << np.uint64(32) | hi.astype(np.uint64)
+        uk, inv = np.unique(key, return_inverse=True)
+        sn = np.bincount(inv, weights=ni).astype(np.int64)
+        sd = np.bincount(inv, weights=dn).astype(np.int64)
+        p = pair_of(ss, qs)
+        for k, n_, d_ in zip(uk.tolist(), sn.tolist(), sd.tolist()):
+            u, v = k >> 32, k & 0xFFFFFFFF
+            in_graph = edge_keys.pop((u, v), None) is not None
+            recs.append((u, v, p if in_graph else p | nat.RC_EDGE_SUM_ONLY, n_, d_))
+    for (u, v), p in edge_keys.items():   # graph edges without table rows
+        recs.append((u, v, p, 0, 0))
+    for n in graph.nodes:
+        if graph.degree(n) == 0:
+            u = int(node(str(n[0]), int(n[1])))
+            recs.append((u, u, nat.RC_NODE_ONLY, 0, 0))
+    arr = np.array(recs, dtype=nat.EDGE_RECORD_DTYPE) if recs else np.zeros(0, nat.EDGE_RECORD_DTYPE)
+    if sample_count is not None:
+        eng.set_sample_count(int(sample_count))
+    eng.import_edges(arr.view(np.uint8))
+    return eng

@@ -132,7 +132,7 @@ def test_matrix_h5_from_run(native, tmp_path):
     samples, _ = simulate(3, 80, seed=12)
     eng = _load(Engine(device=0), samples)
     eng.run()
-    df = SampleSimilarity(eng).get_dissimilarity_df()
+    df = SampleSimilarity.from_engine(eng).get_dissimilarity_df()
     write_matrix(df, tmp_path / "m.h5")
     h = _H5()
     f = h.open(tmp_path / "m.h5")
@@ -185,3 +185,124 @@ def test_two_processes_share_the_pairs(native):
     for _, blob, edges in got:
         assert np.frombuffer(blob, dtype=np.float64).reshape(want.shape).tobytes() == want.tobytes()
         assert edges == ref.stats()["edges"]
+
+
+# ------------------------------------------------- SampleSimilarity(graph, tables)
+
+def _golden_inputs(fx, cols):
+    import networkx as nx
+    exp = fx["expected"]
+    g = nx.Graph()
+    g.add_nodes_from(tuple(n) for n in exp["nodes"])
+    g.add_edges_from((tuple(u), tuple(v)) for u, v in exp["edges"])
+    dfs = []
+    for key, rows in exp["tables"].items():
+        t1, t2 = key.split("|")
+        df = pd.DataFrame([dict(zip(cols, r)) for r in rows], columns=cols)
+        df = df.set_index("label")
+        dfs.append((frozenset((t1, t2)), df))
+    return g, dfs
+
+
+def test_sample_similarity_from_graph_and_tables_golden(native):
+    """The reference constructor SampleSimilarity(graph, comparison_dfs)
+    (filtered_distance.py:162-169) on the reference's own golden graphs and
+    tables: ideal nodes, sample_count and distances as the reference computed
+    them (components, filter and sums on the GPU, graph-only engine)."""
+    import json
+    from rna_clique_amd.similarity import NoIdealComponentsError, SampleSimilarity
+    d = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "post_alignment.json")))
+    checked = 0
+    for fx in d["fixtures"]:
+        exp = fx["expected"]
+        if any(k != "matrix" for k in exp["errors"]):
+            continue
+        g, dfs = _golden_inputs(fx, d["columns"])
+        sim = SampleSimilarity(g, dfs)
+        assert sim.sample_count == exp["sample_count"]
+        assert sorted(map(list, sim.valid.itertuples(index=False, name=None))) == exp["valid"]
+        if exp["matrix"] is None:
+            with pytest.raises(NoIdealComponentsError):
+                sim.get_dissimilarity_df()
+        else:
+            df = sim.get_dissimilarity_df()
+            assert list(df.index) == exp["matrix"]["labels"]
+            assert np.array_equal(df.to_numpy(), np.array(exp["matrix"]["values"]))
+        # a sample_count the graph cannot meet: no ideal component at all
+        with pytest.raises(NoIdealComponentsError):
+            SampleSimilarity(g, dfs, sample_count=exp["sample_count"] + 1).get_dissimilarity_df()
+        checked += 1
+    assert checked >= 15
+
+
+def test_sample_similarity_arbitrary_graph(native):
+    """A graph that is not build_graph(tables): an extra edge without table
+    rows, table rows whose edge is missing from the graph, an isolated node
+    (which still counts toward sample_count) -- against the restated
+    reference semantics (oracle/post_oracle.py)."""
+    import json
+    import networkx as nx
+    from oracle import post_oracle
+    from rna_clique_amd.similarity import SampleSimilarity
+    d = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "post_alignment.json")))
+    fx = next(f for f in d["fixtures"] if not f["expected"]["errors"] and f["expected"]["matrix"])
+    g, dfs = _golden_inputs(fx, d["columns"])
+    edges = list(g.edges)
+    g.remove_edge(*edges[0])          # its table rows now only count toward the sums
+    u, v = edges[1][0], edges[-1][1]
+    if u[0] != v[0]:
+        g.add_edge(u, v)              # an edge no table row gives
+    g.add_node(("zzz_isolated", 7))   # a sample of its own
+    sim = SampleSimilarity(g, dfs)
+    nodes = set(g.nodes)
+    gedges = {tuple(sorted(e)) for e in g.edges}
+    valid = post_oracle.ideal_nodes(nodes, gedges)
+    assert sim.sample_count == post_oracle.sample_count(nodes)
+    assert sorted(map(tuple, sim.valid.itertuples(index=False, name=None))) == sorted(valid)
+    num, den = sim.pair_sums()
+    lab = sim.labels
+    for k, df in dfs:
+        rows = df.reset_index().to_dict("records")
+        ss, qs = rows[0]["ssample"], rows[0]["qsample"]
+        want = post_oracle.pair_sums(ss, qs, rows, valid)
+        a, b = lab.index(ss), lab.index(qs)
+        assert (int(num[a, b]), int(den[a, b])) == want
+
+
+def test_tables_and_graph_reload(native, tmp_path):
+    """The resume path (CS3): rna_clique() writes od2 tables and graph.pkl,
+    SampleSimilarity.from_filenames reads them back and gives the same
+    matrix; find_all_pairs / filtering_step (the reference's phase-1 entry
+    points) produce the same tables."""
+    import glob
+    from rna_clique_amd.filtering_step import filtering_step
+    from rna_clique_amd.rna_clique import rna_clique
+    from rna_clique_amd.similarity import SampleSimilarity
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(4, 150, seed=19, p_iso2=0.2, indel_rate=0.002, p_revcomp=0.3)
+    dirs = []
+    for s in samples:
+        dd = tmp_path / "in" / s.name
+        dd.mkdir(parents=True)
+        s.write_fasta(dd / "transcripts.fasta")
+        dirs.append(dd)
+    sim, pts = rna_clique(dirs, tmp_path / "od1", tmp_path / "od2", None, tmp_path / "graph.pkl",
+                          tmp_path / "matrix.h5", top_genes=120, jobs=2)
+    want = sim.get_dissimilarity_df()
+    fns = sorted(glob.glob(str(tmp_path / "od2" / "*")))
+    assert len(fns) == 6
+    back = SampleSimilarity.from_filenames(tmp_path / "graph.pkl", fns)
+    got = back.get_dissimilarity_df()
+    assert list(got.index) == list(want.index)
+    assert np.array_equal(got.to_numpy(), want.to_numpy())
+    assert back.sample_count == sim.sample_count
+    # phase 1 through the reference's entry points
+    tables, paths, graph, n, p2s = filtering_step(dirs, tmp_path / "f_od1", tmp_path / "f_od2", None,
+                                                 tmp_path / "f_graph.pkl", 120)
+    assert n == 6 and sorted(p2s.values()) == sorted(s.name for s in samples)
+    paths = list(paths)
+    got_tables = list(tables)
+    assert len(got_tables) == len(paths) == 6
+    assert graph.number_of_edges() == sim.graph.number_of_edges()
+    again = SampleSimilarity(graph, list(SampleSimilarity.mapping_from_dfs(got_tables)))
+    assert np.array_equal(again.get_dissimilarity_df().to_numpy(), want.to_numpy())

@@ -1,0 +1,141 @@
+"""GPU: the BASELINE.json configurations, not toy sizes.
+
+* C1 (4 x 1000, `-n 1000`) and the reference's own install test shape
+  (8 taxa x 1000 transcripts, tests/verify_install/test_install.sh:14-18)
+  end to end through rna_clique() from FASTA files: full oracle check of every
+  HSP, table row, edge, ideal node and distance, and the reference's only
+  results-level check -- neighbour joining on the matrix gives the simulated
+  tree (Robinson-Foulds 0, verify_distances.py:39-55).
+* C2 (8 x 10 000): full oracle check (every directed search on the oracle's
+  thread pool).
+* C3 (32 x 50 000) at full size, plain and with isoforms, indels, minus-strand
+  genes, recent paralogs and poly-A tails: the oracle on sampled pairs (bit
+  exact: HSPs, tables, unfiltered sums), size-independent properties of the
+  whole run (symmetric hollow matrix, determinism, filtered <= unfiltered
+  sums), and the NJ tree of all 32 samples.
+"""
+import itertools
+
+import numpy as np
+import pytest
+
+from oracle.parity import check_pairs, full_check
+from treecheck import nj_splits, robinson_foulds, tree_splits
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine_run(samples, **kw):
+    from rna_clique_amd.engine import Engine
+    eng = Engine(device=0, **kw)
+    for s in samples:
+        eng.add_sample(s.name, s.seq, s.tx_offsets, s.gene, s.iso)
+    eng.run()
+    return eng
+
+
+def _rf_to_truth(tree, samples, labels, matrix):
+    """RF distance between the NJ tree of `matrix` (rows = labels) and the
+    simulated tree (leaf li is sample samples[li])."""
+    parent, _, leaves = tree
+    name_of_leaf = {leaf: samples[i].name for i, leaf in enumerate(leaves)}
+    truth = tree_splits(parent, leaves, name_of_leaf)
+    return robinson_foulds(nj_splits(matrix, list(labels)), truth)
+
+
+def _run_api(tmp_path, samples, top_genes):
+    from rna_clique_amd.rna_clique import rna_clique
+    dirs = []
+    for s in samples:
+        d = tmp_path / "in" / s.name
+        d.mkdir(parents=True)
+        s.write_fasta(d / "transcripts.fasta")
+        dirs.append(d)
+    od1 = tmp_path / "od1"
+    sim, pts = rna_clique(dirs, od1, tmp_path / "od2", None, tmp_path / "graph.pkl",
+                          tmp_path / "matrix.h5", top_genes=top_genes, jobs=4)
+    return sim, pts, od1
+
+
+@pytest.mark.parametrize("cfg", ["C1", "install8"])
+def test_config_end_to_end_with_tree(native, tmp_path, cfg):
+    """FASTA files -> rna_clique() -> matrix.h5 at C1 and at the reference's
+    install-test shape, every number checked against the oracles, and the NJ
+    tree of the matrix equal to the simulated tree."""
+    from rna_clique_amd.select_top_genes import load_top_fasta
+    from rna_clique_amd.simulate import CONFIGS, simulate
+    kw = dict(CONFIGS["C1"]) if cfg == "C1" else dict(taxa=8, genes=1000, seed=487)
+    samples, tree = simulate(**kw)
+    sim, pts, od1 = _run_api(tmp_path, samples, top_genes=1000)
+    top = [load_top_fasta(od1 / f"{s.name}_top.fasta") for s in samples]
+    assert [str(t.path) for t in top] == sim.engine.labels
+    msgs, summary = full_check(sim.engine, top)
+    assert not msgs, "\n".join(msgs[:10])
+    df = sim.get_dissimilarity_df()
+    assert np.array_equal(df.to_numpy(), summary["matrix"])
+    names = [{str(k): v for k, v in pts.items()}[p] for p in df.index]
+    assert _rf_to_truth(tree, samples, names, df.to_numpy()) == 0
+
+
+def test_config_C2_full_oracle(native):
+    """C2: 8 samples x 10 000 genes, every HSP of the 56 directed searches and
+    every row, edge, ideal node and distance bit-exact against the oracles."""
+    from rna_clique_amd.simulate import CONFIGS, simulate
+    samples, tree = simulate(**CONFIGS["C2"])
+    eng = _engine_run(samples)
+    msgs, summary = full_check(eng, samples)
+    assert not msgs, "\n".join(msgs[:10])
+    assert summary["ideal_nodes"] > 0.9 * 8 * 10000
+    labels, mat = eng.distance()
+    assert _rf_to_truth(tree, samples, labels, mat) == 0
+
+
+def _c3_properties(eng, samples, tree, pairs):
+    N = len(samples)
+    st = eng.stats()
+    assert st["sample_count"] == N
+    assert st["hsps"] > 0 and st["ideal_components"] > 0
+    labels, mat = eng.distance()
+    assert np.array_equal(mat, mat.T) and not mat.diagonal().any()
+    off = mat[~np.eye(N, dtype=bool)]
+    assert (off > 0).all() and (off < 1).all()
+    num, den = eng.pair_sums()
+    unum, uden = eng.pair_sums(unfiltered=True)
+    for a, b in itertools.combinations(range(N), 2):
+        assert 0 < num[a, b] <= unum[a, b] and 0 < den[a, b] <= uden[a, b]
+    # determinism: a second run of the whole path gives the same bits
+    eng.run()
+    assert np.array_equal(eng.distance()[1], mat)
+    assert eng.stats() == st
+    msgs = check_pairs(eng, samples, pairs)
+    assert not msgs, "\n".join(msgs[:10])
+    assert _rf_to_truth(tree, samples, labels, mat) == 0
+    return st
+
+
+C3_PAIRS = [(0, 1), (5, 17), (12, 31), (30, 31)]
+
+
+def test_config_C3_full_size(native):
+    """C3 at full size (32 x 50 000, ~1.6 Gbp): sampled pairs bit-exact vs the
+    oracle, whole-run properties, NJ tree."""
+    from rna_clique_amd.simulate import CONFIGS, simulate
+    samples, tree = simulate(**CONFIGS["C3"])
+    eng = _engine_run(samples)
+    st = _c3_properties(eng, samples, tree, C3_PAIRS)
+    # one isoform per ortholog and no paralogs: every component is an ideal clique
+    assert st["components"] == st["ideal_components"] == 50000
+    eng.close()
+
+
+def test_config_C3_correctness_variant(native):
+    """C3 with 10 % two-isoform genes, indels, half the genes on the minus
+    strand per sample, 2 % recently duplicated genes and poly-A tails: RBH ties
+    and non-ideal components at scale."""
+    from rna_clique_amd.simulate import CONFIGS, simulate
+    samples, tree = simulate(**CONFIGS["C3"], p_iso2=0.1, indel_rate=0.002, p_revcomp=0.5,
+                             p_paralog=0.02, polya=(0.2, 15, 40))
+    eng = _engine_run(samples)
+    st = _c3_properties(eng, samples, tree, C3_PAIRS)
+    assert st["components"] > st["ideal_components"] > 40000
+    eng.close()

@@ -216,7 +216,7 @@ def test_sample_similarity_numbers():
     labels = ["od1/c_top.fasta", "od1/a_top.fasta", "od1/b_top.fasta"]
     num = np.array([[0, 7, 5], [7, 0, 11], [5, 11, 0]])
     den = np.array([[0, 9, 13], [9, 0, 17], [13, 17, 0]])
-    sim = SampleSimilarity(FakeEngine(labels, num, den, [(0, 4), (1, 4)]))
+    sim = SampleSimilarity.from_engine(FakeEngine(labels, num, den, [(0, 4), (1, 4)]))
     assert sim.samples == sorted(labels)
     s = sim.get_similarities()
     assert s[[labels[0], labels[1]]] == Fraction(7, 9) == s[[labels[1], labels[0]]]
@@ -233,7 +233,7 @@ def test_sample_similarity_numbers():
 
 def test_sample_similarity_no_ideal():
     from rna_clique_amd.similarity import NoIdealComponentsError, SampleSimilarity
-    sim = SampleSimilarity(FakeEngine(["a", "b"], [[0, 0], [0, 0]], [[0, 0], [0, 0]]))
+    sim = SampleSimilarity.from_engine(FakeEngine(["a", "b"], [[0, 0], [0, 0]], [[0, 0], [0, 0]]))
     with pytest.raises(NoIdealComponentsError):
         sim.get_dissimilarity_df()
 
