@@ -39,9 +39,27 @@ def parse_args():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the wall-clock leg (FASTA files -> rna_clique() -> matrix.h5)")
-    ap.add_argument("--cpu-pairs", type=int, default=1,
-                    help="sample pairs the CPU baseline times (2 directed searches each)")
+    ap.add_argument("--cpu-pairs", type=int, default=0,
+                    help="sample pairs the CPU baseline times (2 directed searches each; "
+                         "default 2 x the worker count)")
+    ap.add_argument("--cpu-workers", type=int, default=0,
+                    help="CPU baseline processes (default: the usable cores, at most 16)")
     return ap.parse_args()
+
+
+def src_hash():
+    """Hash of the engine's sources (csrc + the C ABI header): profiles under
+    profiles/ carry it, and a PMC figure is only reported for the sources it
+    was measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    base = os.path.join(ROOT, "rna_clique_amd", "csrc")
+    for name in sorted(os.listdir(base)):
+        with open(os.path.join(base, name), "rb") as f:
+            h.update(name.encode() + b"\0" + f.read())
+    with open(os.path.join(ROOT, "include", "rcgpu.h"), "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def algorithmic_bytes(samples, hsps_per_pair, word=28):
@@ -61,41 +79,68 @@ def algorithmic_bytes(samples, hsps_per_pair, word=28):
     return tot + 32 * hsps_per_pair
 
 
-def traffic_from_profile(config, world):
-    """HBM bytes per step of the seed + extend kernels from the committed PMC
-    profile (profiles/<round>/<config>_pmc.json, FETCH_SIZE doubled per the
-    gfx950 note + WRITE_SIZE; collected with scripts/gpu_pmc.sh), or None."""
+def pmc_profile(config, world):
+    """The newest committed PMC summary (profiles/<tag>/<config>_pmc.json,
+    scripts/pmc_summary.py) measured on these very sources, or None."""
     import glob
     if world != 1:
         return None
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"{config}_pmc.json")))
-    if not files:
-        return None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    return d.get("traffic_bytes_seed_extend")
+    h = src_hash()
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"{config}_pmc.json")), reverse=True):
+        with open(f) as fh:
+            d = json.load(fh)
+        if d.get("src_hash") == h:
+            d["file"] = os.path.relpath(f, ROOT)
+            return d
+    return None
 
 
-def cpu_baseline(samples, n_pairs=1):
-    """The C oracle (same algorithm, one core) on a bounded sample of the same
-    workload: `n_pairs` sample pairs, both directed searches each, plus the
-    post-alignment oracle on them. Returns pairs/s."""
+_CPU_SAMPLES = None
+
+
+def _cpu_pair(ab):
+    """One sample pair on the CPU port: both directed searches (C oracle) and
+    the post-alignment path (RBH, table) -- a worker of cpu_baseline."""
     from oracle.align import OracleDB
     from oracle import post_oracle
     from oracle.parity import hits_for_post
+    a, b = ab
+    sub = [_CPU_SAMPLES[a], _CPU_SAMPLES[b]]
+    db = OracleDB(sub)
+    hs = {(0, 1): db.align(0, 1, dust=(20, 64, 1)), (1, 0): db.align(1, 0, dust=(20, 64, 1))}
+    names = [s.name for s in sub]
+    post_oracle.run_pipeline(names, hits_for_post(sub, db, hs), post_oracle.default_parse_id)
+    return ab
+
+
+def cpu_baseline(samples, workers, n_pairs):
+    """The CPU port of the same algorithm (oracle/: the C alignment oracle and
+    the post-alignment oracle) on `workers` processes, one sample pair per
+    task, over `n_pairs` of the workload's pairs. Runs before the GPU is
+    initialised (forked workers). Returns (pairs/s, seconds)."""
+    import itertools
+    import multiprocessing as mp
+    global _CPU_SAMPLES
+    _CPU_SAMPLES = samples
+    pairs = list(itertools.combinations(range(len(samples)), 2))
+    step = max(1, len(pairs) // n_pairs)
+    todo = pairs[::step][:n_pairs]
     t0 = time.perf_counter()
-    done = 0
-    for k in range(n_pairs):
-        a, b = 2 * k, 2 * k + 1
-        sub = [samples[a], samples[b]]
-        db = OracleDB(sub)
-        hs = {(0, 1): db.align(0, 1), (1, 0): db.align(1, 0)}
-        hits = hits_for_post(sub, db, hs)
-        names = [s.name for s in sub]
-        post_oracle.run_pipeline(names, hits, post_oracle.default_parse_id)
-        done += 1
+    with mp.get_context("fork").Pool(workers) as pool:
+        done = len(list(pool.imap_unordered(_cpu_pair, todo)))
     dt = time.perf_counter() - t0
-    return done / dt, dt
+    return done / dt, dt, done
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def e2e_wall_clock(samples, genes, rank, world, dist, ref):
@@ -175,6 +220,18 @@ def main():
     t_gen = time.perf_counter() - t_gen
     n = len(samples)
     pairs = n * (n - 1) // 2
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        # the CPU port on this host's cores, before anything touches the GPU
+        from oracle.parity import oracle_threads
+        workers = args.cpu_workers or oracle_threads()
+        n_cpu = args.cpu_pairs or 2 * workers
+        v, secs, done = cpu_baseline(samples, workers, n_cpu)
+        cpu = {"value": round(v, 4), "unit": "sample-pairs/s", "cores": workers, "kind": "port",
+               "cpu": cpu_model(), "extrapolated": True,
+               "sample": f"{done} of {pairs} {args.config} sample pairs (both directed searches with DUST "
+                         f"+ reciprocal best hits / table each, one pair per process, {workers} processes) "
+                         f"in {secs:.1f} s; pairs/s extrapolated to the whole workload"}
     eng = Engine(device=device, shard_rank=rank, shard_count=world)
     for s in samples:
         eng.add_sample(s.name, s.seq, s.tx_offsets, s.gene, s.iso)
@@ -218,24 +275,33 @@ def main():
         if dist:
             dist.destroy_process_group()
         return
-    # roofline of the dominant kernel pair (seed + extend), SURVEY.md §8d byte
-    # model over this rank's share of the pairs; time = HIP events on the
-    # engine's stream around the two launches
+    # roofline of the dominant kernel pair (seed + extension), SURVEY.md §8d
+    # byte model over this rank's share of the pairs; time = HIP events on
+    # the engine's stream around those launches
     hsps = st["hsps"]
     avg_k = sum(kern_ms) / len(kern_ms)
     bytes_launch = algorithmic_bytes(samples, hsps) * (1.0 / world)
     achieved = bytes_launch / (avg_k * 1e-3) / 1e9
+    prof = pmc_profile(args.config, world)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic_from_profile(args.config, world),
-            "kernel": "seed_kernel + extend_kernel", "kernel_ms": round(avg_k, 3),
+            "traffic": prof.get("traffic_bytes_seed_extend") if prof else None,
+            "traffic_source": prof["file"] if prof else "no PMC profile of these sources (src_hash "
+                                                       f"{src_hash()})",
+            "kernel": "seed_kernel + extension kernels", "kernel_ms": round(avg_k, 3),
             "bytes_per_launch": int(bytes_launch)}
-    cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        v, secs = cpu_baseline(samples, args.cpu_pairs)
-        cpu = {"value": round(v, 5), "unit": "sample-pairs/s", "cores": 1, "kind": "port",
-               "sample": f"{args.cpu_pairs} of {pairs} {args.config} sample pairs "
-                         f"(2 directed searches each + RBH/graph oracle), {secs:.1f} s"}
+    if prof and prof.get("issue"):
+        # the extension is bound by instruction issue, not bytes: VALU+SALU
+        # instructions per step over its measured time vs the issue peak
+        iss = prof["issue"]
+        t_ext = tm["align_kernel_ms"] * 1e-3
+        roof["issue_extension"] = {"bound": "issue", "unit": "G wave-instr/s",
+                                   "achieved": round(iss["wave_instr"] / t_ext / 1e9, 1),
+                                   "peak": iss["peak_g_per_s"],
+                                   "frac": round(iss["wave_instr"] / t_ext / 1e9 / iss["peak_g_per_s"], 4),
+                                   "valu_per_wave_step": iss.get("valu_per_wave_step")}
+    if cpu:
+        cpu["gpu_speedup"] = round(value / cpu["value"], 1)
     line = {
         "metric": "sample-pairs/sec (all-vs-all alignment -> RBH graph -> distance matrix)",
         "value": round(value, 3), "unit": "sample-pairs/s", "n_gpus": world,

@@ -114,6 +114,7 @@ typedef struct rc_timing {
     double ext_fullband;      /* extensions recomputed with the full 64-diagonal band */
     double ext_deferred;      /* candidates past the two-candidate staging slot */
     double big_passes;        /* (query gene, subject sample) seed passes run from global memory */
+    double tiles;             /* alignment passes (tiles) of this shard's samples */
 } rc_timing;
 
 void rc_default_opts(rc_opts *opts);

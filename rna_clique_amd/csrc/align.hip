@@ -1503,7 +1503,7 @@ __global__ void group_write_kernel(GroupParams P)
          gi += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t si = (gi % (uint64_t)P.N) * sg + gi / (uint64_t)P.N;
         const uint32_t o = P.gc_off[gi], c = P.gc_cnt[gi];
-        uint64_t w = P.scan[si];
+        uint64_t w = P.base + P.scan[si];
         const uint64_t gg = grp_index(P.gene_begin + (uint32_t)(si % sg), (int)(si / sg), P.n_genes);
         if (P.cnt[si]) {
             P.grp_off[gg] = (uint32_t)w;

@@ -210,6 +210,7 @@ struct GroupParams {
     const uint64_t *scan;         // exclusive scan of cnt
     uint32_t *grp_off, *grp_cnt;  // global-gene group table
     DHsp *out;
+    uint64_t base;                // first slot of this launch's direct groups in out (tiles append)
     // mirrored groups, over all candidates
     const unsigned long long *shard_prefix;
     uint64_t n_cand, cand_cap;

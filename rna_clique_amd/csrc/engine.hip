@@ -208,16 +208,25 @@ int32_t bits10(int32_t score_half)
 
 struct SampleRec {
     std::string label;
-    uint64_t base = 0, nbases = 0;
+    uint64_t base = 0, nbases = 0;   // base: position in the concatenation of all samples (host bookkeeping)
     uint32_t tx_begin = 0, n_tx = 0;
     uint32_t gene_begin = 0, n_genes = 0;
+    bool resident = true;            // bases on this GPU (rc_add_sample with a sequence)
+    uint64_t abase = 0;              // resident: offset in d_ascii (a multiple of TILE_ALIGN)
 };
+
+// Samples start at multiples of TILE_ALIGN bases in d_ascii and in a tile's
+// packed arrays: a 2^POS_TX_SHIFT-base block of the position -> transcript
+// table never spans two samples, whatever samples a tile holds.
+static const uint64_t TILE_ALIGN = 1ull << POS_TX_SHIFT;
+static uint64_t align_up(uint64_t x) { return (x + TILE_ALIGN - 1) & ~(TILE_ALIGN - 1); }
 
 struct rc_engine {
     rc_opts o{};
     hipStream_t st = nullptr;
     std::vector<SampleRec> samples;
-    uint64_t total_bases = 0;   // input bases added so far (they go straight to d_ascii)
+    uint64_t total_bases = 0;   // input bases added so far (all samples)
+    uint64_t ascii_used = 0;    // bytes of d_ascii in use (resident samples, TILE_ALIGN-aligned)
     std::vector<uint64_t> tx_start{0};
     std::vector<int32_t> tx_sample, tx_gene_id, tx_iso;
     bool has_amb = false;
@@ -232,8 +241,23 @@ struct rc_engine {
     int32_t max_len = 0;
     uint64_t n_items = 0;
     int index_bits = 16;
-    uint64_t n_kpos = 0, n_index = 0;   // k-mer slots of all samples / entries of this shard's index
-    std::vector<uint64_t> h_koff;       // closed-form k-mer slot prefix per transcript
+    uint64_t n_index = 0;               // entries of the loaded tile's index
+    std::vector<uint64_t> h_koff;       // closed-form k-mer slot prefix per tile transcript
+    std::vector<TxInfo> h_tx;           // every transcript; start = position in the loaded tile
+
+    // tiles of this shard (plan_tiles) and the one whose tables are loaded
+    struct Tile {
+        std::vector<int> samples;                 // ascending
+        std::vector<std::pair<int, int>> pairs;   // (a, b), a < b
+    };
+    std::vector<Tile> tiles;
+    int64_t tiles_for = -1;
+    int tile_loaded = -1;
+    std::vector<uint64_t> tile_pos;     // first base of each sample in the loaded tile
+    uint64_t tile_total = 0;
+    bool tile_direct = false;           // the loaded tile is d_ascii's layout (no gathered copy)
+    uint32_t tile_ntx = 0;
+    uint64_t hsp_used = 0;              // HSPs appended to d_hsp by the tiles of this run
 
     // external HSPs
     bool external = false;
@@ -249,7 +273,8 @@ struct rc_engine {
     int32_t sample_count_given = 0; // > 0: the ideal test's sample count (rc_set_sample_count)
 
     // device buffers
-    DBuf<uint8_t> d_ascii;
+    DBuf<uint8_t> d_ascii, d_tile_ascii;
+    DBuf<TxInfo> d_tile_tx;
     DBuf<uint64_t> d_F, d_RC, d_AF, d_ARC;
     DBuf<TxInfo> d_tx;
     DBuf<uint32_t> d_tx_gene, d_gene_tx_off, d_gene_tx, d_sample_gene_begin, d_sample_tx_begin;
@@ -282,7 +307,6 @@ struct rc_engine {
     DBuf<uint8_t> d_big_segT;
     uint64_t big_list_cap = 1 << 16;
     uint32_t big_cap = 1 << 13;
-    uint64_t n_big = 0;   // entries of the last run (rc_timing)
     DBuf<uint32_t> d_grp_off, d_grp_cnt;
     DBuf<unsigned long long> d_count;
     DBuf<unsigned int> d_status;
@@ -392,18 +416,23 @@ int rc_add_sample(rc_engine *e, const char *label, const char *seq, const uint64
             return fail(RC_E_LIMIT, "transcripts longer than 16 Mbp are not supported");
     }
     const uint64_t nb = tx_offsets[n_tx];
-    if (nb && !seq) return fail(RC_E_ARG, "null sequence");
     SampleRec s;
     s.label = label;
     s.base = e->total_bases;
     s.nbases = nb;
     s.tx_begin = (uint32_t)e->tx_sample.size();
     s.n_tx = n_tx;
-    // the bases go straight to HBM (the ASCII array the pack kernels read);
-    // the device array grows geometrically, old contents moved device-side
-    if (nb) {
+    // seq == NULL with bases: a sample another GPU aligns (sharded runs hold
+    // only the samples of their own pairs); its transcripts and genes still
+    // count (graph nodes, e-value statistics)
+    s.resident = nb == 0 || seq != nullptr;
+    // the bases go straight to HBM (the ASCII array the pack kernels read), at
+    // a TILE_ALIGN boundary (the gap filled with 'A'); the device array grows
+    // geometrically, old contents moved device-side
+    if (nb && seq) {
         CHK(set_device(e));
-        const uint64_t need = e->total_bases + nb + 64;
+        s.abase = align_up(e->ascii_used);
+        const uint64_t need = align_up(s.abase + nb) + 64;
         if (need > e->d_ascii.cap) {
             const size_t cap = std::max<size_t>({(size_t)need, 2 * e->d_ascii.cap, (size_t)1 << 28});
             uint8_t *np = nullptr;
@@ -411,18 +440,20 @@ int rc_add_sample(rc_engine *e, const char *label, const char *seq, const uint64
                 (void)hipGetLastError();
                 return fail(RC_E_NOMEM, "hipMalloc of " + std::to_string(cap) + " bytes failed");
             }
-            if (e->total_bases)
-                HIPCHK(hipMemcpyAsync(np, e->d_ascii.p, e->total_bases, hipMemcpyDeviceToDevice, e->st));
+            if (e->ascii_used)
+                HIPCHK(hipMemcpyAsync(np, e->d_ascii.p, e->ascii_used, hipMemcpyDeviceToDevice, e->st));
             HIPCHK(hipStreamSynchronize(e->st));
             e->d_ascii.release();
             e->d_ascii.p = np;
             e->d_ascii.cap = cap;
         }
-        HIPCHK(hipMemcpyAsync(e->d_ascii.p + e->total_bases, seq, nb, hipMemcpyHostToDevice, e->st));
+        HIPCHK(hipMemsetAsync(e->d_ascii.p + e->ascii_used, 'A', need - e->ascii_used, e->st));
+        HIPCHK(hipMemcpyAsync(e->d_ascii.p + s.abase, seq, nb, hipMemcpyHostToDevice, e->st));
         if (!e->has_amb) e->has_amb = !all_acgt(seq, nb);
         HIPCHK(hipStreamSynchronize(e->st));   // the caller's buffer is not retained
-        e->total_bases += nb;
+        e->ascii_used = s.abase + nb;
     }
+    e->total_bases += nb;
     const int32_t sid = (int32_t)e->samples.size();
     for (uint32_t t = 0; t < n_tx; t++) {
         e->tx_start.push_back(s.base + tx_offsets[t + 1]);
@@ -457,15 +488,15 @@ int rc_add_hsps(rc_engine *e, int32_t q, int32_t s, const rc_hsp *h, uint64_t n)
 static void shard_pairs(rc_engine *e);
 
 // Shard plan. The C(N,2) sample pairs (a < b) are the cells
-// of the (query a, subject b) triangle; shard_count shards each take one
-// rectangle [a0, a1) x [b0, b1) of it, found by recursive bisection that
-// minimises the largest shard's modelled time:
-//   pair work    1 x (L_a + L_b) per pair (seed hits, extension, RBH)
-//   query scan   5 x L_a per query sample of the shard (seed-kernel word lookups)
-//   index       11 x L_b per subject sample (the shard's 16-mer index)
-// (coefficients from C3 per-shard timings, scripts/shard_time.py). A
-// rectangle keeps both the shard's subjects (its index) and its queries
-// (its seed-kernel gene range) contiguous sample ranges and small. Pairs are
+// of the (a, b) triangle; shard_count shards each take one rectangle
+// [a0, a1) x [b0, b1) of it, found by recursive bisection that minimises the
+// largest shard's modelled time. Both directed searches of a pair run on its
+// shard, so the shard's samples -- the ones it holds, indexes and scans --
+// are [a0, a1) u [b0, b1):
+//   pair work    2 x (L_a + L_b) per pair (seed hits, extension, RBH)
+//   samples     16 x L_s per sample of the shard (query-word lookups 5, the
+//               16-mer index 11)
+// (coefficients from C3 per-shard timings, scripts/shard_time.py). Pairs are
 // numbered shard by shard, subject-major inside a shard; one shard gives the
 // plain subject-major order (0,1), (0,2), (1,2), (0,3), ...
 namespace plan {
@@ -493,7 +524,8 @@ struct Planner {
             const int ae = std::min(r.a1, b);
             if (ae > r.a0) pw += S(r.a0, ae) + (double)(ae - r.a0) * (SL[b + 1] - SL[b]);
         }
-        return pw + 5.0 * S(r.a0, r.a1) + 11.0 * S(r.b0, r.b1);
+        const double both = S(r.a0, r.a1) + S(r.b0, r.b1) - S(std::max(r.a0, r.b0), std::min(r.a1, r.b1));
+        return 2.0 * pw + 16.0 * both;
     }
     std::pair<double, std::vector<Rect>> best(Rect r, int k)
     {
@@ -565,6 +597,7 @@ static int upload(rc_engine *e)
     CHK(set_device(e));
     const int N = (int)e->samples.size();
     if (N < 2) return fail(RC_E_ARG, "need at least two samples");
+    if (N > 256) return fail(RC_E_LIMIT, "more than 256 samples per engine");
     const uint32_t n_tx = (uint32_t)e->tx_sample.size();
     // genes: per sample distinct gene ids ascending; a gene's transcripts in input order
     e->tx_gene.assign(n_tx, 0);
@@ -613,8 +646,7 @@ static int upload(rc_engine *e)
         if (e->gene_tx_off[g + 1] - e->gene_tx_off[g] > (uint32_t)MAX_ISO)
             return fail(RC_E_LIMIT, "gene " + std::to_string(e->gene_id[g]) + " has more than 127 transcripts");
     // pairs (a < b) in the shard plan's order (plan::plan_pairs): every
-    // shard a contiguous pair range whose subjects b -- the samples its
-    // index covers -- and queries a are contiguous sample ranges; items =
+    // shard a rectangle [a0, a1) x [b0, b1) of the pair triangle; items =
     // (pair, gene of b). (Outputs are per pair and do not depend on this.)
     {
         std::vector<int64_t> bases(N);
@@ -632,31 +664,15 @@ static int upload(rc_engine *e)
         e->pair_item_begin.push_back((uint32_t)items);
     }
     e->n_items = items;
-    if (N > 256) return fail(RC_E_LIMIT, "more than 256 samples per engine");
     shard_pairs(e);
+    // the samples of this shard's pairs must be on this GPU
+    for (uint64_t p = e->pair0; p < e->pair1; p++)
+        for (int s : {(int)e->pair_a[p], (int)e->pair_b[p]})
+            if (!e->samples[s].resident)
+                return fail(RC_E_STATE, "sample " + e->samples[s].label +
+                                            " is aligned by this shard but was added without its sequence");
 
-    // device copies
-    const uint64_t total = e->total_bases;
-    const uint64_t nwords = (total + 31) / 32 + 4;
-    CHK(e->d_ascii.ensure(total + 64));   // (already holds the bases when total > 0)
-    // packed arrays carry FRONT_PAD zero words in front (backward windows of
-    // the first transcript read them); the kernels see p + FRONT_PAD
-    CHK(e->d_F.ensure(nwords + FRONT_PAD));
-    CHK(e->d_RC.ensure(nwords + FRONT_PAD));
-    HIPCHK(hipMemsetAsync(e->d_F.p, 0, (nwords + FRONT_PAD) * 8, e->st));
-    HIPCHK(hipMemsetAsync(e->d_RC.p, 0, (nwords + FRONT_PAD) * 8, e->st));
-    if (e->has_amb) {
-        CHK(e->d_AF.ensure(nwords + FRONT_PAD));
-        CHK(e->d_ARC.ensure(nwords + FRONT_PAD));
-        HIPCHK(hipMemsetAsync(e->d_AF.p, 0, (nwords + FRONT_PAD) * 8, e->st));
-        HIPCHK(hipMemsetAsync(e->d_ARC.p, 0, (nwords + FRONT_PAD) * 8, e->st));
-    }
-    std::vector<TxInfo> txi(n_tx);
-    for (uint32_t t = 0; t < n_tx; t++) {
-        txi[t].start = e->tx_start[t];
-        txi[t].len = (uint32_t)(e->tx_start[t + 1] - e->tx_start[t]);
-        txi[t].sample = e->tx_sample[t];
-    }
+    // device copies of what does not change between runs
     auto up = [&](auto &buf, const auto &vec) -> int {
         using T = typename std::remove_reference<decltype(vec)>::type::value_type;
         CHK(buf.ensure(vec.size()));
@@ -664,7 +680,13 @@ static int upload(rc_engine *e)
             HIPCHK(hipMemcpyAsync(buf.p, vec.data(), vec.size() * sizeof(T), hipMemcpyHostToDevice, e->st));
         return RC_OK;
     };
-    CHK(up(e->d_tx, txi));
+    e->h_tx.assign(n_tx, TxInfo{});
+    for (uint32_t t = 0; t < n_tx; t++) {
+        e->h_tx[t].start = 0;   // a position in the current tile (load_tile)
+        e->h_tx[t].len = (uint32_t)(e->tx_start[t + 1] - e->tx_start[t]);
+        e->h_tx[t].sample = e->tx_sample[t];
+    }
+    CHK(up(e->d_tx, e->h_tx));
     CHK(up(e->d_tx_gene, e->tx_gene));
     std::vector<uint32_t> tx_pos(n_tx, 0);
     for (uint32_t g = 0; g < n_genes; g++)
@@ -679,39 +701,6 @@ static int upload(rc_engine *e)
     CHK(up(e->d_pair_a, e->pair_a));
     CHK(up(e->d_pair_b, e->pair_b));
     CHK(up(e->d_pair_index, e->pair_index));
-    // k-mer positions per transcript (closed form when there are no ambiguous bases)
-    std::vector<uint64_t> koff(n_tx + 1, 0);
-    for (uint32_t t = 0; t < n_tx; t++) {
-        const int64_t L = (int64_t)txi[t].len;
-        koff[t + 1] = koff[t] + (uint64_t)(L >= W16 ? L - W16 + 1 : 0);
-    }
-    CHK(up(e->d_kpos_off, koff));
-    e->h_koff = koff;
-    // base position -> transcript, per 2^POS_TX_SHIFT-base block; first base of each sample
-    if (total >= (1ull << 32)) return fail(RC_E_LIMIT, "more than 2^32 bases on one GPU: shard the samples");
-    // (host vectors outlive the async copies: the stream is synchronized below)
-    std::vector<uint32_t> pos_tx((total >> POS_TX_SHIFT) + 2, 0);
-    std::vector<uint64_t> spos(N + 1);
-    {
-        uint32_t t = 0;
-        for (size_t b = 0; b < pos_tx.size(); b++) {
-            const uint64_t p = (uint64_t)b << POS_TX_SHIFT;
-            while (t + 1 < n_tx && e->tx_start[t + 1] <= p) t++;
-            pos_tx[b] = t;
-        }
-        CHK(up(e->d_pos_tx, pos_tx));
-        for (int si = 0; si <= N; si++) spos[si] = si < N ? e->tx_start[e->sample_tx_begin[si]] : total;
-        CHK(up(e->d_sample_pos, spos));
-    }
-    // transcript-start bit per base, one guard word in front and two behind
-    std::vector<uint64_t> txb((total >> 6) + 4, 0);
-    for (uint32_t t = 0; t < n_tx; t++) {
-        const uint64_t p = e->tx_start[t] + 64;
-        txb[p >> 6] |= 1ull << (p & 63);
-    }
-    CHK(up(e->d_txstart, txb));
-    e->n_kpos = koff[n_tx];   // upper bound; exact count for the no-ambiguity case
-    if (e->n_kpos > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "more than 2^32 seed positions on one GPU");
     // statistics tables
     std::vector<int32_t> thr((size_t)N * (e->max_len + 1));
     for (int T = 0; T < N; T++)
@@ -725,7 +714,7 @@ static int upload(rc_engine *e)
     CHK(e->d_status.ensure(4));
     CHK(e->d_count.ensure(16));
     HIPCHK(hipStreamSynchronize(e->st));
-
+    e->tile_loaded = -1;
     e->uploaded = true;
     return RC_OK;
 }
@@ -740,31 +729,194 @@ static double ev_ms(rc_engine *e, int a, int b)
     return ms;
 }
 
-// The seed index of this shard: every 16-mer position of the samples that are
-// second samples (subjects) of its pairs -- a contiguous sample range, so a
-// contiguous range of transcripts and of k-mer position slots.
+// ------------------------------------------------------------------------
+// tiles
+// ------------------------------------------------------------------------
+//
+// A tile is the unit of one alignment pass: a set of samples packed into one
+// working copy (positions relative to the tile, < 2^32) and indexed together,
+// and the directed searches between them. A shard's pairs form a rectangle
+// [a0, a1) x [b0, b1) of the pair triangle; when its samples fit one tile
+// (rc_opts-independent cap RC_TILE_BASES, default 2^32 - 2^24 bases) the
+// shard is one tile, else the a- and b-ranges are cut into chunks of at most
+// half the cap and every (a chunk, b chunk) with pairs is a tile. Each pass
+// appends its HSPs to the shard's store; reciprocal best hits then run over
+// all the shard's pairs.
+
+static uint64_t tile_cap()
+{
+    const char *v = getenv("RC_TILE_BASES");   // test knob: force small tiles
+    if (v) return std::max<uint64_t>(strtoull(v, nullptr, 10), TILE_ALIGN);
+    return (1ull << 32) - (1ull << 24);
+}
+
+static void plan_tiles(rc_engine *e)
+{
+    e->tiles.clear();
+    std::vector<std::pair<int, int>> pairs;
+    for (uint64_t p = e->pair0; p < e->pair1; p++) pairs.push_back({e->pair_a[p], e->pair_b[p]});
+    if (pairs.empty()) return;
+    auto bases = [&](int s) { return align_up(e->samples[s].nbases); };
+    const uint64_t cap = tile_cap();
+    std::vector<int> A, B, U;
+    for (auto &pr : pairs) {
+        A.push_back(pr.first);
+        B.push_back(pr.second);
+        U.push_back(pr.first);
+        U.push_back(pr.second);
+    }
+    for (auto *v : {&A, &B, &U}) {
+        std::sort(v->begin(), v->end());
+        v->erase(std::unique(v->begin(), v->end()), v->end());
+    }
+    uint64_t ub = 0;
+    for (int s : U) ub += bases(s);
+    auto chunks = [&](const std::vector<int> &R, uint64_t lim) {
+        std::vector<std::vector<int>> out(1);
+        uint64_t acc = 0;
+        for (int s : R) {
+            if (!out.back().empty() && acc + bases(s) > lim) {
+                out.push_back({});
+                acc = 0;
+            }
+            out.back().push_back(s);
+            acc += bases(s);
+        }
+        return out;
+    };
+    const auto CA = ub <= cap ? std::vector<std::vector<int>>{U} : chunks(A, cap / 2);
+    const auto CB = ub <= cap ? std::vector<std::vector<int>>{U} : chunks(B, cap / 2);
+    for (size_t j = 0; j < CB.size(); j++)
+        for (size_t i = 0; i < CA.size(); i++) {
+            rc_engine::Tile t;
+            std::vector<char> ina(e->samples.size(), 0), inb(e->samples.size(), 0);
+            for (int s : CA[i]) ina[s] = 1;
+            for (int s : CB[j]) inb[s] = 1;
+            for (auto &pr : pairs)
+                if (ina[pr.first] && inb[pr.second]) t.pairs.push_back(pr);
+            if (t.pairs.empty()) continue;
+            for (auto &pr : t.pairs) {
+                t.samples.push_back(pr.first);
+                t.samples.push_back(pr.second);
+            }
+            std::sort(t.samples.begin(), t.samples.end());
+            t.samples.erase(std::unique(t.samples.begin(), t.samples.end()), t.samples.end());
+            e->tiles.push_back(t);
+        }
+}
+
+// Device tables of tile ti: packed working copy (gathered from d_ascii unless
+// the tile is d_ascii's layout), transcript starts, sample ranges, the
+// position -> transcript blocks and transcript-start bits, and the tile's
+// transcripts for the index. Kept while the same tile is loaded.
+static int load_tile(rc_engine *e, int ti)
+{
+    const rc_engine::Tile &T = e->tiles[ti];
+    const int N = (int)e->samples.size();
+    const uint32_t n_tx = (uint32_t)e->tx_sample.size();
+    e->tile_pos.assign(N + 1, 0);
+    std::vector<char> in(N, 0);
+    for (int s : T.samples) in[s] = 1;
+    // layout: tile samples in ascending order, each at a TILE_ALIGN boundary;
+    // d_ascii holds exactly that layout when the tile is every resident sample
+    uint64_t pos = 0;
+    bool direct = true;
+    for (int s = 0; s < N; s++) {
+        if (!in[s]) continue;
+        e->tile_pos[s] = pos;
+        direct = direct && e->samples[s].abase == pos;
+        pos += align_up(e->samples[s].nbases);
+    }
+    for (int s = 0; s < N; s++)
+        if (e->samples[s].resident && e->samples[s].nbases && !in[s]) direct = false;
+    const uint64_t total = pos;
+    if (total >= (1ull << 32)) return fail(RC_E_LIMIT, "a tile of more than 2^32 bases");
+    // sample ranges, monotone over all N + 1 (a sample outside the tile is empty)
+    std::vector<uint64_t> spos(N + 1);
+    {
+        uint64_t next = total;
+        for (int s = N; s >= 0; s--) {
+            if (s < N && in[s]) next = e->tile_pos[s];
+            spos[s] = next;
+        }
+    }
+    e->tile_total = total;
+    e->tile_direct = direct;
+    if (e->tile_loaded == ti) return RC_OK;
+    auto up = [&](auto &buf, const auto &vec) -> int {
+        using Tv = typename std::remove_reference<decltype(vec)>::type::value_type;
+        CHK(buf.ensure(vec.size()));
+        if (!vec.empty())
+            HIPCHK(hipMemcpyAsync(buf.p, vec.data(), vec.size() * sizeof(Tv), hipMemcpyHostToDevice, e->st));
+        return RC_OK;
+    };
+    // transcript starts in the tile; the tile's transcripts (index) with their
+    // closed-form k-mer slots; blocks of positions -> transcript
+    std::vector<TxInfo> ttx;
+    std::vector<uint64_t> koff(1, 0);
+    std::vector<uint32_t> pos_tx((total >> POS_TX_SHIFT) + 2, 0);
+    std::vector<uint64_t> txb((total >> 6) + 4, 0);
+    auto setbit = [&](uint64_t p) {
+        const uint64_t q = p + 64;
+        txb[q >> 6] |= 1ull << (q & 63);
+    };
+    for (int s = 0; s < N; s++) {
+        if (!in[s]) continue;
+        const SampleRec &S = e->samples[s];
+        const uint64_t p0 = e->tile_pos[s];
+        for (uint32_t t = S.tx_begin; t < S.tx_begin + S.n_tx; t++) {
+            const uint64_t st = p0 + (e->tx_start[t] - S.base);
+            e->h_tx[t].start = st;
+            ttx.push_back(e->h_tx[t]);
+            const int64_t L = (int64_t)e->h_tx[t].len;
+            koff.push_back(koff.back() + (uint64_t)(L >= W16 ? L - W16 + 1 : 0));
+            setbit(st);
+        }
+        // the sample's padding is a boundary too (DUST runs end there)
+        if (S.nbases < align_up(S.nbases)) setbit(p0 + S.nbases);
+        // position blocks of this sample -> its transcripts
+        uint32_t t = S.tx_begin;
+        for (uint64_t b = p0 >> POS_TX_SHIFT; b < (p0 + align_up(S.nbases)) >> POS_TX_SHIFT; b++) {
+            const uint64_t p = b << POS_TX_SHIFT;
+            while (t + 1 < S.tx_begin + S.n_tx && p0 + (e->tx_start[t + 1] - S.base) <= p) t++;
+            pos_tx[b] = t;
+        }
+    }
+    if (koff.back() > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "more than 2^32 seed positions in a tile");
+    CHK(up(e->d_tx, e->h_tx));
+    CHK(up(e->d_tile_tx, ttx));
+    CHK(up(e->d_kpos_off, koff));
+    CHK(up(e->d_pos_tx, pos_tx));
+    CHK(up(e->d_sample_pos, spos));
+    CHK(up(e->d_txstart, txb));
+    e->h_koff = koff;
+    e->tile_ntx = (uint32_t)ttx.size();
+    // the packed working copy's source: d_ascii itself or a gathered copy
+    if (!direct) {
+        CHK(e->d_tile_ascii.ensure(total + 64));
+        HIPCHK(hipMemsetAsync(e->d_tile_ascii.p, 'A', total + 64, e->st));
+        for (int s = 0; s < N; s++)
+            if (in[s] && e->samples[s].nbases)
+                HIPCHK(hipMemcpyAsync(e->d_tile_ascii.p + e->tile_pos[s], e->d_ascii.p + e->samples[s].abase,
+                                      e->samples[s].nbases, hipMemcpyDeviceToDevice, e->st));
+    }
+    HIPCHK(hipStreamSynchronize(e->st));   // host vectors outlive the copies
+    e->tile_loaded = ti;
+    (void)n_tx;
+    return RC_OK;
+}
+
+// The seed index of the loaded tile: every 16-mer position of its transcripts.
 static int build_index(rc_engine *e)
 {
     const bool amb = e->has_amb;
-    int slo = (int)e->samples.size(), shi = -1;
-    for (uint64_t p = e->pair0; p < e->pair1; p++) {
-        slo = std::min(slo, (int)e->pair_b[p]);
-        shi = std::max(shi, (int)e->pair_b[p]);
-        if (!e->o.symmetric) {   // both samples of a pair are subjects
-            slo = std::min(slo, (int)e->pair_a[p]);
-            shi = std::max(shi, (int)e->pair_a[p]);
-        }
-    }
-    const uint32_t t0 = shi < 0 ? 0 : e->sample_tx_begin[slo];
-    const uint32_t t1 = shi < 0 ? 0 : e->sample_tx_begin[shi + 1];
-    const uint32_t n_tx = t1 - t0;
-    uint64_t npos = e->h_koff[t1] - e->h_koff[t0];
-    uint64_t *ent_base = e->d_ent.p;
-    const uint64_t *offs = e->d_kpos_off.p + t0;   // closed-form slots (no ambiguous bases)
+    const uint32_t n_tx = e->tile_ntx;
+    uint64_t npos = e->h_koff[n_tx];
+    const uint64_t *offs = e->d_kpos_off.p;   // closed-form slots (no ambiguous bases)
     if (amb) {
         CHK(e->d_kcnt.ensure(n_tx + 1));
         HIPCHK(hipMemsetAsync(e->d_kcnt.p, 0, (n_tx + 1) * sizeof(uint64_t), e->st));
-        if (n_tx) launch_kmer_count(e->d_tx.p + t0, n_tx, e->d_AF.p + FRONT_PAD, e->d_kcnt.p, e->st);
+        if (n_tx) launch_kmer_count(e->d_tile_tx.p, n_tx, e->d_AF.p + FRONT_PAD, e->d_kcnt.p, e->st);
         size_t tmp = 0;
         CHK(e->d_kpos_rel.ensure(n_tx + 1));
         HIPCHK(rocprim::exclusive_scan(nullptr, tmp, e->d_kcnt.p, e->d_kpos_rel.p, (uint64_t)0, (size_t)n_tx + 1,
@@ -778,9 +930,8 @@ static int build_index(rc_engine *e)
     }
     CHK(e->d_ent.ensure(std::max<uint64_t>(npos, 1)));
     CHK(e->d_ent2.ensure(std::max<uint64_t>(npos, 1)));
-    ent_base = amb ? e->d_ent.p : e->d_ent.p - e->h_koff[t0];   // the kernel writes at absolute slots
-    if (n_tx) launch_kmer_fill(amb, e->d_tx.p + t0, n_tx, e->d_F.p + FRONT_PAD, amb ? e->d_AF.p + FRONT_PAD : nullptr,
-                               offs, ent_base, e->st);
+    if (n_tx) launch_kmer_fill(amb, e->d_tile_tx.p, n_tx, e->d_F.p + FRONT_PAD, amb ? e->d_AF.p + FRONT_PAD : nullptr,
+                               offs, e->d_ent.p, e->st);
     // sort on the k-mer (bits 32..63); the fill order is position order and the
     // onesweep radix sort is stable, so positions stay ascending per k-mer.
     // rocPRIM sorts up to 2^20 items with a merge sort that did not keep that
@@ -792,7 +943,7 @@ static int build_index(rc_engine *e)
     CHK(e->d_tmp.ensure(tmp));
     HIPCHK(rocprim::radix_sort_keys(e->d_tmp.p, tmp, e->d_ent.p, e->d_ent2.p, (size_t)npos, bb, 64u, e->st));
     // bucket table over the top k-mer bits: about one bucket per indexed
-    // position of this shard, at most 2^28 (RC_INDEX_BITS_MAX; 28 measured
+    // position of this tile, at most 2^28 (RC_INDEX_BITS_MAX; 28 measured
     // best at C3 -- a 1 GiB table instead of 4 GiB, same seed-kernel time)
     const char *ibv = getenv("RC_INDEX_BITS_MAX");
     const int bmax = ibv ? std::max(16, std::min(30, atoi(ibv))) : 28;
@@ -812,7 +963,7 @@ static Db make_db(rc_engine *e)
     db.RC = e->d_RC.p + FRONT_PAD;
     db.AF = e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr;
     db.ARC = e->has_amb ? e->d_ARC.p + FRONT_PAD : nullptr;
-    db.total = e->total_bases;
+    db.total = e->tile_total;
     db.tx = e->d_tx.p;
     db.tx_gene = e->d_tx_gene.p;
     db.gene_tx_off = e->d_gene_tx_off.p;
@@ -835,34 +986,36 @@ static void shard_pairs(rc_engine *e)
     e->item1 = e->pair_item_begin[e->pair1];
 }
 
-// Seed plan of this shard: every owned pair is aligned once, lower-numbered
-// sample as query. Returns the query-gene range to scan and, per query sample,
-// the bit set of its subject samples.
-static void shard_plan(rc_engine *e, uint32_t &g0, uint32_t &g1, std::vector<uint64_t> &tmask)
+// The directed searches of tile ti: per query sample the bit set of its
+// subject samples (spec 5b: only a -> b of a pair), and the runs of
+// consecutive query samples (one seed launch each: their genes are contiguous).
+static void tile_plan(rc_engine *e, int ti, std::vector<uint64_t> &tmask, std::vector<std::pair<int, int>> &runs)
 {
     const int N = (int)e->samples.size();
     tmask.assign((size_t)4 * N, 0);
-    int smin = N, smax = -1;
-    for (uint64_t p = e->pair0; p < e->pair1; p++) {
-        const int qa = e->pair_a[p], sb = e->pair_b[p];
-        tmask[4 * qa + (sb >> 6)] |= 1ull << (sb & 63);
-        smin = std::min(smin, qa);
-        smax = std::max(smax, qa);
+    std::vector<char> q(N, 0);
+    for (auto &pr : e->tiles[ti].pairs) {
+        const int a = pr.first, b = pr.second;
+        tmask[4 * a + (b >> 6)] |= 1ull << (b & 63);
+        q[a] = 1;
         if (!e->o.symmetric) {   // the pair's second directed search: query b, subject a
-            tmask[4 * sb + (qa >> 6)] |= 1ull << (qa & 63);
-            smin = std::min(smin, sb);
-            smax = std::max(smax, sb);
+            tmask[4 * b + (a >> 6)] |= 1ull << (a & 63);
+            q[b] = 1;
         }
     }
-    if (smax < 0) {
-        g0 = g1 = 0;
-        return;
+    runs.clear();
+    for (int s = 0; s < N;) {
+        if (!q[s]) {
+            s++;
+            continue;
+        }
+        int t = s;
+        while (t < N && q[t]) t++;
+        runs.push_back({s, t});
+        s = t;
     }
-    g0 = e->sample_gene_begin[smin];
-    g1 = e->sample_gene_begin[smax + 1];
 }
 
-// External HSPs -> device groups in canonical (query gene, subject sample) order.
 static int load_external(rc_engine *e)
 {
     const int N = (int)e->samples.size();
@@ -898,37 +1051,63 @@ static int load_external(rc_engine *e)
     return RC_OK;
 }
 
-static int do_align(rc_engine *e)
+// d_hsp grows across tiles with its contents kept
+static int grow_hsp(rc_engine *e, uint64_t n)
 {
-    CHK(upload(e));
-    CHK(set_device(e));
-    e->aligned = e->finished = e->rbh_done = false;
-    e->tm = rc_timing{};
-    if (e->external) {
-        HIPCHK(hipEventRecord(e->ev[0], e->st));
-        CHK(load_external(e));
-        HIPCHK(hipEventRecord(e->ev[1], e->st));
-        HIPCHK(hipEventSynchronize(e->ev[1]));
-        e->tm.align_ms = ev_ms(e, 0, 1);
-        e->aligned = true;
-        return RC_OK;
+    if (n <= e->d_hsp.cap && e->d_hsp.p) return RC_OK;
+    const size_t cap = std::max<size_t>(n, e->d_hsp.cap + e->d_hsp.cap / 2);
+    DHsp *np = nullptr;
+    if (hipMalloc((void **)&np, cap * sizeof(DHsp)) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(RC_E_NOMEM, "hipMalloc of " + std::to_string(cap * sizeof(DHsp)) + " bytes failed");
     }
-    const uint64_t total = e->total_bases;
+    if (e->hsp_used) HIPCHK(hipMemcpyAsync(np, e->d_hsp.p, e->hsp_used * sizeof(DHsp), hipMemcpyDeviceToDevice, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    e->d_hsp.release();
+    e->d_hsp.p = np;
+    e->d_hsp.cap = cap;
+    return RC_OK;
+}
+
+// One alignment pass over tile ti: pack, DUST, index, seeds (one launch per
+// run of query samples), extension, and the (query gene, subject sample) HSP
+// groups appended to the shard's store.
+static int align_tile(rc_engine *e, int ti)
+{
+    CHK(load_tile(e, ti));
+    const int N = (int)e->samples.size();
+    const uint64_t total = e->tile_total;
     const uint64_t nwords = (total + 31) / 32 + 2;
+    const uint32_t n_genes = (uint32_t)e->gene_sample.size();
+    const size_t ngrp = (size_t)n_genes * N;
+    // packed working copy (FRONT_PAD zero words in front, zero words behind)
+    CHK(e->d_F.ensure(nwords + 4 + FRONT_PAD));
+    CHK(e->d_RC.ensure(nwords + 4 + FRONT_PAD));
+    HIPCHK(hipMemsetAsync(e->d_F.p, 0, FRONT_PAD * 8, e->st));
+    HIPCHK(hipMemsetAsync(e->d_RC.p, 0, FRONT_PAD * 8, e->st));
+    HIPCHK(hipMemsetAsync(e->d_F.p + FRONT_PAD + nwords, 0, 4 * 8, e->st));
+    HIPCHK(hipMemsetAsync(e->d_RC.p + FRONT_PAD + nwords, 0, 4 * 8, e->st));
+    if (e->has_amb) {
+        CHK(e->d_AF.ensure(nwords + 4 + FRONT_PAD));
+        CHK(e->d_ARC.ensure(nwords + 4 + FRONT_PAD));
+        HIPCHK(hipMemsetAsync(e->d_AF.p, 0, (nwords + 4 + FRONT_PAD) * 8, e->st));
+        HIPCHK(hipMemsetAsync(e->d_ARC.p, 0, (nwords + 4 + FRONT_PAD) * 8, e->st));
+    }
     HIPCHK(hipEventRecord(e->ev[0], e->st));
-    launch_pack(e->d_ascii.p, total, nwords, e->d_F.p + FRONT_PAD, e->d_RC.p + FRONT_PAD,
-                e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr, e->has_amb ? e->d_ARC.p + FRONT_PAD : nullptr, e->st);
+    launch_pack(e->tile_direct ? e->d_ascii.p : e->d_tile_ascii.p, total, nwords, e->d_F.p + FRONT_PAD,
+                e->d_RC.p + FRONT_PAD, e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr,
+                e->has_amb ? e->d_ARC.p + FRONT_PAD : nullptr, e->st);
     HIPCHK(hipGetLastError());
     if (e->o.dust_level > 0) {
-        // DUST masks of the query transcripts (every transcript), bit per base
+        // DUST masks of the tile's transcripts (the query side), bit per base
         const size_t mw = (total >> 6) + 4;
         CHK(e->d_dmask.ensure(mw));
         HIPCHK(hipMemsetAsync(e->d_dmask.p, 0, mw * 8, e->st));
         const uint32_t dblocks = 256 * 16;   // resident lanes of the chunk kernel (their slot scratch)
         CHK(e->d_dust_scratch.ensure(dust_scratch_words(dblocks)));
         launch_dust(e->has_amb, total, e->d_F.p + FRONT_PAD, e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr,
-                    e->d_txstart.p + 1, e->d_tx.p, (uint32_t)e->tx_sample.size(), e->o.dust_level,
-                    e->o.dust_window, e->o.dust_linker, e->d_dust_scratch.p, dblocks, e->d_dmask.p + 1, e->st);
+                    e->d_txstart.p + 1, e->d_tile_tx.p, e->tile_ntx, e->o.dust_level, e->o.dust_window,
+                    e->o.dust_linker, e->d_dust_scratch.p, dblocks, e->d_dmask.p + 1, e->st);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->ev[1], e->st));
@@ -936,29 +1115,32 @@ static int do_align(rc_engine *e)
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e->ev[2], e->st));
 
-    const int N = (int)e->samples.size();
-    uint32_t g0, g1;
     std::vector<uint64_t> tmask;
-    shard_plan(e, g0, g1, tmask);
+    std::vector<std::pair<int, int>> runs;
+    tile_plan(e, ti, tmask, runs);
     CHK(e->d_tmask.ensure(tmask.size()));
     HIPCHK(hipMemcpyAsync(e->d_tmask.p, tmask.data(), tmask.size() * 8, hipMemcpyHostToDevice, e->st));
-    const uint32_t n_genes = (uint32_t)e->gene_sample.size();
-    const uint64_t sg = (uint64_t)(g1 - g0);
-    const size_t ngrp = (size_t)n_genes * N;
-    const size_t nsgrp = (size_t)sg * N;
-    CHK(e->d_grp_off.ensure(ngrp));
-    CHK(e->d_grp_cnt.ensure(ngrp));
-    CHK(e->d_gc_off.ensure(nsgrp));
-    CHK(e->d_gc_cnt.ensure(nsgrp));
-    CHK(e->d_gcount.ensure(nsgrp + 1));
-    CHK(e->d_gscan.ensure(nsgrp + 1));
+    // per run: its genes [g0, g1) and its slice of the (gene, sample) arrays
+    const size_t R = runs.size();
+    std::vector<uint32_t> rg0(R), rg1(R);
+    std::vector<size_t> gcb(R + 1, 0), cnb(R + 1, 0);
+    for (size_t r = 0; r < R; r++) {
+        rg0[r] = e->sample_gene_begin[runs[r].first];
+        rg1[r] = e->sample_gene_begin[runs[r].second];
+        gcb[r + 1] = gcb[r] + (size_t)(rg1[r] - rg0[r]) * N;
+        cnb[r + 1] = cnb[r] + (size_t)(rg1[r] - rg0[r]) * N + 1;
+    }
+    CHK(e->d_gc_off.ensure(std::max<size_t>(gcb[R], 1)));
+    CHK(e->d_gc_cnt.ensure(std::max<size_t>(gcb[R], 1)));
+    CHK(e->d_gcount.ensure(std::max<size_t>(cnb[R], 1)));
+    CHK(e->d_gscan.ensure(std::max<size_t>(cnb[R], 1)));
     CHK(e->d_shard_cnt.ensure(2 * NSHARD));
     CHK(e->d_shard_prefix.ensure(NSHARD + 1));
-    if (e->seed_cap == 0) {
-        const uint64_t nb = std::max<uint64_t>(sg, 1) * (uint64_t)std::max(N - 1, 1);
-        e->seed_cap = nb * 16 / NSHARD + 4096;
-        e->cand_cap = nb * 2 / NSHARD + 1024;
-        e->ovf_cap = nb / 4 + 1024;
+    {
+        const uint64_t nb = std::max<uint64_t>(gcb[R] / std::max(N, 1), 1) * (uint64_t)std::max(N - 1, 1);
+        e->seed_cap = std::max<uint64_t>(e->seed_cap, nb * 16 / NSHARD + 4096);
+        e->cand_cap = std::max<uint64_t>(e->cand_cap, nb * 2 / NSHARD + 1024);
+        e->ovf_cap = std::max<uint64_t>(e->ovf_cap, nb / 4 + 1024);
     }
     Db db = make_db(e);
     Index ix;
@@ -970,100 +1152,106 @@ static int do_align(rc_engine *e)
     std::vector<unsigned long long> shard_cnt(2 * NSHARD);
     CHK(e->d_count.ensure(16));
     unsigned long long *big_n = e->d_count.p + 12, *big_retry_n = e->d_count.p + 13;
-    e->n_big = 0;
+    uint64_t n_big = 0;
+    HIPCHK(hipEventRecord(e->ev[3], e->st));
     for (int attempt = 0;; attempt++) {
         if (attempt == 6) return fail(RC_E_NOMEM, "seed/candidate buffers kept overflowing");
         if (e->seed_cap * NSHARD > 0xFFFFFFFFull || e->cand_cap * NSHARD > 0xFFFFFFFFull)
-            return fail(RC_E_LIMIT, "more than 2^32 seeds or candidates on one GPU: use more shards");
+            return fail(RC_E_LIMIT, "more than 2^32 seeds or candidates in a tile: use more shards or smaller tiles");
         CHK(e->d_seeds.ensure(e->seed_cap * NSHARD));
         CHK(e->d_cands.ensure(e->cand_cap * NSHARD));
         CHK(e->d_big_out.ensure(e->big_list_cap));
         HIPCHK(hipMemsetAsync(e->d_shard_cnt.p, 0, 2 * NSHARD * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
-        HIPCHK(hipMemsetAsync(big_n, 0, 2 * sizeof(unsigned long long), e->st));
-        if (nsgrp) HIPCHK(hipMemsetAsync(e->d_gc_cnt.p, 0, nsgrp * 4, e->st));
-        SeedParams S{};
-        S.word = e->o.word_size;
-        S.stride = e->o.word_size - W16 + 1;
-        {
-            const char *pm = getenv("RC_SEED_PRE");   // A/B knob; 1 = hit-list pre-test
-            S.pre_mode = pm ? atoi(pm) : 1;
-        }
-        S.sym = e->o.symmetric;
-        S.gene_begin = g0;
-        S.gene_end = g1;
-        S.seeds = e->d_seeds.p;
-        S.seed_cap = e->seed_cap;
-        S.seed_count = e->d_shard_cnt.p;
-        S.cands = e->d_cands.p;
-        S.cand_cap = e->cand_cap;
-        S.cand_count = e->d_shard_cnt.p + NSHARD;
-        S.gc_off = e->d_gc_off.p;
-        S.gc_cnt = e->d_gc_cnt.p;
-        S.tmask = e->d_tmask.p;
-        S.status = e->d_status.p;
-        S.big_out = e->d_big_out.p;
-        S.big_n = big_n;
-        S.big_retry_n = big_retry_n;
-        S.big_list_cap = e->big_list_cap;
+        if (gcb[R]) HIPCHK(hipMemsetAsync(e->d_gc_cnt.p, 0, gcb[R] * 4, e->st));
         CHK(e->d_prof.ensure(8));
         HIPCHK(hipMemsetAsync(e->d_prof.p, 0, 8 * sizeof(unsigned long long), e->st));
-        S.prof = e->d_prof.p;
-        HIPCHK(hipEventRecord(e->ev[3], e->st));
-        launch_seed(e->has_amb, db, ix, S, e->st);
-        HIPCHK(hipGetLastError());
-        unsigned int status = 0;
-        unsigned long long nb = 0;   // (big_n: d_count[12], next to the extension's counters [0, 8))
-        HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
-        HIPCHK(hipMemcpyAsync(&nb, big_n, sizeof nb, hipMemcpyDeviceToHost, e->st));
-        HIPCHK(hipStreamSynchronize(e->st));
-        if (status & 2u) return fail(RC_E_LIMIT, "a query gene has more than 127 isoforms");
-        if (status & 8u) {   // the big-pass list itself overflowed
-            e->big_list_cap = std::max<uint64_t>(4 * e->big_list_cap, nb + 1024);
-            continue;
-        }
-        bool again = (status & 1u) != 0;
-        // (gene, sample) passes whose seeds overflow LDS: global-memory passes,
-        // at most BIG_CHUNK workgroups per launch; entries that overflow big_cap
-        // too are collected and rerun with twice the scratch
-        const uint64_t BIG_CHUNK = 2048;
-        uint64_t *list = e->d_big_out.p;
-        e->n_big = nb;
-        while (!again && nb) {
-            if ((uint64_t)e->big_cap > (1ull << 22)) return fail(RC_E_LIMIT, "a (query gene, subject sample) pass has more than 2^22 seeds");
-            const uint64_t chunk = std::min<uint64_t>(nb, BIG_CHUNK);
-            CHK(e->d_big_list.ensure(nb));
-            CHK(e->d_big_retry.ensure(nb));
-            CHK(e->d_big_seeds.ensure(chunk * e->big_cap));
-            CHK(e->d_big_seg.ensure(chunk * (e->big_cap + 1)));
-            CHK(e->d_big_segT.ensure(chunk * e->big_cap));
-            if (list != e->d_big_list.p)
-                HIPCHK(hipMemcpyAsync(e->d_big_list.p, list, nb * 8, hipMemcpyDeviceToDevice, e->st));
-            HIPCHK(hipMemsetAsync(big_retry_n, 0, sizeof(unsigned long long), e->st));
-            SeedParams B = S;
-            B.big_retry = e->d_big_retry.p;
-            B.big_list_cap = nb;
-            B.big_cap = e->big_cap;
-            B.big_seeds = e->d_big_seeds.p;
-            B.big_seg = e->d_big_seg.p;
-            B.big_segT = e->d_big_segT.p;
-            for (uint64_t c0 = 0; c0 < nb; c0 += chunk) {
-                B.big_list = e->d_big_list.p + c0;
-                launch_seed_big(e->has_amb, db, ix, B, (uint32_t)std::min<uint64_t>(chunk, nb - c0), e->st);
-                HIPCHK(hipGetLastError());
+        bool again = false;
+        n_big = 0;
+        for (size_t r = 0; r < R && !again; r++) {
+            HIPCHK(hipMemsetAsync(big_n, 0, 2 * sizeof(unsigned long long), e->st));
+            SeedParams S{};
+            S.word = e->o.word_size;
+            S.stride = e->o.word_size - W16 + 1;
+            {
+                const char *pm = getenv("RC_SEED_PRE");   // A/B knob; 1 = hit-list pre-test
+                S.pre_mode = pm ? atoi(pm) : 1;
             }
-            unsigned long long nr = 0;
+            S.sym = e->o.symmetric;
+            S.gene_begin = rg0[r];
+            S.gene_end = rg1[r];
+            S.seeds = e->d_seeds.p;
+            S.seed_cap = e->seed_cap;
+            S.seed_count = e->d_shard_cnt.p;
+            S.cands = e->d_cands.p;
+            S.cand_cap = e->cand_cap;
+            S.cand_count = e->d_shard_cnt.p + NSHARD;
+            S.gc_off = e->d_gc_off.p + gcb[r];
+            S.gc_cnt = e->d_gc_cnt.p + gcb[r];
+            S.tmask = e->d_tmask.p;
+            S.status = e->d_status.p;
+            S.big_out = e->d_big_out.p;
+            S.big_n = big_n;
+            S.big_retry_n = big_retry_n;
+            S.big_list_cap = e->big_list_cap;
+            S.prof = e->d_prof.p;
+            launch_seed(e->has_amb, db, ix, S, e->st);
+            HIPCHK(hipGetLastError());
+            unsigned int status = 0;
+            unsigned long long nb = 0;   // (big_n: d_count[12], next to the extension's counters [0, 11))
             HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
-            HIPCHK(hipMemcpyAsync(&nr, big_retry_n, sizeof nr, hipMemcpyDeviceToHost, e->st));
+            HIPCHK(hipMemcpyAsync(&nb, big_n, sizeof nb, hipMemcpyDeviceToHost, e->st));
             HIPCHK(hipStreamSynchronize(e->st));
-            if (status & 16u) return fail(RC_E_LIMIT, "a candidate has more than 65535 seeds");
+            if (status & 2u) return fail(RC_E_LIMIT, "a query gene has more than 127 isoforms");
+            if (status & 8u) {   // the big-pass list itself overflowed
+                e->big_list_cap = std::max<uint64_t>(4 * e->big_list_cap, nb + 1024);
+                again = true;
+                break;
+            }
             again = (status & 1u) != 0;
-            nb = nr;
-            // the retry entries become the next list (buffers swapped, not copied)
-            std::swap(e->d_big_list.p, e->d_big_retry.p);
-            std::swap(e->d_big_list.cap, e->d_big_retry.cap);
-            list = e->d_big_list.p;
-            if (nb) e->big_cap *= 2;
+            // (gene, sample) passes whose seeds overflow LDS: global-memory
+            // passes, at most BIG_CHUNK workgroups per launch; entries that
+            // overflow big_cap too are rerun with twice the scratch
+            const uint64_t BIG_CHUNK = 2048;
+            uint64_t *list = e->d_big_out.p;
+            n_big += nb;
+            while (!again && nb) {
+                if ((uint64_t)e->big_cap > (1ull << 22))
+                    return fail(RC_E_LIMIT, "a (query gene, subject sample) pass has more than 2^22 seeds");
+                const uint64_t chunk = std::min<uint64_t>(nb, BIG_CHUNK);
+                CHK(e->d_big_list.ensure(nb));
+                CHK(e->d_big_retry.ensure(nb));
+                CHK(e->d_big_seeds.ensure(chunk * e->big_cap));
+                CHK(e->d_big_seg.ensure(chunk * (e->big_cap + 1)));
+                CHK(e->d_big_segT.ensure(chunk * e->big_cap));
+                if (list != e->d_big_list.p)
+                    HIPCHK(hipMemcpyAsync(e->d_big_list.p, list, nb * 8, hipMemcpyDeviceToDevice, e->st));
+                HIPCHK(hipMemsetAsync(big_retry_n, 0, sizeof(unsigned long long), e->st));
+                SeedParams B = S;
+                B.big_retry = e->d_big_retry.p;
+                B.big_list_cap = nb;
+                B.big_cap = e->big_cap;
+                B.big_seeds = e->d_big_seeds.p;
+                B.big_seg = e->d_big_seg.p;
+                B.big_segT = e->d_big_segT.p;
+                for (uint64_t c0 = 0; c0 < nb; c0 += chunk) {
+                    B.big_list = e->d_big_list.p + c0;
+                    launch_seed_big(e->has_amb, db, ix, B, (uint32_t)std::min<uint64_t>(chunk, nb - c0), e->st);
+                    HIPCHK(hipGetLastError());
+                }
+                unsigned long long nr = 0;
+                HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
+                HIPCHK(hipMemcpyAsync(&nr, big_retry_n, sizeof nr, hipMemcpyDeviceToHost, e->st));
+                HIPCHK(hipStreamSynchronize(e->st));
+                if (status & 16u) return fail(RC_E_LIMIT, "a candidate has more than 65535 seeds");
+                again = (status & 1u) != 0;
+                nb = nr;
+                // the retry entries become the next list (buffers swapped, not copied)
+                std::swap(e->d_big_list.p, e->d_big_retry.p);
+                std::swap(e->d_big_list.cap, e->d_big_retry.cap);
+                list = e->d_big_list.p;
+                if (nb) e->big_cap *= 2;
+            }
         }
         HIPCHK(hipEventRecord(e->ev[9], e->st));
         HIPCHK(hipMemcpyAsync(shard_cnt.data(), e->d_shard_cnt.p, 2 * NSHARD * 8, hipMemcpyDeviceToHost, e->st));
@@ -1077,13 +1265,12 @@ static int do_align(rc_engine *e)
         e->seed_cap = std::max<uint64_t>(e->seed_cap, ms * 5 / 4 + 4096);
         e->cand_cap = std::max<uint64_t>(e->cand_cap, mc * 5 / 4 + 1024);
     }
-    e->tm.big_passes = (double)e->n_big;
+    e->tm.big_passes += (double)n_big;
     std::vector<unsigned long long> prefix(NSHARD + 1, 0);
     for (int i = 0; i < NSHARD; i++) prefix[i + 1] = prefix[i] + shard_cnt[NSHARD + i];
     const uint64_t n_cand = prefix[NSHARD];
-    e->n_seeds = 0;
     for (int i = 0; i < NSHARD; i++) e->n_seeds += shard_cnt[i];
-    e->n_cands = n_cand;
+    e->n_cands += n_cand;
     HIPCHK(hipMemcpyAsync(e->d_shard_prefix.p, prefix.data(), (NSHARD + 1) * 8, hipMemcpyHostToDevice, e->st));
     // --- extension ---
     const uint64_t slots = e->cand_cap * NSHARD;
@@ -1095,7 +1282,7 @@ static int do_align(rc_engine *e)
     for (int attempt = 0;; attempt++) {
         if (attempt == 4) return fail(RC_E_NOMEM, "HSP overflow buffer kept overflowing");
         CHK(e->d_ovf.ensure(e->ovf_cap));
-        HIPCHK(hipMemsetAsync(e->d_count.p, 0, 16 * sizeof(unsigned long long), e->st));
+        HIPCHK(hipMemsetAsync(e->d_count.p, 0, 12 * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
         ExtParams X;
         X.xdrop = e->o.xdrop_half;
@@ -1140,10 +1327,6 @@ static int do_align(rc_engine *e)
         HIPCHK(hipMemcpyAsync(ctr, e->d_count.p + 1, sizeof ctr, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipStreamSynchronize(e->st));
-        e->tm.ext_steps = (double)ctr[0];
-        e->tm.ext_calls = (double)ctr[1];
-        e->tm.ext_fullband = (double)ctr[3];
-        e->tm.ext_deferred = (double)ctr[5];
         if (ctr[8] || ctr[9]) {   // built with RC_ROW_TIMING: wave cycles in transitions / steps
             fprintf(stderr, "row kernel wave-cycles: transitions %.4g steps %.4g\n", (double)ctr[8], (double)ctr[9]);
             unsigned long long pr[8];
@@ -1151,24 +1334,25 @@ static int do_align(rc_engine *e)
             fprintf(stderr, "seed kernel block-cycles: words %.4g scan %.4g hits %.4g sort %.4g write %.4g\n",
                     (double)pr[0], (double)pr[1], (double)pr[2], (double)pr[3], (double)pr[4]);
         }
-        if (!(status & 1u)) break;
+        if (!(status & 1u)) {
+            e->tm.ext_steps += (double)ctr[0];
+            e->tm.ext_calls += (double)ctr[1];
+            e->tm.ext_fullband += (double)ctr[3];
+            e->tm.ext_deferred += (double)ctr[5];
+            break;
+        }
         e->ovf_cap = std::max<uint64_t>(e->ovf_cap, ovn * 5 / 4 + 1024);
     }
-    // --- groups: (query gene, subject sample) -> contiguous HSPs ---
-    // Direct groups (query sample < subject sample) come first in d_hsp, in
-    // candidate order; mirrored groups (the subject->query direction of the
-    // same alignments) follow, each sorted into the order that search emits.
+    // --- groups: (query gene, subject sample) -> contiguous HSPs, appended ---
+    // Direct groups of every run first, in candidate order; mirrored groups
+    // (spec 5b: the subject->query direction of the same alignments) follow,
+    // each sorted into the order that search emits.
     GroupParams G{};
-    G.gene_begin = g0;
-    G.gene_end = g1;
     G.N = N;
-    G.gc_off = e->d_gc_off.p;
-    G.gc_cnt = e->d_gc_cnt.p;
     G.cand_nh = e->d_cand_nh.p;
     G.cand_hsp = e->d_cand_hsp.p;
     G.cand_ovf = e->d_cand_ovf.p;
     G.ovf = e->d_ovf.p;
-    G.cnt = e->d_gcount.p;
     G.shard_prefix = e->d_shard_prefix.p;
     G.n_cand = n_cand;
     G.cand_cap = e->cand_cap;
@@ -1176,18 +1360,8 @@ static int do_align(rc_engine *e)
     G.tx_pos = e->d_tx_pos.p;
     G.tx = e->d_tx.p;
     G.n_genes = n_genes;
-    CHK(e->d_mcnt.ensure(ngrp + 1));
-    CHK(e->d_mcur.ensure(ngrp));
-    CHK(e->d_mscan.ensure(ngrp + 1));
-    G.mcnt = e->d_mcnt.p;
-    G.mcur = e->d_mcur.p;
-    HIPCHK(hipMemsetAsync(e->d_grp_cnt.p, 0, ngrp * 4, e->st));
-    HIPCHK(hipMemsetAsync(e->d_grp_off.p, 0, ngrp * 4, e->st));
-    HIPCHK(hipMemsetAsync(e->d_gcount.p + nsgrp, 0, 4, e->st));
-    HIPCHK(hipMemsetAsync(e->d_mcnt.p, 0, (ngrp + 1) * 4, e->st));
-    HIPCHK(hipMemsetAsync(e->d_mcur.p, 0, ngrp * 4, e->st));
-    launch_group(G, 0, e->st);
-    if (e->o.symmetric) launch_group(G, 2, e->st);   // mirrored groups (spec 5b)
+    G.grp_off = e->d_grp_off.p;
+    G.grp_cnt = e->d_grp_cnt.p;
     auto exscan = [&](const uint32_t *in, uint64_t *out, size_t n) -> int {
         size_t tmp = 0;
         HIPCHK(rocprim::exclusive_scan(nullptr, tmp, in, out, (uint64_t)0, n, rocprim::plus<uint64_t>(), e->st));
@@ -1195,37 +1369,106 @@ static int do_align(rc_engine *e)
         HIPCHK(rocprim::exclusive_scan(e->d_tmp.p, tmp, in, out, (uint64_t)0, n, rocprim::plus<uint64_t>(), e->st));
         return RC_OK;
     };
-    CHK(exscan(e->d_gcount.p, e->d_gscan.p, nsgrp + 1));
-    CHK(exscan(e->d_mcnt.p, e->d_mscan.p, ngrp + 1));
-    uint64_t nd = 0, nm = 0;
-    HIPCHK(hipMemcpyAsync(&nd, e->d_gscan.p + nsgrp, 8, hipMemcpyDeviceToHost, e->st));
-    HIPCHK(hipMemcpyAsync(&nm, e->d_mscan.p + ngrp, 8, hipMemcpyDeviceToHost, e->st));
-    HIPCHK(hipStreamSynchronize(e->st));
-    const uint64_t nh = nd + nm;
-    if (nh > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "more than 2^32 HSPs on one GPU: use more shards");
-    CHK(e->d_hsp.ensure(nh));
-    CHK(e->d_mkey.ensure(2 * nm + 2));
-    G.scan = e->d_gscan.p;
-    G.mscan = e->d_mscan.p;
-    G.grp_off = e->d_grp_off.p;
-    G.grp_cnt = e->d_grp_cnt.p;
-    G.out = e->d_hsp.p;
-    G.mbase = nd;
-    G.mkey = e->d_mkey.p;
-    launch_group(G, 1, e->st);
+    auto run_group = [&](size_t r) {
+        GroupParams g = G;
+        g.gene_begin = rg0[r];
+        g.gene_end = rg1[r];
+        g.gc_off = e->d_gc_off.p + gcb[r];
+        g.gc_cnt = e->d_gc_cnt.p + gcb[r];
+        g.cnt = e->d_gcount.p + cnb[r];
+        g.scan = e->d_gscan.p + cnb[r];
+        return g;
+    };
+    std::vector<uint64_t> nd(R, 0);
+    for (size_t r = 0; r < R; r++) {
+        const size_t nsgrp = cnb[r + 1] - cnb[r] - 1;
+        HIPCHK(hipMemsetAsync(e->d_gcount.p + cnb[r] + nsgrp, 0, 4, e->st));
+        launch_group(run_group(r), 0, e->st);
+        CHK(exscan(e->d_gcount.p + cnb[r], e->d_gscan.p + cnb[r], nsgrp + 1));
+        HIPCHK(hipMemcpyAsync(&nd[r], e->d_gscan.p + cnb[r] + nsgrp, 8, hipMemcpyDeviceToHost, e->st));
+    }
+    uint64_t nm = 0;
     if (e->o.symmetric) {
+        CHK(e->d_mcnt.ensure(ngrp + 1));
+        CHK(e->d_mcur.ensure(ngrp));
+        CHK(e->d_mscan.ensure(ngrp + 1));
+        G.mcnt = e->d_mcnt.p;
+        G.mcur = e->d_mcur.p;
+        HIPCHK(hipMemsetAsync(e->d_mcnt.p, 0, (ngrp + 1) * 4, e->st));
+        HIPCHK(hipMemsetAsync(e->d_mcur.p, 0, ngrp * 4, e->st));
+        launch_group(G, 2, e->st);   // mirrored groups (spec 5b)
+        CHK(exscan(e->d_mcnt.p, e->d_mscan.p, ngrp + 1));
+        HIPCHK(hipMemcpyAsync(&nm, e->d_mscan.p + ngrp, 8, hipMemcpyDeviceToHost, e->st));
+    }
+    HIPCHK(hipStreamSynchronize(e->st));
+    uint64_t ndt = 0;
+    for (uint64_t v : nd) ndt += v;
+    const uint64_t nh = e->hsp_used + ndt + nm;
+    if (nh > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "more than 2^32 HSPs on one GPU: use more shards");
+    CHK(grow_hsp(e, nh));
+    uint64_t base = e->hsp_used;
+    for (size_t r = 0; r < R; r++) {
+        GroupParams g = run_group(r);
+        g.out = e->d_hsp.p;
+        g.base = base;
+        launch_group(g, 1, e->st);
+        base += nd[r];
+    }
+    if (e->o.symmetric) {
+        CHK(e->d_mkey.ensure(2 * nm + 2));
+        G.mscan = e->d_mscan.p;
+        G.out = e->d_hsp.p;
+        G.mbase = base;
+        G.mkey = e->d_mkey.p;
         launch_group(G, 3, e->st);
         launch_group(G, 4, e->st);
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e->ev[4], e->st));
     HIPCHK(hipEventSynchronize(e->ev[4]));
-    e->n_hsps = nh;
-    e->tm.pack_ms = ev_ms(e, 0, 1);
-    e->tm.index_ms = ev_ms(e, 1, 2);
-    e->tm.align_ms = ev_ms(e, 2, 4);
-    e->tm.seed_kernel_ms = ev_ms(e, 3, 9);
-    e->tm.align_kernel_ms = ev_ms(e, 10, 11);
+    e->hsp_used = nh;
+    e->tm.pack_ms += ev_ms(e, 0, 1);
+    e->tm.index_ms += ev_ms(e, 1, 2);
+    e->tm.align_ms += ev_ms(e, 2, 4);
+    e->tm.seed_kernel_ms += ev_ms(e, 3, 9);
+    e->tm.align_kernel_ms += ev_ms(e, 10, 11);
+    return RC_OK;
+}
+
+static int do_align(rc_engine *e)
+{
+    CHK(upload(e));
+    CHK(set_device(e));
+    e->aligned = e->finished = e->rbh_done = false;
+    e->tm = rc_timing{};
+    if (e->external) {
+        HIPCHK(hipEventRecord(e->ev[0], e->st));
+        CHK(load_external(e));
+        HIPCHK(hipEventRecord(e->ev[1], e->st));
+        HIPCHK(hipEventSynchronize(e->ev[1]));
+        e->tm.align_ms = ev_ms(e, 0, 1);
+        e->aligned = true;
+        return RC_OK;
+    }
+    const int N = (int)e->samples.size();
+    const size_t ngrp = (size_t)e->gene_sample.size() * N;
+    CHK(e->d_grp_off.ensure(ngrp));
+    CHK(e->d_grp_cnt.ensure(ngrp));
+    HIPCHK(hipMemsetAsync(e->d_grp_cnt.p, 0, ngrp * 4, e->st));
+    HIPCHK(hipMemsetAsync(e->d_grp_off.p, 0, ngrp * 4, e->st));
+    if (e->tiles_for != (int64_t)e->pair0 || e->tiles.empty()) {
+        plan_tiles(e);
+        e->tiles_for = (int64_t)e->pair0;
+        e->tile_loaded = -1;
+    }
+    e->hsp_used = 0;
+    e->n_seeds = e->n_cands = 0;
+    // the tile loaded last goes first (its tables stay on the device)
+    const int nt = (int)e->tiles.size();
+    const int first = (e->tile_loaded >= 0 && e->tile_loaded < nt) ? e->tile_loaded : 0;
+    for (int k = 0; k < nt; k++) CHK(align_tile(e, (first + k) % nt));
+    e->tm.tiles = (double)nt;
+    e->n_hsps = e->hsp_used;
     e->aligned = true;
     return RC_OK;
 }
@@ -1656,12 +1899,18 @@ int rc_dust_mask(rc_engine *e, int32_t s, uint8_t *buf, uint64_t cap, uint64_t *
         std::memset(buf, 0, S.nbases);
         return RC_OK;
     }
+    // the mask of the loaded tile, where the sample sits at tile_pos[s]
+    if (e->tile_loaded < 0) return fail(RC_E_STATE, "no tile loaded");
+    const auto &ts = e->tiles[e->tile_loaded].samples;
+    if (std::find(ts.begin(), ts.end(), s) == ts.end())
+        return fail(RC_E_STATE, "the sample is not in the last alignment pass (tile)");
     CHK(set_device(e));
-    const uint64_t w0 = S.base >> 6, w1 = (S.base + S.nbases + 63) >> 6;
+    const uint64_t b0 = e->tile_pos[s];
+    const uint64_t w0 = b0 >> 6, w1 = (b0 + S.nbases + 63) >> 6;
     std::vector<uint64_t> words(w1 - w0);
     HIPCHK(hipMemcpy(words.data(), e->d_dmask.p + 1 + w0, words.size() * 8, hipMemcpyDeviceToHost));
     for (uint64_t i = 0; i < S.nbases; i++) {
-        const uint64_t p = S.base + i;
+        const uint64_t p = b0 + i;
         buf[i] = (uint8_t)((words[(p >> 6) - w0] >> (p & 63)) & 1);
     }
     return RC_OK;

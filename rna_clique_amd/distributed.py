@@ -1,17 +1,19 @@
 """Multi-GPU: one engine per GPU, sample pairs sharded, one edge exchange.
 
-SURVEY.md §8e. Every rank loads the same samples. rc_plan_pairs gives every
-rank one rectangle [a0, a1) x [b0, b1) of the (query a, subject b) pair
-triangle, chosen by recursive bisection against a cost model of pair work,
-query-word lookups and index build, so each rank's subjects (its seed index)
-and its queries are short contiguous sample ranges; each rank
-aligns its pairs (seed + extend, both directions at once) and runs top-N /
-reciprocal best hits for them, which yields its share of the gene matches
-tables and graph edges. The ideal-clique filter needs the whole
-graph, so the edge records (20 B each: two node ids, the pair, and the edge's
-nident and length - gaps sums) are all-gathered once -- over RCCL on GPUs,
-gloo on CPU -- and every rank runs connected components, the ideal filter and
-the pair sums over all of them. That is the only collective on the data path.
+SURVEY.md §8e. rc_plan_pairs gives every rank one rectangle [a0, a1) x
+[b0, b1) of the (a, b) pair triangle, chosen by recursive bisection against a
+cost model of pair work and per-sample work (query-word lookups, index), so
+each rank's samples are two short contiguous ranges. A rank holds the
+sequences of those samples only (`needed_samples`; the others are added as
+metadata: transcripts and genes, no bases), aligns its pairs -- both directed
+searches, in tiles of at most 2^32 bases when its samples do not fit one
+pass -- and runs top-N / reciprocal best hits for them, which yields its share
+of the gene matches tables and graph edges. The ideal-clique filter needs the
+whole graph, so the edge records (20 B each: two node ids, the pair, and the
+edge's nident and length - gaps sums) are all-gathered once -- over RCCL on
+GPUs, gloo on CPU -- and every rank runs connected components, the ideal
+filter and the pair sums over all of them. That is the only collective on the
+data path.
 """
 from __future__ import annotations
 
@@ -50,6 +52,43 @@ def plan_pairs(sample_bases, shard_count):
                                       pa.ctypes.data_as(ctypes.c_void_p), pb.ctypes.data_as(ctypes.c_void_p),
                                       out.ctypes.data_as(ctypes.c_void_p)))
     return list(zip(pa[:m].tolist(), pb[:m].tolist())), out
+
+
+def needed_samples(sample_bases, shard_count, rank):
+    """The samples whose sequences rank `rank` needs: those of its pairs."""
+    order, first = plan_pairs(sample_bases, shard_count)
+    out = set()
+    for a, b in order[int(first[rank]):int(first[rank + 1])]:
+        out.add(a)
+        out.add(b)
+    return out
+
+
+def hbm_footprint(sample_bases, sample_genes, shard_count, tile_bases=(1 << 32) - (1 << 24),
+                  hsps_per_gene=1.0):
+    """Modelled HBM bytes of every rank (a planning aid: bench and tests check
+    that a configuration fits 288 GB per GPU before running it). Per rank:
+    its samples' bases (1 B each, resident), one tile's working set (packed
+    forward + reverse complement 0.5 B/base, the 16-mer index and its sort
+    buffer 16 B/base, seeds and candidates ~ 3 B/base, DUST mask), its HSP
+    store (56 B per HSP, both directed searches of every pair) and the
+    (gene, sample) group table and graph arrays over all genes."""
+    import math
+    order, first = plan_pairs(sample_bases, shard_count)
+    n = len(sample_bases)
+    genes = sum(sample_genes)
+    out = []
+    for r in range(shard_count):
+        pairs = order[int(first[r]):int(first[r + 1])]
+        samples = {s for p in pairs for s in p}
+        resident = sum(sample_bases[s] for s in samples)
+        tile = min(resident, tile_bases)
+        work = tile * (0.5 + 16 + 3 + 0.25) + (1 << 30) * 4   # + bucket table (2^28 x 4 B) and slack
+        hsps = sum(sample_genes[a] + sample_genes[b] for a, b in pairs) * hsps_per_gene * 56
+        groups = genes * n * 8 + genes * 32
+        edges = sum(min(sample_genes[a], sample_genes[b]) for a, b in pairs) * 20 * shard_count
+        out.append(int(resident + work + hsps + groups + edges + math.comb(n, 2) * 64))
+    return out
 
 
 def all_gather_records(local, record_size, process_group=None, device=None):

@@ -65,7 +65,10 @@ class Engine:
 
     # ------------------------------------------------------------- inputs
     def add_sample(self, label, seq, tx_offsets, gene, iso):
-        seq = np.ascontiguousarray(seq, dtype=np.uint8)
+        """seq None: a sample this engine does not align (a sharded run holds
+        only the samples of its own pairs) -- its transcripts and genes still
+        count for the graph and the e-value statistics."""
+        seq = None if seq is None else np.ascontiguousarray(seq, dtype=np.uint8)
         offs = np.ascontiguousarray(tx_offsets, dtype=np.uint64)
         gene = np.ascontiguousarray(gene, dtype=np.int32)
         iso = np.ascontiguousarray(iso, dtype=np.int32)
@@ -75,7 +78,7 @@ class Engine:
         sid = ctypes.c_int32()
         P = ctypes.POINTER
         nat.check(nat.lib().rc_add_sample(
-            self._h, str(label).encode(), seq.ctypes.data_as(ctypes.c_char_p),
+            self._h, str(label).encode(), None if seq is None else seq.ctypes.data_as(ctypes.c_char_p),
             offs.ctypes.data_as(P(ctypes.c_uint64)), gene.ctypes.data_as(P(ctypes.c_int32)),
             iso.ctypes.data_as(P(ctypes.c_int32)), n_tx, ctypes.byref(sid)))
         self.labels.append(str(label))

@@ -53,8 +53,11 @@ def run_engine(samples, top_matches=1, evalue=1e-99, keep_all=True, device=0,
     world, rank = distributed.world(process_group)
     eng = Engine(top_matches=top_matches, keep_all=keep_all, evalue=evalue,
                  device=device, shard_rank=rank, shard_count=world, **engine_kwargs)
-    for s in samples:
-        eng.add_sample(str(s.path), s.seq, s.tx_offsets, s.gene, s.iso)
+    # a shard holds the sequences of its own pairs' samples only
+    need = distributed.needed_samples([int(s.tx_offsets[-1]) for s in samples], world, rank) \
+        if world > 1 else range(len(samples))
+    for i, s in enumerate(samples):
+        eng.add_sample(str(s.path), s.seq if i in need else None, s.tx_offsets, s.gene, s.iso)
     if world == 1:
         eng.run()
     else:

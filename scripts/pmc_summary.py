@@ -2,6 +2,10 @@
 
 Usage: python scripts/pmc_summary.py gpurun_out/pmc_C3 profiles/<round>/C3_pmc.json [commit]
 
+The summary is stamped with bench.src_hash() of the sources in this tree
+(run it on the tree the profile was measured on); bench.py reports PMC
+traffic only from a summary whose stamp matches its own sources.
+
 HBM traffic follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in
 KiB; on gfx950 FETCH_SIZE reports half the bytes of wide coalesced reads, so
 it is doubled (uncalibrated for other access widths; see that section).
@@ -25,18 +29,44 @@ def short(name):
     return name.split("(")[0][-40:]
 
 
+ISSUE_PEAK_G = 256 * 4 * 2.4   # wave instructions / ns: 256 CUs x 4 SIMDs x 2.4 GHz (one issue per SIMD clock)
+
+
+def _ext_steps(src):
+    """Greedy row steps of the profiled bench step (bench JSON in the pass logs)."""
+    for f in sorted(glob.glob(src.rstrip("/") + "_p*.log")):
+        for line in open(f):
+            if line.startswith("{"):
+                try:
+                    return json.loads(line)["phases_ms"]["ext_steps"]
+                except (ValueError, KeyError):
+                    pass
+    return None
+
+
 def main(src, dst, commit=None):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import src_hash
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     for f in sorted(glob.glob(os.path.join(src, "p*", "*counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
             agg[short(r["Kernel_Name"])][r["Counter_Name"]] += float(r["Counter_Value"])
-    out = {"source": src, "commit": commit, "note": "per bench step (1 step, C3); FETCH_SIZE/WRITE_SIZE KiB",
+    out = {"source": src, "commit": commit, "src_hash": src_hash(),
+           "note": "per bench step (1 step); FETCH_SIZE/WRITE_SIZE KiB; FETCH_SIZE doubled "
+                   "for HBM bytes (MI355X_MICROARCH.md, HBM)",
            "kernels": {k: dict(v) for k, v in agg.items()}}
     tb = 0.0
-    for k in ("seed_kernel", "extend_rows_kernel", "extend_kernel", "ext_finish_kernel"):
+    for k in ("seed_kernel", "extend_rows_kernel", "extend_kernel", "ext_finish_kernel", "first_finish_kernel"):
         v = agg.get(k, {})
         tb += 2 * 1024 * v.get("FETCH_SIZE", 0.0) + 1024 * v.get("WRITE_SIZE", 0.0)
     out["traffic_bytes_seed_extend"] = int(tb)
+    ext = agg.get("extend_rows_kernel", {})
+    if "SQ_INSTS_VALU" in ext:
+        steps = _ext_steps(src)
+        wi = ext.get("SQ_INSTS_VALU", 0.0) + ext.get("SQ_INSTS_SALU", 0.0)
+        out["issue"] = {"kernel": "extend_rows_kernel", "wave_instr": wi, "peak_g_per_s": ISSUE_PEAK_G,
+                        "valu": ext.get("SQ_INSTS_VALU"), "salu": ext.get("SQ_INSTS_SALU"),
+                        "valu_per_wave_step": round(ext["SQ_INSTS_VALU"] / (steps / 2), 1) if steps else None}
     with open(dst, "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
     print(json.dumps({k: out["kernels"].get(k) for k in ("seed_kernel", "extend_rows_kernel")}, indent=1))

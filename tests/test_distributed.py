@@ -88,3 +88,36 @@ def test_gloo_edge_exchange_world2(sizes):
 def test_world_without_init_is_single():
     from rna_clique_amd import distributed
     assert distributed.world() == (1, 0)
+
+
+def test_plan_covers_every_pair_once_and_needed_samples():
+    """rc_plan_pairs (no device): every pair in exactly one shard, and each
+    shard's needed samples are exactly its pairs' samples (two ranges)."""
+    from rna_clique_amd import distributed
+    rng = np.random.default_rng(3)
+    for n, shards in [(5, 2), (32, 8), (64, 8), (128, 8)]:
+        bases = rng.integers(40_000_000, 60_000_000, size=n)
+        order, first = distributed.plan_pairs(bases, shards)
+        assert sorted(map(tuple, order)) == [(a, b) for a in range(n) for b in range(a + 1, n)]
+        assert first[0] == 0 and first[-1] == len(order) and all(np.diff(first) >= 0)
+        for r in range(shards):
+            need = distributed.needed_samples(bases, shards, r)
+            own = order[first[r]:first[r + 1]]
+            assert need == {s for p in own for s in p}
+
+
+def test_c5_fits_hbm_per_rank():
+    """BASELINE C5 (128 samples x 100 000 genes, 200 bp - 5 kb transcripts,
+    ~33 Gbp) on 8 GPUs: every rank's modelled HBM footprint (resident samples,
+    one tile's working set, its HSP store, the group table) is within the
+    288 GB of an MI355X, and within it with room to spare at the configuration's
+    mean transcript length."""
+    from rna_clique_amd import distributed
+    n, genes, mean_len = 128, 100_000, 2600
+    bases = [genes * mean_len] * n
+    fp = distributed.hbm_footprint(bases, [genes] * n, 8)
+    assert max(fp) < 288e9, [f / 1e9 for f in fp]
+    assert max(fp) < 0.6 * 288e9
+    # sharding divides the resident bases and the HSP store
+    one = distributed.hbm_footprint(bases, [genes] * n, 1)[0]
+    assert max(fp) < 0.65 * one

@@ -306,3 +306,70 @@ def test_tables_and_graph_reload(native, tmp_path):
     assert graph.number_of_edges() == sim.graph.number_of_edges()
     again = SampleSimilarity(graph, list(SampleSimilarity.mapping_from_dfs(got_tables)))
     assert np.array_equal(again.get_dissimilarity_df().to_numpy(), want.to_numpy())
+
+
+def test_tiles_match_one_pass(native, monkeypatch):
+    """A shard whose samples do not fit one alignment pass is cut into tiles
+    (a- and b-chunks, positions relative to each tile, HSPs appended): forced
+    here with a small RC_TILE_BASES, the results equal one pass bit for bit."""
+    from rna_clique_amd.engine import Engine
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(6, 150, seed=23, p_iso2=0.2, indel_rate=0.002, p_revcomp=0.3,
+                          polya=(0.2, 15, 40))
+    ref = _load(Engine(device=0), samples)
+    ref.run()
+    per = max(int(s.tx_offsets[-1]) for s in samples)
+    monkeypatch.setenv("RC_TILE_BASES", str(3 * per))
+    eng = _load(Engine(device=0), samples)
+    eng.run()
+    assert eng.timings()["tiles"] > 1
+    for q in range(6):
+        for s in range(6):
+            if q != s:
+                assert eng.hsps(q, s).tobytes() == ref.hsps(q, s).tobytes(), (q, s)
+    for a, b in itertools.combinations(range(6), 2):
+        assert eng.pair_rows(a, b).tobytes() == ref.pair_rows(a, b).tobytes()
+    assert np.array_equal(eng.distance()[1], ref.distance()[1])
+    msgs, _ = full_check(eng, samples)
+    assert not msgs, "\n".join(msgs[:10])
+
+
+@pytest.mark.parametrize("shards", [3, 5])
+def test_shards_hold_only_their_samples(native, monkeypatch, shards):
+    """Sharded engines given only the sequences of their own pairs' samples
+    (the others as metadata) -- and, for 5 shards, cut into tiles too --
+    equal the unsharded engine."""
+    from rna_clique_amd import distributed
+    from rna_clique_amd.engine import Engine
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(7, 100, seed=29, p_iso2=0.2, indel_rate=0.002, p_revcomp=0.3)
+    ref = _load(Engine(device=0), samples)
+    ref.run()
+    bases = [int(s.tx_offsets[-1]) for s in samples]
+    if shards == 5:
+        monkeypatch.setenv("RC_TILE_BASES", str(2 * max(bases)))
+    engines = []
+    for r in range(shards):
+        need = distributed.needed_samples(bases, shards, r)
+        assert len(need) < len(samples) or shards < 3
+        e = Engine(device=0, shard_rank=r, shard_count=shards)
+        for i, s in enumerate(samples):
+            e.add_sample(s.name, s.seq if i in need else None, s.tx_offsets, s.gene, s.iso)
+        e.align()
+        e.finish()
+        engines.append(e)
+    allb = np.concatenate([e.export_edges() for e in engines])
+    pairs = engines[0].pair_order()
+    for e in engines:
+        e.import_edges(allb)
+        assert np.array_equal(e.distance()[1], ref.distance()[1])
+        for p in range(*e.shard_pairs()):
+            a, b = pairs[p]
+            assert e.pair_rows(a, b).tobytes() == ref.pair_rows(a, b).tobytes()
+    # a shard missing one of its own samples refuses to run
+    from rna_clique_amd._native import NativeError
+    bad = Engine(device=0, shard_rank=0, shard_count=shards)
+    for i, s in enumerate(samples):
+        bad.add_sample(s.name, None, s.tx_offsets, s.gene, s.iso)
+    with pytest.raises(NativeError):
+        bad.align()
