@@ -136,8 +136,17 @@ class SampleSimilarity:
     def _pairs(self):
         return itertools.combinations(range(len(self.labels)), 2)
 
+    def _table_pairs(self):
+        """The pairs whose tables this engine holds: all of them, or on a
+        sharded run (world > 1) this rank's pairs only -- each rank then
+        holds (and rna_clique(store_dfs=True) / write_pair_tables write) a
+        disjoint part of the table set, the union over ranks being the whole."""
+        if getattr(self.engine, "shard_count", 1) > 1:
+            return sorted(tuple(sorted(p)) for p in self.engine.owned_pairs())
+        return self._pairs()
+
     def _table_iter(self):
-        for a, b in self._pairs():
+        for a, b in self._table_pairs():
             yield (self.labels[a], self.labels[b]), pair_table(self.engine, a, b, self.labels)
 
     @property

@@ -373,3 +373,94 @@ def test_shards_hold_only_their_samples(native, monkeypatch, shards):
         bad.add_sample(s.name, None, s.tx_offsets, s.gene, s.iso)
     with pytest.raises(NativeError):
         bad.align()
+
+
+def test_device_edge_exchange_and_sharded_tables(native):
+    """The device-pointer edge path (rc_export_edges / rc_import_edges with
+    on_device=1, what the RCCL exchange uses): shard engines export into
+    CUDA tensors, the concatenation is imported from device memory, and the
+    result equals the unsharded engine. SampleSimilarity(store_dfs=True) on a
+    shard holds that shard's tables; the union over shards is the full set."""
+    import torch
+    from rna_clique_amd.engine import Engine
+    from rna_clique_amd.similarity import SampleSimilarity
+    from rna_clique_amd.tables import pair_table
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(5, 120, seed=37, p_iso2=0.2, indel_rate=0.002)
+    ref = _load(Engine(device=0), samples)
+    ref.run()
+    engines = [_load(Engine(device=0, shard_rank=r, shard_count=3), samples) for r in range(3)]
+    rs = engines[0].edge_record_size()
+    parts = []
+    for e in engines:
+        e.align()
+        e.finish()
+        t = torch.empty(max(e.local_edge_count() * rs, 1), dtype=torch.uint8, device="cuda")
+        n = e.export_edges(t)
+        assert n == e.local_edge_count()
+        torch.cuda.synchronize()
+        assert t[:n * rs].cpu().numpy().tobytes() == e.export_edges().tobytes()
+        parts.append(t[:n * rs])
+    allt = torch.cat(parts)
+    torch.cuda.synchronize()
+    seen = {}
+    for e in engines:
+        e.import_edges(allt, allt.numel() // rs)
+        assert np.array_equal(e.distance()[1], ref.distance()[1])
+        sim = SampleSimilarity.from_engine(e, store_dfs=True)
+        assert np.array_equal(sim.get_dissimilarity_df().to_numpy(),
+                              SampleSimilarity.from_engine(ref).get_dissimilarity_df().to_numpy())
+        for k, df in sim.comparison_dfs.items():
+            assert k not in seen
+            seen[k] = df
+    labels = ref.labels
+    assert len(seen) == 10
+    for a, b in itertools.combinations(range(5), 2):
+        want = pair_table(ref, a, b, labels)
+        got = seen[(labels[a], labels[b])] if (labels[a], labels[b]) in seen else \
+            seen[(labels[b], labels[a])]
+        pd.testing.assert_frame_equal(got, want)
+
+
+def _rccl_worker(port, q):
+    import os as _os
+    import torch
+    import torch.distributed as dist
+    _os.environ["MASTER_ADDR"] = "127.0.0.1"
+    _os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        from rna_clique_amd import distributed
+        from rna_clique_amd.engine import Engine
+        from rna_clique_amd.simulate import simulate
+        samples, _ = simulate(4, 100, seed=41)
+        eng = _load(Engine(device=0, shard_rank=0, shard_count=1), samples)
+        distributed.sharded_run(eng)        # RCCL branch: device export, all-gather, device import
+        q.put(eng.distance()[1].tobytes())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_exchange_world1(native):
+    """exchange_edges over an RCCL process group (world 1 on the one GPU of
+    the test box: the device-to-device branch end to end)."""
+    import socket
+    import torch.multiprocessing as mp
+    from rna_clique_amd.engine import Engine
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(4, 100, seed=41)
+    ref = _load(Engine(device=0), samples)
+    ref.run()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(port, q))
+    p.start()
+    got = q.get(timeout=300)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert got == ref.distance()[1].tobytes()

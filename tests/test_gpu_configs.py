@@ -139,3 +139,17 @@ def test_config_C3_correctness_variant(native):
     st = _c3_properties(eng, samples, tree, C3_PAIRS)
     assert st["components"] > st["ideal_components"] > 40000
     eng.close()
+
+
+def test_config_C4_full_size(native):
+    """C4 (64 x 50 000, ~3.3 Gbp, 2016 pairs on one GPU): sampled pairs
+    bit-exact vs the oracle, whole-run properties and the NJ tree of all 64
+    samples (BASELINE configs[3])."""
+    from rna_clique_amd.simulate import CONFIGS, simulate
+    samples, tree = simulate(**CONFIGS["C4"])
+    eng = _engine_run(samples)
+    st = _c3_properties(eng, samples, tree, [(0, 1), (7, 40), (33, 63), (62, 63)])
+    # the 64-taxon tree is deeper: a few hundred genes miss an edge between
+    # distant samples and their components are not ideal cliques
+    assert st["components"] == 50000 and st["ideal_components"] > 49000
+    eng.close()
