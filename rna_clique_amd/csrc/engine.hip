@@ -30,8 +30,9 @@ void launch_bucket_fill(const uint64_t *, uint64_t, int, uint32_t *, hipStream_t
 void launch_seed(bool, const Db &, const Index &, const SeedParams &, hipStream_t);
 void launch_seed_big(bool, const Db &, const Index &, const SeedParams &, uint32_t, hipStream_t);
 void launch_dust(bool, uint64_t, const uint64_t *, const uint64_t *, const uint64_t *, const TxInfo *, uint32_t, int,
-                 int, int, uint32_t *, uint32_t, uint64_t *, hipStream_t);
+                 int, int, uint32_t *, uint64_t *, uint32_t, uint64_t *, hipStream_t);
 uint32_t dust_scratch_words(uint32_t);
+uint64_t dust_event_words(uint32_t);
 void launch_extend(bool, const Db &, const ExtParams &, hipStream_t);
 void launch_extend_rows(bool, const Db &, const ExtParams &, int, hipStream_t);
 void launch_group(const GroupParams &, int, hipStream_t);
@@ -284,6 +285,7 @@ struct rc_engine {
     DBuf<uint32_t> d_bucket, d_pos_tx;
     DBuf<uint64_t> d_sample_pos, d_txstart, d_kpos_rel, d_dmask;
     DBuf<uint32_t> d_dust_scratch;
+    DBuf<uint64_t> d_dust_events;
     DBuf<unsigned long long> d_prof;
     DBuf<uint8_t> d_tmp;
     DBuf<int32_t> d_thr, d_bits10;
@@ -1103,11 +1105,12 @@ static int align_tile(rc_engine *e, int ti)
         const size_t mw = (total >> 6) + 4;
         CHK(e->d_dmask.ensure(mw));
         HIPCHK(hipMemsetAsync(e->d_dmask.p, 0, mw * 8, e->st));
-        const uint32_t dblocks = 256 * 16;   // resident lanes of the chunk kernel (their slot scratch)
+        const uint32_t dblocks = 256 * 20;   // at least the resident waves of the chunk kernel: their scratch
         CHK(e->d_dust_scratch.ensure(dust_scratch_words(dblocks)));
+        CHK(e->d_dust_events.ensure(dust_event_words(dblocks)));
         launch_dust(e->has_amb, total, e->d_F.p + FRONT_PAD, e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr,
                     e->d_txstart.p + 1, e->d_tile_tx.p, e->tile_ntx, e->o.dust_level, e->o.dust_window,
-                    e->o.dust_linker, e->d_dust_scratch.p, dblocks, e->d_dmask.p + 1, e->st);
+                    e->o.dust_linker, e->d_dust_scratch.p, e->d_dust_events.p, dblocks, e->d_dmask.p + 1, e->st);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(e->ev[1], e->st));

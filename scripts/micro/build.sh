@@ -2,7 +2,9 @@
 set -e
 cd "$(dirname "$0")/../.."
 mkdir -p bin
-for v in 0; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -DDUST_VARIANT=$v -o bin/dust_micro_$v \
-    scripts/micro/dust_micro.hip rna_clique_amd/csrc/dust.hip
-done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fgpu-rdc -o bin/dust_micro \
+  scripts/micro/dust_micro.hip rna_clique_amd/csrc/dust.hip
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fgpu-rdc -DRC_DUST_PROF -o bin/dust_micro_prof \
+  scripts/micro/dust_micro.hip rna_clique_amd/csrc/dust.hip
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fgpu-rdc -DRC_DUST_PROF -DRC_DUST_NO_B -o bin/dust_micro_noB \
+  scripts/micro/dust_micro.hip rna_clique_amd/csrc/dust.hip

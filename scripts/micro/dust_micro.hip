@@ -6,8 +6,12 @@
 #include <vector>
 namespace rcg {
 void launch_dust(bool, uint64_t, const uint64_t *, const uint64_t *, const uint64_t *, const TxInfo *, uint32_t, int,
-                 int, int, uint32_t *, uint32_t, uint64_t *, hipStream_t);
+                 int, int, uint32_t *, uint64_t *, uint32_t, uint64_t *, hipStream_t);
 uint32_t dust_scratch_words(uint32_t);
+uint64_t dust_event_words(uint32_t);
+#ifdef RC_DUST_PROF
+extern __device__ unsigned long long g_dust_prof[4];
+#endif
 }
 using namespace rcg;
 int main(int argc, char **argv)
@@ -19,21 +23,30 @@ int main(int argc, char **argv)
     for (auto &v : h) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; v = x; }
     std::vector<uint64_t> tb((total >> 6) + 4, 0);
     for (uint64_t p = 0; p < total; p += 1000) { const uint64_t q = p + 64; tb[q >> 6] |= 1ull << (q & 63); }
-    uint64_t *F, *TB, *M; uint32_t *S;
+    uint64_t *F, *TB, *M, *E; uint32_t *S;
     hipMalloc(&F, nw * 8); hipMalloc(&TB, tb.size() * 8); hipMalloc(&M, tb.size() * 8);
-    const uint32_t blocks = 256 * 16;
+    const uint32_t blocks = argc > 2 ? (uint32_t)atoi(argv[2]) : 256 * 10;
     hipMalloc(&S, (size_t)dust_scratch_words(blocks) * 4);
+    hipMalloc(&E, (size_t)dust_event_words(blocks) * 8);
     hipMemcpy(F, h.data(), nw * 8, hipMemcpyHostToDevice);
     hipMemcpy(TB, tb.data(), tb.size() * 8, hipMemcpyHostToDevice);
     hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
     for (int it = 0; it < 3; it++) {
         hipMemset(M, 0, tb.size() * 8);
         hipEventRecord(a, 0);
-        launch_dust(false, total, F, nullptr, TB + 1, nullptr, 0, 20, 64, 1, S, blocks, M + 1, 0);
+#ifdef RC_DUST_PROF
+        unsigned long long z[4] = {0, 0, 0, 0};
+        hipMemcpyToSymbol(HIP_SYMBOL(g_dust_prof), z, sizeof z);
+#endif
+        launch_dust(false, total, F, nullptr, TB + 1, nullptr, 0, 20, 64, 1, S, E, blocks, M + 1, 0);
         hipEventRecord(b, 0);
         hipEventSynchronize(b);
         float ms; hipEventElapsedTime(&ms, a, b);
         printf("dust %.3f ms (%s)\n", ms, hipGetErrorString(hipGetLastError()));
+#ifdef RC_DUST_PROF
+        hipMemcpyFromSymbol(z, HIP_SYMBOL(g_dust_prof), sizeof z);
+        printf("  wave-cycles A %.3g B %.3g  events %llu  iterations %llu\n", (double)z[0], (double)z[1], z[2], z[3]);
+#endif
     }
     std::vector<uint64_t> m(tb.size());
     hipMemcpy(m.data(), M, m.size() * 8, hipMemcpyDeviceToHost);

@@ -107,6 +107,11 @@ def _c3_properties(eng, samples, tree, pairs):
     eng.run()
     assert np.array_equal(eng.distance()[1], mat)
     assert eng.stats() == st
+    # DUST masks of two whole samples, base for base
+    from oracle.align import OracleDB
+    for i in (pairs[0][0], pairs[-1][1]):
+        want = OracleDB([samples[i]]).dust_mask(0, *eng.dust)
+        assert np.array_equal(eng.dust_mask(i), want), i
     msgs = check_pairs(eng, samples, pairs)
     assert not msgs, "\n".join(msgs[:10])
     assert _rf_to_truth(tree, samples, labels, mat) == 0
