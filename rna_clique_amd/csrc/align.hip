@@ -500,38 +500,90 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
         }
         SEED_TICK(2);
         const uint32_t nseed = sh_nseed;
-        // sort by (k1, y). Up to SBLOCK seeds: one per thread, bitonic in
+        // sort by (k1, y). Chunks of SBLOCK seeds: one per thread, bitonic in
         // registers -- partners within the wave by lane exchange, the few
-        // stages across waves through LDS; beyond: bitonic in LDS
+        // stages across waves through the chunk's LDS. Then (LDS pass) merge
+        // rounds of sorted runs: each seed's place is its index in its run plus
+        // its rank in the partner run (a binary search there), all reads before
+        // a barrier, then written in place. Global-memory passes (BIG): one
+        // bitonic network over the whole pass instead.
+        auto seed_gt = [](const LSeed &a, const LSeed &b) { return (a.k1 > b.k1) || (a.k1 == b.k1 && a.y > b.y); };
         uint32_t np2 = 1;
-        while (np2 < nseed) np2 <<= 1;
-        if (np2 <= SBLOCK) {
-            LSeed v = {~0ull, 0xFFFFFFFFu, 0u};
-            if ((uint32_t)tid < nseed) v = seeds[tid];
-            for (uint32_t kk = 2; kk <= np2; kk <<= 1) {
-                for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
-                    LSeed o;
-                    if (j >= 64) {
-                        __syncthreads();
-                        seeds[tid] = v;
-                        __syncthreads();
-                        o = seeds[tid ^ j];
-                    } else {
-                        const int jj = (int)j;
-                        o.k1 = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(v.k1 >> 32), jj) << 32) |
-                               (uint32_t)__shfl_xor((int)(uint32_t)v.k1, jj);
-                        o.y = (uint32_t)__shfl_xor((int)v.y, jj);
-                        o.len = (uint32_t)__shfl_xor((int)v.len, jj);
+        if (!BIG || nseed <= SBLOCK) {
+            const uint32_t nch = (nseed + SBLOCK - 1) / SBLOCK;
+            for (uint32_t c = 0; c < nch; c++) {
+                LSeed *cs = seeds + (size_t)c * SBLOCK;
+                const uint32_t cn = min(nseed - c * (uint32_t)SBLOCK, (uint32_t)SBLOCK);
+                uint32_t cp2 = 1;
+                while (cp2 < cn) cp2 <<= 1;
+                LSeed v = {~0ull, 0xFFFFFFFFu, 0u};
+                if ((uint32_t)tid < cn) v = cs[tid];
+                for (uint32_t kk = 2; kk <= cp2; kk <<= 1) {
+                    for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+                        LSeed o;
+                        if (j >= 64) {
+                            __syncthreads();
+                            if ((uint32_t)tid < cp2) cs[tid] = v;
+                            __syncthreads();
+                            o = (uint32_t)tid < cp2 ? cs[tid ^ j] : v;
+                        } else {
+                            const int jj = (int)j;
+                            o.k1 = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(v.k1 >> 32), jj) << 32) |
+                                   (uint32_t)__shfl_xor((int)(uint32_t)v.k1, jj);
+                            o.y = (uint32_t)__shfl_xor((int)v.y, jj);
+                            o.len = (uint32_t)__shfl_xor((int)v.len, jj);
+                        }
+                        const bool gt = seed_gt(v, o);
+                        const bool want_min = ((tid & j) == 0) == ((tid & kk) == 0);
+                        if (gt == want_min) v = o;
                     }
-                    const bool gt = (v.k1 > o.k1) || (v.k1 == o.k1 && v.y > o.y);
-                    const bool want_min = ((tid & j) == 0) == ((tid & kk) == 0);
-                    if (gt == want_min) v = o;
                 }
+                __syncthreads();
+                if ((uint32_t)tid < cn) cs[tid] = v;
             }
             __syncthreads();
-            if ((uint32_t)tid < nseed) seeds[tid] = v;
-            __syncthreads();
-            np2 = 1;   // sorted
+            if (!BIG) {
+                constexpr int MPT = SEED_CAP / SBLOCK;   // seeds per thread in a merge round
+                for (uint32_t w = SBLOCK; w < nseed; w <<= 1) {
+                    LSeed mv[MPT];
+                    uint32_t mdst[MPT];
+#pragma unroll
+                    for (int m = 0; m < MPT; m++) {
+                        const uint32_t i = (uint32_t)(m * SBLOCK + tid);
+                        mdst[m] = ~0u;
+                        if (i >= nseed) continue;
+                        mv[m] = seeds[i];
+                        const uint32_t a0 = i / (2 * w) * (2 * w), b0 = a0 + w;
+                        if (b0 >= nseed) {   // a run without a partner stays
+                            mdst[m] = i;
+                            continue;
+                        }
+                        const bool inA = i < b0;
+                        // partner run [p0, p1): A's seeds go before equal B seeds
+                        const uint32_t p0 = inA ? b0 : a0, p1 = inA ? min(b0 + w, nseed) : b0;
+                        uint32_t lo = p0, n = p1 - p0;
+                        while (n) {
+                            const uint32_t h = n >> 1;
+                            const LSeed &o = seeds[lo + h];
+                            const bool before = inA ? seed_gt(mv[m], o) : !seed_gt(o, mv[m]);
+                            if (before) {
+                                lo += h + 1;
+                                n -= h + 1;
+                            } else {
+                                n = h;
+                            }
+                        }
+                        mdst[m] = a0 + (i - (inA ? a0 : b0)) + (lo - p0);
+                    }
+                    __syncthreads();
+#pragma unroll
+                    for (int m = 0; m < MPT; m++)
+                        if (mdst[m] != ~0u) seeds[mdst[m]] = mv[m];
+                    __syncthreads();
+                }
+            }
+        } else {
+            while (np2 < nseed) np2 <<= 1;
         }
         for (uint32_t i = nseed + tid; i < np2; i += SBLOCK) {
             seeds[i].k1 = ~0ull;
@@ -544,9 +596,8 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     const uint32_t ixj = i ^ j;
                     if (ixj > i) {
                         LSeed a = seeds[i], b = seeds[ixj];
-                        const bool gt = (a.k1 > b.k1) || (a.k1 == b.k1 && a.y > b.y);
                         const bool up = (i & kk) == 0;
-                        if (gt == up) {
+                        if (seed_gt(a, b) == up) {
                             seeds[i] = b;
                             seeds[ixj] = a;
                         }
