@@ -291,14 +291,16 @@ def main():
             "kernel": "seed_kernel + extension kernels", "kernel_ms": round(avg_k, 3),
             "bytes_per_launch": int(bytes_launch)}
     if prof and prof.get("issue"):
-        # the extension is bound by instruction issue, not bytes: VALU+SALU
-        # instructions per step over its measured time vs the issue peak
+        # the extension is bound by VALU issue, not bytes: its VALU instructions
+        # per step over its measured time vs the VALU issue peak (a wave64
+        # instruction holds a 32-lane SIMD for 2 clocks)
         iss = prof["issue"]
         t_ext = tm["align_kernel_ms"] * 1e-3
-        roof["issue_extension"] = {"bound": "issue", "unit": "G wave-instr/s",
-                                   "achieved": round(iss["wave_instr"] / t_ext / 1e9, 1),
-                                   "peak": iss["peak_g_per_s"],
-                                   "frac": round(iss["wave_instr"] / t_ext / 1e9 / iss["peak_g_per_s"], 4),
+        peak = iss.get("valu_peak_g_per_s", 256 * 4 * 2.4 / 2)
+        roof["issue_extension"] = {"bound": "valu", "unit": "G wave-VALU/s",
+                                   "achieved": round(iss["valu"] / t_ext / 1e9, 1), "peak": peak,
+                                   "frac": round(iss["valu"] / t_ext / 1e9 / peak, 4),
+                                   "salu_g_per_s": round(iss["salu"] / t_ext / 1e9, 1),
                                    "valu_per_wave_step": iss.get("valu_per_wave_step")}
     if cpu:
         cpu["gpu_speedup"] = round(value / cpu["value"], 1)

@@ -1053,9 +1053,9 @@ __device__ __forceinline__ int rw_from_lower(int v, int edge, int rl)
 {
     if constexpr (RW == 16) {
         return __builtin_amdgcn_update_dpp(edge, v, 0x111, 0xF, 0xF, false);   // row_shr:1
-    } else {
-        const int x = __builtin_amdgcn_update_dpp(edge, v, 0x138, 0xF, 0xF, false);   // wave_shr:1
-        return (FIX && rl == 0) ? edge : x;
+    } else {   // wave_shr:1, lane 0 reads 0 (bound_ctrl); FIX puts `edge` at the row starts
+        const int x = __builtin_amdgcn_mov_dpp(v, 0x138, 0xF, 0xF, true);
+        return FIX ? (rl == 0 ? edge : x) : x;   // without FIX, edge is 0
     }
 }
 // lane rl <- rl + 1 inside the row (rl RW - 1 gets `edge`)
@@ -1064,9 +1064,9 @@ __device__ __forceinline__ int rw_from_upper(int v, int edge, int rl)
 {
     if constexpr (RW == 16) {
         return __builtin_amdgcn_update_dpp(edge, v, 0x101, 0xF, 0xF, false);   // row_shl:1
-    } else {
-        const int x = __builtin_amdgcn_update_dpp(edge, v, 0x130, 0xF, 0xF, false);   // wave_shl:1
-        return (FIX && rl == RW - 1) ? edge : x;
+    } else {   // wave_shl:1, lane 63 reads 0 (bound_ctrl); FIX puts `edge` at the row ends
+        const int x = __builtin_amdgcn_mov_dpp(v, 0x130, 0xF, 0xF, true);
+        return FIX ? (rl == RW - 1 ? edge : x) : x;   // without FIX, edge is 0
     }
 }
 // max over the row, in every lane of the row
@@ -1097,12 +1097,28 @@ __device__ __forceinline__ uint32_t rw_mask(uint64_t m, int row)
     return (uint32_t)(m >> (RW * row)) & (RW == 32 ? 0xFFFFFFFFu : 0xFFFFu);
 }
 
+// x != 0 ? ~0 : 0 on a wave-uniform value, kept in scalar registers
+__device__ __forceinline__ uint32_t s_nonzero(uint32_t x)
+{
+    uint32_t r;
+    asm volatile("s_cmp_lg_u32 %1, 0\n\ts_cselect_b32 %0, -1, 0" : "=s"(r) : "s"(x) : "scc");
+    return r;
+}
+// lane masks of single compares (one v_cmp each, combined in scalar registers)
+__device__ __forceinline__ uint64_t m_gt(int a, int b) { return __builtin_amdgcn_ballot_w64(a > b); }
+__device__ __forceinline__ uint64_t m_ge(int a, int b) { return __builtin_amdgcn_ballot_w64(a >= b); }
+__device__ __forceinline__ uint64_t m_lt(int a, int b) { return __builtin_amdgcn_ballot_w64(a < b); }
+__device__ __forceinline__ uint64_t m_eq(int a, int b) { return __builtin_amdgcn_ballot_w64(a == b); }
+// lane mask of a condition (the HIP __ballot goes through an int and two extra vector ops)
+__device__ __forceinline__ uint64_t ballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
+
 // spread a wave mask to whole rows: every lane of a row with a set lane (scalar work)
 template <int RW>
 __device__ __forceinline__ uint64_t rw_spread(uint64_t m)
 {
-    if constexpr (RW == 32) {
-        return ((m & 0xFFFFFFFFull) ? 0xFFFFFFFFull : 0ull) | ((m & 0xFFFFFFFF00000000ull) ? 0xFFFFFFFF00000000ull : 0ull);
+    if constexpr (RW == 32) {   // per 32-bit half, scalar ops (the compiler turns a test of the high half into a vector compare)
+        const uint32_t lo = s_nonzero((uint32_t)m), hi = s_nonzero((uint32_t)(m >> 32));
+        return (uint64_t)lo | ((uint64_t)hi << 32);
     } else {
         uint64_t r = 0;
         for (int i = 0; i < 4; i++)
@@ -1392,9 +1408,9 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
         t_tr += c1t - c0t;
 #endif
         const bool ext = act >= A_STEP_R;
-        const uint64_t mext = __ballot(ext);
+        const uint64_t mext = m_ge(act, A_STEP_R);
         if (!mext) break;
-        steps += (unsigned long long)__builtin_popcount(rw_bits<RW>(mext));
+        steps += (unsigned long long)__builtin_amdgcn_readfirstlane((int)__builtin_popcount(rw_bits<RW>(mext)));
         // ---------------- one greedy step of every extending row ----------------
         if (ext) {
             d6 += 6;
@@ -1427,20 +1443,24 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
             R = ni;
             goe = ng;
             const bool live = ni >= 0;
-            // row-wide decisions as lane masks (scalar), applied with v_cndmask
-            const uint64_t mimp = rw_spread<RW>(__ballot(live && score > best));
+            // row-wide decisions as lane masks (scalar), applied with v_cndmask.
+            // A lane X-dropped this step has score < best, a dead one INT_MIN:
+            // score > best implies live.
+            const uint64_t mlive = m_ge(ni, 0);
+            const uint64_t mimp = rw_spread<RW>(m_gt(score, best));
             if (mimp) {
                 const int mk = rw_max<RW>(live ? score * RW + (RW - 1 - rl) : INT_MIN);
                 best = lane_sel(mimp, mk >> (RW == 32 ? 5 : 4), best);
                 bl = lane_sel(mimp, RW - 1 - (mk & (RW - 1)), bl);
-                const uint64_t mwin = mimp & __ballot(rl == bl);
+                const uint64_t mwin = mimp & m_eq(rl, bl);
                 wi = lane_sel(mwin, R, wi);
                 wg = lane_sel(mwin, goe, wg);
                 wd = lane_sel(mwin, d6, wd);
             }
             // bound >= score, so a lane that can still beat best is live
-            const uint64_t mcont = rw_spread<RW>(__ballot(live && bound > best)) & __ballot(d6 < 6 * DMAX);
-            const uint64_t medge = rw_spread<RW>(__ballot(live && (rl == 0 || rl == RW - 1)));
+            constexpr uint64_t EDGES = RW == 32 ? 0x8000000180000001ull : 0x8001800180018001ull;   // rl 0 and RW - 1
+            const uint64_t mcont = rw_spread<RW>(mlive & m_gt(bound, best)) & m_lt(d6, 6 * DMAX);
+            const uint64_t medge = rw_spread<RW>(mlive & EDGES);
             act = lane_sel(mcont, lane_sel(medge, (int)A_ABORT, act), act - (A_STEP_R - A_RDONE));
         }
 #ifdef RC_ROW_TIMING

@@ -29,7 +29,9 @@ def short(name):
     return name.split("(")[0][-40:]
 
 
-ISSUE_PEAK_G = 256 * 4 * 2.4   # wave instructions / ns: 256 CUs x 4 SIMDs x 2.4 GHz (one issue per SIMD clock)
+# VALU issue peak, wave instructions / ns: 256 CUs x 4 SIMDs x 2.4 GHz, a wave64
+# VALU instruction occupying a 32-lane SIMD for 2 clocks (MI355X_MICROARCH.md)
+VALU_PEAK_G = 256 * 4 * 2.4 / 2
 
 
 def _ext_steps(src):
@@ -64,7 +66,7 @@ def main(src, dst, commit=None):
     if "SQ_INSTS_VALU" in ext:
         steps = _ext_steps(src)
         wi = ext.get("SQ_INSTS_VALU", 0.0) + ext.get("SQ_INSTS_SALU", 0.0)
-        out["issue"] = {"kernel": "extend_rows_kernel", "wave_instr": wi, "peak_g_per_s": ISSUE_PEAK_G,
+        out["issue"] = {"kernel": "extend_rows_kernel", "wave_instr": wi, "valu_peak_g_per_s": VALU_PEAK_G,
                         "valu": ext.get("SQ_INSTS_VALU"), "salu": ext.get("SQ_INSTS_SALU"),
                         "valu_per_wave_step": round(ext["SQ_INSTS_VALU"] / (steps / 2), 1) if steps else None}
     with open(dst, "w") as fh:
