@@ -1032,7 +1032,7 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
 // copies of both transcripts staged next to the forward ones.
 
 #ifndef ROW_MIN_WAVES
-#define ROW_MIN_WAVES 6
+#define ROW_MIN_WAVES 7   // measured best at C3 (5-8 tried, r02)
 #endif
 
 // max over the 16 lanes of each DPP row, in every lane of the row
@@ -1139,18 +1139,24 @@ __device__ __forceinline__ int lane_sel(uint64_t m, int a, int b)
 template <bool AMB>
 __device__ __forceinline__ int slide_fwd(const uint32_t *S, uint32_t pa, uint32_t pb, int maxn, uint32_t moff)
 {
-    int n = 0;
-    while (n < maxn) {
-        uint64_t x = win3(S, pa + (uint32_t)n) ^ win3(S, pb + (uint32_t)n);
-        if (AMB) x |= win3(S, pa + (uint32_t)n + moff) | win3(S, pb + (uint32_t)n + moff);
-        if (x == 0) {
+    // the first window outside any loop (a mismatch within 32 bases is the
+    // common case); lanes on a run of 32+ matches continue in the loop
+    uint64_t x = win3(S, pa) ^ win3(S, pb);
+    if (AMB) x |= win3(S, pa + moff) | win3(S, pb + moff);
+    int n = x ? (int)(__builtin_ctzll(x) >> 1) : 32;
+    if (n == 32 && maxn > 32) {
+        for (;;) {
+            x = win3(S, pa + (uint32_t)n) ^ win3(S, pb + (uint32_t)n);
+            if (AMB) x |= win3(S, pa + (uint32_t)n + moff) | win3(S, pb + (uint32_t)n + moff);
+            if (x) {
+                n += (int)(__builtin_ctzll(x) >> 1);
+                break;
+            }
             n += 32;
-            continue;
+            if (n >= maxn) break;
         }
-        n += __builtin_ctzll(x) >> 1;
-        return n < maxn ? n : maxn;
     }
-    return maxn > 0 ? maxn : 0;
+    return min(n, max(maxn, 0));
 }
 
 
@@ -1410,7 +1416,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
         const bool ext = act >= A_STEP_R;
         const uint64_t mext = m_ge(act, A_STEP_R);
         if (!mext) break;
-        steps += (unsigned long long)__builtin_amdgcn_readfirstlane((int)__builtin_popcount(rw_bits<RW>(mext)));
+        steps += (unsigned long long)(__builtin_popcountll(rw_spread<RW>(mext)) / RW);   // scalar
         // ---------------- one greedy step of every extending row ----------------
         if (ext) {
             d6 += 6;
@@ -1750,8 +1756,8 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
         if (amb) RC_LAUNCH_ROWS(true, 16, ROW_MIN_WAVES); else RC_LAUNCH_ROWS(false, 16, ROW_MIN_WAVES);
     } else if (mw == 5) {
         if (amb) RC_LAUNCH_ROWS(true, 32, 5); else RC_LAUNCH_ROWS(false, 32, 5);
-    } else if (mw == 7) {
-        if (amb) RC_LAUNCH_ROWS(true, 32, 7); else RC_LAUNCH_ROWS(false, 32, 7);
+    } else if (mw == 6) {
+        if (amb) RC_LAUNCH_ROWS(true, 32, 6); else RC_LAUNCH_ROWS(false, 32, 6);
     } else if (mw == 8) {
         if (amb) RC_LAUNCH_ROWS(true, 32, 8); else RC_LAUNCH_ROWS(false, 32, 8);
     } else {

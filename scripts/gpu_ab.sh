@@ -1,16 +1,9 @@
-# A/B runs: GPU parity tests, then the bench without the CPU baseline, once per
-# value of an environment variable. Usage: bash scripts/gpu_ab.sh VAR "v1 v2 ..." [config] [steps]
+# A/B runs of the quick bench under environment knobs (engine getenv):
+# Usage: bash scripts/gpu_ab.sh "RC_ROW_WAVES=7" "RC_ROW_WAVES=8" ...
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-VAR=$1; VALS=$2; CFG=${3:-C3}; STEPS=${4:-3}
-for v in $VALS; do
-  export $VAR=$v
-  timeout -k 10 300 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/gpu_tests_$v.log 2>&1
-  rc=$?; echo "[$VAR=$v] pytest rc=$rc"; tail -2 gpurun_out/gpu_tests_$v.log
-  [ $rc -eq 0 ] || exit $rc
-  timeout -k 10 300 python bench.py --config "$CFG" --steps "$STEPS" --warmup 1 --no-cpu-baseline > gpurun_out/bench_$v.json 2> gpurun_out/bench_$v.err
-  rc=$?; echo "[$VAR=$v] bench rc=$rc"
-  [ $rc -eq 0 ] || exit $rc
-  python -c "import json;d=json.load(open('gpurun_out/bench_$v.json'));print(d['value'],d['ms_per_step']);print(d['phases_ms'])"
+for kv in "" "$@"; do
+  env $kv timeout -k 10 300 python bench.py --config C3 --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > gpurun_out/ab.json 2> gpurun_out/ab.err || exit $?
+  python -c "import json,sys;d=json.load(open('gpurun_out/ab.json'));p=d['phases_ms'];print(sys.argv[1] or 'default', d['value'], d['ms_per_step'], 'seed', p['seed_kernel_ms'], 'ext', p['align_kernel_ms'], 'pack', p['pack_ms'], 'index', p['index_ms'])" "$kv"
 done
