@@ -1453,12 +1453,26 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
             // A lane X-dropped this step has score < best, a dead one INT_MIN:
             // score > best implies live.
             const uint64_t mlive = m_ge(ni, 0);
-            const uint64_t mimp = rw_spread<RW>(m_gt(score, best));
+            const uint64_t mi = m_gt(score, best);
+            const uint64_t mimp = rw_spread<RW>(mi);
             if (mimp) {
-                const int mk = rw_max<RW>(live ? score * RW + (RW - 1 - rl) : INT_MIN);
-                best = lane_sel(mimp, mk >> (RW == 32 ? 5 : 4), best);
-                bl = lane_sel(mimp, RW - 1 - (mk & (RW - 1)), bl);
-                const uint64_t mwin = mimp & m_eq(rl, bl);
+                uint64_t mwin;
+                const uint32_t lo = (uint32_t)mi, hi = (uint32_t)(mi >> 32);
+                if (RW == 32 && !(lo & (lo - 1)) && !(hi & (hi - 1))) {
+                    // at most one improving lane per row (the usual case): it is
+                    // the row's new best, read out directly, no row reduction
+                    const int a = lo ? __builtin_ctz(lo) : 0, b = hi ? __builtin_ctz(hi) : 0;
+                    const int s0 = __builtin_amdgcn_readlane(score, a), s1 = __builtin_amdgcn_readlane(score, 32 + b);
+                    constexpr uint64_t ROW0 = 0xFFFFFFFFull;
+                    best = lane_sel(mimp & ROW0, s0, lane_sel(mimp & ~ROW0, s1, best));
+                    bl = lane_sel(mimp & ROW0, a, lane_sel(mimp & ~ROW0, b, bl));
+                    mwin = mi;
+                } else {
+                    const int mk = rw_max<RW>(live ? score * RW + (RW - 1 - rl) : INT_MIN);
+                    best = lane_sel(mimp, mk >> (RW == 32 ? 5 : 4), best);
+                    bl = lane_sel(mimp, RW - 1 - (mk & (RW - 1)), bl);
+                    mwin = mimp & m_eq(rl, bl);
+                }
                 wi = lane_sel(mwin, R, wi);
                 wg = lane_sel(mwin, goe, wg);
                 wd = lane_sel(mwin, d6, wd);
