@@ -115,6 +115,7 @@ typedef struct rc_timing {
     double ext_deferred;      /* candidates past the two-candidate staging slot */
     double big_passes;        /* (query gene, subject sample) seed passes run from global memory */
     double tiles;             /* alignment passes (tiles) of this shard's samples */
+    double dust_ms;           /* device time of DUST (on its own stream, beside the index build) */
 } rc_timing;
 
 void rc_default_opts(rc_opts *opts);

@@ -338,7 +338,7 @@ __global__ void dust_linker_kernel(const TxInfo *__restrict__ tx, uint32_t n_tx,
 
 void launch_dust(bool amb, uint64_t total, const uint64_t *F, const uint64_t *AF, const uint64_t *txstart,
                  const TxInfo *tx, uint32_t n_tx, int level, int window, int linker, uint32_t *scratch,
-                 uint64_t *events, uint32_t scratch_blocks, uint64_t *mask, hipStream_t st)
+                 uint64_t *events, uint32_t scratch_blocks, int max_waves, uint64_t *mask, hipStream_t st)
 {
     if (total == 0) return;
     const uint64_t nchunk = (total + DCHUNK - 1) / DCHUNK;
@@ -349,6 +349,8 @@ void launch_dust(bool amb, uint64_t total, const uint64_t *F, const uint64_t *AF
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per_cu, amb ? (const void *)dust_kernel<true> : (const void *)dust_kernel<false>, DW, 0);
+    // max_waves > 0: at most that many waves per SIMD (room for kernels on other streams)
+    if (max_waves > 0) per_cu = std::min(per_cu, 4 * max_waves);
     const uint64_t resident = (uint64_t)std::max(ncu, 1) * (uint64_t)std::max(per_cu, 1);
     const uint64_t g = std::min<uint64_t>(std::min<uint64_t>((nchunk + DW - 1) / DW, scratch_blocks), resident);
     const uint64_t nwords = (total + 31) / 32 + 2;   // readable packed words (the arrays carry padding)

@@ -30,7 +30,7 @@ void launch_bucket_fill(const uint64_t *, uint64_t, int, uint32_t *, hipStream_t
 void launch_seed(bool, const Db &, const Index &, const SeedParams &, hipStream_t);
 void launch_seed_big(bool, const Db &, const Index &, const SeedParams &, uint32_t, hipStream_t);
 void launch_dust(bool, uint64_t, const uint64_t *, const uint64_t *, const uint64_t *, const TxInfo *, uint32_t, int,
-                 int, int, uint32_t *, uint64_t *, uint32_t, uint64_t *, hipStream_t);
+                 int, int, uint32_t *, uint64_t *, uint32_t, int, uint64_t *, hipStream_t);
 uint32_t dust_scratch_words(uint32_t);
 uint64_t dust_event_words(uint32_t);
 void launch_extend(bool, const Db &, const ExtParams &, hipStream_t);
@@ -225,6 +225,7 @@ static uint64_t align_up(uint64_t x) { return (x + TILE_ALIGN - 1) & ~(TILE_ALIG
 struct rc_engine {
     rc_opts o{};
     hipStream_t st = nullptr;
+    hipStream_t st2 = nullptr;   // DUST beside the index build
     std::vector<SampleRec> samples;
     uint64_t total_bases = 0;   // input bases added so far (all samples)
     uint64_t ascii_used = 0;    // bytes of d_ascii in use (resident samples, TILE_ALIGN-aligned)
@@ -330,11 +331,15 @@ struct rc_engine {
     std::vector<unsigned long long> h_num, h_den, h_num_all, h_den_all, h_stats;
     rc_timing tm{};
     hipEvent_t ev[16] = {};
+    hipEvent_t evd[2] = {};   // DUST start / end on st2
 
     ~rc_engine()
     {
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t x : evd)
+            if (x) (void)hipEventDestroy(x);
+        if (st2) (void)hipStreamDestroy(st2);
         if (st) (void)hipStreamDestroy(st);
     }
 };
@@ -384,10 +389,16 @@ int rc_create(const rc_opts *opts, rc_engine **out)
     if (opts->device < 0 || opts->device >= ndev) return fail(RC_E_ARG, "bad device ordinal");
     rc_engine *e = new rc_engine();
     e->o = *opts;
-    if (hipSetDevice(e->o.device) != hipSuccess || hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(e->o.device) != hipSuccess || hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->st2, hipStreamNonBlocking) != hipSuccess) {
         delete e;
         return fail(RC_E_HIP, "stream creation failed");
     }
+    for (auto &ev : e->evd)
+        if (hipEventCreate(&ev) != hipSuccess) {
+            delete e;
+            return fail(RC_E_HIP, "event creation failed");
+        }
     for (auto &ev : e->ev)
         if (hipEventCreate(&ev) != hipSuccess) {
             delete e;
@@ -1100,22 +1111,34 @@ static int align_tile(rc_engine *e, int ti)
                 e->d_RC.p + FRONT_PAD, e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr,
                 e->has_amb ? e->d_ARC.p + FRONT_PAD : nullptr, e->st);
     HIPCHK(hipGetLastError());
-    if (e->o.dust_level > 0) {
-        // DUST masks of the tile's transcripts (the query side), bit per base
+    const bool dust = e->o.dust_level > 0;
+    if (dust) {
         const size_t mw = (total >> 6) + 4;
         CHK(e->d_dmask.ensure(mw));
         HIPCHK(hipMemsetAsync(e->d_dmask.p, 0, mw * 8, e->st));
+    }
+    HIPCHK(hipEventRecord(e->ev[1], e->st));
+    if (dust) {
+        // DUST masks of the tile's transcripts (the query side), bit per base,
+        // on the second stream: a compute-bound scan beside the HBM-bound
+        // index build (RC_DUST_WAVES caps its waves per SIMD)
         const uint32_t dblocks = 256 * 20;   // at least the resident waves of the chunk kernel: their scratch
         CHK(e->d_dust_scratch.ensure(dust_scratch_words(dblocks)));
         CHK(e->d_dust_events.ensure(dust_event_words(dblocks)));
+        const char *dwv = getenv("RC_DUST_WAVES");
+        const int dwaves = dwv ? atoi(dwv) : 0;   // 0: every resident wave (measured best; 1-3 starve DUST)
+        HIPCHK(hipStreamWaitEvent(e->st2, e->ev[1], 0));
+        HIPCHK(hipEventRecord(e->evd[0], e->st2));
         launch_dust(e->has_amb, total, e->d_F.p + FRONT_PAD, e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr,
                     e->d_txstart.p + 1, e->d_tile_tx.p, e->tile_ntx, e->o.dust_level, e->o.dust_window,
-                    e->o.dust_linker, e->d_dust_scratch.p, e->d_dust_events.p, dblocks, e->d_dmask.p + 1, e->st);
+                    e->o.dust_linker, e->d_dust_scratch.p, e->d_dust_events.p, dblocks, dwaves, e->d_dmask.p + 1,
+                    e->st2);
         HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(e->evd[1], e->st2));
     }
-    HIPCHK(hipEventRecord(e->ev[1], e->st));
     CHK(build_index(e));
     HIPCHK(hipGetLastError());
+    if (dust) HIPCHK(hipStreamWaitEvent(e->st, e->evd[1], 0));
     HIPCHK(hipEventRecord(e->ev[2], e->st));
 
     std::vector<uint64_t> tmask;
@@ -1432,6 +1455,10 @@ static int align_tile(rc_engine *e, int ti)
     e->hsp_used = nh;
     e->tm.pack_ms += ev_ms(e, 0, 1);
     e->tm.index_ms += ev_ms(e, 1, 2);
+    if (e->o.dust_level > 0 && !e->external) {
+        float dms = 0;
+        if (hipEventElapsedTime(&dms, e->evd[0], e->evd[1]) == hipSuccess) e->tm.dust_ms += dms;
+    }
     e->tm.align_ms += ev_ms(e, 2, 4);
     e->tm.seed_kernel_ms += ev_ms(e, 3, 9);
     e->tm.align_kernel_ms += ev_ms(e, 10, 11);

@@ -5,5 +5,5 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 for kv in "" "$@"; do
   env $kv timeout -k 10 300 python bench.py --config C3 --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > gpurun_out/ab.json 2> gpurun_out/ab.err || exit $?
-  python -c "import json,sys;d=json.load(open('gpurun_out/ab.json'));p=d['phases_ms'];print(sys.argv[1] or 'default', d['value'], d['ms_per_step'], 'seed', p['seed_kernel_ms'], 'ext', p['align_kernel_ms'], 'pack', p['pack_ms'], 'index', p['index_ms'])" "$kv"
+  python scripts/ab_line.py gpurun_out/ab.json "$kv"
 done

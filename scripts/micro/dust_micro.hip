@@ -6,7 +6,7 @@
 #include <vector>
 namespace rcg {
 void launch_dust(bool, uint64_t, const uint64_t *, const uint64_t *, const uint64_t *, const TxInfo *, uint32_t, int,
-                 int, int, uint32_t *, uint64_t *, uint32_t, uint64_t *, hipStream_t);
+                 int, int, uint32_t *, uint64_t *, uint32_t, int, uint64_t *, hipStream_t);
 uint32_t dust_scratch_words(uint32_t);
 uint64_t dust_event_words(uint32_t);
 #ifdef RC_DUST_PROF
@@ -38,7 +38,7 @@ int main(int argc, char **argv)
         unsigned long long z[4] = {0, 0, 0, 0};
         hipMemcpyToSymbol(HIP_SYMBOL(g_dust_prof), z, sizeof z);
 #endif
-        launch_dust(false, total, F, nullptr, TB + 1, nullptr, 0, 20, 64, 1, S, E, blocks, M + 1, 0);
+        launch_dust(false, total, F, nullptr, TB + 1, nullptr, 0, 20, 64, 1, S, E, blocks, 0, M + 1, 0);
         hipEventRecord(b, 0);
         hipEventSynchronize(b);
         float ms; hipEventElapsedTime(&ms, a, b);
