@@ -111,11 +111,15 @@ typedef struct rc_timing {
     double align_kernel_ms;   /* device time of the extension kernel */
     double ext_steps;         /* greedy X-drop steps executed (wave-level) */
     double ext_calls;         /* greedy extensions (left + right per HSP attempt) */
-    double ext_fullband;      /* extensions recomputed with the full 64-diagonal band */
-    double ext_deferred;      /* candidates past the two-candidate staging slot */
+    double ext_fullband;      /* candidates whose frontier left the row kernel's sub-band (extended whole
+                                 by the one-wave full-band kernel; RC_ROW64=1: by 64-lane rows first) */
+    double ext_deferred;      /* candidates the one-wave kernel took (sub-band exits, seeds outside the
+                                 first HSP box, transcripts past the row staging slot) */
     double big_passes;        /* (query gene, subject sample) seed passes run from global memory */
     double tiles;             /* alignment passes (tiles) of this shard's samples */
     double dust_ms;           /* device time of DUST (on its own stream, beside the index build) */
+    double band_bound;        /* extensions whose frontier reached the 64-diagonal band edge (spec 3) */
+    double maxhsp_bound;      /* candidates with a seed outside their MAX_HSP (8) HSP boxes (spec 3) */
 } rc_timing;
 
 void rc_default_opts(rc_opts *opts);

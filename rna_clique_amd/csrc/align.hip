@@ -773,7 +773,7 @@ __device__ __forceinline__ int slide(const uint32_t *A, const uint32_t *AM, PT p
 template <bool AMB, bool BACK, typename PT>
 __device__ __forceinline__ ExtRes ext_wave(const uint32_t *A, const uint32_t *AM, PT pa, int alen,
                                            const uint32_t *B, const uint32_t *BM, PT pb, int blen, int X,
-                                           int lane, uint32_t &steps)
+                                           int lane, uint32_t &steps, uint32_t &edge)
 {
     constexpr int EBIT = 26, OBIT = 13;
     constexpr int GMASK = 8191;
@@ -814,6 +814,8 @@ __device__ __forceinline__ ExtRes ext_wave(const uint32_t *A, const uint32_t *AM
         goe = ng;
         const bool live = ni >= 0;
         if (!__ballot(live)) break;
+        // the 64-diagonal band binds (spec 3): a live diagonal at its edge
+        if (__ballot(live && (lane == 0 || lane == BAND - 1))) edge = 1;
         if (__ballot(live && score > best.score)) {
             // (score, lowest lane) as one key: score * 64 + (63 - lane)
             const int mk = wave_max(live ? score * 64 + (63 - lane) : INT_MIN);
@@ -839,10 +841,11 @@ __device__ __forceinline__ void process_candidate(const uint32_t *QO, const uint
                                                   const uint32_t *TFM, PT tf, int Lq, int Lt, const GSeed *sd,
                                                   int ns, int X, int lane, int &bqa, int &bqb, int &bsa, int &bsb,
                                                   int &bsc, int &bd, int &bg, int &bo, int &bni, int &nh,
-                                                  uint32_t &steps, uint32_t &exts)
+                                                  uint32_t &steps, uint32_t &exts, uint32_t &edges, uint32_t &capped)
 {
     nh = 0;
-    for (int c0 = 0; c0 < ns && nh < MAX_HSP; c0 += 64) {
+    int next = ns;   // the first seed not examined (MAX_HSP reached before it)
+    for (int c0 = 0; c0 < ns && next == ns; c0 += 64) {
         // lane i holds seed c0 + i; the loop broadcasts them with readlane
         int sx = 0, sy = 0, sl = 0;
         if (c0 + lane < ns) {
@@ -852,16 +855,22 @@ __device__ __forceinline__ void process_candidate(const uint32_t *QO, const uint
             sl = (int)g.len;
         }
         const int nc = min(ns - c0, 64);
-        for (int si = 0; si < nc && nh < MAX_HSP; si++) {
+        for (int si = 0; si < nc; si++) {
+            if (nh >= MAX_HSP) {
+                next = c0 + si;
+                break;
+            }
             const int x = __builtin_amdgcn_readlane(sx, si), y = __builtin_amdgcn_readlane(sy, si);
             const int len = __builtin_amdgcn_readlane(sl, si);
             const bool inside = lane < nh && bqa <= x && x + len <= bqb && bsa <= y && y + len <= bsb;
             if (__ballot(inside)) continue;
+            uint32_t eg = 0;
             const ExtRes r = ext_wave<AMB, false, PT>(QO, QOM, qo + (PT)(x + len), Lq - (x + len), TF, TFM,
-                                                      tf + (PT)(y + len), Lt - (y + len), X, lane, steps);
+                                                      tf + (PT)(y + len), Lt - (y + len), X, lane, steps, eg);
             const ExtRes l = ext_wave<AMB, true, PT>(QO, QOM, qo + (PT)x, x, TF, TFM, tf + (PT)y, y, X, lane,
-                                                     steps);
+                                                     steps, eg);
             exts += 2;
+            edges += eg;
             if (lane == nh) {
                 bqa = x - l.i; bqb = x + len + r.i; bsa = y - l.j; bsb = y + len + r.j;
                 bsc = l.score + 2 * len + r.score;
@@ -869,6 +878,15 @@ __device__ __forceinline__ void process_candidate(const uint32_t *QO, const uint
                 bni = len + (l.i + l.j - 2 * l.d + l.g) / 2 + (r.i + r.j - 2 * r.d + r.g) / 2;
             }
             nh++;
+        }
+    }
+    // MAX_HSP binds (spec 3) when a seed past the cap lies outside every box
+    for (int i = next; i < ns; i++) {
+        const GSeed g = sd[i];
+        const int x = (int)g.x, y = (int)g.y, len = (int)g.len;
+        if (!__ballot(lane < nh && bqa <= x && x + len <= bqb && bsa <= y && y + len <= bsb)) {
+            capped++;
+            break;
         }
     }
 }
@@ -908,7 +926,7 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
     };
     const Cand *__restrict__ cands = P.cands;
     const TxInfo *__restrict__ txs = db.tx;
-    uint32_t steps = 0, exts = 0, ncands = 0;
+    uint32_t steps = 0, exts = 0, ncands = 0, edges = 0, capped = 0;
     for (; li < n_work; li += nwaves) {
         const uint64_t ci = locate(li);
         const Cand cd = cands[ci];
@@ -939,7 +957,7 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
             process_candidate<AMB, uint32_t>(reinterpret_cast<const uint32_t *>(QO), QOM, (uint32_t)SPAD,
                                              reinterpret_cast<const uint32_t *>(TF), TFM, (uint32_t)SPAD, Lq, Lt, sd,
                                              ns, P.xdrop, lane, bqa, bqb, bsa, bsb, bsc, bd, bg, bo, bni, nh, steps,
-                                             exts);
+                                             exts, edges, capped);
         } else {
             // global arrays carry two zero words in front, so backward windows
             // of the first transcript stay in bounds (positions may go to -32)
@@ -948,7 +966,7 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
                                             reinterpret_cast<const uint32_t *>(db.F),
                                             reinterpret_cast<const uint32_t *>(db.AF), (int64_t)st.start, Lq, Lt,
                                             sd, ns, P.xdrop, lane, bqa, bqb, bsa, bsb, bsc, bd, bg, bo, bni, nh,
-                                            steps, exts);
+                                            steps, exts, edges, capped);
         }
         // purge HSPs with common endpoints: by (score desc, index asc)
         int rank = 0;
@@ -1010,6 +1028,8 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
         atomicAdd(&P.counters[0], (unsigned long long)steps);
         atomicAdd(&P.counters[1], (unsigned long long)exts);
         atomicAdd(&P.counters[2], (unsigned long long)ncands);
+        if (edges) atomicAdd(&P.counters[7], (unsigned long long)edges);     // extensions the band bound
+        if (capped) atomicAdd(&P.counters[10], (unsigned long long)capped);  // candidates MAX_HSP bound
     }
 }
 
@@ -1074,8 +1094,12 @@ template <int RW>
 __device__ __forceinline__ int rw_max(int v)
 {
     v = row_max(v);
-    if constexpr (RW == 32) {
+    if constexpr (RW >= 32) {
         const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);   // DPP rows 0<->1, 2<->3
+        v = max((int)r[0], (int)r[1]);
+    }
+    if constexpr (RW == 64) {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);   // the two halves
         v = max((int)r[0], (int)r[1]);
     }
     return v;
@@ -1087,13 +1111,16 @@ __device__ __forceinline__ uint32_t rw_bits(uint64_t m)
     if constexpr (RW == 16)
         return ((m & 0xFFFFull) ? 1u : 0u) | ((m & 0xFFFF0000ull) ? 2u : 0u) | ((m & 0xFFFF00000000ull) ? 4u : 0u) |
                ((m >> 48) ? 8u : 0u);
-    else
+    else if constexpr (RW == 32)
         return ((uint32_t)m ? 1u : 0u) | ((m >> 32) ? 2u : 0u);
+    else
+        return m ? 1u : 0u;
 }
 // the RW bits of this lane's row in a wave mask
 template <int RW>
 __device__ __forceinline__ uint32_t rw_mask(uint64_t m, int row)
 {
+    if constexpr (RW == 64) return (uint32_t)m;   // (callers take the low half only)
     return (uint32_t)(m >> (RW * row)) & (RW == 32 ? 0xFFFFFFFFu : 0xFFFFu);
 }
 
@@ -1119,6 +1146,9 @@ __device__ __forceinline__ uint64_t rw_spread(uint64_t m)
     if constexpr (RW == 32) {   // per 32-bit half, scalar ops (the compiler turns a test of the high half into a vector compare)
         const uint32_t lo = s_nonzero((uint32_t)m), hi = s_nonzero((uint32_t)(m >> 32));
         return (uint64_t)lo | ((uint64_t)hi << 32);
+    } else if constexpr (RW == 64) {
+        const uint32_t a = s_nonzero((uint32_t)m | (uint32_t)(m >> 32));
+        return (uint64_t)a | ((uint64_t)a << 32);
     } else {
         uint64_t r = 0;
         for (int i = 0; i < 4; i++)
@@ -1216,7 +1246,9 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
     // record of the next one is prefetched (one dword per lane) while the
     // current one is extended
     const uint32_t chunk = (uint32_t)max(P.chunk, 1);
-    const uint32_t ncand = (uint32_t)P.n_cand;
+    // list mode: the candidates are P.list[0, *P.list_n) (a previous row
+    // kernel's deferrals), else the linear index space over the shards
+    const uint32_t ncand = P.list ? (uint32_t)*P.list_n : (uint32_t)P.n_cand;
     uint32_t lnx = 0;
     auto grab = [&]() {
         unsigned long long b = 0;
@@ -1232,9 +1264,10 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
         if (rl == 0) RL.st[which] = sh;
         return (uint64_t)sh * P.cand_cap + (l - sprefix[sh]);
     };
+    auto cslot = [&](uint32_t l, int which) -> uint64_t { return P.list ? (uint64_t)P.list[l] : slot(l, which); };
     auto load_rec = [&](uint32_t l) -> int {
         if (l >= ncand || rl >= CAND_DWORDS) return 0;
-        return reinterpret_cast<const int *>(P.cands + slot(l, RS_SHN))[rl];
+        return reinterpret_cast<const int *>(P.cands + cslot(l, RS_SHN))[rl];
     };
     auto defer = [&](uint64_t ci) {   // row-uniform; extend_kernel takes the candidate whole
         if (rl == 0) {
@@ -1298,7 +1331,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                     act = A_DONE;
                     continue;
                 }
-                const uint64_t ci = slot(lnx, RS_SHARD);
+                const uint64_t ci = cslot(lnx, RS_SHARD);
                 if (rl < CAND_DWORDS) meta[RM_REC + rl] = recv;
                 if (rl == 0) {
                     meta[RM_CLO] = (int)(uint32_t)ci;
@@ -1469,7 +1502,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                     mwin = mi;
                 } else {
                     const int mk = rw_max<RW>(live ? score * RW + (RW - 1 - rl) : INT_MIN);
-                    best = lane_sel(mimp, mk >> (RW == 32 ? 5 : 4), best);
+                    best = lane_sel(mimp, mk >> (RW == 64 ? 6 : (RW == 32 ? 5 : 4)), best);
                     bl = lane_sel(mimp, RW - 1 - (mk & (RW - 1)), bl);
                     mwin = mimp & m_eq(rl, bl);
                 }
@@ -1478,9 +1511,11 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                 wd = lane_sel(mwin, d6, wd);
             }
             // bound >= score, so a lane that can still beat best is live
-            constexpr uint64_t EDGES = RW == 32 ? 0x8000000180000001ull : 0x8001800180018001ull;   // rl 0 and RW - 1
+            // a live lane at a sub-band edge: the candidate goes to a wider
+            // pass; 64-lane rows are the spec's band itself (no edge abort)
+            constexpr uint64_t EDGES = RW == 64 ? 0ull : (RW == 32 ? 0x8000000180000001ull : 0x8001800180018001ull);
             const uint64_t mcont = rw_spread<RW>(mlive & m_gt(bound, best)) & m_lt(d6, 6 * DMAX);
-            const uint64_t medge = rw_spread<RW>(mlive & EDGES);
+            const uint64_t medge = RW == 64 ? 0ull : rw_spread<RW>(mlive & EDGES);
             act = lane_sel(mcont, lane_sel(medge, (int)A_ABORT, act), act - (A_STEP_R - A_RDONE));
         }
 #ifdef RC_ROW_TIMING
@@ -1757,36 +1792,69 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
 {
     if (P.n_cand == 0) return;
     ExtParams W = P;
+    W.list = nullptr;
+    W.list_n = nullptr;
     const int rw = row_width == 16 ? 16 : 32;
-    const size_t lds = ((size_t)(EBLOCK / rw) * (amb ? 8 : 4) * (size_t)P.dsw + 2) * 8;
-#define RC_LAUNCH_ROWS(A, RWV, MW)                                                                        \
+    auto lds_of = [&](int w) { return ((size_t)(EBLOCK / w) * (amb ? 8 : 4) * (size_t)P.dsw + 2) * 8; };
+#define RC_LAUNCH_ROWS(A, RWV, MW, PRM)                                                                   \
     do {                                                                                                  \
         auto kern = extend_rows_kernel<A, RWV, MW>;                                                       \
-        hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, lds)), dim3(EBLOCK), lds, st, db, W);         \
+        const size_t lds = lds_of(RWV);                                                                   \
+        hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, lds)), dim3(EBLOCK), lds, st, db, PRM);       \
     } while (0)
     const char *mwv = getenv("RC_ROW_WAVES");
     const int mw = mwv ? atoi(mwv) : ROW_MIN_WAVES;
+    // pass 1: 16- or 32-diagonal rows over every candidate
     if (rw == 16) {
-        if (amb) RC_LAUNCH_ROWS(true, 16, ROW_MIN_WAVES); else RC_LAUNCH_ROWS(false, 16, ROW_MIN_WAVES);
+        if (amb) RC_LAUNCH_ROWS(true, 16, ROW_MIN_WAVES, W); else RC_LAUNCH_ROWS(false, 16, ROW_MIN_WAVES, W);
     } else if (mw == 5) {
-        if (amb) RC_LAUNCH_ROWS(true, 32, 5); else RC_LAUNCH_ROWS(false, 32, 5);
+        if (amb) RC_LAUNCH_ROWS(true, 32, 5, W); else RC_LAUNCH_ROWS(false, 32, 5, W);
     } else if (mw == 6) {
-        if (amb) RC_LAUNCH_ROWS(true, 32, 6); else RC_LAUNCH_ROWS(false, 32, 6);
+        if (amb) RC_LAUNCH_ROWS(true, 32, 6, W); else RC_LAUNCH_ROWS(false, 32, 6, W);
     } else if (mw == 8) {
-        if (amb) RC_LAUNCH_ROWS(true, 32, 8); else RC_LAUNCH_ROWS(false, 32, 8);
+        if (amb) RC_LAUNCH_ROWS(true, 32, 8, W); else RC_LAUNCH_ROWS(false, 32, 8, W);
     } else {
-        if (amb) RC_LAUNCH_ROWS(true, 32, ROW_MIN_WAVES); else RC_LAUNCH_ROWS(false, 32, ROW_MIN_WAVES);
+        if (amb) RC_LAUNCH_ROWS(true, 32, ROW_MIN_WAVES, W); else RC_LAUNCH_ROWS(false, 32, ROW_MIN_WAVES, W);
     }
+    // pass 2 (RC_ROW64=1; off by default: at C3 neutral, at C3v 7 % slower,
+    // because 40 % of what it finishes still has seeds outside the first box
+    // and is redone whole by the one-wave kernel): the candidates whose
+    // frontier left the sub-band, on 64-lane rows (the spec's whole band)
+    const char *r64 = getenv("RC_ROW64");
+    if (!(r64 && atoi(r64))) {
+        ExtParams W3 = W;
+        uint64_t g = (P.n_cand + 255) / 256;
+        if (g > 65536) g = 65536;
+        hipLaunchKernelGGL(first_finish_kernel, dim3((unsigned)g), dim3(256), 0, st, W3);
+        if (amb) {
+            auto kern = extend_kernel<true>;
+            hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W3);
+        } else {
+            auto kern = extend_kernel<false>;
+            hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W3);
+        }
+        return;
+    }
+    ExtParams W2 = W;
+    W2.list = P.defer;
+    W2.list_n = P.defer_count;
+    W2.defer = P.defer2;
+    W2.defer_count = P.defer2_count;
+    W2.work = P.work2;
+    if (amb) RC_LAUNCH_ROWS(true, 64, ROW_MIN_WAVES, W2); else RC_LAUNCH_ROWS(false, 64, ROW_MIN_WAVES, W2);
 #undef RC_LAUNCH_ROWS
     uint64_t g = (P.n_cand + 255) / 256;
     if (g > 65536) g = 65536;
-    hipLaunchKernelGGL(first_finish_kernel, dim3((unsigned)g), dim3(256), 0, st, W);
+    ExtParams W3 = W;
+    W3.defer = P.defer2;
+    W3.defer_count = P.defer2_count;
+    hipLaunchKernelGGL(first_finish_kernel, dim3((unsigned)g), dim3(256), 0, st, W3);
     if (amb) {
         auto kern = extend_kernel<true>;
-        hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W);
+        hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W3);
     } else {
         auto kern = extend_kernel<false>;
-        hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W);
+        hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W3);
     }
 }
 

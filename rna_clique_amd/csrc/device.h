@@ -182,6 +182,11 @@ struct ExtParams {
     unsigned long long *work;     // row kernel: work counter
     uint32_t *defer;
     unsigned long long *defer_count;
+    const uint32_t *list;               // row kernel list mode: candidate slots list[0, *list_n)
+    const unsigned long long *list_n;
+    uint32_t *defer2;                   // the 64-lane pass's deferrals (-> extend_kernel)
+    unsigned long long *defer2_count;
+    unsigned long long *work2;
 };
 
 // DHsp.strand carries, besides the strand (bit 0), the direction flags of a

@@ -298,7 +298,7 @@ struct rc_engine {
     DBuf<int32_t> d_cand_box;
     DBuf<DRow> d_rows_tmp;
     DBuf<DEdge> d_edges_tmp;
-    DBuf<uint32_t> d_cand_ovf, d_gc_off, d_gc_cnt, d_gcount, d_defer;
+    DBuf<uint32_t> d_cand_ovf, d_gc_off, d_gc_cnt, d_gcount, d_defer, d_defer2;
     DBuf<uint64_t> d_gscan, d_mscan, d_mkey, d_tmask;
     DBuf<uint32_t> d_mcnt, d_mcur, d_tx_pos;
     DBuf<unsigned long long> d_shard_cnt, d_shard_prefix;
@@ -1305,10 +1305,12 @@ static int align_tile(rc_engine *e, int ti)
     CHK(e->d_cand_ovf.ensure(slots));
     CHK(e->d_cand_box.ensure(slots * BOX_REC));
     CHK(e->d_defer.ensure(std::max<uint64_t>(n_cand, 1)));
+    CHK(e->d_defer2.ensure(std::max<uint64_t>(n_cand, 1)));
     for (int attempt = 0;; attempt++) {
         if (attempt == 4) return fail(RC_E_NOMEM, "HSP overflow buffer kept overflowing");
         CHK(e->d_ovf.ensure(e->ovf_cap));
         HIPCHK(hipMemsetAsync(e->d_count.p, 0, 12 * sizeof(unsigned long long), e->st));
+        HIPCHK(hipMemsetAsync(e->d_count.p + 14, 0, 2 * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
         ExtParams X;
         X.xdrop = e->o.xdrop_half;
@@ -1333,6 +1335,9 @@ static int align_tile(rc_engine *e, int ti)
         X.defer = e->d_defer.p;
         X.defer_count = e->d_count.p + 6;
         X.work = e->d_count.p + 7;
+        X.defer2 = e->d_defer2.p;
+        X.defer2_count = e->d_count.p + 14;
+        X.work2 = e->d_count.p + 15;
         X.cand_box = e->d_cand_box.p;
         {
             const char *cv = getenv("RC_ROW_CHUNK");
@@ -1347,7 +1352,8 @@ static int align_tile(rc_engine *e, int ti)
         }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e->ev[11], e->st));
-        unsigned long long ovn = 0, ctr[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long ovn = 0, ctr[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, nfull = 0;
+        HIPCHK(hipMemcpyAsync(&nfull, e->d_count.p + 14, sizeof nfull, hipMemcpyDeviceToHost, e->st));
         unsigned int status = 0;
         HIPCHK(hipMemcpyAsync(&ovn, e->d_count.p, sizeof ovn, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipMemcpyAsync(ctr, e->d_count.p + 1, sizeof ctr, hipMemcpyDeviceToHost, e->st));
@@ -1363,8 +1369,12 @@ static int align_tile(rc_engine *e, int ti)
         if (!(status & 1u)) {
             e->tm.ext_steps += (double)ctr[0];
             e->tm.ext_calls += (double)ctr[1];
-            e->tm.ext_fullband += (double)ctr[3];
+            // candidates the one-wave kernel took (the 64-lane pass's list, or the row kernel's)
+            const char *r64 = getenv("RC_ROW64");
+            e->tm.ext_fullband += (r64 && atoi(r64)) ? (double)nfull : (double)ctr[3];
             e->tm.ext_deferred += (double)ctr[5];
+            e->tm.band_bound += (double)ctr[7];
+            e->tm.maxhsp_bound += (double)ctr[10];
             break;
         }
         e->ovf_cap = std::max<uint64_t>(e->ovf_cap, ovn * 5 / 4 + 1024);

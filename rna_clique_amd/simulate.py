@@ -248,4 +248,9 @@ CONFIGS = {
     "C3": dict(taxa=32, genes=50000, seed=489, len_loc=950, len_n=100, len_p=0.5),
     "C4": dict(taxa=64, genes=50000, seed=490, len_loc=950, len_n=100, len_p=0.5),
     "C5": dict(taxa=128, genes=100000, seed=491, len_uniform=(200, 5000)),
+    # C3 with the features of real transcriptomes (correctness variant of the
+    # GPU tests; a bench workload too): 10 % two-isoform genes, indels, half the
+    # genes on the minus strand, 2 % recent paralogs, poly-A tails on 20 %
+    "C3v": dict(taxa=32, genes=50000, seed=489, len_loc=950, len_n=100, len_p=0.5, p_iso2=0.1,
+                indel_rate=0.002, p_revcomp=0.5, p_paralog=0.02, polya=(0.2, 15, 40)),
 }

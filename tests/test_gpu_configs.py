@@ -90,9 +90,20 @@ def test_config_C2_full_oracle(native):
     assert _rf_to_truth(tree, samples, labels, mat) == 0
 
 
-def _c3_properties(eng, samples, tree, pairs):
+def _record(name, eng):
+    """Engine counters of a config run (incl. how often the spec's 64-diagonal
+    band and MAX_HSP cap bound), kept under gpurun_out/ for the docs."""
+    import json
+    import os
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(os.path.join("gpurun_out", f"counters_{name}.json"), "w") as f:
+        json.dump({"timings": eng.timings(), "stats": eng.stats()}, f)
+
+
+def _c3_properties(eng, samples, tree, pairs, name="C3"):
     N = len(samples)
     st = eng.stats()
+    _record(name, eng)
     assert st["sample_count"] == N
     assert st["hsps"] > 0 and st["ideal_components"] > 0
     labels, mat = eng.distance()
@@ -138,10 +149,9 @@ def test_config_C3_correctness_variant(native):
     strand per sample, 2 % recently duplicated genes and poly-A tails: RBH ties
     and non-ideal components at scale."""
     from rna_clique_amd.simulate import CONFIGS, simulate
-    samples, tree = simulate(**CONFIGS["C3"], p_iso2=0.1, indel_rate=0.002, p_revcomp=0.5,
-                             p_paralog=0.02, polya=(0.2, 15, 40))
+    samples, tree = simulate(**CONFIGS["C3v"])
     eng = _engine_run(samples)
-    st = _c3_properties(eng, samples, tree, C3_PAIRS)
+    st = _c3_properties(eng, samples, tree, C3_PAIRS, name="C3_variant")
     assert st["components"] > st["ideal_components"] > 40000
     eng.close()
 
@@ -153,7 +163,7 @@ def test_config_C4_full_size(native):
     from rna_clique_amd.simulate import CONFIGS, simulate
     samples, tree = simulate(**CONFIGS["C4"])
     eng = _engine_run(samples)
-    st = _c3_properties(eng, samples, tree, [(0, 1), (7, 40), (33, 63), (62, 63)])
+    st = _c3_properties(eng, samples, tree, [(0, 1), (7, 40), (33, 63), (62, 63)], name="C4")
     # the 64-taxon tree is deeper: a few hundred genes miss an edge between
     # distant samples and their components are not ideal cliques
     assert st["components"] == 50000 and st["ideal_components"] > 49000
