@@ -120,6 +120,8 @@ typedef struct rc_timing {
     double dust_ms;           /* device time of DUST (on its own stream, beside the index build) */
     double band_bound;        /* extensions whose frontier reached the 64-diagonal band edge (spec 3) */
     double maxhsp_bound;      /* candidates with a seed outside their MAX_HSP (8) HSP boxes (spec 3) */
+    double ext_second;        /* shared searches: candidates whose reverse search starts at another seed
+                                 (a second first-seed extension) */
 } rc_timing;
 
 void rc_default_opts(rc_opts *opts);

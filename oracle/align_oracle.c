@@ -44,6 +44,20 @@
  *     penalty -2 / linear gap 2.5): in half-score units match +2, mismatch -4,
  *     gap -5, so score(i, j, d) = i + j - 6d. Band of 64 diagonals around the
  *     seed diagonal, X = xdrop_half (108 = 100 bits, BLAST's final x-dropoff).
+ * 4b. Canonical roles. The greedy step breaks ties between moves (mismatch,
+ *     then insertion, then deletion) and between diagonals (lowest) in the
+ *     order of its two sequences, so run with query and subject swapped it can
+ *     return a different (equally scored) end point or gap count. Every
+ *     extension is therefore evaluated with the LOWER-numbered sample's
+ *     sequence in the first role (i, the insertion side), whichever sample is
+ *     the query of the directed search; the walk itself (the base pairs it
+ *     visits, outward from the seed) is the same in both directions. Then the
+ *     extension of a given seed is one geometric result in both directed
+ *     searches of a pair, and the GPU can share it between them (DESIGN.md
+ *     §4). Each search keeps its own seeds, seed order, containment, MAX_HSP,
+ *     purge and e-value cut. BLAST's own tie-breaking is unpinned here
+ *     (BLAST+ is absent), so this restates no departure that could be
+ *     checked; it fixes the one arbitrary choice the restatement had.
  *  5. Purge HSPs sharing a start or end point (keep higher score, then earlier),
  *     keep HSPs whose e-value <= evalue (Karlin-Altschul, lambda 1.28, K 0.46,
  *     H 0.85, alpha 1.5, beta -2 for 1/-2 linear; BLAST length adjustment).
@@ -496,8 +510,20 @@ static void push_core(core_vec *cv, const core_hsp *h)
     cv->v[cv->n++] = *h;
 }
 
+/* spec 4b: the greedy primitive with the lower-numbered sample in the first
+ * (diagonal i) role; swap = the query sample is the higher-numbered one */
+static ext_result greedy_canon(const walker *Q, int32_t qlen, const walker *T, int32_t tlen, int32_t X, int swap)
+{
+    if (!swap) return greedy_ext(Q, qlen, T, tlen, X);
+    ext_result r = greedy_ext(T, tlen, Q, qlen, X);
+    const int32_t t = r.i;
+    r.i = r.j;
+    r.j = t;
+    return r;
+}
+
 static void process_candidate(const seqdb *db, uint32_t qtx, int strand, uint32_t stx,
-                              const seed *sd, int ns, int32_t X, core_vec *out)
+                              const seed *sd, int ns, int32_t X, int swap, core_vec *out)
 {
     hsp_box H[MAX_HSP];
     int nh = 0;
@@ -510,10 +536,10 @@ static void process_candidate(const seqdb *db, uint32_t qtx, int strand, uint32_
         if (c) continue;
         walker qa = {db->c, qs, Lq, strand, 0, x + len};
         walker ta = {db->c, ts, Lt, 0, 0, y + len};
-        ext_result r = greedy_ext(&qa, Lq - (x + len), &ta, Lt - (y + len), X);
+        ext_result r = greedy_canon(&qa, Lq - (x + len), &ta, Lt - (y + len), X, swap);
         walker qb = {db->c, qs, Lq, strand, 1, x - 1};
         walker tb = {db->c, ts, Lt, 0, 1, y - 1};
-        ext_result l = greedy_ext(&qb, x, &tb, y, X);
+        ext_result l = greedy_canon(&qb, x, &tb, y, X, swap);
         hsp_box b;
         b.qa = x - l.i; b.qb = x + len + r.i; b.sa = y - l.j; b.sb = y + len + r.j;
         b.score = l.score + 2 * len + r.score;
@@ -656,7 +682,7 @@ static void core_search(const uint8_t *codes, const uint64_t *tx_start, const in
                 for (uint64_t i = 0; i < nsd;) {
                     uint64_t j = i;
                     while (j < nsd && sd[j].tx == sd[i].tx) j++;
-                    process_candidate(&db, q, strand, sd[i].tx, sd + i, (int)(j - i), P->xdrop_half, cv);
+                    process_candidate(&db, q, strand, sd[i].tx, sd + i, (int)(j - i), P->xdrop_half, qsample > tsample, cv);
                     i = j;
                 }
             }

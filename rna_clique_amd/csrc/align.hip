@@ -154,8 +154,13 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
     __shared__ uint32_t tcnt[MAX_SAMPLES], tpre[MAX_SAMPLES + 1];
     __shared__ uint32_t wsum[SBLOCK / 64];
     __shared__ uint32_t sh_nseed, sh_flags;
-    __shared__ unsigned long long sh_sbase, sh_cbase;
+    __shared__ unsigned long long sh_sbase, sh_cbase, sh_lbase;
 
+    // shared searches: every maximal run is found (lookups see no DUST mask);
+    // each seed then records which of the two directed searches has a usable
+    // word in it (SEED_F: this query's mask, SEED_R: the subject's)
+    const uint64_t *const dm = P.share ? P.dmask : nullptr;
+    if (P.share) db.dmask = nullptr;
     const int Q = db.gene_sample[g];
     const uint32_t t0 = db.gene_tx_off[g];
     const uint32_t niso = db.gene_tx_off[g + 1] - t0;
@@ -218,7 +223,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                 T0 = min(T0, 64 * w + __builtin_ctzll(tm[w]));
                 Tr = max(Tr, 64 * w + 64 - __builtin_clzll(tm[w]));
             }
-        if (P.sym) T0 = max(T0, Q + 1);
+        if (P.sym || P.share) T0 = max(T0, Q + 1);
     }
     int T1 = Tr;
     const uint32_t qpb0 = (uint32_t)db.sample_pos_begin[Q], qpb1 = (uint32_t)db.sample_pos_begin[Q + 1];
@@ -463,13 +468,35 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     }
                     const int len = l + W16 + r;
                     if (len < P.word) continue;
+                    uint32_t dfl = 0;
+                    if (P.share) {
+                        // forward search (query Q, oriented): its aligned words in
+                        // [x, x + len) -- the first is p (an aligned word in [x, p)
+                        // would make the hit non-canonical); reverse search (query
+                        // the subject, oriented by the strand): its aligned words in
+                        // the run's span there. Without DUST both always exist (a
+                        // run of W = s + 15 bases holds an aligned word).
+                        bool okF = !dm, okR = !dm;
+                        const int x = p - l, y = off - l, Lt = (int)st.len;
+                        for (int pp = p; !okF && pp + W16 <= x + len; pp += stride) {
+                            const int64_t f = (int64_t)qg.qs + (strand ? (int64_t)(qg.Lq - pp - W16) : (int64_t)pp);
+                            okF = (win_bits(dm, f) & 0xFFFFull) == 0;
+                        }
+                        const int r0 = strand ? Lt - y - len : y;   // the run in the reverse query's orientation
+                        for (int pp = (r0 + stride - 1) / stride * stride; !okR && pp + W16 <= r0 + len; pp += stride) {
+                            const int64_t f = (int64_t)st.start + (strand ? (int64_t)(Lt - pp - W16) : (int64_t)pp);
+                            okR = (win_bits(dm, f) & 0xFFFFull) == 0;
+                        }
+                        dfl = (okF ? SEED_F : 0u) | (okR ? SEED_R : 0u);
+                        if (!dfl) continue;
+                    }
                     const uint32_t slot = atomicAdd(&sh_nseed, 1u);
                     if (slot < cap) {
                         LSeed sd;
                         sd.k1 = ((uint64_t)ii << 57) | ((uint64_t)strand << 56) | ((uint64_t)stx << 24) |
                                 (uint64_t)(uint32_t)(p - l);
                         sd.y = (uint32_t)(off - l);
-                        sd.len = (uint32_t)len;
+                        sd.len = (uint32_t)len | dfl;
                         seeds[slot] = sd;
                     } else {
                         atomicOr(&sh_flags, 1u);
@@ -650,33 +677,77 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                 gs.len = seeds[i].len;
                 P.seeds[sbase + i] = gs;
             }
-            for (uint32_t sg = tid; sg < nseg; sg += SBLOCK) {
-                const uint32_t b0 = seg_begin[sg], b1 = seg_begin[sg + 1];
-                const uint64_t k1 = seeds[b0].k1;
-                const uint32_t gtx = (uint32_t)(k1 >> 24);
-                const int T = seg_T[sg];
-                uint32_t rk = 0;   // rank among earlier candidates of the same sample
-                if (T1 - T0 == 1)
-                    rk = sg;
-                else
-                    for (uint32_t s2 = 0; s2 < sg; s2++) rk += seg_T[s2] == T;
-                if (b1 - b0 > 0xFFFFu) atomicOr(P.status, 16u);   // seed_cnt is 16 bits
-                Cand c;
-                c.seed_off = (uint32_t)(sbase + b0);
-                c.q_gtx = iso_gtx[(uint32_t)(k1 >> 57)];
-                c.s_gtx = gtx;
-                c.seed_cnt = (uint16_t)(b1 - b0);
-                c.strand = (uint8_t)((k1 >> 56) & 1);
-                c.pad = 0;
-                const uint32_t qi = (uint32_t)(k1 >> 57);
-                c.q0 = c.strand ? total - iso_start[qi] - (uint64_t)iso_len[qi] : iso_start[qi];
-                const TxInfo st = db.tx[gtx];
-                c.s0 = st.start;
-                c.Lq = (int32_t)iso_len[qi];
-                c.Lt = (int32_t)st.len;
-                c.qsam = Q;
-                c.ssam = st.sample;
-                P.cands[cbase + tpre[T] + rk] = c;
+            // rounds of SBLOCK candidates (uniform: the list2 append is a block scan)
+            for (uint32_t c0 = 0; c0 < nseg; c0 += SBLOCK) {
+                const uint32_t sg = c0 + tid;
+                uint32_t want = 0;
+                uint64_t cslot = 0;
+                if (sg < nseg) {
+                    const uint32_t b0 = seg_begin[sg], b1 = seg_begin[sg + 1];
+                    const uint64_t k1 = seeds[b0].k1;
+                    const uint32_t gtx = (uint32_t)(k1 >> 24);
+                    const int T = seg_T[sg];
+                    uint32_t rk = 0;   // rank among earlier candidates of the same sample
+                    if (T1 - T0 == 1)
+                        rk = sg;
+                    else
+                        for (uint32_t s2 = 0; s2 < sg; s2++) rk += seg_T[s2] == T;
+                    if (b1 - b0 > 0xFFFFu) atomicOr(P.status, 16u);   // seed_cnt is 16 bits
+                    Cand c;
+                    c.seed_off = (uint32_t)(sbase + b0);
+                    c.q_gtx = iso_gtx[(uint32_t)(k1 >> 57)];
+                    c.s_gtx = gtx;
+                    c.seed_cnt = (uint16_t)(b1 - b0);
+                    c.strand = (uint8_t)((k1 >> 56) & 1);
+                    c.dflags = 1;
+                    c.e0 = 0;
+                    c.e1 = SEED_NONE;
+                    if (P.share) {
+                        // each search's first seed: forward (x, y) order is the
+                        // sorted order; reverse order is (y, x) on the plus strand,
+                        // (y + len, x + len) descending on the minus strand (the
+                        // reverse query is the subject's reverse complement there)
+                        int fF = -1, fR = -1;
+                        uint64_t bk = ~0ull;
+                        for (uint32_t i = b0; i < b1; i++) {
+                            const uint32_t sl = seeds[i].len;
+                            if ((sl & SEED_F) && fF < 0) fF = (int)(i - b0);
+                            if (sl & SEED_R) {
+                                const uint32_t sx = (uint32_t)(seeds[i].k1 & 0xFFFFFFull), sy = seeds[i].y, ln = sl & SEED_LEN;
+                                const uint64_t key = c.strand ? ((uint64_t)~(sy + ln) << 32) | (uint32_t)~(sx + ln)
+                                                              : ((uint64_t)sy << 32) | sx;
+                                if (key < bk) {
+                                    bk = key;
+                                    fR = (int)(i - b0);
+                                }
+                            }
+                        }
+                        c.dflags = (uint8_t)((fF >= 0 ? 1 : 0) | (fR >= 0 ? 2 : 0));
+                        c.e0 = (uint16_t)(fF >= 0 ? fF : fR);
+                        c.e1 = (fF >= 0 && fR >= 0 && fR != fF) ? (uint16_t)fR : SEED_NONE;
+                        want = c.e1 != SEED_NONE ? 1u : 0u;
+                    }
+                    const uint32_t qi = (uint32_t)(k1 >> 57);
+                    c.q0 = c.strand ? total - iso_start[qi] - (uint64_t)iso_len[qi] : iso_start[qi];
+                    const TxInfo st = db.tx[gtx];
+                    c.s0 = st.start;
+                    c.Lq = (int32_t)iso_len[qi];
+                    c.Lt = (int32_t)st.len;
+                    c.qsam = (uint16_t)Q;
+                    c.ssam = (uint16_t)st.sample;
+                    cslot = cbase + tpre[T] + rk;
+                    P.cands[cslot] = c;
+                }
+                if (P.share) {
+                    uint32_t tot;
+                    const uint32_t pos = block_exscan(want, wsum, tot);
+                    if (tot) {
+                        if (tid == 0) sh_lbase = atomicAdd(P.list2_n, (unsigned long long)tot);
+                        __syncthreads();
+                        if (want) P.list2[sh_lbase + pos] = (uint32_t)cslot;
+                        __syncthreads();
+                    }
+                }
             }
         }
         for (int T = T0 + tid; T < T1; T += SBLOCK) {
@@ -833,6 +904,104 @@ __device__ __forceinline__ ExtRes ext_wave(const uint32_t *A, const uint32_t *AM
     return best;
 }
 
+// Both extensions of one seed (x, y, len): right from its end, left from its
+// start. swap (spec 4b): the query is the higher-numbered sample, so the
+// greedy primitive runs with the subject in the first role and its end
+// point is swapped back.
+template <bool AMB, typename PT>
+__device__ __forceinline__ void extend_seed(const uint32_t *QO, const uint32_t *QOM, PT qo, const uint32_t *TF,
+                                            const uint32_t *TFM, PT tf, int Lq, int Lt, int x, int y, int len, int X,
+                                            int lane, uint32_t &steps, uint32_t &eg, bool swap, ExtRes &r, ExtRes &l)
+{
+    if (!swap) {
+        r = ext_wave<AMB, false, PT>(QO, QOM, qo + (PT)(x + len), Lq - (x + len), TF, TFM, tf + (PT)(y + len),
+                                     Lt - (y + len), X, lane, steps, eg);
+        l = ext_wave<AMB, true, PT>(QO, QOM, qo + (PT)x, x, TF, TFM, tf + (PT)y, y, X, lane, steps, eg);
+    } else {
+        r = ext_wave<AMB, false, PT>(TF, TFM, tf + (PT)(y + len), Lt - (y + len), QO, QOM, qo + (PT)(x + len),
+                                     Lq - (x + len), X, lane, steps, eg);
+        l = ext_wave<AMB, true, PT>(TF, TFM, tf + (PT)y, y, QO, QOM, qo + (PT)x, x, X, lane, steps, eg);
+        int t = r.i;
+        r.i = r.j;
+        r.j = t;
+        t = l.i;
+        l.i = l.j;
+        l.j = t;
+    }
+}
+
+// Shared searches: one directed search of a candidate on one wave, in the
+// forward search's coordinates (query = the lower sample, which is also the
+// first role of spec 4b). The search's seeds (dbit) are taken in ITS order
+// -- forward: (x, y); reverse: (y, x) on the plus strand, (y + len, x + len)
+// descending on the minus strand -- by selection: the next seed extended is
+// the first in that order outside every box so far (a seed inside a box
+// stays inside as boxes are added, so this is the sequential rule of spec 3).
+template <bool AMB, typename PT>
+__device__ __forceinline__ void process_search(const uint32_t *QO, const uint32_t *QOM, PT qo, const uint32_t *TF,
+                                               const uint32_t *TFM, PT tf, int Lq, int Lt, const GSeed *sd, int ns,
+                                               int X, int lane, uint32_t dbit, int strand, int &bqa, int &bqb,
+                                               int &bsa, int &bsb, int &bsc, int &bd, int &bg, int &bo, int &bni,
+                                               int &nh, uint32_t &steps, uint32_t &exts, uint32_t &edges,
+                                               uint32_t &capped)
+{
+    nh = 0;
+    for (;;) {
+        unsigned long long bk = ~0ull;
+        int bi = 0;
+        for (int c0 = 0; c0 < ns; c0 += 64) {
+            const int i = c0 + lane;
+            if (i >= ns) continue;
+            const GSeed g = sd[i];
+            if (!(g.len & dbit)) continue;
+            const uint32_t x = g.x, y = g.y, len = g.len & SEED_LEN;
+            bool in = false;
+            for (int h = 0; h < nh; h++) {
+                const int qa = __builtin_amdgcn_readlane(bqa, h), qb = __builtin_amdgcn_readlane(bqb, h);
+                const int sa = __builtin_amdgcn_readlane(bsa, h), sb = __builtin_amdgcn_readlane(bsb, h);
+                in = in || (qa <= (int)x && (int)(x + len) <= qb && sa <= (int)y && (int)(y + len) <= sb);
+            }
+            if (in) continue;
+            const unsigned long long key =
+                dbit == SEED_F ? ((unsigned long long)x << 32) | y
+                               : (strand ? ((unsigned long long)(uint32_t)~(y + len) << 32) | (uint32_t)~(x + len)
+                                         : ((unsigned long long)y << 32) | x);
+            if (key < bk) {
+                bk = key;
+                bi = i;
+            }
+        }
+        unsigned long long m = bk;
+        for (int o = 32; o; o >>= 1) {
+            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(m >> 32), o);
+            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)m, o);
+            const unsigned long long v = ((unsigned long long)hi << 32) | lo;
+            m = v < m ? v : m;
+        }
+        if (m == ~0ull) break;
+        if (nh >= MAX_HSP) {   // MAX_HSP binds (spec 3): a seed outside every box remains
+            capped++;
+            break;
+        }
+        const int src = __ffsll((unsigned long long)__ballot(bk == m)) - 1;
+        const int si = __shfl(bi, src);
+        const GSeed g = sd[si];
+        const int x = (int)g.x, y = (int)g.y, len = (int)(g.len & SEED_LEN);
+        uint32_t eg = 0;
+        ExtRes r, l;
+        extend_seed<AMB, PT>(QO, QOM, qo, TF, TFM, tf, Lq, Lt, x, y, len, X, lane, steps, eg, false, r, l);
+        exts += 2;
+        edges += eg;
+        if (lane == nh) {
+            bqa = x - l.i; bqb = x + len + r.i; bsa = y - l.j; bsb = y + len + r.j;
+            bsc = l.score + 2 * len + r.score;
+            bd = l.d + r.d; bg = l.g + r.g; bo = l.o + r.o;
+            bni = len + (l.i + l.j - 2 * l.d + l.g) / 2 + (r.i + r.j - 2 * r.d + r.g) / 2;
+        }
+        nh++;
+    }
+}
+
 // One candidate (all its seeds) on one wave. QO: oriented query (its base u at
 // qo + u), TF: subject forward (base v at tf + v); right extensions walk
 // forward from the seed end, left extensions backwards from the seed start.
@@ -841,7 +1010,8 @@ __device__ __forceinline__ void process_candidate(const uint32_t *QO, const uint
                                                   const uint32_t *TFM, PT tf, int Lq, int Lt, const GSeed *sd,
                                                   int ns, int X, int lane, int &bqa, int &bqb, int &bsa, int &bsb,
                                                   int &bsc, int &bd, int &bg, int &bo, int &bni, int &nh,
-                                                  uint32_t &steps, uint32_t &exts, uint32_t &edges, uint32_t &capped)
+                                                  uint32_t &steps, uint32_t &exts, uint32_t &edges, uint32_t &capped,
+                                                  bool swap)
 {
     nh = 0;
     int next = ns;   // the first seed not examined (MAX_HSP reached before it)
@@ -852,7 +1022,7 @@ __device__ __forceinline__ void process_candidate(const uint32_t *QO, const uint
             const GSeed g = sd[c0 + lane];
             sx = (int)g.x;
             sy = (int)g.y;
-            sl = (int)g.len;
+            sl = (int)(g.len & SEED_LEN);
         }
         const int nc = min(ns - c0, 64);
         for (int si = 0; si < nc; si++) {
@@ -865,10 +1035,8 @@ __device__ __forceinline__ void process_candidate(const uint32_t *QO, const uint
             const bool inside = lane < nh && bqa <= x && x + len <= bqb && bsa <= y && y + len <= bsb;
             if (__ballot(inside)) continue;
             uint32_t eg = 0;
-            const ExtRes r = ext_wave<AMB, false, PT>(QO, QOM, qo + (PT)(x + len), Lq - (x + len), TF, TFM,
-                                                      tf + (PT)(y + len), Lt - (y + len), X, lane, steps, eg);
-            const ExtRes l = ext_wave<AMB, true, PT>(QO, QOM, qo + (PT)x, x, TF, TFM, tf + (PT)y, y, X, lane,
-                                                     steps, eg);
+            ExtRes r, l;
+            extend_seed<AMB, PT>(QO, QOM, qo, TF, TFM, tf, Lq, Lt, x, y, len, X, lane, steps, eg, swap, r, l);
             exts += 2;
             edges += eg;
             if (lane == nh) {
@@ -883,7 +1051,7 @@ __device__ __forceinline__ void process_candidate(const uint32_t *QO, const uint
     // MAX_HSP binds (spec 3) when a seed past the cap lies outside every box
     for (int i = next; i < ns; i++) {
         const GSeed g = sd[i];
-        const int x = (int)g.x, y = (int)g.y, len = (int)g.len;
+        const int x = (int)g.x, y = (int)g.y, len = (int)(g.len & SEED_LEN);
         if (!__ballot(lane < nh && bqa <= x && x + len <= bqb && bsa <= y && y + len <= bsb)) {
             capped++;
             break;
@@ -941,6 +1109,10 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
         const uint64_t *QA = strand ? db.RC : db.F;
         const uint64_t *QAM = strand ? db.ARC : db.AF;
         const uint64_t q0 = strand ? total - qt.start - (uint64_t)Lq : qt.start;
+        // spec 4b: the lower-numbered sample in the greedy's first role
+        const bool swap = qt.sample > st.sample;
+        // shared searches: this work item is one directed search of the candidate
+        const uint32_t dbit = P.dir ? SEED_R : SEED_F;
         if (Lq + SPAD <= STAGE_BASES && Lt + SPAD <= STAGE_BASES) {
             uint64_t *QO = stg[wid][0], *TF = stg[wid][1];
             stage_seq(QO, QA, q0, Lq, lane);
@@ -954,10 +1126,23 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
             }
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            process_candidate<AMB, uint32_t>(reinterpret_cast<const uint32_t *>(QO), QOM, (uint32_t)SPAD,
-                                             reinterpret_cast<const uint32_t *>(TF), TFM, (uint32_t)SPAD, Lq, Lt, sd,
-                                             ns, P.xdrop, lane, bqa, bqb, bsa, bsb, bsc, bd, bg, bo, bni, nh, steps,
-                                             exts, edges, capped);
+            if (P.share)
+                process_search<AMB, uint32_t>(reinterpret_cast<const uint32_t *>(QO), QOM, (uint32_t)SPAD,
+                                              reinterpret_cast<const uint32_t *>(TF), TFM, (uint32_t)SPAD, Lq, Lt,
+                                              sd, ns, P.xdrop, lane, dbit, strand, bqa, bqb, bsa, bsb, bsc, bd, bg,
+                                              bo, bni, nh, steps, exts, edges, capped);
+            else
+                process_candidate<AMB, uint32_t>(reinterpret_cast<const uint32_t *>(QO), QOM, (uint32_t)SPAD,
+                                                 reinterpret_cast<const uint32_t *>(TF), TFM, (uint32_t)SPAD, Lq, Lt,
+                                                 sd, ns, P.xdrop, lane, bqa, bqb, bsa, bsb, bsc, bd, bg, bo, bni, nh,
+                                                 steps, exts, edges, capped, swap);
+        } else if (P.share) {
+            process_search<AMB, int64_t>(reinterpret_cast<const uint32_t *>(QA),
+                                         reinterpret_cast<const uint32_t *>(QAM), (int64_t)q0,
+                                         reinterpret_cast<const uint32_t *>(db.F),
+                                         reinterpret_cast<const uint32_t *>(db.AF), (int64_t)st.start, Lq, Lt, sd,
+                                         ns, P.xdrop, lane, dbit, strand, bqa, bqb, bsa, bsb, bsc, bd, bg, bo, bni,
+                                         nh, steps, exts, edges, capped);
         } else {
             // global arrays carry two zero words in front, so backward windows
             // of the first transcript stay in bounds (positions may go to -32)
@@ -966,7 +1151,7 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
                                             reinterpret_cast<const uint32_t *>(db.F),
                                             reinterpret_cast<const uint32_t *>(db.AF), (int64_t)st.start, Lq, Lt,
                                             sd, ns, P.xdrop, lane, bqa, bqb, bsa, bsb, bsc, bd, bg, bo, bni, nh,
-                                            steps, exts, edges, capped);
+                                            steps, exts, edges, capped, swap);
         }
         // purge HSPs with common endpoints: by (score desc, index asc)
         int rank = 0;
@@ -987,7 +1172,9 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
         // DB) and the mirrored one (subject length, query sample's DB)
         const int thr_f = P.thr[(size_t)st.sample * (size_t)(P.max_len + 1) + (size_t)Lq];
         const int thr_r = P.thr[(size_t)qt.sample * (size_t)(P.max_len + 1) + (size_t)Lt];
-        const bool pf = bsc >= thr_f, pr = P.sym && bsc >= thr_r;
+        // shared searches: the forward item applies the forward cut, the
+        // reverse item the reverse one (its records go to the _r arrays)
+        const bool pf = (!P.share || !P.dir) && bsc >= thr_f, pr = (P.sym || (P.share && P.dir)) && bsc >= thr_r;
         const bool out = kept && (pf || pr);
         const uint64_t om = __ballot(out);
         const int nout = __popcll(om);
@@ -1016,12 +1203,12 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
             h.score_half = bsc;
             h.bits10 = P.bits10[bsc];
             h.strand = strand | (pf ? HSP_FWD : 0) | (pr ? HSP_REV : 0) | (lane << HSP_IDX_SHIFT);
-            if (rk == 0) P.cand_hsp[ci] = h;
+            if (rk == 0) (P.share && P.dir ? P.cand_hsp_r : P.cand_hsp)[ci] = h;
             else if ((uint64_t)obase + (rk - 1) < P.ovf_cap) P.ovf[obase + rk - 1] = h;
         }
         if (lane == 0) {
-            P.cand_nh[ci] = (uint8_t)nout;
-            P.cand_ovf[ci] = obase;
+            (P.share && P.dir ? P.cand_nh_r : P.cand_nh)[ci] = (uint8_t)nout;
+            (P.share && P.dir ? P.cand_ovf_r : P.cand_ovf)[ci] = obase;
         }
     }
     if (lane == 0 && P.counters) {
@@ -1195,7 +1382,7 @@ enum { RM_REC = 0, RM_CLO = CAND_DWORDS, RM_CHI, RM_QB, RM_TB, RM_X, RM_Y, RM_LE
        RM_RSC, RM_RI, RM_RJ, RM_RD, RM_RGO, RM_N };
 // fields of the record (dword offsets, layout of Cand)
 enum { RC_SOFF = 0, RC_QTX = 1, RC_STX = 2, RC_CNT_STRAND = 3, RC_Q0 = 4, RC_S0 = 6, RC_LQ = 8, RC_LT = 9,
-       RC_QSAM = 10, RC_SSAM = 11 };
+       RC_SAMS = 10, RC_E01 = 11 };
 // work cursors of a row
 enum { RS_LEND, RS_SHARD, RS_SHN, RS_N };
 // row actions (transition actions < A_DONE; extending: A_STEP_R / A_STEP_L = their done action + 4)
@@ -1269,11 +1456,16 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
         if (l >= ncand || rl >= CAND_DWORDS) return 0;
         return reinterpret_cast<const int *>(P.cands + cslot(l, RS_SHN))[rl];
     };
+    // this pass's first-seed results (shared searches: pass 1 -> cand_box,
+    // pass 2 over list2 -> cand_box2)
+    int32_t *const box_out = P.which ? P.cand_box2 : P.cand_box;
     auto defer = [&](uint64_t ci) {   // row-uniform; extend_kernel takes the candidate whole
         if (rl == 0) {
-            const unsigned long long di = atomicAdd(P.defer_count, 1ull);
-            P.defer[di] = (uint32_t)ci;
-            P.cand_box[ci * BOX_REC + FX_STATUS] = -1;
+            if (!P.share) {   // shared searches: first_finish_kernel lists each search on its own
+                const unsigned long long di = atomicAdd(P.defer_count, 1ull);
+                P.defer[di] = (uint32_t)ci;
+            }
+            box_out[ci * BOX_REC + FX_STATUS] = -1;
         }
     };
     if (rl == 0) {
@@ -1288,6 +1480,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
     int R = -1, goe = 0, wi = 0, wg = 0, wd = 0, best = 0, bl = RC0, d6 = 0;   // d6 = 6 x greedy step
     uint32_t pa = 0, pb = 0;
     int alen = 0, blen = 0;
+    bool swap = false;                                    // spec 4b: query = the higher-numbered sample
     unsigned long long steps = 0;                         // row steps (wave-uniform count)
 
     auto ext_init = [&](int done_act) {
@@ -1358,7 +1551,8 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                 const uint64_t *QA = strand ? db.RC : db.F;
                 const uint64_t *qw = QA + (q0 >> 5), *tw = db.F + (s0 >> 5);
                 {
-                    const GSeed g0 = P.seeds[(uint32_t)meta[RM_REC + RC_SOFF]];
+                    const uint32_t e01 = (uint32_t)meta[RM_REC + RC_E01];
+                    const GSeed g0 = P.seeds[(uint32_t)meta[RM_REC + RC_SOFF] + (P.which ? e01 >> 16 : e01 & 0xFFFFu)];
                     const uint64_t a0 = rl < nwq ? qw[rl] : 0ull, a1 = rl + RW < nwq ? qw[rl + RW] : 0ull;
                     const uint64_t b0 = rl < nwt ? tw[rl] : 0ull, b1 = rl + RW < nwt ? tw[rl + RW] : 0ull;
                     if (rl < nwq) stg[rl] = a0;
@@ -1368,7 +1562,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                     if (rl == 0) {
                         meta[RM_X] = (int)g0.x;
                         meta[RM_Y] = (int)g0.y;
-                        meta[RM_LEN] = (int)g0.len;
+                        meta[RM_LEN] = (int)(g0.len & SEED_LEN);
                     }
                 }
                 for (int w = rl + 2 * RW; w < nwq; w += RW) stg[w] = qw[w];
@@ -1396,15 +1590,25 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                 if (rl == 0) atomicAdd(&rcnt[1], 1u);
                 // right extension from the seed's end
                 const int x = meta[RM_X], y = meta[RM_Y], len = meta[RM_LEN];
+                const uint32_t sams = (uint32_t)meta[RM_REC + RC_SAMS];
+                swap = (sams & 0xFFFFu) > (sams >> 16);
                 pa = qb + (uint32_t)(x + len);
                 alen = Lq - (x + len);
                 pb = tb + (uint32_t)(y + len);
                 blen = Lt - (y + len);
+                if (swap) {
+                    const uint32_t t = pa; pa = pb; pb = t;
+                    const int u = alen; alen = blen; blen = u;
+                }
                 ext_init(A_RDONE);
             } else if (act == A_RDONE || act == A_LDONE) {
                 const int src = RW * row + bl;
-                const int ei = __shfl(wi, src), ed = __shfl(wd, src) / 6, ego = __shfl(wg, src);
-                const int ej = ei - (bl - RC0);
+                int ei = __shfl(wi, src);
+                const int ed = __shfl(wd, src) / 6, ego = __shfl(wg, src);
+                int ej = ei - (bl - RC0);
+                if (swap) {
+                    const int t = ei; ei = ej; ej = t;
+                }
                 if (act == A_RDONE) {
                     if (rl == 0) {
                         meta[RM_RSC] = best;
@@ -1421,6 +1625,10 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                     alen = x;
                     pb = btr + (uint32_t)(Lt - y);
                     blen = y;
+                    if (swap) {
+                        const uint32_t t = pa; pa = pb; pb = t;
+                        const int u = alen; alen = blen; blen = u;
+                    }
                     ext_init(A_LDONE);
                 } else {
                     // both results of the first seed: first_finish_kernel builds the box
@@ -1432,7 +1640,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                     if (rl == FX_L + 2) v = ej;
                     if (rl == FX_L + 3) v = ed;
                     if (rl == FX_L + 4) v = ego;
-                    if (rl < BOX_REC) P.cand_box[ci * BOX_REC + rl] = v;
+                    if (rl < BOX_REC) box_out[ci * BOX_REC + rl] = v;
                     act = A_FETCH;
                 }
             } else {   // A_ABORT: the sub-band overflowed
@@ -1549,51 +1757,79 @@ __global__ __launch_bounds__(256) void first_finish_kernel(ExtParams P)
             if (P.shard_prefix[mid] <= li) lo = mid; else hi = mid;
         }
         const uint64_t ci = (uint64_t)lo * P.cand_cap + (li - P.shard_prefix[lo]);
-        const int *fx = P.cand_box + ci * BOX_REC;
-        if (fx[FX_STATUS] < 0) continue;   // deferred by the row kernel
+        if (!P.share && P.cand_box[ci * BOX_REC + FX_STATUS] < 0) continue;   // deferred by the row kernel
         const Cand cd = P.cands[ci];
-        const GSeed s0 = P.seeds[cd.seed_off];
-        const int x = (int)s0.x, y = (int)s0.y, len = (int)s0.len;
-        const int rsc = fx[FX_R], ri = fx[FX_R + 1], rj = fx[FX_R + 2], rd = fx[FX_R + 3], rgo = fx[FX_R + 4];
-        const int lsc = fx[FX_L], lI = fx[FX_L + 1], lJ = fx[FX_L + 2], ld = fx[FX_L + 3], lgo = fx[FX_L + 4];
-        const int lg = lgo & GMASK, lo2 = (lgo >> OBIT) & GMASK, rg = rgo & GMASK, ro = (rgo >> OBIT) & GMASK;
-        const int bqa = x - lI, bqb = x + len + ri, bsa = y - lJ, bsb = y + len + rj;
-        bool all_in = true;
-        for (uint32_t i = 1; i < cd.seed_cnt && all_in; i++) {
-            const GSeed s = P.seeds[cd.seed_off + i];
-            all_in = bqa <= (int)s.x && (int)(s.x + s.len) <= bqb && bsa <= (int)s.y && (int)(s.y + s.len) <= bsb;
-        }
-        if (!all_in) {
-            const unsigned long long di = atomicAdd(P.defer_count, 1ull);
-            P.defer[di] = (uint32_t)ci;
-            continue;
-        }
-        const int bsc = lsc + 2 * len + rsc, bd = ld + rd, bg = lg + rg, bo = lo2 + ro;
-        const int bni = len + (lI + lJ - 2 * ld + lg) / 2 + (ri + rj - 2 * rd + rg) / 2;
-        const int thr_f = P.thr[(size_t)cd.ssam * (size_t)(P.max_len + 1) + (size_t)cd.Lq];
-        const int thr_r = P.thr[(size_t)cd.qsam * (size_t)(P.max_len + 1) + (size_t)cd.Lt];
-        const bool pf = bsc >= thr_f, pr = P.sym && bsc >= thr_r;
-        if (pf || pr) {
-            DHsp h;
-            h.q_tx = cd.q_gtx;
-            h.s_tx = cd.s_gtx;
-            if (!cd.strand) {
-                h.qstart = bqa + 1; h.qend = bqb; h.sstart = bsa + 1; h.send = bsb;
-            } else {
-                h.qstart = cd.Lq - bqb + 1; h.qend = cd.Lq - bqa; h.sstart = bsb; h.send = bsa + 1;
+        // shared searches: each directed search of the candidate on its own --
+        // its first seed's box (cand_box, or cand_box2 when the reverse
+        // search's first seed is another seed), its own seeds, its own cut
+        const int ndir = P.share ? 2 : 1;
+        for (int dir = 0; dir < ndir; dir++) {
+            DHsp *const hsp_out = dir ? P.cand_hsp_r : P.cand_hsp;
+            uint8_t *const nh_out = dir ? P.cand_nh_r : P.cand_nh;
+            uint32_t *const ovf_out = dir ? P.cand_ovf_r : P.cand_ovf;
+            if (P.share && !((cd.dflags >> dir) & 1)) {   // this search found no seed here
+                nh_out[ci] = 0;
+                ovf_out[ci] = 0;
+                continue;
             }
-            h.gaps = bg;
-            h.gapopen = bo;
-            h.mismatch = bd - bg;
-            h.nident = bni;
-            h.length = bni + bd;
-            h.score_half = bsc;
-            h.bits10 = P.bits10[bsc];
-            h.strand = cd.strand | (pf ? HSP_FWD : 0) | (pr ? HSP_REV : 0);
-            P.cand_hsp[ci] = h;
+            const bool second = dir == 1 && cd.e1 != SEED_NONE;
+            const int *fx = (second ? P.cand_box2 : P.cand_box) + ci * BOX_REC;
+            const uint32_t dbit = !P.share ? 0u : (dir ? SEED_R : SEED_F);
+            auto defer_dir = [&]() {
+                const unsigned long long di = atomicAdd(dir ? P.defer_r_count : P.defer_count, 1ull);
+                (dir ? P.defer_r : P.defer)[di] = (uint32_t)ci;
+            };
+            if (fx[FX_STATUS] < 0) {   // (shared searches) the row kernel gave it up
+                defer_dir();
+                continue;
+            }
+            const uint32_t e = second ? cd.e1 : cd.e0;
+            const GSeed s0 = P.seeds[cd.seed_off + e];
+            const int x = (int)s0.x, y = (int)s0.y, len = (int)(s0.len & SEED_LEN);
+            const int rsc = fx[FX_R], ri = fx[FX_R + 1], rj = fx[FX_R + 2], rd = fx[FX_R + 3], rgo = fx[FX_R + 4];
+            const int lsc = fx[FX_L], lI = fx[FX_L + 1], lJ = fx[FX_L + 2], ld = fx[FX_L + 3], lgo = fx[FX_L + 4];
+            const int lg = lgo & GMASK, lo2 = (lgo >> OBIT) & GMASK, rg = rgo & GMASK, ro = (rgo >> OBIT) & GMASK;
+            const int bqa = x - lI, bqb = x + len + ri, bsa = y - lJ, bsb = y + len + rj;
+            bool all_in = true;
+            for (uint32_t i = 0; i < cd.seed_cnt && all_in; i++) {
+                if (i == e) continue;
+                const GSeed s = P.seeds[cd.seed_off + i];
+                if (dbit && !(s.len & dbit)) continue;
+                const int sl = (int)(s.len & SEED_LEN);
+                all_in = bqa <= (int)s.x && (int)s.x + sl <= bqb && bsa <= (int)s.y && (int)s.y + sl <= bsb;
+            }
+            if (!all_in) {
+                defer_dir();
+                continue;
+            }
+            const int bsc = lsc + 2 * len + rsc, bd = ld + rd, bg = lg + rg, bo = lo2 + ro;
+            const int bni = len + (lI + lJ - 2 * ld + lg) / 2 + (ri + rj - 2 * rd + rg) / 2;
+            const int thr_f = P.thr[(size_t)cd.ssam * (size_t)(P.max_len + 1) + (size_t)cd.Lq];
+            const int thr_r = P.thr[(size_t)cd.qsam * (size_t)(P.max_len + 1) + (size_t)cd.Lt];
+            const bool pf = (!P.share || dir == 0) && bsc >= thr_f;
+            const bool pr = (P.sym || (P.share && dir == 1)) && bsc >= thr_r;
+            if (pf || pr) {
+                DHsp h;
+                h.q_tx = cd.q_gtx;
+                h.s_tx = cd.s_gtx;
+                if (!cd.strand) {
+                    h.qstart = bqa + 1; h.qend = bqb; h.sstart = bsa + 1; h.send = bsb;
+                } else {
+                    h.qstart = cd.Lq - bqb + 1; h.qend = cd.Lq - bqa; h.sstart = bsb; h.send = bsa + 1;
+                }
+                h.gaps = bg;
+                h.gapopen = bo;
+                h.mismatch = bd - bg;
+                h.nident = bni;
+                h.length = bni + bd;
+                h.score_half = bsc;
+                h.bits10 = P.bits10[bsc];
+                h.strand = cd.strand | (pf ? HSP_FWD : 0) | (pr ? HSP_REV : 0);
+                hsp_out[ci] = h;
+            }
+            nh_out[ci] = (uint8_t)((pf || pr) ? 1 : 0);
+            ovf_out[ci] = 0;
         }
-        P.cand_nh[ci] = (uint8_t)((pf || pr) ? 1 : 0);
-        P.cand_ovf[ci] = 0;
     }
 }
 
@@ -1804,6 +2040,38 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
     } while (0)
     const char *mwv = getenv("RC_ROW_WAVES");
     const int mw = mwv ? atoi(mwv) : ROW_MIN_WAVES;
+    if (P.share) {
+        // shared searches: first seeds e0 over every candidate, then e1 over
+        // list2 (reverse searches whose first seed is another seed), then each
+        // directed search checked (or listed for extend_kernel) on its own
+        W.which = 0;
+        if (amb) RC_LAUNCH_ROWS(true, 32, ROW_MIN_WAVES, W); else RC_LAUNCH_ROWS(false, 32, ROW_MIN_WAVES, W);
+        ExtParams W2 = W;
+        W2.which = 1;
+        W2.list = P.list2;
+        W2.list_n = P.list2_n;
+        W2.work = P.work3;
+        if (amb) RC_LAUNCH_ROWS(true, 32, ROW_MIN_WAVES, W2); else RC_LAUNCH_ROWS(false, 32, ROW_MIN_WAVES, W2);
+        uint64_t g = (P.n_cand + 255) / 256;
+        if (g > 65536) g = 65536;
+        hipLaunchKernelGGL(first_finish_kernel, dim3((unsigned)g), dim3(256), 0, st, W);
+        for (int dir = 0; dir < 2; dir++) {
+            ExtParams W3 = W;
+            W3.dir = dir;
+            if (dir) {
+                W3.defer = P.defer_r;
+                W3.defer_count = P.defer_r_count;
+            }
+            if (amb) {
+                auto kern = extend_kernel<true>;
+                hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W3);
+            } else {
+                auto kern = extend_kernel<false>;
+                hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W3);
+            }
+        }
+        return;
+    }
     // pass 1: 16- or 32-diagonal rows over every candidate
     if (rw == 16) {
         if (amb) RC_LAUNCH_ROWS(true, 16, ROW_MIN_WAVES, W); else RC_LAUNCH_ROWS(false, 16, ROW_MIN_WAVES, W);

@@ -99,8 +99,12 @@ constexpr int NSHARD = 256;    // output allocation shards (spread the atomics)
 
 // Seed (maximal exact run >= W) of one candidate, oriented query coordinates.
 struct GSeed {
-    uint32_t x, y, len;
+    uint32_t x, y, len;   // len: bits 0-29; shared searches: SEED_F / SEED_R in bits 30, 31
 };
+// Shared searches (RC_SHARE): the directed searches a seed belongs to (it
+// holds a usable word of that search's query: spec 1, 1b, 2)
+constexpr uint32_t SEED_F = 1u << 30, SEED_R = 1u << 31, SEED_LEN = SEED_F - 1u;
+constexpr uint16_t SEED_NONE = 0xFFFFu;
 
 // Candidate = (query transcript, strand, subject transcript) with >= 1 seed.
 // Self-contained (48 B): the extension reads one record, no transcript table.
@@ -108,11 +112,17 @@ struct Cand {
     uint32_t seed_off;     // absolute index of its first seed (sorted by (x, y))
     uint32_t q_gtx, s_gtx;
     uint16_t seed_cnt;
-    uint8_t strand, pad;
+    uint8_t strand;
+    uint8_t dflags;        // shared searches: bit 0 the forward search has seeds, bit 1 the reverse one
     uint64_t q0;           // first base of the oriented query: in F (strand 0) or RC (strand 1)
     uint64_t s0;           // first base of the subject in F
     int32_t Lq, Lt;        // transcript lengths
-    int32_t qsam, ssam;    // samples of query and subject
+    uint16_t qsam, ssam;   // samples of query and subject
+    // seeds (indices in the candidate) the row kernel extends first: e0 into
+    // cand_box (the forward search's first seed, or the reverse one's when the
+    // forward search has none), e1 into cand_box2 (the reverse search's first
+    // seed when it is another seed; SEED_NONE otherwise)
+    uint16_t e0, e1;
 };
 constexpr int CAND_DWORDS = (int)(sizeof(Cand) / 4);
 static_assert(sizeof(Cand) == 48, "Cand is read as 12 dwords");
@@ -129,6 +139,10 @@ struct SeedParams {
     int32_t stride;               // W - 16 + 1
     int32_t pre_mode;             // canonical pre-test: 1 = previous word's hits (LDS), 0 = sequence windows
     int32_t sym;                  // spec 5b: subjects are higher-numbered samples only
+    int32_t share;                // shared searches: query = lower sample, seeds carry SEED_F / SEED_R
+    const uint64_t *dmask;        // shared searches: the DUST mask (db.dmask is then left out of lookups)
+    uint32_t *list2;              // shared searches: slots of the candidates with e1 != SEED_NONE
+    unsigned long long *list2_n;
     uint32_t gene_begin, gene_end;   // shard
     GSeed *seeds;
     uint64_t seed_cap;            // per allocation shard
@@ -187,6 +201,20 @@ struct ExtParams {
     uint32_t *defer2;                   // the 64-lane pass's deferrals (-> extend_kernel)
     unsigned long long *defer2_count;
     unsigned long long *work2;
+    // shared searches (RC_SHARE): one candidate set serves both directed
+    // searches of a pair; the reverse search's HSPs go to the _r arrays
+    int32_t share;
+    int32_t which;                      // row kernel: 0 seed e0 -> cand_box, 1 seed e1 -> cand_box2
+    int32_t dir;                        // extend_kernel: 0 forward search, 1 reverse search
+    int32_t *cand_box2;
+    DHsp *cand_hsp_r;
+    uint8_t *cand_nh_r;
+    uint32_t *cand_ovf_r;
+    uint32_t *defer_r;                  // first_finish_kernel: the reverse searches extend_kernel redoes
+    unsigned long long *defer_r_count;
+    const uint32_t *list2;              // candidates with e1 != SEED_NONE (the seed kernel's list)
+    const unsigned long long *list2_n;
+    unsigned long long *work3;          // work counter of the row kernel's pass over list2
 };
 
 // DHsp.strand carries, besides the strand (bit 0), the direction flags of a

@@ -295,7 +295,12 @@ struct rc_engine {
     DBuf<Cand> d_cands;
     DBuf<DHsp> d_cand_hsp, d_ovf;
     DBuf<uint8_t> d_cand_nh;
-    DBuf<int32_t> d_cand_box;
+    DBuf<int32_t> d_cand_box, d_cand_box2;
+    // shared searches (RC_SHARE, default): the reverse search's HSPs per candidate
+    DBuf<DHsp> d_cand_hsp_r;
+    DBuf<uint8_t> d_cand_nh_r;
+    DBuf<uint32_t> d_cand_ovf_r, d_defer_r, d_list2;
+    bool share = false;
     DBuf<DRow> d_rows_tmp;
     DBuf<DEdge> d_edges_tmp;
     DBuf<uint32_t> d_cand_ovf, d_gc_off, d_gc_cnt, d_gcount, d_defer, d_defer2;
@@ -1011,7 +1016,7 @@ static void tile_plan(rc_engine *e, int ti, std::vector<uint64_t> &tmask, std::v
         const int a = pr.first, b = pr.second;
         tmask[4 * a + (b >> 6)] |= 1ull << (b & 63);
         q[a] = 1;
-        if (!e->o.symmetric) {   // the pair's second directed search: query b, subject a
+        if (!e->o.symmetric && !e->share) {   // the pair's second directed search: query b, subject a
             tmask[4 * b + (a >> 6)] |= 1ull << (a & 63);
             q[b] = 1;
         }
@@ -1143,6 +1148,12 @@ static int align_tile(rc_engine *e, int ti)
 
     std::vector<uint64_t> tmask;
     std::vector<std::pair<int, int>> runs;
+    {
+        // both directed searches of a pair from one candidate set (query =
+        // the lower sample); RC_SHARE=0 runs them one by one
+        const char *sv = getenv("RC_SHARE");
+        e->share = !e->o.symmetric && !(sv && atoi(sv) == 0);
+    }
     tile_plan(e, ti, tmask, runs);
     CHK(e->d_tmask.ensure(tmask.size()));
     HIPCHK(hipMemcpyAsync(e->d_tmask.p, tmask.data(), tmask.size() * 8, hipMemcpyHostToDevice, e->st));
@@ -1176,7 +1187,7 @@ static int align_tile(rc_engine *e, int ti)
     ix.bits = e->index_bits;
     // --- seeds ---
     std::vector<unsigned long long> shard_cnt(2 * NSHARD);
-    CHK(e->d_count.ensure(16));
+    CHK(e->d_count.ensure(24));
     unsigned long long *big_n = e->d_count.p + 12, *big_retry_n = e->d_count.p + 13;
     uint64_t n_big = 0;
     HIPCHK(hipEventRecord(e->ev[3], e->st));
@@ -1186,6 +1197,8 @@ static int align_tile(rc_engine *e, int ti)
             return fail(RC_E_LIMIT, "more than 2^32 seeds or candidates in a tile: use more shards or smaller tiles");
         CHK(e->d_seeds.ensure(e->seed_cap * NSHARD));
         CHK(e->d_cands.ensure(e->cand_cap * NSHARD));
+        if (e->share) CHK(e->d_list2.ensure(e->cand_cap * NSHARD));
+        HIPCHK(hipMemsetAsync(e->d_count.p + 16, 0, sizeof(unsigned long long), e->st));
         CHK(e->d_big_out.ensure(e->big_list_cap));
         HIPCHK(hipMemsetAsync(e->d_shard_cnt.p, 0, 2 * NSHARD * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
@@ -1204,6 +1217,10 @@ static int align_tile(rc_engine *e, int ti)
                 S.pre_mode = pm ? atoi(pm) : 1;
             }
             S.sym = e->o.symmetric;
+            S.share = e->share ? 1 : 0;
+            S.dmask = e->o.dust_level > 0 ? e->d_dmask.p + 1 : nullptr;
+            S.list2 = e->d_list2.p;
+            S.list2_n = e->d_count.p + 16;
             S.gene_begin = rg0[r];
             S.gene_end = rg1[r];
             S.seeds = e->d_seeds.p;
@@ -1304,6 +1321,13 @@ static int align_tile(rc_engine *e, int ti)
     CHK(e->d_cand_nh.ensure(slots));
     CHK(e->d_cand_ovf.ensure(slots));
     CHK(e->d_cand_box.ensure(slots * BOX_REC));
+    if (e->share) {
+        CHK(e->d_cand_box2.ensure(slots * BOX_REC));
+        CHK(e->d_cand_hsp_r.ensure(slots));
+        CHK(e->d_cand_nh_r.ensure(slots));
+        CHK(e->d_cand_ovf_r.ensure(slots));
+        CHK(e->d_defer_r.ensure(std::max<uint64_t>(n_cand, 1)));
+    }
     CHK(e->d_defer.ensure(std::max<uint64_t>(n_cand, 1)));
     CHK(e->d_defer2.ensure(std::max<uint64_t>(n_cand, 1)));
     for (int attempt = 0;; attempt++) {
@@ -1311,8 +1335,9 @@ static int align_tile(rc_engine *e, int ti)
         CHK(e->d_ovf.ensure(e->ovf_cap));
         HIPCHK(hipMemsetAsync(e->d_count.p, 0, 12 * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_count.p + 14, 0, 2 * sizeof(unsigned long long), e->st));
+        HIPCHK(hipMemsetAsync(e->d_count.p + 17, 0, 2 * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
-        ExtParams X;
+        ExtParams X{};
         X.xdrop = e->o.xdrop_half;
         X.sym = e->o.symmetric;
         X.max_len = e->max_len;
@@ -1339,6 +1364,18 @@ static int align_tile(rc_engine *e, int ti)
         X.defer2_count = e->d_count.p + 14;
         X.work2 = e->d_count.p + 15;
         X.cand_box = e->d_cand_box.p;
+        X.share = e->share ? 1 : 0;
+        X.which = 0;
+        X.dir = 0;
+        X.cand_box2 = e->d_cand_box2.p;
+        X.cand_hsp_r = e->d_cand_hsp_r.p;
+        X.cand_nh_r = e->d_cand_nh_r.p;
+        X.cand_ovf_r = e->d_cand_ovf_r.p;
+        X.defer_r = e->d_defer_r.p;
+        X.defer_r_count = e->d_count.p + 17;
+        X.list2 = e->d_list2.p;
+        X.list2_n = e->d_count.p + 16;
+        X.work3 = e->d_count.p + 18;
         {
             const char *cv = getenv("RC_ROW_CHUNK");
             X.chunk = cv ? atoi(cv) : 8;
@@ -1354,6 +1391,9 @@ static int align_tile(rc_engine *e, int ti)
         HIPCHK(hipEventRecord(e->ev[11], e->st));
         unsigned long long ovn = 0, ctr[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, nfull = 0;
         HIPCHK(hipMemcpyAsync(&nfull, e->d_count.p + 14, sizeof nfull, hipMemcpyDeviceToHost, e->st));
+        unsigned long long ndr = 0, nl2 = 0;   // shared searches: reverse searches redone whole, second first seeds
+        HIPCHK(hipMemcpyAsync(&ndr, e->d_count.p + 17, sizeof ndr, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipMemcpyAsync(&nl2, e->d_count.p + 16, sizeof nl2, hipMemcpyDeviceToHost, e->st));
         unsigned int status = 0;
         HIPCHK(hipMemcpyAsync(&ovn, e->d_count.p, sizeof ovn, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipMemcpyAsync(ctr, e->d_count.p + 1, sizeof ctr, hipMemcpyDeviceToHost, e->st));
@@ -1372,7 +1412,8 @@ static int align_tile(rc_engine *e, int ti)
             // candidates the one-wave kernel took (the 64-lane pass's list, or the row kernel's)
             const char *r64 = getenv("RC_ROW64");
             e->tm.ext_fullband += (r64 && atoi(r64)) ? (double)nfull : (double)ctr[3];
-            e->tm.ext_deferred += (double)ctr[5];
+            e->tm.ext_deferred += (double)ctr[5] + (double)ndr;
+            e->tm.ext_second += e->share ? (double)nl2 : 0.0;
             e->tm.band_bound += (double)ctr[7];
             e->tm.maxhsp_bound += (double)ctr[10];
             break;
@@ -1424,7 +1465,15 @@ static int align_tile(rc_engine *e, int ti)
         HIPCHK(hipMemcpyAsync(&nd[r], e->d_gscan.p + cnb[r] + nsgrp, 8, hipMemcpyDeviceToHost, e->st));
     }
     uint64_t nm = 0;
-    if (e->o.symmetric) {
+    // the other direction's groups: mirror images (spec 5b), or the reverse
+    // searches of the shared candidate set (their own HSPs, in their order)
+    const bool mirror = e->o.symmetric || e->share;
+    if (e->share) {
+        G.cand_nh = e->d_cand_nh_r.p;
+        G.cand_hsp = e->d_cand_hsp_r.p;
+        G.cand_ovf = e->d_cand_ovf_r.p;
+    }
+    if (mirror) {
         CHK(e->d_mcnt.ensure(ngrp + 1));
         CHK(e->d_mcur.ensure(ngrp));
         CHK(e->d_mscan.ensure(ngrp + 1));
@@ -1445,12 +1494,15 @@ static int align_tile(rc_engine *e, int ti)
     uint64_t base = e->hsp_used;
     for (size_t r = 0; r < R; r++) {
         GroupParams g = run_group(r);
+        g.cand_nh = e->d_cand_nh.p;
+        g.cand_hsp = e->d_cand_hsp.p;
+        g.cand_ovf = e->d_cand_ovf.p;
         g.out = e->d_hsp.p;
         g.base = base;
         launch_group(g, 1, e->st);
         base += nd[r];
     }
-    if (e->o.symmetric) {
+    if (mirror) {
         CHK(e->d_mkey.ensure(2 * nm + 2));
         G.mscan = e->d_mscan.p;
         G.out = e->d_hsp.p;

@@ -48,12 +48,16 @@ def test_simulated_parity(native, seed, taxa, genes, iso, indel):
     assert summary["hsps"] > 0 and summary["ideal_nodes"] > 0
 
 
-@pytest.mark.parametrize("symmetric,dust", [(True, False), (False, False), (False, (20, 64, 1)),
-                                           (False, (12, 48, 3))])
-def test_alignment_modes(native, symmetric, dust):
+@pytest.mark.parametrize("symmetric,dust,share", [(True, False, 1), (False, False, 1), (False, (20, 64, 1), 1),
+                                                 (False, (12, 48, 3), 1), (False, False, 0),
+                                                 (False, (20, 64, 1), 0)])
+def test_alignment_modes(native, monkeypatch, symmetric, dust, share):
     """Both alignment modes (independent directed searches / spec 5b) and
     DUST on, off, or with other parameters, on isoforms, indels, minus-strand
-    transcripts and poly-A tails."""
+    transcripts and poly-A tails. Independent searches run from one shared
+    candidate set by default (share 1) or one search after the other
+    (RC_SHARE=0); both must equal the oracle's two independent searches."""
+    monkeypatch.setenv("RC_SHARE", str(share))
     from rna_clique_amd.simulate import simulate
     samples, _ = simulate(4, 120, seed=12, p_iso2=0.2, indel_rate=0.003, p_revcomp=0.5,
                           polya=(0.3, 10, 40))
