@@ -156,11 +156,10 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
     __shared__ uint32_t sh_nseed, sh_flags;
     __shared__ unsigned long long sh_sbase, sh_cbase, sh_lbase;
 
-    // shared searches: every maximal run is found (lookups see no DUST mask);
-    // each seed then records which of the two directed searches has a usable
-    // word in it (SEED_F: this query's mask, SEED_R: the subject's)
-    const uint64_t *const dm = P.share ? P.dmask : nullptr;
-    if (P.share) db.dmask = nullptr;
+    // shared searches: the forward pass finds this query's seeds (its usable
+    // words, as its own search does); each seed also records whether the
+    // reverse search (query = the subject) has a usable word in it (SEED_R)
+    const uint64_t *const dm = P.share ? db.dmask : nullptr;
     const int Q = db.gene_sample[g];
     const uint32_t t0 = db.gene_tx_off[g];
     const uint32_t niso = db.gene_tx_off[g + 1] - t0;
@@ -468,27 +467,25 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     }
                     const int len = l + W16 + r;
                     if (len < P.word) continue;
-                    uint32_t dfl = 0;
+                    uint32_t dfl = P.rev ? SEED_F : 0u;
                     if (P.share) {
-                        // forward search (query Q, oriented): its aligned words in
-                        // [x, x + len) -- the first is p (an aligned word in [x, p)
-                        // would make the hit non-canonical); reverse search (query
-                        // the subject, oriented by the strand): its aligned words in
-                        // the run's span there. Without DUST both always exist (a
-                        // run of W = s + 15 bases holds an aligned word).
-                        bool okF = !dm, okR = !dm;
-                        const int x = p - l, y = off - l, Lt = (int)st.len;
-                        for (int pp = p; !okF && pp + W16 <= x + len; pp += stride) {
-                            const int64_t f = (int64_t)qg.qs + (strand ? (int64_t)(qg.Lq - pp - W16) : (int64_t)pp);
-                            okF = (win_bits(dm, f) & 0xFFFFull) == 0;
+                        // the reverse search (query = the subject, oriented by the
+                        // strand): an aligned word of it in the run's span there,
+                        // unmasked. Without DUST one always exists (a run of W =
+                        // s + 15 bases holds an aligned word). A query transcript
+                        // with a masked base: its reverse searches are the reverse
+                        // pass's (they may have seeds this pass does not find).
+                        bool okR = !dm;
+                        if (dm && !P.tx_masked[iso_gtx[ii]]) {
+                            const int y = off - l, Lt = (int)st.len;
+                            const int r0 = strand ? Lt - y - len : y;   // the run in the reverse query's orientation
+                            for (int pp = (r0 + stride - 1) / stride * stride; !okR && pp + W16 <= r0 + len;
+                                 pp += stride) {
+                                const int64_t f = (int64_t)st.start + (strand ? (int64_t)(Lt - pp - W16) : (int64_t)pp);
+                                okR = (win_bits(dm, f) & 0xFFFFull) == 0;
+                            }
                         }
-                        const int r0 = strand ? Lt - y - len : y;   // the run in the reverse query's orientation
-                        for (int pp = (r0 + stride - 1) / stride * stride; !okR && pp + W16 <= r0 + len; pp += stride) {
-                            const int64_t f = (int64_t)st.start + (strand ? (int64_t)(Lt - pp - W16) : (int64_t)pp);
-                            okR = (win_bits(dm, f) & 0xFFFFull) == 0;
-                        }
-                        dfl = (okF ? SEED_F : 0u) | (okR ? SEED_R : 0u);
-                        if (!dfl) continue;
+                        dfl = SEED_F | (okR ? SEED_R : 0u);
                     }
                     const uint32_t slot = atomicAdd(&sh_nseed, 1u);
                     if (slot < cap) {
@@ -699,7 +696,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     c.s_gtx = gtx;
                     c.seed_cnt = (uint16_t)(b1 - b0);
                     c.strand = (uint8_t)((k1 >> 56) & 1);
-                    c.dflags = 1;
+                    c.dflags = P.rev ? 5 : 1;
                     c.e0 = 0;
                     c.e1 = SEED_NONE;
                     if (P.share) {
@@ -943,7 +940,7 @@ __device__ __forceinline__ void process_search(const uint32_t *QO, const uint32_
                                                int X, int lane, uint32_t dbit, int strand, int &bqa, int &bqb,
                                                int &bsa, int &bsb, int &bsc, int &bd, int &bg, int &bo, int &bni,
                                                int &nh, uint32_t &steps, uint32_t &exts, uint32_t &edges,
-                                               uint32_t &capped)
+                                               uint32_t &capped, bool swap)
 {
     nh = 0;
     for (;;) {
@@ -989,7 +986,7 @@ __device__ __forceinline__ void process_search(const uint32_t *QO, const uint32_
         const int x = (int)g.x, y = (int)g.y, len = (int)(g.len & SEED_LEN);
         uint32_t eg = 0;
         ExtRes r, l;
-        extend_seed<AMB, PT>(QO, QOM, qo, TF, TFM, tf, Lq, Lt, x, y, len, X, lane, steps, eg, false, r, l);
+        extend_seed<AMB, PT>(QO, QOM, qo, TF, TFM, tf, Lq, Lt, x, y, len, X, lane, steps, eg, swap, r, l);
         exts += 2;
         edges += eg;
         if (lane == nh) {
@@ -1130,7 +1127,7 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
                 process_search<AMB, uint32_t>(reinterpret_cast<const uint32_t *>(QO), QOM, (uint32_t)SPAD,
                                               reinterpret_cast<const uint32_t *>(TF), TFM, (uint32_t)SPAD, Lq, Lt,
                                               sd, ns, P.xdrop, lane, dbit, strand, bqa, bqb, bsa, bsb, bsc, bd, bg,
-                                              bo, bni, nh, steps, exts, edges, capped);
+                                              bo, bni, nh, steps, exts, edges, capped, swap);
             else
                 process_candidate<AMB, uint32_t>(reinterpret_cast<const uint32_t *>(QO), QOM, (uint32_t)SPAD,
                                                  reinterpret_cast<const uint32_t *>(TF), TFM, (uint32_t)SPAD, Lq, Lt,
@@ -1142,7 +1139,7 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
                                          reinterpret_cast<const uint32_t *>(db.F),
                                          reinterpret_cast<const uint32_t *>(db.AF), (int64_t)st.start, Lq, Lt, sd,
                                          ns, P.xdrop, lane, dbit, strand, bqa, bqb, bsa, bsb, bsc, bd, bg, bo, bni,
-                                         nh, steps, exts, edges, capped);
+                                         nh, steps, exts, edges, capped, swap);
         } else {
             // global arrays carry two zero words in front, so backward windows
             // of the first transcript stay in bounds (positions may go to -32)
@@ -1915,22 +1912,27 @@ __global__ void mirror_scatter_kernel(GroupParams P, int pass)
     for (uint64_t li = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; li < P.n_cand;
          li += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t ci = cand_slot(P, li);
-        const uint32_t nh = P.cand_nh[ci];
+        // shared searches: a reverse-pass candidate's own (forward-array) HSPs
+        // already are the reverse search's, query = its higher sample
+        const bool own = P.cands && (P.cands[ci].dflags & 4);
+        const uint32_t nh = own ? P.cand_nh_f[ci] : P.cand_nh[ci];
         if (!nh) continue;
-        const uint32_t ov = P.cand_ovf[ci];
+        const uint32_t ov = own ? P.cand_ovf_f[ci] : P.cand_ovf[ci];
         for (uint32_t k = 0; k < nh; k++) {
-            const DHsp &h = k ? P.ovf[ov + k - 1] : P.cand_hsp[ci];
-            if (!(h.strand & HSP_REV)) continue;
-            const uint64_t gi = grp_index(P.tx_gene[h.s_tx], P.tx[h.q_tx].sample, P.n_genes);
+            const DHsp &h = k ? P.ovf[ov + k - 1] : (own ? P.cand_hsp_f[ci] : P.cand_hsp[ci]);
+            if (!(h.strand & (own ? HSP_FWD : HSP_REV))) continue;
+            // the reverse search's query tx (its gene and isoform position) and subject tx
+            const uint32_t rq = own ? h.q_tx : h.s_tx, rs = own ? h.s_tx : h.q_tx;
+            const uint64_t gi = grp_index(P.tx_gene[rq], P.tx[rs].sample, P.n_genes);
             if (pass == 0) {
                 atomicAdd(&P.mcnt[gi], 1u);
             } else {
                 const uint64_t slot = P.mbase + P.mscan[gi] + atomicAdd(&P.mcur[gi], 1u);
-                P.out[slot] = mirror_hsp(h);
+                P.out[slot] = own ? h : mirror_hsp(h);
                 // order: (isoform position, strand) then (subject tx, index)
-                P.mkey[2 * (slot - P.mbase)] = ((uint64_t)P.tx_pos[h.s_tx] << 1) | (uint64_t)(h.strand & 1);
+                P.mkey[2 * (slot - P.mbase)] = ((uint64_t)P.tx_pos[rq] << 1) | (uint64_t)(h.strand & 1);
                 P.mkey[2 * (slot - P.mbase) + 1] =
-                    ((uint64_t)h.q_tx << 8) | (uint64_t)((h.strand >> HSP_IDX_SHIFT) & 7);
+                    ((uint64_t)rs << 8) | (uint64_t)((h.strand >> HSP_IDX_SHIFT) & 7);
             }
         }
     }

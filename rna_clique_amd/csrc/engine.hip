@@ -27,6 +27,7 @@ void launch_kmer_count(const TxInfo *, uint32_t, const uint64_t *, uint64_t *, h
 void launch_kmer_fill(bool, const TxInfo *, uint32_t, const uint64_t *, const uint64_t *, const uint64_t *,
                       uint64_t *, hipStream_t);
 void launch_bucket_fill(const uint64_t *, uint64_t, int, uint32_t *, hipStream_t);
+void launch_tx_masked(const TxInfo *, uint32_t, const uint64_t *, uint8_t *, hipStream_t);
 void launch_seed(bool, const Db &, const Index &, const SeedParams &, hipStream_t);
 void launch_seed_big(bool, const Db &, const Index &, const SeedParams &, uint32_t, hipStream_t);
 void launch_dust(bool, uint64_t, const uint64_t *, const uint64_t *, const uint64_t *, const TxInfo *, uint32_t, int,
@@ -282,6 +283,16 @@ struct rc_engine {
     DBuf<uint32_t> d_tx_gene, d_gene_tx_off, d_gene_tx, d_sample_gene_begin, d_sample_tx_begin;
     DBuf<int32_t> d_gene_sample;
     DBuf<uint64_t> d_kpos_off, d_kcnt;
+    // shared searches with DUST: masked transcripts (flags per tile tx and per
+    // global tx), their index, the global id of each tile tx
+    DBuf<uint8_t> d_tile_masked, d_tx_masked;
+    DBuf<TxInfo> d_mtile_tx;
+    DBuf<uint64_t> d_mkpos_off, d_ment, d_ment2;
+    DBuf<uint32_t> d_mbucket;
+    std::vector<uint32_t> tile_gid;
+    int mindex_bits = 16;
+    uint64_t n_mindex = 0;
+    uint32_t n_masked_tx = 0;
     DBuf<uint64_t> d_ent, d_ent2;   // (k-mer << 32 | position), unsorted / sorted
     DBuf<uint32_t> d_bucket, d_pos_tx;
     DBuf<uint64_t> d_sample_pos, d_txstart, d_kpos_rel, d_dmask;
@@ -871,6 +882,7 @@ static int load_tile(rc_engine *e, int ti)
     // transcript starts in the tile; the tile's transcripts (index) with their
     // closed-form k-mer slots; blocks of positions -> transcript
     std::vector<TxInfo> ttx;
+    std::vector<uint32_t> gid;
     std::vector<uint64_t> koff(1, 0);
     std::vector<uint32_t> pos_tx((total >> POS_TX_SHIFT) + 2, 0);
     std::vector<uint64_t> txb((total >> 6) + 4, 0);
@@ -886,6 +898,7 @@ static int load_tile(rc_engine *e, int ti)
             const uint64_t st = p0 + (e->tx_start[t] - S.base);
             e->h_tx[t].start = st;
             ttx.push_back(e->h_tx[t]);
+            gid.push_back(t);
             const int64_t L = (int64_t)e->h_tx[t].len;
             koff.push_back(koff.back() + (uint64_t)(L >= W16 ? L - W16 + 1 : 0));
             setbit(st);
@@ -908,6 +921,7 @@ static int load_tile(rc_engine *e, int ti)
     CHK(up(e->d_sample_pos, spos));
     CHK(up(e->d_txstart, txb));
     e->h_koff = koff;
+    e->tile_gid = gid;
     e->tile_ntx = (uint32_t)ttx.size();
     // the packed working copy's source: d_ascii itself or a gathered copy
     if (!direct) {
@@ -924,17 +938,18 @@ static int load_tile(rc_engine *e, int ti)
     return RC_OK;
 }
 
-// The seed index of the loaded tile: every 16-mer position of its transcripts.
-static int build_index(rc_engine *e)
+// A seed index: every 16-mer position of the transcripts txl[0, n_tx), whose
+// slots koff / kpos (closed form when no base is ambiguous) give the order.
+static int build_index_of(rc_engine *e, const TxInfo *txl, uint32_t n_tx, uint64_t npos, const uint64_t *kpos,
+                          DBuf<uint64_t> &ent, DBuf<uint64_t> &ent2, DBuf<uint32_t> &bucket, int &bits_out,
+                          uint64_t &n_out)
 {
     const bool amb = e->has_amb;
-    const uint32_t n_tx = e->tile_ntx;
-    uint64_t npos = e->h_koff[n_tx];
-    const uint64_t *offs = e->d_kpos_off.p;   // closed-form slots (no ambiguous bases)
+    const uint64_t *offs = kpos;
     if (amb) {
         CHK(e->d_kcnt.ensure(n_tx + 1));
         HIPCHK(hipMemsetAsync(e->d_kcnt.p, 0, (n_tx + 1) * sizeof(uint64_t), e->st));
-        if (n_tx) launch_kmer_count(e->d_tile_tx.p, n_tx, e->d_AF.p + FRONT_PAD, e->d_kcnt.p, e->st);
+        if (n_tx) launch_kmer_count(txl, n_tx, e->d_AF.p + FRONT_PAD, e->d_kcnt.p, e->st);
         size_t tmp = 0;
         CHK(e->d_kpos_rel.ensure(n_tx + 1));
         HIPCHK(rocprim::exclusive_scan(nullptr, tmp, e->d_kcnt.p, e->d_kpos_rel.p, (uint64_t)0, (size_t)n_tx + 1,
@@ -946,10 +961,10 @@ static int build_index(rc_engine *e)
         HIPCHK(hipStreamSynchronize(e->st));
         offs = e->d_kpos_rel.p;
     }
-    CHK(e->d_ent.ensure(std::max<uint64_t>(npos, 1)));
-    CHK(e->d_ent2.ensure(std::max<uint64_t>(npos, 1)));
-    if (n_tx) launch_kmer_fill(amb, e->d_tile_tx.p, n_tx, e->d_F.p + FRONT_PAD, amb ? e->d_AF.p + FRONT_PAD : nullptr,
-                               offs, e->d_ent.p, e->st);
+    CHK(ent.ensure(std::max<uint64_t>(npos, 1)));
+    CHK(ent2.ensure(std::max<uint64_t>(npos, 1)));
+    if (n_tx) launch_kmer_fill(amb, txl, n_tx, e->d_F.p + FRONT_PAD, amb ? e->d_AF.p + FRONT_PAD : nullptr,
+                               offs, ent.p, e->st);
     // sort on the k-mer (bits 32..63); the fill order is position order and the
     // onesweep radix sort is stable, so positions stay ascending per k-mer.
     // rocPRIM sorts up to 2^20 items with a merge sort that did not keep that
@@ -957,20 +972,65 @@ static int build_index(rc_engine *e)
     // positions are unique).
     const unsigned bb = npos <= (1ull << 20) ? 0u : 32u;
     size_t tmp = 0;
-    HIPCHK(rocprim::radix_sort_keys(nullptr, tmp, e->d_ent.p, e->d_ent2.p, (size_t)npos, bb, 64u, e->st));
+    HIPCHK(rocprim::radix_sort_keys(nullptr, tmp, ent.p, ent2.p, (size_t)npos, bb, 64u, e->st));
     CHK(e->d_tmp.ensure(tmp));
-    HIPCHK(rocprim::radix_sort_keys(e->d_tmp.p, tmp, e->d_ent.p, e->d_ent2.p, (size_t)npos, bb, 64u, e->st));
+    HIPCHK(rocprim::radix_sort_keys(e->d_tmp.p, tmp, ent.p, ent2.p, (size_t)npos, bb, 64u, e->st));
     // bucket table over the top k-mer bits: about one bucket per indexed
-    // position of this tile, at most 2^28 (RC_INDEX_BITS_MAX; 28 measured
-    // best at C3 -- a 1 GiB table instead of 4 GiB, same seed-kernel time)
+    // position, at most 2^28 (RC_INDEX_BITS_MAX; 28 measured best at C3 -- a
+    // 1 GiB table instead of 4 GiB, same seed-kernel time)
     const char *ibv = getenv("RC_INDEX_BITS_MAX");
     const int bmax = ibv ? std::max(16, std::min(30, atoi(ibv))) : 28;
     int bits = 16;
     while (bits < bmax && (1ull << bits) < npos) bits++;
-    e->index_bits = bits;
-    CHK(e->d_bucket.ensure((1ull << e->index_bits) + 1));
-    launch_bucket_fill(e->d_ent2.p, npos, e->index_bits, e->d_bucket.p, e->st);
-    e->n_index = npos;
+    bits_out = bits;
+    CHK(bucket.ensure((1ull << bits) + 1));
+    launch_bucket_fill(ent2.p, npos, bits, bucket.p, e->st);
+    n_out = npos;
+    return RC_OK;
+}
+
+// The seed index of the loaded tile: every 16-mer position of its transcripts.
+static int build_index(rc_engine *e)
+{
+    return build_index_of(e, e->d_tile_tx.p, e->tile_ntx, e->h_koff[e->tile_ntx], e->d_kpos_off.p, e->d_ent,
+                          e->d_ent2, e->d_bucket, e->index_bits, e->n_index);
+}
+
+// Shared searches with DUST: the tile's transcripts holding a masked base (a
+// reverse search whose SUBJECT is such a transcript may have seeds the
+// forward pass does not find: runs whose forward words are all masked), their
+// per-transcript flags for the seed kernel, and their own index.
+static int build_masked_index(rc_engine *e)
+{
+    const uint32_t n = e->tile_ntx;
+    CHK(e->d_tile_masked.ensure(std::max<uint32_t>(n, 1)));
+    launch_tx_masked(e->d_tile_tx.p, n, e->d_dmask.p + 1, e->d_tile_masked.p, e->st);
+    HIPCHK(hipGetLastError());
+    std::vector<uint8_t> hm(n);
+    if (n) HIPCHK(hipMemcpyAsync(hm.data(), e->d_tile_masked.p, n, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    std::vector<uint8_t> txm(e->h_tx.size(), 0);
+    std::vector<TxInfo> mt;
+    std::vector<uint64_t> mk(1, 0);
+    for (uint32_t i = 0; i < n; i++) {
+        txm[e->tile_gid[i]] = hm[i];
+        if (!hm[i]) continue;
+        const TxInfo &t = e->h_tx[e->tile_gid[i]];
+        mt.push_back(t);
+        mk.push_back(mk.back() + (uint64_t)(t.len >= (uint32_t)W16 ? t.len - W16 + 1 : 0));
+    }
+    CHK(e->d_tx_masked.ensure(std::max<size_t>(txm.size(), 1)));
+    if (!txm.empty())
+        HIPCHK(hipMemcpyAsync(e->d_tx_masked.p, txm.data(), txm.size(), hipMemcpyHostToDevice, e->st));
+    CHK(e->d_mtile_tx.ensure(std::max<size_t>(mt.size(), 1)));
+    CHK(e->d_mkpos_off.ensure(mk.size()));
+    if (!mt.empty())
+        HIPCHK(hipMemcpyAsync(e->d_mtile_tx.p, mt.data(), mt.size() * sizeof(TxInfo), hipMemcpyHostToDevice, e->st));
+    HIPCHK(hipMemcpyAsync(e->d_mkpos_off.p, mk.data(), mk.size() * 8, hipMemcpyHostToDevice, e->st));
+    e->n_masked_tx = (uint32_t)mt.size();
+    CHK(build_index_of(e, e->d_mtile_tx.p, (uint32_t)mt.size(), mk.back(), e->d_mkpos_off.p, e->d_ment, e->d_ment2,
+                       e->d_mbucket, e->mindex_bits, e->n_mindex));
+    HIPCHK(hipStreamSynchronize(e->st));   // host vectors outlive the copies
     return RC_OK;
 }
 
@@ -1144,37 +1204,70 @@ static int align_tile(rc_engine *e, int ti)
     CHK(build_index(e));
     HIPCHK(hipGetLastError());
     if (dust) HIPCHK(hipStreamWaitEvent(e->st, e->evd[1], 0));
-    HIPCHK(hipEventRecord(e->ev[2], e->st));
-
-    std::vector<uint64_t> tmask;
-    std::vector<std::pair<int, int>> runs;
     {
         // both directed searches of a pair from one candidate set (query =
         // the lower sample); RC_SHARE=0 runs them one by one
         const char *sv = getenv("RC_SHARE");
         e->share = !e->o.symmetric && !(sv && atoi(sv) == 0);
     }
+    // shared searches with DUST: the reverse searches whose subject holds a
+    // masked base come from a reverse pass over those transcripts' own index
+    const bool revpass = e->share && dust;
+    if (revpass) CHK(build_masked_index(e));
+    HIPCHK(hipEventRecord(e->ev[2], e->st));
+
+    std::vector<uint64_t> tmask;
+    std::vector<std::pair<int, int>> runs;
     tile_plan(e, ti, tmask, runs);
+    const size_t R = runs.size();   // forward runs; reverse-pass runs follow
+    if (revpass && e->n_mindex) {
+        std::vector<uint64_t> rmask((size_t)4 * N, 0);
+        std::vector<char> q(N, 0);
+        for (auto &pr : e->tiles[ti].pairs) {
+            rmask[4 * pr.second + (pr.first >> 6)] |= 1ull << (pr.first & 63);
+            q[pr.second] = 1;
+        }
+        for (int s0 = 0; s0 < N;) {
+            if (!q[s0]) {
+                s0++;
+                continue;
+            }
+            int t = s0;
+            while (t < N && q[t]) t++;
+            runs.push_back({s0, t});
+            s0 = t;
+        }
+        tmask.insert(tmask.end(), rmask.begin(), rmask.end());
+    }
+    const size_t RT = runs.size();
     CHK(e->d_tmask.ensure(tmask.size()));
     HIPCHK(hipMemcpyAsync(e->d_tmask.p, tmask.data(), tmask.size() * 8, hipMemcpyHostToDevice, e->st));
     // per run: its genes [g0, g1) and its slice of the (gene, sample) arrays
-    const size_t R = runs.size();
-    std::vector<uint32_t> rg0(R), rg1(R);
-    std::vector<size_t> gcb(R + 1, 0), cnb(R + 1, 0);
-    for (size_t r = 0; r < R; r++) {
+    std::vector<uint32_t> rg0(RT), rg1(RT);
+    std::vector<size_t> gcb(RT + 1, 0), cnb(R + 1, 0);
+    for (size_t r = 0; r < RT; r++) {
         rg0[r] = e->sample_gene_begin[runs[r].first];
         rg1[r] = e->sample_gene_begin[runs[r].second];
         gcb[r + 1] = gcb[r] + (size_t)(rg1[r] - rg0[r]) * N;
-        cnb[r + 1] = cnb[r] + (size_t)(rg1[r] - rg0[r]) * N + 1;
+        if (r < R) cnb[r + 1] = cnb[r] + (size_t)(rg1[r] - rg0[r]) * N + 1;
     }
-    CHK(e->d_gc_off.ensure(std::max<size_t>(gcb[R], 1)));
-    CHK(e->d_gc_cnt.ensure(std::max<size_t>(gcb[R], 1)));
+    CHK(e->d_gc_off.ensure(std::max<size_t>(gcb[RT], 1)));
+    CHK(e->d_gc_cnt.ensure(std::max<size_t>(gcb[RT], 1)));
     CHK(e->d_gcount.ensure(std::max<size_t>(cnb[R], 1)));
     CHK(e->d_gscan.ensure(std::max<size_t>(cnb[R], 1)));
     CHK(e->d_shard_cnt.ensure(2 * NSHARD));
     CHK(e->d_shard_prefix.ensure(NSHARD + 1));
     {
-        const uint64_t nb = std::max<uint64_t>(gcb[R] / std::max(N, 1), 1) * (uint64_t)std::max(N - 1, 1);
+        // (query gene, subject sample) searches of the tile; a reverse-pass
+        // search only meets its subjects' masked transcripts (weighted by them)
+        uint64_t nb = 1;
+        for (size_t r = 0; r < RT; r++)
+            for (int q = runs[r].first; q < runs[r].second; q++) {
+                uint64_t ns = 0;
+                for (int w = 0; w < 4; w++) ns += (uint64_t)__builtin_popcountll(tmask[(r < R ? 0 : 4 * (size_t)N) + 4 * q + w]);
+                const uint64_t g = e->sample_gene_begin[q + 1] - e->sample_gene_begin[q];
+                nb += r < R ? g * ns : (g * ns * (e->n_mindex + 1)) / (e->n_index + 1) + g;
+            }
         e->seed_cap = std::max<uint64_t>(e->seed_cap, nb * 16 / NSHARD + 4096);
         e->cand_cap = std::max<uint64_t>(e->cand_cap, nb * 2 / NSHARD + 1024);
         e->ovf_cap = std::max<uint64_t>(e->ovf_cap, nb / 4 + 1024);
@@ -1185,6 +1278,10 @@ static int align_tile(rc_engine *e, int ti)
     ix.bucket = e->d_bucket.p;
     ix.pos_tx = e->d_pos_tx.p;
     ix.bits = e->index_bits;
+    Index ixm = ix;   // the reverse pass's: masked transcripts only
+    ixm.ent = e->d_ment2.p;
+    ixm.bucket = e->d_mbucket.p;
+    ixm.bits = e->mindex_bits;
     // --- seeds ---
     std::vector<unsigned long long> shard_cnt(2 * NSHARD);
     CHK(e->d_count.ensure(24));
@@ -1202,12 +1299,13 @@ static int align_tile(rc_engine *e, int ti)
         CHK(e->d_big_out.ensure(e->big_list_cap));
         HIPCHK(hipMemsetAsync(e->d_shard_cnt.p, 0, 2 * NSHARD * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
-        if (gcb[R]) HIPCHK(hipMemsetAsync(e->d_gc_cnt.p, 0, gcb[R] * 4, e->st));
+        if (gcb[RT]) HIPCHK(hipMemsetAsync(e->d_gc_cnt.p, 0, gcb[RT] * 4, e->st));
         CHK(e->d_prof.ensure(8));
         HIPCHK(hipMemsetAsync(e->d_prof.p, 0, 8 * sizeof(unsigned long long), e->st));
         bool again = false;
         n_big = 0;
-        for (size_t r = 0; r < R && !again; r++) {
+        for (size_t r = 0; r < RT && !again; r++) {
+            const bool rev = r >= R;
             HIPCHK(hipMemsetAsync(big_n, 0, 2 * sizeof(unsigned long long), e->st));
             SeedParams S{};
             S.word = e->o.word_size;
@@ -1217,8 +1315,9 @@ static int align_tile(rc_engine *e, int ti)
                 S.pre_mode = pm ? atoi(pm) : 1;
             }
             S.sym = e->o.symmetric;
-            S.share = e->share ? 1 : 0;
-            S.dmask = e->o.dust_level > 0 ? e->d_dmask.p + 1 : nullptr;
+            S.share = e->share && !rev ? 1 : 0;
+            S.rev = rev ? 1 : 0;
+            S.tx_masked = revpass ? e->d_tx_masked.p : nullptr;
             S.list2 = e->d_list2.p;
             S.list2_n = e->d_count.p + 16;
             S.gene_begin = rg0[r];
@@ -1231,14 +1330,14 @@ static int align_tile(rc_engine *e, int ti)
             S.cand_count = e->d_shard_cnt.p + NSHARD;
             S.gc_off = e->d_gc_off.p + gcb[r];
             S.gc_cnt = e->d_gc_cnt.p + gcb[r];
-            S.tmask = e->d_tmask.p;
+            S.tmask = e->d_tmask.p + (rev ? 4 * (size_t)N : 0);
             S.status = e->d_status.p;
             S.big_out = e->d_big_out.p;
             S.big_n = big_n;
             S.big_retry_n = big_retry_n;
             S.big_list_cap = e->big_list_cap;
             S.prof = e->d_prof.p;
-            launch_seed(e->has_amb, db, ix, S, e->st);
+            launch_seed(e->has_amb, db, rev ? ixm : ix, S, e->st);
             HIPCHK(hipGetLastError());
             unsigned int status = 0;
             unsigned long long nb = 0;   // (big_n: d_count[12], next to the extension's counters [0, 11))
@@ -1279,7 +1378,7 @@ static int align_tile(rc_engine *e, int ti)
                 B.big_segT = e->d_big_segT.p;
                 for (uint64_t c0 = 0; c0 < nb; c0 += chunk) {
                     B.big_list = e->d_big_list.p + c0;
-                    launch_seed_big(e->has_amb, db, ix, B, (uint32_t)std::min<uint64_t>(chunk, nb - c0), e->st);
+                    launch_seed_big(e->has_amb, db, rev ? ixm : ix, B, (uint32_t)std::min<uint64_t>(chunk, nb - c0), e->st);
                     HIPCHK(hipGetLastError());
                 }
                 unsigned long long nr = 0;
@@ -1472,6 +1571,10 @@ static int align_tile(rc_engine *e, int ti)
         G.cand_nh = e->d_cand_nh_r.p;
         G.cand_hsp = e->d_cand_hsp_r.p;
         G.cand_ovf = e->d_cand_ovf_r.p;
+        G.cands = e->d_cands.p;
+        G.cand_nh_f = e->d_cand_nh.p;
+        G.cand_hsp_f = e->d_cand_hsp.p;
+        G.cand_ovf_f = e->d_cand_ovf.p;
     }
     if (mirror) {
         CHK(e->d_mcnt.ensure(ngrp + 1));

@@ -751,6 +751,26 @@ void launch_bucket_fill(const uint64_t *ent, uint64_t n, int bits, uint32_t *buc
     hipLaunchKernelGGL(bucket_fill_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, ent, n, bits, bucket);
 }
 
+// 1 iff transcript i of the list holds a DUST-masked base (one thread each)
+__global__ void tx_masked_kernel(const TxInfo *txl, uint32_t n, const uint64_t *dmask, uint8_t *out)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const TxInfo t = txl[i];
+    uint64_t any = 0;
+    for (uint32_t u = 0; u < t.len && !any; u += 64) {
+        const uint32_t k = t.len - u < 64 ? t.len - u : 64;
+        const uint64_t w = win_bits(dmask, (int64_t)(t.start + u));
+        any = k == 64 ? w : (w & ((1ull << k) - 1ull));
+    }
+    out[i] = any ? 1 : 0;
+}
+
+void launch_tx_masked(const TxInfo *txl, uint32_t n, const uint64_t *dmask, uint8_t *out, hipStream_t st)
+{
+    if (n) hipLaunchKernelGGL(tx_masked_kernel, dim3((n + 255) / 256), dim3(256), 0, st, txl, n, dmask, out);
+}
+
 // After pass 2 and the scans: each item's rows and edges from its slots to
 // their offsets, labels made pair-global (F rows: + the item's F_sel base; R
 // rows: + the pair's F_sel total + the item's R_sel base).
