@@ -122,6 +122,8 @@ typedef struct rc_timing {
     double maxhsp_bound;      /* candidates with a seed outside their MAX_HSP (8) HSP boxes (spec 3) */
     double ext_second;        /* shared searches: candidates whose reverse search starts at another seed
                                  (a second first-seed extension) */
+    double near_index;        /* shared searches with DUST: entries of the reverse pass's near-mask index */
+    double reverse_seeds;     /* shared searches with DUST: reverse-search seeds only the reverse pass finds */
 } rc_timing;
 
 void rc_default_opts(rc_opts *opts);

@@ -153,7 +153,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
     __shared__ uint32_t iso_len[MAX_ISO], iso_gtx[MAX_ISO], iso_pre[MAX_ISO + 1];
     __shared__ uint32_t tcnt[MAX_SAMPLES], tpre[MAX_SAMPLES + 1];
     __shared__ uint32_t wsum[SBLOCK / 64];
-    __shared__ uint32_t sh_nseed, sh_flags;
+    __shared__ uint32_t sh_nseed, sh_flags, sh_rs0, sh_rs1;
     __shared__ unsigned long long sh_sbase, sh_cbase, sh_lbase;
 
     // shared searches: the forward pass finds this query's seeds (its usable
@@ -226,12 +226,43 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
     }
     int T1 = Tr;
     const uint32_t qpb0 = (uint32_t)db.sample_pos_begin[Q], qpb1 = (uint32_t)db.sample_pos_begin[Q + 1];
+    // the reverse pass's seeds of this gene's transcripts: [sh_rs0, sh_rs1) of rs_key
+    if (P.rs_n) {
+        if (tid < 2) {
+            const uint32_t key = g + (uint32_t)tid;
+            uint32_t lo = 0, n = P.rs_n;
+            while (n) {
+                const uint32_t h = n >> 1;
+                if (P.rs_key[lo + h] < key) {
+                    lo += h + 1;
+                    n -= h + 1;
+                } else {
+                    n = h;
+                }
+            }
+            (tid ? sh_rs1 : sh_rs0) = lo;
+        }
+        __syncthreads();
+    }
     while (T0 < Tr) {
         if (tid == 0) {
             sh_nseed = 0;
             sh_flags = 0;
         }
         __syncthreads();
+        if (P.rs_n && sh_rs1 > sh_rs0) {
+            // reverse-only seeds (SEED_R, no usable word of this query inside)
+            // with a subject in this pass's samples
+            for (uint32_t i = sh_rs0 + (uint32_t)tid; i < sh_rs1; i += SBLOCK) {
+                const LSeed sd = P.rs_rec[P.rs_idx[i]];
+                const int T = db.tx[(uint32_t)(sd.k1 >> 24)].sample;
+                if (T < T0 || T >= T1 || !((tm[T >> 6] >> (T & 63)) & 1)) continue;
+                const uint32_t slot = atomicAdd(&sh_nseed, 1u);
+                if (slot < cap) seeds[slot] = sd;
+                else atomicOr(&sh_flags, 1u);
+            }
+            __syncthreads();
+        }
         // words p of the oriented query at stride s, one per thread; hits are
         // the entries of the word's bucket with its key and a position in the
         // subject samples [T0, T1) (samples are contiguous in position)
@@ -467,16 +498,40 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     }
                     const int len = l + W16 + r;
                     if (len < P.word) continue;
-                    uint32_t dfl = P.rev ? SEED_F : 0u;
+                    if (P.rev) {
+                        // the reverse pass: only runs the forward pass cannot see
+                        // go on -- no usable aligned word of the subject (the
+                        // forward query, oriented by the strand) inside -- as
+                        // SEED_R seeds of the forward candidate (subject tx,
+                        // strand, this tx) in its coordinates
+                        const int La = (int)st.len, ya = off - l, pb = p - l;
+                        const int xa = strand ? La - ya - len : ya;
+                        bool fwd = false;
+                        for (int u = (xa + stride - 1) / stride * stride; !fwd && u + W16 <= xa + len; u += stride)
+                            fwd = word_usable<AMB>(db, st.start, La, strand, u, total);
+                        if (fwd) continue;
+                        LSeed sd;
+                        sd.k1 = ((uint64_t)P.tx_pos[stx] << 57) | ((uint64_t)strand << 56) |
+                                ((uint64_t)iso_gtx[ii] << 24) | (uint64_t)(uint32_t)xa;
+                        sd.y = (uint32_t)(strand ? qg.Lq - pb - len : pb);
+                        sd.len = (uint32_t)len | SEED_R;
+                        const unsigned long long k = atomicAdd(P.rseed_n, 1ull);
+                        if (k < P.rseed_cap) {
+                            P.rseeds[k] = sd;
+                            P.rseed_gene[k] = db.tx_gene[stx];
+                        }
+                        continue;
+                    }
+                    uint32_t dfl = 0u;
                     if (P.share) {
                         // the reverse search (query = the subject, oriented by the
                         // strand): an aligned word of it in the run's span there,
                         // unmasked. Without DUST one always exists (a run of W =
-                        // s + 15 bases holds an aligned word). A query transcript
-                        // with a masked base: its reverse searches are the reverse
-                        // pass's (they may have seeds this pass does not find).
+                        // s + 15 bases holds an aligned word). Runs of the reverse
+                        // search with no usable word of this query inside come
+                        // from the reverse pass (P.rs_*).
                         bool okR = !dm;
-                        if (dm && !P.tx_masked[iso_gtx[ii]]) {
+                        if (dm) {
                             const int y = off - l, Lt = (int)st.len;
                             const int r0 = strand ? Lt - y - len : y;   // the run in the reverse query's orientation
                             for (int pp = (r0 + stride - 1) / stride * stride; !okR && pp + W16 <= r0 + len;
@@ -503,6 +558,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
             }
             __syncthreads();
         }
+        if (P.rev) break;   // the reverse pass keeps no seeds of its own
         if (sh_flags & 1u) {   // too many seeds: fewer subject samples per pass
             if (T1 - T0 == 1) {
                 // one subject sample alone overflows: the global-memory pass
@@ -696,7 +752,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     c.s_gtx = gtx;
                     c.seed_cnt = (uint16_t)(b1 - b0);
                     c.strand = (uint8_t)((k1 >> 56) & 1);
-                    c.dflags = P.rev ? 5 : 1;
+                    c.dflags = 1;
                     c.e0 = 0;
                     c.e1 = SEED_NONE;
                     if (P.share) {
@@ -1912,23 +1968,20 @@ __global__ void mirror_scatter_kernel(GroupParams P, int pass)
     for (uint64_t li = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; li < P.n_cand;
          li += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t ci = cand_slot(P, li);
-        // shared searches: a reverse-pass candidate's own (forward-array) HSPs
-        // already are the reverse search's, query = its higher sample
-        const bool own = P.cands && (P.cands[ci].dflags & 4);
-        const uint32_t nh = own ? P.cand_nh_f[ci] : P.cand_nh[ci];
+        const uint32_t nh = P.cand_nh[ci];
         if (!nh) continue;
-        const uint32_t ov = own ? P.cand_ovf_f[ci] : P.cand_ovf[ci];
+        const uint32_t ov = P.cand_ovf[ci];
         for (uint32_t k = 0; k < nh; k++) {
-            const DHsp &h = k ? P.ovf[ov + k - 1] : (own ? P.cand_hsp_f[ci] : P.cand_hsp[ci]);
-            if (!(h.strand & (own ? HSP_FWD : HSP_REV))) continue;
+            const DHsp &h = k ? P.ovf[ov + k - 1] : P.cand_hsp[ci];
+            if (!(h.strand & HSP_REV)) continue;
             // the reverse search's query tx (its gene and isoform position) and subject tx
-            const uint32_t rq = own ? h.q_tx : h.s_tx, rs = own ? h.s_tx : h.q_tx;
+            const uint32_t rq = h.s_tx, rs = h.q_tx;
             const uint64_t gi = grp_index(P.tx_gene[rq], P.tx[rs].sample, P.n_genes);
             if (pass == 0) {
                 atomicAdd(&P.mcnt[gi], 1u);
             } else {
                 const uint64_t slot = P.mbase + P.mscan[gi] + atomicAdd(&P.mcur[gi], 1u);
-                P.out[slot] = own ? h : mirror_hsp(h);
+                P.out[slot] = mirror_hsp(h);
                 // order: (isoform position, strand) then (subject tx, index)
                 P.mkey[2 * (slot - P.mbase)] = ((uint64_t)P.tx_pos[rq] << 1) | (uint64_t)(h.strand & 1);
                 P.mkey[2 * (slot - P.mbase) + 1] =

@@ -113,8 +113,7 @@ struct Cand {
     uint32_t q_gtx, s_gtx;
     uint16_t seed_cnt;
     uint8_t strand;
-    uint8_t dflags;        // shared searches: bit 0 the forward search has seeds, bit 1 the reverse
-                           // one; bit 2: a reverse-pass candidate (query = the higher sample)
+    uint8_t dflags;        // shared searches: bit 0 the forward search has seeds, bit 1 the reverse one
     uint64_t q0;           // first base of the oriented query: in F (strand 0) or RC (strand 1)
     uint64_t s0;           // first base of the subject in F
     int32_t Lq, Lt;        // transcript lengths
@@ -141,9 +140,22 @@ struct SeedParams {
     int32_t pre_mode;             // canonical pre-test: 1 = previous word's hits (LDS), 0 = sequence windows
     int32_t sym;                  // spec 5b: subjects are higher-numbered samples only
     int32_t share;                // shared searches: query = lower sample, seeds carry SEED_F / SEED_R
-    const uint8_t *tx_masked;     // shared searches with DUST: per global tx, 1 = holds a masked base
-                                  // (its reverse searches come from the reverse pass)
-    int32_t rev;                  // the reverse pass: queries = higher samples, subjects = masked tx only
+    // Shared searches with DUST. The reverse pass (rev = 1; queries = the
+    // higher samples, subjects = the near-mask index) emits the reverse-search
+    // seeds the forward pass cannot find (no usable word of the lower sample's
+    // transcript inside) as SEED_R seeds in forward-candidate coordinates:
+    // rseeds[i] with the forward query's gene in rseed_gene[i]. The forward
+    // pass merges them into its candidates: rs_key = those genes sorted,
+    // rs_idx = the permutation, rs_n entries.
+    int32_t rev;
+    const uint32_t *tx_pos;       // isoform index of a transcript in its gene
+    LSeed *rseeds;
+    uint32_t *rseed_gene;
+    uint64_t rseed_cap;
+    unsigned long long *rseed_n;
+    const LSeed *rs_rec;
+    const uint32_t *rs_key, *rs_idx;
+    uint32_t rs_n;
     uint32_t *list2;              // shared searches: slots of the candidates with e1 != SEED_NONE
     unsigned long long *list2_n;
     uint32_t gene_begin, gene_end;   // shard
@@ -258,12 +270,6 @@ struct GroupParams {
     uint64_t mbase;               // first output slot of the mirrored region
     uint64_t *mkey;               // order keys of the mirrored region (parallel to out)
     uint32_t n_genes;
-    // shared searches: candidates (dflags bit 2 = reverse-pass candidate) and
-    // the forward arrays, where reverse-pass candidates keep their HSPs
-    const Cand *cands;
-    const uint8_t *cand_nh_f;
-    const DHsp *cand_hsp_f;
-    const uint32_t *cand_ovf_f;
 };
 
 // Parameters of the two reciprocal-best-hit passes.

@@ -9,6 +9,7 @@
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -28,6 +29,8 @@ void launch_kmer_fill(bool, const TxInfo *, uint32_t, const uint64_t *, const ui
                       uint64_t *, hipStream_t);
 void launch_bucket_fill(const uint64_t *, uint64_t, int, uint32_t *, hipStream_t);
 void launch_tx_masked(const TxInfo *, uint32_t, const uint64_t *, uint8_t *, hipStream_t);
+void launch_near_fill(bool, const TxInfo *, uint32_t, const uint8_t *, const uint64_t *, const uint64_t *,
+                      const uint64_t *, uint64_t *, uint64_t, unsigned long long *, hipStream_t);
 void launch_seed(bool, const Db &, const Index &, const SeedParams &, hipStream_t);
 void launch_seed_big(bool, const Db &, const Index &, const SeedParams &, uint32_t, hipStream_t);
 void launch_dust(bool, uint64_t, const uint64_t *, const uint64_t *, const uint64_t *, const TxInfo *, uint32_t, int,
@@ -283,16 +286,19 @@ struct rc_engine {
     DBuf<uint32_t> d_tx_gene, d_gene_tx_off, d_gene_tx, d_sample_gene_begin, d_sample_tx_begin;
     DBuf<int32_t> d_gene_sample;
     DBuf<uint64_t> d_kpos_off, d_kcnt;
-    // shared searches with DUST: masked transcripts (flags per tile tx and per
-    // global tx), their index, the global id of each tile tx
-    DBuf<uint8_t> d_tile_masked, d_tx_masked;
-    DBuf<TxInfo> d_mtile_tx;
-    DBuf<uint64_t> d_mkpos_off, d_ment, d_ment2;
+    // shared searches with DUST: masked tile transcripts, the near-mask index
+    // of the reverse pass, its reverse-only seeds (sorted by forward gene)
+    DBuf<uint8_t> d_tile_masked;
+    DBuf<uint64_t> d_ment, d_ment2;
     DBuf<uint32_t> d_mbucket;
     std::vector<uint32_t> tile_gid;
     int mindex_bits = 16;
-    uint64_t n_mindex = 0;
-    uint32_t n_masked_tx = 0;
+    uint64_t n_mindex = 0, mnear_cap = 0;
+    DBuf<LSeed> d_rseeds;
+    DBuf<uint32_t> d_rseed_gene, d_rs_key, d_rs_idx;
+    DBuf<unsigned long long> d_rctr;   // [0] near-index entries, [1] reverse-only seeds
+    DBuf<uint64_t> d_rtmask;
+    uint64_t rseed_cap = 0, n_rseeds = 0;
     DBuf<uint64_t> d_ent, d_ent2;   // (k-mer << 32 | position), unsorted / sorted
     DBuf<uint32_t> d_bucket, d_pos_tx;
     DBuf<uint64_t> d_sample_pos, d_txstart, d_kpos_rel, d_dmask;
@@ -938,6 +944,27 @@ static int load_tile(rc_engine *e, int ti)
     return RC_OK;
 }
 
+// Sort index entries ent[0, npos) on key bits [bb, 64) into ent2 and build the
+// bucket table over the top k-mer bits: about one bucket per entry (times
+// 2^extra), at most 2^28 (RC_INDEX_BITS_MAX; 28 measured best at C3 -- a 1 GiB
+// table instead of 4 GiB, same seed-kernel time)
+static int sort_index(rc_engine *e, DBuf<uint64_t> &ent, DBuf<uint64_t> &ent2, uint64_t npos, unsigned bb, int extra,
+                      DBuf<uint32_t> &bucket, int &bits_out)
+{
+    size_t tmp = 0;
+    HIPCHK(rocprim::radix_sort_keys(nullptr, tmp, ent.p, ent2.p, (size_t)npos, bb, 64u, e->st));
+    CHK(e->d_tmp.ensure(tmp));
+    HIPCHK(rocprim::radix_sort_keys(e->d_tmp.p, tmp, ent.p, ent2.p, (size_t)npos, bb, 64u, e->st));
+    const char *ibv = getenv("RC_INDEX_BITS_MAX");
+    const int bmax = ibv ? std::max(16, std::min(30, atoi(ibv))) : 28;
+    int bits = 16;
+    while (bits < bmax && (1ull << bits) < (npos << extra)) bits++;
+    bits_out = bits;
+    CHK(bucket.ensure((1ull << bits) + 1));
+    launch_bucket_fill(ent2.p, npos, bits, bucket.p, e->st);
+    return RC_OK;
+}
+
 // A seed index: every 16-mer position of the transcripts txl[0, n_tx), whose
 // slots koff / kpos (closed form when no base is ambiguous) give the order.
 static int build_index_of(rc_engine *e, const TxInfo *txl, uint32_t n_tx, uint64_t npos, const uint64_t *kpos,
@@ -970,21 +997,7 @@ static int build_index_of(rc_engine *e, const TxInfo *txl, uint32_t n_tx, uint64
     // rocPRIM sorts up to 2^20 items with a merge sort that did not keep that
     // order for a partial bit range: there, sort all 64 bits (same result,
     // positions are unique).
-    const unsigned bb = npos <= (1ull << 20) ? 0u : 32u;
-    size_t tmp = 0;
-    HIPCHK(rocprim::radix_sort_keys(nullptr, tmp, ent.p, ent2.p, (size_t)npos, bb, 64u, e->st));
-    CHK(e->d_tmp.ensure(tmp));
-    HIPCHK(rocprim::radix_sort_keys(e->d_tmp.p, tmp, ent.p, ent2.p, (size_t)npos, bb, 64u, e->st));
-    // bucket table over the top k-mer bits: about one bucket per indexed
-    // position, at most 2^28 (RC_INDEX_BITS_MAX; 28 measured best at C3 -- a
-    // 1 GiB table instead of 4 GiB, same seed-kernel time)
-    const char *ibv = getenv("RC_INDEX_BITS_MAX");
-    const int bmax = ibv ? std::max(16, std::min(30, atoi(ibv))) : 28;
-    int bits = 16;
-    while (bits < bmax && (1ull << bits) < npos) bits++;
-    bits_out = bits;
-    CHK(bucket.ensure((1ull << bits) + 1));
-    launch_bucket_fill(ent2.p, npos, bits, bucket.p, e->st);
+    CHK(sort_index(e, ent, ent2, npos, npos <= (1ull << 20) ? 0u : 32u, 0, bucket, bits_out));
     n_out = npos;
     return RC_OK;
 }
@@ -996,41 +1009,37 @@ static int build_index(rc_engine *e)
                           e->d_ent2, e->d_bucket, e->index_bits, e->n_index);
 }
 
-// Shared searches with DUST: the tile's transcripts holding a masked base (a
-// reverse search whose SUBJECT is such a transcript may have seeds the
-// forward pass does not find: runs whose forward words are all masked), their
-// per-transcript flags for the seed kernel, and their own index.
+// Shared searches with DUST: the reverse pass's index. A reverse search whose
+// SUBJECT a holds a masked base may have seeds the forward pass does not find
+// (runs none of whose aligned words of a is usable); every 16-mer of such a
+// run has a masked base of a nearby, so the index holds only the positions of
+// masked transcripts with a masked base in [pos - 16, pos + 48)
+// (near_fill_kernel), sorted on all 64 key bits, with 4 buckets per entry.
 static int build_masked_index(rc_engine *e)
 {
     const uint32_t n = e->tile_ntx;
     CHK(e->d_tile_masked.ensure(std::max<uint32_t>(n, 1)));
     launch_tx_masked(e->d_tile_tx.p, n, e->d_dmask.p + 1, e->d_tile_masked.p, e->st);
     HIPCHK(hipGetLastError());
-    std::vector<uint8_t> hm(n);
-    if (n) HIPCHK(hipMemcpyAsync(hm.data(), e->d_tile_masked.p, n, hipMemcpyDeviceToHost, e->st));
-    HIPCHK(hipStreamSynchronize(e->st));
-    std::vector<uint8_t> txm(e->h_tx.size(), 0);
-    std::vector<TxInfo> mt;
-    std::vector<uint64_t> mk(1, 0);
-    for (uint32_t i = 0; i < n; i++) {
-        txm[e->tile_gid[i]] = hm[i];
-        if (!hm[i]) continue;
-        const TxInfo &t = e->h_tx[e->tile_gid[i]];
-        mt.push_back(t);
-        mk.push_back(mk.back() + (uint64_t)(t.len >= (uint32_t)W16 ? t.len - W16 + 1 : 0));
+    CHK(e->d_rctr.ensure(4));
+    if (!e->mnear_cap) e->mnear_cap = e->tile_total / 32 + (1u << 20);
+    unsigned long long cnt = 0;
+    for (;;) {
+        CHK(e->d_ment.ensure(e->mnear_cap));
+        CHK(e->d_ment2.ensure(e->mnear_cap));
+        HIPCHK(hipMemsetAsync(e->d_rctr.p, 0, sizeof(unsigned long long), e->st));
+        launch_near_fill(e->has_amb, e->d_tile_tx.p, n, e->d_tile_masked.p, e->d_F.p + FRONT_PAD,
+                         e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr, e->d_dmask.p + 1, e->d_ment.p, e->mnear_cap,
+                         e->d_rctr.p, e->st);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(&cnt, e->d_rctr.p, sizeof cnt, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipStreamSynchronize(e->st));
+        if (cnt <= e->mnear_cap) break;
+        e->mnear_cap = cnt + cnt / 4 + (1u << 20);
     }
-    CHK(e->d_tx_masked.ensure(std::max<size_t>(txm.size(), 1)));
-    if (!txm.empty())
-        HIPCHK(hipMemcpyAsync(e->d_tx_masked.p, txm.data(), txm.size(), hipMemcpyHostToDevice, e->st));
-    CHK(e->d_mtile_tx.ensure(std::max<size_t>(mt.size(), 1)));
-    CHK(e->d_mkpos_off.ensure(mk.size()));
-    if (!mt.empty())
-        HIPCHK(hipMemcpyAsync(e->d_mtile_tx.p, mt.data(), mt.size() * sizeof(TxInfo), hipMemcpyHostToDevice, e->st));
-    HIPCHK(hipMemcpyAsync(e->d_mkpos_off.p, mk.data(), mk.size() * 8, hipMemcpyHostToDevice, e->st));
-    e->n_masked_tx = (uint32_t)mt.size();
-    CHK(build_index_of(e, e->d_mtile_tx.p, (uint32_t)mt.size(), mk.back(), e->d_mkpos_off.p, e->d_ment, e->d_ment2,
-                       e->d_mbucket, e->mindex_bits, e->n_mindex));
-    HIPCHK(hipStreamSynchronize(e->st));   // host vectors outlive the copies
+    CHK(sort_index(e, e->d_ment, e->d_ment2, cnt, 0u, 2, e->d_mbucket, e->mindex_bits));
+    e->n_mindex = cnt;
+    e->tm.near_index += (double)cnt;
     return RC_OK;
 }
 
@@ -1092,6 +1101,90 @@ static void tile_plan(rc_engine *e, int ti, std::vector<uint64_t> &tmask, std::v
         runs.push_back({s, t});
         s = t;
     }
+}
+
+// The reverse pass of shared searches with DUST: queries = the
+// higher sample of each pair of tile ti, subjects = the near-mask index ixm.
+// It keeps only the reverse-search runs the forward pass cannot see, as SEED_R
+// seeds in forward-candidate coordinates; they are sorted by the forward
+// query's gene (rs_key, rs_idx) for the forward pass to merge. n_rs = count.
+static int reverse_pass(rc_engine *e, int ti, const Db &db, const Index &ixm, uint32_t &n_rs)
+{
+    const int N = (int)e->samples.size();
+    std::vector<uint64_t> rmask((size_t)4 * N, 0);
+    std::vector<char> q(N, 0);
+    for (auto &pr : e->tiles[ti].pairs) {
+        rmask[4 * pr.second + (pr.first >> 6)] |= 1ull << (pr.first & 63);
+        q[pr.second] = 1;
+    }
+    std::vector<std::pair<int, int>> runs;
+    for (int s0 = 0; s0 < N;) {
+        if (!q[s0]) {
+            s0++;
+            continue;
+        }
+        int t = s0;
+        while (t < N && q[t]) t++;
+        runs.push_back({s0, t});
+        s0 = t;
+    }
+    CHK(e->d_rtmask.ensure(rmask.size()));
+    HIPCHK(hipMemcpyAsync(e->d_rtmask.p, rmask.data(), rmask.size() * 8, hipMemcpyHostToDevice, e->st));
+    CHK(e->d_rctr.ensure(4));
+    CHK(e->d_big_out.ensure(std::max<uint64_t>(e->big_list_cap, 1)));
+    if (!e->rseed_cap) e->rseed_cap = 1u << 20;
+    unsigned long long cnt = 0;
+    for (;;) {
+        CHK(e->d_rseeds.ensure(e->rseed_cap));
+        CHK(e->d_rseed_gene.ensure(e->rseed_cap));
+        HIPCHK(hipMemsetAsync(e->d_rctr.p + 1, 0, 2 * sizeof(unsigned long long), e->st));
+        HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
+        for (auto &r : runs) {
+            SeedParams S{};
+            S.word = e->o.word_size;
+            S.stride = e->o.word_size - W16 + 1;
+            const char *pm = getenv("RC_SEED_PRE");
+            S.pre_mode = pm ? atoi(pm) : 1;
+            S.rev = 1;
+            S.tx_pos = e->d_tx_pos.p;
+            S.rseeds = e->d_rseeds.p;
+            S.rseed_gene = e->d_rseed_gene.p;
+            S.rseed_cap = e->rseed_cap;
+            S.rseed_n = e->d_rctr.p + 1;
+            S.gene_begin = e->sample_gene_begin[r.first];
+            S.gene_end = e->sample_gene_begin[r.second];
+            S.tmask = e->d_rtmask.p;
+            S.status = e->d_status.p;
+            S.big_out = e->d_big_out.p;   // (never used: the pass keeps no seeds of its own)
+            S.big_n = e->d_rctr.p + 2;
+            S.big_list_cap = 0;
+            launch_seed(e->has_amb, db, ixm, S, e->st);
+            HIPCHK(hipGetLastError());
+        }
+        unsigned int status = 0;
+        HIPCHK(hipMemcpyAsync(&cnt, e->d_rctr.p + 1, sizeof cnt, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipStreamSynchronize(e->st));
+        if (status & 2u) return fail(RC_E_LIMIT, "a query gene has more than 127 isoforms");
+        if (cnt <= e->rseed_cap) break;
+        e->rseed_cap = cnt + cnt / 4 + 1024;
+    }
+    if (cnt > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "more than 2^32 reverse-only seeds in a tile");
+    n_rs = (uint32_t)cnt;
+    e->n_rseeds += cnt;
+    e->tm.reverse_seeds += (double)cnt;
+    if (cnt) {
+        CHK(e->d_rs_key.ensure(cnt));
+        CHK(e->d_rs_idx.ensure(cnt));
+        size_t tmp = 0;
+        rocprim::counting_iterator<uint32_t> iota(0u);
+        HIPCHK(rocprim::radix_sort_pairs(nullptr, tmp, e->d_rseed_gene.p, e->d_rs_key.p, iota, e->d_rs_idx.p,
+                                         (size_t)cnt, 0u, 32u, e->st));
+        CHK(e->d_tmp.ensure(tmp));
+        HIPCHK(rocprim::radix_sort_pairs(e->d_tmp.p, tmp, e->d_rseed_gene.p, e->d_rs_key.p, iota, e->d_rs_idx.p,
+                                         (size_t)cnt, 0u, 32u, e->st));
+    }
+    return RC_OK;
 }
 
 static int load_external(rc_engine *e)
@@ -1210,8 +1303,8 @@ static int align_tile(rc_engine *e, int ti)
         const char *sv = getenv("RC_SHARE");
         e->share = !e->o.symmetric && !(sv && atoi(sv) == 0);
     }
-    // shared searches with DUST: the reverse searches whose subject holds a
-    // masked base come from a reverse pass over those transcripts' own index
+    // shared searches with DUST: reverse-search runs with no usable word of
+    // the forward query inside come from a reverse pass over a near-mask index
     const bool revpass = e->share && dust;
     if (revpass) CHK(build_masked_index(e));
     HIPCHK(hipEventRecord(e->ev[2], e->st));
@@ -1219,27 +1312,7 @@ static int align_tile(rc_engine *e, int ti)
     std::vector<uint64_t> tmask;
     std::vector<std::pair<int, int>> runs;
     tile_plan(e, ti, tmask, runs);
-    const size_t R = runs.size();   // forward runs; reverse-pass runs follow
-    if (revpass && e->n_mindex) {
-        std::vector<uint64_t> rmask((size_t)4 * N, 0);
-        std::vector<char> q(N, 0);
-        for (auto &pr : e->tiles[ti].pairs) {
-            rmask[4 * pr.second + (pr.first >> 6)] |= 1ull << (pr.first & 63);
-            q[pr.second] = 1;
-        }
-        for (int s0 = 0; s0 < N;) {
-            if (!q[s0]) {
-                s0++;
-                continue;
-            }
-            int t = s0;
-            while (t < N && q[t]) t++;
-            runs.push_back({s0, t});
-            s0 = t;
-        }
-        tmask.insert(tmask.end(), rmask.begin(), rmask.end());
-    }
-    const size_t RT = runs.size();
+    const size_t R = runs.size(), RT = R;
     CHK(e->d_tmask.ensure(tmask.size()));
     HIPCHK(hipMemcpyAsync(e->d_tmask.p, tmask.data(), tmask.size() * 8, hipMemcpyHostToDevice, e->st));
     // per run: its genes [g0, g1) and its slice of the (gene, sample) arrays
@@ -1258,15 +1331,13 @@ static int align_tile(rc_engine *e, int ti)
     CHK(e->d_shard_cnt.ensure(2 * NSHARD));
     CHK(e->d_shard_prefix.ensure(NSHARD + 1));
     {
-        // (query gene, subject sample) searches of the tile; a reverse-pass
-        // search only meets its subjects' masked transcripts (weighted by them)
+        // (query gene, subject sample) searches of the tile
         uint64_t nb = 1;
         for (size_t r = 0; r < RT; r++)
             for (int q = runs[r].first; q < runs[r].second; q++) {
                 uint64_t ns = 0;
-                for (int w = 0; w < 4; w++) ns += (uint64_t)__builtin_popcountll(tmask[(r < R ? 0 : 4 * (size_t)N) + 4 * q + w]);
-                const uint64_t g = e->sample_gene_begin[q + 1] - e->sample_gene_begin[q];
-                nb += r < R ? g * ns : (g * ns * (e->n_mindex + 1)) / (e->n_index + 1) + g;
+                for (int w = 0; w < 4; w++) ns += (uint64_t)__builtin_popcountll(tmask[4 * q + w]);
+                nb += (uint64_t)(e->sample_gene_begin[q + 1] - e->sample_gene_begin[q]) * ns;
             }
         e->seed_cap = std::max<uint64_t>(e->seed_cap, nb * 16 / NSHARD + 4096);
         e->cand_cap = std::max<uint64_t>(e->cand_cap, nb * 2 / NSHARD + 1024);
@@ -1288,6 +1359,8 @@ static int align_tile(rc_engine *e, int ti)
     unsigned long long *big_n = e->d_count.p + 12, *big_retry_n = e->d_count.p + 13;
     uint64_t n_big = 0;
     HIPCHK(hipEventRecord(e->ev[3], e->st));
+    uint32_t n_rs = 0;
+    if (revpass && e->n_mindex) CHK(reverse_pass(e, ti, db, ixm, n_rs));
     for (int attempt = 0;; attempt++) {
         if (attempt == 6) return fail(RC_E_NOMEM, "seed/candidate buffers kept overflowing");
         if (e->seed_cap * NSHARD > 0xFFFFFFFFull || e->cand_cap * NSHARD > 0xFFFFFFFFull)
@@ -1305,7 +1378,6 @@ static int align_tile(rc_engine *e, int ti)
         bool again = false;
         n_big = 0;
         for (size_t r = 0; r < RT && !again; r++) {
-            const bool rev = r >= R;
             HIPCHK(hipMemsetAsync(big_n, 0, 2 * sizeof(unsigned long long), e->st));
             SeedParams S{};
             S.word = e->o.word_size;
@@ -1315,9 +1387,12 @@ static int align_tile(rc_engine *e, int ti)
                 S.pre_mode = pm ? atoi(pm) : 1;
             }
             S.sym = e->o.symmetric;
-            S.share = e->share && !rev ? 1 : 0;
-            S.rev = rev ? 1 : 0;
-            S.tx_masked = revpass ? e->d_tx_masked.p : nullptr;
+            S.share = e->share ? 1 : 0;
+            S.tx_pos = e->d_tx_pos.p;
+            S.rs_rec = e->d_rseeds.p;
+            S.rs_key = e->d_rs_key.p;
+            S.rs_idx = e->d_rs_idx.p;
+            S.rs_n = n_rs;
             S.list2 = e->d_list2.p;
             S.list2_n = e->d_count.p + 16;
             S.gene_begin = rg0[r];
@@ -1330,14 +1405,14 @@ static int align_tile(rc_engine *e, int ti)
             S.cand_count = e->d_shard_cnt.p + NSHARD;
             S.gc_off = e->d_gc_off.p + gcb[r];
             S.gc_cnt = e->d_gc_cnt.p + gcb[r];
-            S.tmask = e->d_tmask.p + (rev ? 4 * (size_t)N : 0);
+            S.tmask = e->d_tmask.p;
             S.status = e->d_status.p;
             S.big_out = e->d_big_out.p;
             S.big_n = big_n;
             S.big_retry_n = big_retry_n;
             S.big_list_cap = e->big_list_cap;
             S.prof = e->d_prof.p;
-            launch_seed(e->has_amb, db, rev ? ixm : ix, S, e->st);
+            launch_seed(e->has_amb, db, ix, S, e->st);
             HIPCHK(hipGetLastError());
             unsigned int status = 0;
             unsigned long long nb = 0;   // (big_n: d_count[12], next to the extension's counters [0, 11))
@@ -1378,7 +1453,7 @@ static int align_tile(rc_engine *e, int ti)
                 B.big_segT = e->d_big_segT.p;
                 for (uint64_t c0 = 0; c0 < nb; c0 += chunk) {
                     B.big_list = e->d_big_list.p + c0;
-                    launch_seed_big(e->has_amb, db, rev ? ixm : ix, B, (uint32_t)std::min<uint64_t>(chunk, nb - c0), e->st);
+                    launch_seed_big(e->has_amb, db, ix, B, (uint32_t)std::min<uint64_t>(chunk, nb - c0), e->st);
                     HIPCHK(hipGetLastError());
                 }
                 unsigned long long nr = 0;
@@ -1571,10 +1646,6 @@ static int align_tile(rc_engine *e, int ti)
         G.cand_nh = e->d_cand_nh_r.p;
         G.cand_hsp = e->d_cand_hsp_r.p;
         G.cand_ovf = e->d_cand_ovf_r.p;
-        G.cands = e->d_cands.p;
-        G.cand_nh_f = e->d_cand_nh.p;
-        G.cand_hsp_f = e->d_cand_hsp.p;
-        G.cand_ovf_f = e->d_cand_ovf.p;
     }
     if (mirror) {
         CHK(e->d_mcnt.ensure(ngrp + 1));

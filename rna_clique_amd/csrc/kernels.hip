@@ -771,6 +771,54 @@ void launch_tx_masked(const TxInfo *txl, uint32_t n, const uint64_t *dmask, uint
     if (n) hipLaunchKernelGGL(tx_masked_kernel, dim3((n + 255) / 256), dim3(256), 0, st, txl, n, dmask, out);
 }
 
+// The reverse pass's index (shared searches with DUST): the 16-mer positions
+// of masked transcripts with a DUST-masked base in [pos - 16, pos + 48). A
+// run between a and b none of whose aligned words of a is usable has a masked
+// base of a within [pos - 12, pos + 28) of every 16-mer pos it holds (any 28
+// bases of the run hold a whole word of a's grid, and that word is masked),
+// so the hits of such runs are all here. One wave per
+// transcript, one atomic per 64 positions: the order is arbitrary and the
+// sort orders all 64 key bits. Entries past `cap` are counted, not written.
+template <bool AMB>
+__global__ __launch_bounds__(256) void near_fill_kernel(const TxInfo *__restrict__ tx, uint32_t n_tx,
+                                                        const uint8_t *__restrict__ masked,
+                                                        const uint64_t *__restrict__ F,
+                                                        const uint64_t *__restrict__ AF,
+                                                        const uint64_t *__restrict__ dmask, uint64_t *__restrict__ ent,
+                                                        uint64_t cap, unsigned long long *count)
+{
+    const uint32_t t = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (t >= n_tx || !masked[t]) return;
+    const TxInfo ti = tx[t];
+    const int64_t nwin = (int64_t)ti.len - W16 + 1;
+    for (int64_t o0 = 0; o0 < nwin; o0 += 64) {
+        const int64_t o = o0 + lane;
+        const uint64_t p = ti.start + (uint64_t)o;
+        bool ok = o < nwin && win_bits(dmask, (int64_t)p - 16) != 0;
+        if (AMB && ok) ok = (win(AF, p) & 0xFFFFFFFFull) == 0;
+        const uint64_t m = __ballot(ok);
+        if (!m) continue;
+        unsigned long long b = 0;
+        if (lane == 0) b = atomicAdd(count, (unsigned long long)__popcll(m));
+        b = (unsigned long long)__shfl((long long)b, 0);
+        const uint64_t i = b + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (ok && i < cap) ent[i] = ((uint64_t)(uint32_t)win(F, p) << 32) | p;
+    }
+}
+
+void launch_near_fill(bool amb, const TxInfo *tx, uint32_t n_tx, const uint8_t *masked, const uint64_t *F,
+                      const uint64_t *AF, const uint64_t *dmask, uint64_t *ent, uint64_t cap,
+                      unsigned long long *count, hipStream_t st)
+{
+    if (!n_tx) return;
+    const dim3 g((n_tx + 3) / 4);
+    if (amb)
+        hipLaunchKernelGGL(near_fill_kernel<true>, g, dim3(256), 0, st, tx, n_tx, masked, F, AF, dmask, ent, cap, count);
+    else
+        hipLaunchKernelGGL(near_fill_kernel<false>, g, dim3(256), 0, st, tx, n_tx, masked, F, AF, dmask, ent, cap, count);
+}
+
 // After pass 2 and the scans: each item's rows and edges from its slots to
 // their offsets, labels made pair-global (F rows: + the item's F_sel base; R
 // rows: + the pair's F_sel total + the item's R_sel base).

@@ -65,6 +65,10 @@ def test_alignment_modes(native, monkeypatch, symmetric, dust, share):
     msgs, summary = full_check(eng, samples)
     assert not msgs, "\n".join(msgs[:10])
     assert summary["hsps"] > 0 and summary["ideal_nodes"] > 0
+    if share and dust == (20, 64, 1):
+        # this corpus has reverse-search runs no forward word finds (poly-A
+        # context): the reverse pass's seeds merged into forward candidates
+        assert eng.timings()["reverse_seeds"] > 0
 
 
 @pytest.mark.parametrize("dust", [None, (30, 64, 1), (4, 32, 1), (11, 20, 2), (49, 64, 1)])
