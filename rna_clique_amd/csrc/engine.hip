@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <array>
+#include <functional>
 #include <map>
 #include <numeric>
 #include <string>
@@ -353,7 +354,7 @@ struct rc_engine {
     std::vector<unsigned long long> h_num, h_den, h_num_all, h_den_all, h_stats;
     rc_timing tm{};
     hipEvent_t ev[16] = {};
-    hipEvent_t evd[2] = {};   // DUST start / end on st2
+    hipEvent_t evd[3] = {};   // DUST start / end on st2, its start condition on st
 
     ~rc_engine()
     {
@@ -969,7 +970,7 @@ static int sort_index(rc_engine *e, DBuf<uint64_t> &ent, DBuf<uint64_t> &ent2, u
 // slots koff / kpos (closed form when no base is ambiguous) give the order.
 static int build_index_of(rc_engine *e, const TxInfo *txl, uint32_t n_tx, uint64_t npos, const uint64_t *kpos,
                           DBuf<uint64_t> &ent, DBuf<uint64_t> &ent2, DBuf<uint32_t> &bucket, int &bits_out,
-                          uint64_t &n_out)
+                          uint64_t &n_out, const std::function<int()> &after_fill = nullptr)
 {
     const bool amb = e->has_amb;
     const uint64_t *offs = kpos;
@@ -992,6 +993,7 @@ static int build_index_of(rc_engine *e, const TxInfo *txl, uint32_t n_tx, uint64
     CHK(ent2.ensure(std::max<uint64_t>(npos, 1)));
     if (n_tx) launch_kmer_fill(amb, txl, n_tx, e->d_F.p + FRONT_PAD, amb ? e->d_AF.p + FRONT_PAD : nullptr,
                                offs, ent.p, e->st);
+    if (after_fill) CHK(after_fill());
     // sort on the k-mer (bits 32..63); the fill order is position order and the
     // onesweep radix sort is stable, so positions stay ascending per k-mer.
     // rocPRIM sorts up to 2^20 items with a merge sort that did not keep that
@@ -1003,17 +1005,17 @@ static int build_index_of(rc_engine *e, const TxInfo *txl, uint32_t n_tx, uint64
 }
 
 // The seed index of the loaded tile: every 16-mer position of its transcripts.
-static int build_index(rc_engine *e)
+static int build_index(rc_engine *e, const std::function<int()> &after_fill = nullptr)
 {
     return build_index_of(e, e->d_tile_tx.p, e->tile_ntx, e->h_koff[e->tile_ntx], e->d_kpos_off.p, e->d_ent,
-                          e->d_ent2, e->d_bucket, e->index_bits, e->n_index);
+                          e->d_ent2, e->d_bucket, e->index_bits, e->n_index, after_fill);
 }
 
 // Shared searches with DUST: the reverse pass's index. A reverse search whose
 // SUBJECT a holds a masked base may have seeds the forward pass does not find
 // (runs none of whose aligned words of a is usable); every 16-mer of such a
 // run has a masked base of a nearby, so the index holds only the positions of
-// masked transcripts with a masked base in [pos - 16, pos + 48)
+// masked transcripts with a masked base in [pos - 12, pos + 28)
 // (near_fill_kernel), sorted on all 64 key bits, with 4 buckets per entry.
 static int build_masked_index(rc_engine *e)
 {
@@ -1276,16 +1278,19 @@ static int align_tile(rc_engine *e, int ti)
         HIPCHK(hipMemsetAsync(e->d_dmask.p, 0, mw * 8, e->st));
     }
     HIPCHK(hipEventRecord(e->ev[1], e->st));
-    if (dust) {
-        // DUST masks of the tile's transcripts (the query side), bit per base,
-        // on the second stream: a compute-bound scan beside the HBM-bound
-        // index build (RC_DUST_WAVES caps its waves per SIMD)
+    // DUST masks of the tile's transcripts (the query side), bit per base, on
+    // the second stream: a compute-bound scan beside the HBM-bound index
+    // build. It starts once the k-mer fill is done (beside the radix sort):
+    // started with the fill, both ran at a third of their speed
+    // (RC_DUST_EARLY=1 restores that order for A/B runs).
+    auto start_dust = [&]() -> int {
         const uint32_t dblocks = 256 * 20;   // at least the resident waves of the chunk kernel: their scratch
         CHK(e->d_dust_scratch.ensure(dust_scratch_words(dblocks)));
         CHK(e->d_dust_events.ensure(dust_event_words(dblocks)));
         const char *dwv = getenv("RC_DUST_WAVES");
         const int dwaves = dwv ? atoi(dwv) : 0;   // 0: every resident wave (measured best; 1-3 starve DUST)
-        HIPCHK(hipStreamWaitEvent(e->st2, e->ev[1], 0));
+        HIPCHK(hipEventRecord(e->evd[2], e->st));
+        HIPCHK(hipStreamWaitEvent(e->st2, e->evd[2], 0));
         HIPCHK(hipEventRecord(e->evd[0], e->st2));
         launch_dust(e->has_amb, total, e->d_F.p + FRONT_PAD, e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr,
                     e->d_txstart.p + 1, e->d_tile_tx.p, e->tile_ntx, e->o.dust_level, e->o.dust_window,
@@ -1293,8 +1298,12 @@ static int align_tile(rc_engine *e, int ti)
                     e->st2);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e->evd[1], e->st2));
-    }
-    CHK(build_index(e));
+        return RC_OK;
+    };
+    const char *dev = getenv("RC_DUST_EARLY");
+    const bool dust_early = dev && atoi(dev);
+    if (dust && dust_early) CHK(start_dust());
+    CHK(build_index(e, dust && !dust_early ? std::function<int()>(start_dust) : nullptr));
     HIPCHK(hipGetLastError());
     if (dust) HIPCHK(hipStreamWaitEvent(e->st, e->evd[1], 0));
     {

@@ -14,6 +14,7 @@
 // oracle/post_oracle.py (post-alignment, pinned to the reference).
 #include "device.h"
 
+#include <algorithm>
 #include <climits>
 
 namespace rcg {
@@ -123,8 +124,11 @@ __global__ void kmer_count_kernel(const TxInfo *__restrict__ tx, uint32_t n_tx,
     if (threadIdx.x == 0) cnt[t] = s;
 }
 
-// One block per transcript; windows in (gtx, offset) order so that a stable
-// radix sort on the key keeps each key's entries sorted by (gtx, offset).
+// One wave per transcript, grid-stride over the transcripts (a block per
+// transcript spent more time in dispatch than in its stores, and slowed DUST
+// beside it); windows in (gtx, offset) order so that a stable radix sort on
+// the key keeps each key's entries sorted by (gtx, offset). AMB: windows with
+// an ambiguous base are left out (compacted within the wave).
 template <bool AMB>
 __global__ __launch_bounds__(256) void kmer_fill_kernel(const TxInfo *__restrict__ tx, uint32_t n_tx,
                                                         const uint64_t *__restrict__ F,
@@ -132,39 +136,25 @@ __global__ __launch_bounds__(256) void kmer_fill_kernel(const TxInfo *__restrict
                                                         const uint64_t *__restrict__ out_off,
                                                         uint64_t *__restrict__ ent)
 {
-    const uint32_t t = blockIdx.x;
-    if (t >= n_tx) return;
-    const TxInfo ti = tx[t];
-    const int64_t nwin = (int64_t)ti.len - W16 + 1;
-    if (nwin <= 0) return;
-    uint64_t base = out_off[t];
-    __shared__ uint32_t wcnt[4];
-    for (int64_t o0 = 0; o0 < nwin; o0 += blockDim.x) {
-        const int64_t o = o0 + threadIdx.x;
-        bool ok = o < nwin;
-        uint32_t key = 0;
-        if (ok) {
-            key = (uint32_t)win(F, ti.start + o);
-            if (AMB) ok = (win(AF, ti.start + o) & 0xFFFFFFFFull) == 0;
-        }
-        if (!AMB) {
-            if (ok) ent[base + o] = ((uint64_t)key << 32) | (ti.start + (uint64_t)o);
-        } else {
-            const uint64_t m = __ballot(ok);
-            const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-            const uint32_t before = __popcll(m & ((1ull << lane) - 1ull));
-            if (lane == 0) wcnt[wid] = __popcll(m);
-            __syncthreads();
-            uint32_t woff = 0, tot = 0;
-            for (int i = 0; i < (int)(blockDim.x >> 6); i++) {
-                if (i < wid) woff += wcnt[i];
-                tot += wcnt[i];
+    const int lane = threadIdx.x & 63;
+    const uint32_t nwave = gridDim.x * 4u;
+    for (uint32_t t = blockIdx.x * 4u + (threadIdx.x >> 6); t < n_tx; t += nwave) {
+        const TxInfo ti = tx[t];
+        const int64_t nwin = (int64_t)ti.len - W16 + 1;
+        uint64_t base = out_off[t];
+        for (int64_t o0 = 0; o0 < nwin; o0 += 64) {
+            const int64_t o = o0 + lane;
+            bool ok = o < nwin;
+            const uint64_t p = ti.start + (uint64_t)o;
+            const uint32_t key = ok ? (uint32_t)win(F, p) : 0u;
+            if (!AMB) {
+                if (ok) ent[base + (uint64_t)o] = ((uint64_t)key << 32) | p;
+            } else {
+                if (ok) ok = (win(AF, p) & 0xFFFFFFFFull) == 0;
+                const uint64_t m = __ballot(ok);
+                if (ok) ent[base + (uint64_t)__popcll(m & ((1ull << lane) - 1ull))] = ((uint64_t)key << 32) | p;
+                base += (uint64_t)__popcll(m);
             }
-            if (ok) {
-                ent[base + woff + before] = ((uint64_t)key << 32) | (ti.start + (uint64_t)o);
-            }
-            base += tot;
-            __syncthreads();
         }
     }
 }
@@ -175,6 +165,7 @@ __global__ __launch_bounds__(256) void kmer_fill_kernel(const TxInfo *__restrict
 // entries (plus the one before) with every load in flight at once, then the
 // bucket slots from the previous entry's bucket (exclusive) to each entry's.
 constexpr int BF_PER = 4;
+constexpr uint32_t FILL_BLOCKS = 256 * 8;   // grid of the wave-per-transcript fill kernels
 __global__ __launch_bounds__(256) void bucket_fill_kernel(const uint64_t *__restrict__ ent, uint64_t n, int bits,
                                                           uint32_t *__restrict__ bucket)
 {
@@ -739,10 +730,12 @@ void launch_kmer_count(const TxInfo *tx, uint32_t n_tx, const uint64_t *AF, uint
 void launch_kmer_fill(bool amb, const TxInfo *tx, uint32_t n_tx, const uint64_t *F, const uint64_t *AF,
                       const uint64_t *out_off, uint64_t *ent, hipStream_t st)
 {
+    if (!n_tx) return;
+    const dim3 g(std::min<uint32_t>((n_tx + 3) / 4, FILL_BLOCKS));
     if (amb)
-        hipLaunchKernelGGL(kmer_fill_kernel<true>, dim3(n_tx), dim3(256), 0, st, tx, n_tx, F, AF, out_off, ent);
+        hipLaunchKernelGGL(kmer_fill_kernel<true>, g, dim3(256), 0, st, tx, n_tx, F, AF, out_off, ent);
     else
-        hipLaunchKernelGGL(kmer_fill_kernel<false>, dim3(n_tx), dim3(256), 0, st, tx, n_tx, F, AF, out_off, ent);
+        hipLaunchKernelGGL(kmer_fill_kernel<false>, g, dim3(256), 0, st, tx, n_tx, F, AF, out_off, ent);
 }
 
 void launch_bucket_fill(const uint64_t *ent, uint64_t n, int bits, uint32_t *bucket, hipStream_t st)
@@ -772,11 +765,12 @@ void launch_tx_masked(const TxInfo *txl, uint32_t n, const uint64_t *dmask, uint
 }
 
 // The reverse pass's index (shared searches with DUST): the 16-mer positions
-// of masked transcripts with a DUST-masked base in [pos - 16, pos + 48). A
+// of masked transcripts with a DUST-masked base in [pos - 12, pos + 28). A
 // run between a and b none of whose aligned words of a is usable has a masked
-// base of a within [pos - 12, pos + 28) of every 16-mer pos it holds (any 28
-// bases of the run hold a whole word of a's grid, and that word is masked),
-// so the hits of such runs are all here. One wave per
+// base of a there for every 16-mer pos it holds: the 28 bases of the run
+// nearest to [pos, pos + 16) lie in that range and hold a whole word of a's
+// grid (13 consecutive starts hold one), and that word is masked. So the hits
+// of such runs are all here. One wave per
 // transcript, one atomic per 64 positions: the order is arbitrary and the
 // sort orders all 64 key bits. Entries past `cap` are counted, not written.
 template <bool AMB>
@@ -787,23 +781,37 @@ __global__ __launch_bounds__(256) void near_fill_kernel(const TxInfo *__restrict
                                                         const uint64_t *__restrict__ dmask, uint64_t *__restrict__ ent,
                                                         uint64_t cap, unsigned long long *count)
 {
-    const uint32_t t = blockIdx.x * 4u + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (t >= n_tx || !masked[t]) return;
-    const TxInfo ti = tx[t];
-    const int64_t nwin = (int64_t)ti.len - W16 + 1;
-    for (int64_t o0 = 0; o0 < nwin; o0 += 64) {
-        const int64_t o = o0 + lane;
-        const uint64_t p = ti.start + (uint64_t)o;
-        bool ok = o < nwin && win_bits(dmask, (int64_t)p - 16) != 0;
+    const uint32_t nwave = gridDim.x * 4u, t0 = blockIdx.x * 4u + (threadIdx.x >> 6);
+    // the positions of this wave's transcripts: counted, one atomic for all
+    // of them, then written (one counter for every wave: an atomic per 64
+    // positions serialised on it)
+    auto near = [&](const TxInfo &ti, int64_t o, uint64_t &p) -> bool {
+        p = ti.start + (uint64_t)o;
+        bool ok = o <= (int64_t)ti.len - W16 && (win_bits(dmask, (int64_t)p - 12) & ((1ull << 40) - 1ull)) != 0;
         if (AMB && ok) ok = (win(AF, p) & 0xFFFFFFFFull) == 0;
-        const uint64_t m = __ballot(ok);
-        if (!m) continue;
-        unsigned long long b = 0;
-        if (lane == 0) b = atomicAdd(count, (unsigned long long)__popcll(m));
-        b = (unsigned long long)__shfl((long long)b, 0);
-        const uint64_t i = b + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
-        if (ok && i < cap) ent[i] = ((uint64_t)(uint32_t)win(F, p) << 32) | p;
+        return ok;
+    };
+    uint64_t n = 0, p = 0;
+    for (uint32_t t = t0; t < n_tx; t += nwave) {
+        if (!masked[t]) continue;
+        const TxInfo ti = tx[t];
+        for (int64_t o0 = 0; o0 + W16 <= (int64_t)ti.len; o0 += 64) n += (uint64_t)__popcll(__ballot(near(ti, o0 + lane, p)));
+    }
+    if (!n) return;
+    unsigned long long b = 0;
+    if (lane == 0) b = atomicAdd(count, (unsigned long long)n);
+    b = (unsigned long long)__shfl((long long)b, 0);
+    for (uint32_t t = t0; t < n_tx; t += nwave) {
+        if (!masked[t]) continue;
+        const TxInfo ti = tx[t];
+        for (int64_t o0 = 0; o0 + W16 <= (int64_t)ti.len; o0 += 64) {
+            const bool ok = near(ti, o0 + lane, p);
+            const uint64_t m = __ballot(ok);
+            const uint64_t i = b + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
+            if (ok && i < cap) ent[i] = ((uint64_t)(uint32_t)win(F, p) << 32) | p;
+            b += (uint64_t)__popcll(m);
+        }
     }
 }
 
@@ -812,7 +820,7 @@ void launch_near_fill(bool amb, const TxInfo *tx, uint32_t n_tx, const uint8_t *
                       unsigned long long *count, hipStream_t st)
 {
     if (!n_tx) return;
-    const dim3 g((n_tx + 3) / 4);
+    const dim3 g(std::min<uint32_t>((n_tx + 3) / 4, FILL_BLOCKS));
     if (amb)
         hipLaunchKernelGGL(near_fill_kernel<true>, g, dim3(256), 0, st, tx, n_tx, masked, F, AF, dmask, ent, cap, count);
     else
