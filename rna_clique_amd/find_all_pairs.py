@@ -11,29 +11,29 @@ subprocesses on a process pool, all pairs run at once in one engine on the
 GPU (librcgpu.so); with an initialised torch.distributed group the pairs are
 sharded across ranks (distributed.py) and each rank writes the tables of the
 pairs it owns. `cache_dir` (the BLAST database cache) is accepted and unused.
-Tables are written as HDF5 (`write_table`'s "table" format, key
-"gene_matches") when PyTables is importable, else as pickles.
+Tables are written as HDF5 in pandas' "table" format under key
+"gene_matches" (`write_table`; without PyTables, h5.write_frame_table),
+on a thread pool of `jobs` workers.
 """
 from __future__ import annotations
 
 import itertools
 import math
 import multiprocessing
+import threading
+from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 from typing import Callable, Iterable, Optional
 
 from .select_top_genes import load_top_fasta
-from .tables import pair_table, write_table
+from .tables import pair_table, rows_to_table, write_table
 from .transcripts import TranscriptID, default_gene_re
 
 
 def table_extension() -> str:
-    """h5 as the reference writes them when PyTables is importable, else pkl."""
-    try:
-        import tables  # noqa: F401
-        return "h5"
-    except ImportError:
-        return "pkl"
+    """h5, as the reference writes them (pandas table format; written without
+    PyTables when it is absent, h5.write_frame_table)."""
+    return "h5"
 
 
 def make_output_path(dir_: Path, t1: Path, t2: Path, path_to_sample: Optional[Callable] = None,
@@ -66,7 +66,7 @@ def find_all_pairs(inputs: Iterable[Path], output_dir: Path, cache_dir: Optional
     if engine_out is not None:
         engine_out.append(eng)
     ext = table_extension()
-    out_paths = write_pair_tables(eng, inputs, output_dir, path_to_sample, ext)
+    out_paths = write_pair_tables(eng, inputs, output_dir, path_to_sample, ext, jobs)
 
     def tables():
         for a, b in itertools.combinations(range(len(inputs)), 2):
@@ -77,16 +77,23 @@ def find_all_pairs(inputs: Iterable[Path], output_dir: Path, cache_dir: Optional
     return tables(), paths, math.comb(len(inputs), 2)
 
 
-def write_pair_tables(eng, inputs, output_dir, path_to_sample, ext) -> dict:
+def write_pair_tables(eng, inputs, output_dir, path_to_sample, ext, jobs: int = 8) -> dict:
     """Write the tables of the pairs this engine owns; {(a, b): path}."""
     output_dir = Path(output_dir)
     output_dir.mkdir(parents=True, exist_ok=True)
     own = set(eng.owned_pairs())
     out = {}
     for a, b in itertools.combinations(range(len(inputs)), 2):
-        if (a, b) not in own:
-            continue
-        p = make_output_path(output_dir, inputs[a], inputs[b], path_to_sample, ext)
-        write_table(pair_table(eng, a, b), p)
-        out[(a, b)] = p
+        if (a, b) in own:
+            out[(a, b)] = make_output_path(output_dir, inputs[a], inputs[b], path_to_sample, ext)
+    labels = eng.labels
+    lock = threading.Lock()
+
+    def one(ab):
+        with lock:   # the engine's device -> host copies, one pair at a time
+            rows = eng.pair_rows(*ab)
+        write_table(rows_to_table(rows, labels[ab[0]], labels[ab[1]]), out[ab])
+    # table building and writing are numpy / file work: threads overlap them
+    with ThreadPoolExecutor(max_workers=max(1, min(jobs, len(out)))) as ex:
+        list(ex.map(one, list(out)))
     return out

@@ -11,9 +11,10 @@ What changes underneath:
   and networkx;
 * `cache_dir` (BLAST DB cache) is accepted and unused: the seed index lives in
   HBM and is rebuilt per run;
-* gene matches tables are written to `out_dir_2` as `{s1}--{s2}.{ext}`
-  (write_table, gene_matches_tables.py:42-56): "h5" when PyTables is
-  importable, else "pkl" (`table_format` overrides; "none" skips them);
+* gene matches tables are written to `out_dir_2` as `{s1}--{s2}.h5`
+  (write_table, gene_matches_tables.py:42-56: pandas table format, key
+  "gene_matches", written without PyTables when it is absent;
+  `table_format="pkl"` writes pickles, "none" skips them);
 * `output_graph` is the networkx pickle of build_graph (filtering_step.py:
   158-159); pass None to skip building it (it is the slowest host step);
 * `jobs` bounds the host threads of the top-genes step.
@@ -103,7 +104,7 @@ def rna_clique(
         # every rank writes the tables of the pairs it owns (all of them on one GPU)
         from .find_all_pairs import table_extension, write_pair_tables
         write_pair_tables(eng, [s.path for s in samples], out_dir_2, pts.__getitem__,
-                          table_format or table_extension())
+                          table_format or table_extension(), max(1, jobs))
     if writer and output_graph is not None:
         from .filtering_step import dump_graph
         dump_graph(sim.graph, output_graph)

@@ -8,8 +8,8 @@ when a caller asks (store_dfs, od2 files, graph.pkl):
   schema docs/formats.md:231-252), with the index labels the reference keeps.
 * `build_graph` -> the networkx Graph build_graph.py:40-68 makes from those
   tables, with the same node and edge insertion order.
-* `write_table` -> gene_matches_tables.py:42-56 (.pkl via pandas; .h5 needs
-  PyTables, which this image does not have).
+* `write_table` / `read_table` -> gene_matches_tables.py:42-56 (.pkl via
+  pandas; .h5 in pandas' table format, with or without PyTables).
 """
 from __future__ import annotations
 
@@ -29,8 +29,9 @@ def blast_evalue(e):
     "0.0" below 1e-180, else three significant digits (the form shown in
     docs/formats.md:262, e.g. 8.75e-152)."""
     e = np.asarray(e, dtype=np.float64)
-    txt = np.char.mod("%.2e", e)
-    out = txt.astype(np.float64)
+    # a table holds few distinct e-values: print and parse those only
+    u, inv = np.unique(e, return_inverse=True)
+    out = np.char.mod("%.2e", u).astype(np.float64)[inv].reshape(e.shape)
     out[e < 1.0e-180] = 0.0
     return out
 
@@ -38,7 +39,8 @@ def blast_evalue(e):
 def blast_pident(nident, length):
     """pident = 100 * nident / length printed with 3 decimals."""
     p = 100.0 * np.asarray(nident, dtype=np.float64) / np.maximum(np.asarray(length), 1)
-    return np.char.mod("%.3f", p).astype(np.float64)
+    u, inv = np.unique(p, return_inverse=True)   # distinct ratios only
+    return np.char.mod("%.3f", u).astype(np.float64)[inv].reshape(p.shape)
 
 
 def shrink_df(df: pd.DataFrame) -> pd.DataFrame:
@@ -67,8 +69,9 @@ def rows_to_table(rows: np.ndarray, ssample: str, qsample: str) -> pd.DataFrame:
         "reverse": rows["reverse"].astype(bool),
     }, index=pd.Index(rows["label"].astype(np.int64)))
     df = shrink_df(df)
-    df["ssample"] = pd.Categorical([ssample] * len(df))
-    df["qsample"] = pd.Categorical([qsample] * len(df))
+    one = np.zeros(len(df), dtype=np.int8)
+    df["ssample"] = pd.Categorical.from_codes(one, categories=[ssample])
+    df["qsample"] = pd.Categorical.from_codes(one, categories=[qsample])
     return df[TABLE_COLUMNS]
 
 
@@ -79,24 +82,39 @@ def pair_table(engine, a: int, b: int, labels=None) -> pd.DataFrame:
 
 
 def write_table(df: pd.DataFrame, path: Path):
-    """gene_matches_tables.py:42-56."""
+    """gene_matches_tables.py:42-56: .pkl via pandas; .h5 in pandas' table
+    format under key "gene_matches" -- through PyTables when it is importable,
+    else written directly (h5.write_frame_table; read back by PyTables in
+    tests/test_h5_pytables.py)."""
     path = Path(path)
     if path.suffix == ".pkl":
         df.to_pickle(path)
     elif path.suffix == ".h5":
-        df.to_hdf(path, key="gene_matches", format="table")   # needs PyTables
+        try:
+            import tables  # noqa: F401
+        except ImportError:
+            from .h5 import write_frame_table
+            write_frame_table(path, df, key="gene_matches")
+        else:
+            df.to_hdf(path, key="gene_matches", format="table")
     else:
         raise ValueError(f"Could not determine file type for extension {path.suffix}.")
 
 
 def read_table(path: Path) -> pd.DataFrame:
     """gene_matches_tables.py read_table: a table write_table wrote (.pkl is
-    this package's own pickle output; .h5 needs PyTables)."""
+    this package's own pickle output; .h5 through PyTables when importable,
+    else through the HDF5 C library, h5.read_frame_table)."""
     path = Path(path)
     if path.suffix == ".pkl":
         return pd.read_pickle(path)
     if path.suffix == ".h5":
-        return pd.read_hdf(path, key="gene_matches")   # needs PyTables
+        try:
+            import tables  # noqa: F401
+        except ImportError:
+            from .h5 import read_frame_table
+            return read_frame_table(path, key="gene_matches")
+        return pd.read_hdf(path, key="gene_matches")
     raise ValueError(f"Could not determine file type for extension {path.suffix}.")
 
 

@@ -98,9 +98,10 @@ def test_rna_clique_end_to_end(native, tmp_path):
     df = sim.get_dissimilarity_df()
     assert list(df.index) == sorted(t.name for t in top)
     assert np.array_equal(df.to_numpy(), summary["matrix"])
-    # gene matches tables on disk (write_table's pickle form)
+    # gene matches tables on disk (pandas table-format HDF5, key gene_matches)
+    from rna_clique_amd.tables import read_table
     for a, b in itertools.combinations(range(len(samples)), 2):
-        t = pd.read_pickle(od2 / f"{samples[a].name}--{samples[b].name}.pkl")
+        t = read_table(od2 / f"{samples[a].name}--{samples[b].name}.h5")
         rows = sim.engine.pair_rows(a, b)
         assert list(t.index) == rows["label"].tolist()
         assert (t["nident"].to_numpy() == rows["hsp"]["nident"]).all()
