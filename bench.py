@@ -147,11 +147,11 @@ def e2e_wall_clock(samples, genes, rank, world, dist, ref):
     """The metric's second half: wall-clock from the transcripts FASTA files on
     disk to matrix.h5 written, through the drop-in API -- rna_clique() with
     top-gene selection (native FASTA reader, od1/*_top.fasta written), engine
-    load + H2D, the whole GPU path, the distance matrix and the h5 writer.
-    The FASTA files are written (untimed) to a scratch directory first; the
-    gene matches tables and graph.pkl are not written (out_dir_2 /
-    output_graph None). `ref` = (labels, matrix) of the timed steps: the
-    matrix must come out identical."""
+    load + H2D, the whole GPU path, and every output the reference writes:
+    the od2 gene matches tables (pandas table-format HDF5), graph.pkl and
+    matrix.h5. The FASTA files are written (untimed) to a scratch directory
+    first. `ref` = (labels, matrix) of the timed steps: the matrix must come
+    out identical."""
     import shutil
     import numpy as np
     from rna_clique_amd.rna_clique import rna_clique, last_timings
@@ -169,8 +169,8 @@ def e2e_wall_clock(samples, genes, rank, world, dist, ref):
     od1 = os.path.join(root, f"od1_r{rank}")
     out = os.path.join(root, "matrix.h5")
     t0 = time.perf_counter()
-    sim, pts = rna_clique(dirs, od1, None, None, None, out, top_genes=genes,
-                          jobs=16)
+    od2, graph = os.path.join(root, f"od2_r{rank}"), os.path.join(root, f"graph_r{rank}.pkl")
+    sim, pts = rna_clique(dirs, od1, od2, None, graph, out, top_genes=genes, jobs=16)
     dt = time.perf_counter() - t0
     if dist:
         import torch
@@ -185,15 +185,17 @@ def e2e_wall_clock(samples, genes, rank, world, dist, ref):
     idx = [list(labels).index(n) for n in order]
     same = bool(np.array_equal(df.to_numpy(), np.asarray(mat)[np.ix_(idx, idx)]))
     size = os.path.getsize(out) if rank == 0 else None
+    n_tables = len(os.listdir(od2))
+    graph_mb = round(os.path.getsize(graph) / 1e6, 1) if rank == 0 else None
     if dist:
         dist.barrier()
     if rank == 0:
         shutil.rmtree(root, ignore_errors=True)
     return {"wall_clock_s": round(dt, 3), "matrix_h5_bytes": size, "matrix_equal_to_steps": same,
-            "fasta_write_s": round(t_w, 1),
+            "od2_tables": n_tables, "graph_pkl_mb": graph_mb, "fasta_write_s": round(t_w, 1),
             "phases_s": {k: round(v, 3) for k, v in last_timings.items()},
-            "what": "transcripts FASTA on disk -> top-gene selection -> GPU path -> matrix.h5 "
-                    "(gene matches tables and graph.pkl not written)"}
+            "what": "transcripts FASTA on disk -> top-gene selection -> GPU path -> od2/*.h5 gene matches "
+                    "tables + graph.pkl + matrix.h5 (every output the reference writes)"}
 
 
 def main():

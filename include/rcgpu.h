@@ -39,6 +39,7 @@ extern "C" {
                                 NoIdealComponentsError, filtered_distance.py:242-247 */
 #define RC_E_CAPACITY (-6)   /* caller buffer too small */
 #define RC_E_LIMIT (-7)      /* input beyond a documented engine limit */
+#define RC_E_IO (-8)         /* file could not be written */
 
 typedef struct rc_engine rc_engine;
 
@@ -251,6 +252,20 @@ int rc_fasta_parse_rnaspades(const rc_fasta *f, double *cov, int64_t *gene, int6
 int rc_fasta_select(const rc_fasta *f, const uint8_t *keep, uint8_t *seq, uint64_t *tx_offsets);
 /* selected records as Bio.SeqIO.write(..., "fasta") writes them (width 60) */
 int rc_fasta_write(const rc_fasta *f, const uint8_t *keep, const char *path, int32_t width);
+
+/* ---- graph.pkl (host only; graph_pickle.cpp) -------------------------------
+ * Replaces build_graph + pickle.dump (build_graph.py:40-68, filtering_step.py:
+ * 158-159): the tables are added in order (per table: sample indices of
+ * ssample and qsample, the sgene and qgene columns), then the pickle of the
+ * networkx Graph build_graph would make from them is written to `path`
+ * (protocol 4; nodes are (names[sample], gene) tuples; node, neighbour and
+ * edge order as build_graph inserts them). */
+typedef struct rc_gpickle rc_gpickle;
+int rc_graph_pickle_begin(rc_gpickle **out);
+int rc_graph_pickle_add(rc_gpickle *g, int32_t ssample, int32_t qsample, const int64_t *sgene, const int64_t *qgene,
+                        uint64_t n);
+int rc_graph_pickle_write(rc_gpickle *g, const char *path, int32_t n_names, const char *const *names);
+void rc_graph_pickle_free(rc_gpickle *g);
 
 #ifdef __cplusplus
 }

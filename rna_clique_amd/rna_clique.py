@@ -16,7 +16,8 @@ What changes underneath:
   "gene_matches", written without PyTables when it is absent;
   `table_format="pkl"` writes pickles, "none" skips them);
 * `output_graph` is the networkx pickle of build_graph (filtering_step.py:
-  158-159); pass None to skip building it (it is the slowest host step);
+  158-159), written by a native pickle writer from the engine's rows (the
+  same Graph on pickle.load, without building it in Python);
 * `jobs` bounds the host threads of the top-genes step.
 """
 from __future__ import annotations
@@ -105,16 +106,18 @@ def rna_clique(
         from .find_all_pairs import table_extension, write_pair_tables
         write_pair_tables(eng, [s.path for s in samples], out_dir_2, pts.__getitem__,
                           table_format or table_extension(), max(1, jobs))
+    t3 = time.perf_counter()
     if writer and output_graph is not None:
-        from .filtering_step import dump_graph
-        dump_graph(sim.graph, output_graph)
+        sim.write_graph(output_graph)
+    t4 = time.perf_counter()
     if writer and output_matrix is not None:
         write_matrix(sim.get_dissimilarity_df(), output_matrix)
     last_timings.clear()
-    last_timings.update(select_s=t1 - t0, engine_s=t2 - t1, outputs_s=time.perf_counter() - t2)
+    last_timings.update(select_s=t1 - t0, engine_s=t2 - t1, tables_s=t3 - t2, graph_s=t4 - t3,
+                        matrix_s=time.perf_counter() - t4)
     return sim, pts
 
 
 # wall-clock phases of the last rna_clique() call in this process (seconds):
-# top-gene selection, engine (load + GPU path), outputs (tables, graph, matrix)
+# top-gene selection, engine (load + GPU path), od2 tables, graph.pkl, matrix.h5
 last_timings: dict = {}

@@ -180,6 +180,23 @@ class SampleSimilarity:
         self._graph = build_graph(rows())
         return self._graph
 
+    def write_graph(self, path):
+        """graph.pkl (filtering_step.py:158-159): the pickle of `graph`. For an
+        engine run whose graph was never built in Python, the native writer
+        streams the pairs' rows (tables.write_graph_pickle: the same Graph on
+        pickle.load, without per-edge Python inserts)."""
+        if self._graph is None and getattr(self.engine, "shard_count", 1) == 1:
+            from .tables import write_graph_pickle
+
+            def tables():
+                for a, b in self._pairs():
+                    r = self.engine.pair_rows(a, b)
+                    yield a, b, r["sgene"], r["qgene"]
+            write_graph_pickle(path, tables(), self.labels)
+            return
+        from .filtering_step import dump_graph
+        dump_graph(self.graph, path)
+
     @property
     def sample_count(self):
         return self._sample_count

@@ -139,3 +139,27 @@ def build_graph(tables):
         g.add_nodes_from(qn)
         g.add_edges_from(zip(sn, qn))
     return g
+
+
+def write_graph_pickle(path, tables, names):
+    """graph.pkl of the graph build_graph would make from `tables` -- an
+    iterable of (ssample index, qsample index, sgene array, qgene array), in
+    build_graph's table order, sample indices into `names` -- written by the
+    native pickle writer (graph_pickle.cpp) without building it in Python.
+    pickle.load gives the networkx Graph build_graph returns (node,
+    neighbour and edge order included)."""
+    import ctypes
+    from . import _native
+    L = _native.lib()
+    h = ctypes.c_void_p()
+    _native.check(L.rc_graph_pickle_begin(ctypes.byref(h)))
+    try:
+        for sa, qa, sg, qg in tables:
+            sg = np.ascontiguousarray(sg, dtype=np.int64)
+            qg = np.ascontiguousarray(qg, dtype=np.int64)
+            _native.check(L.rc_graph_pickle_add(h, int(sa), int(qa), sg.ctypes.data, qg.ctypes.data, len(sg)))
+        enc = [str(n).encode() for n in names]
+        arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
+        _native.check(L.rc_graph_pickle_write(h, str(path).encode(), len(enc), arr))
+    finally:
+        L.rc_graph_pickle_free(h)
