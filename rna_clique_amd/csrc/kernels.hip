@@ -389,50 +389,47 @@ __global__ void rbh_kernel(RbhParams P, int pass)
                 erows++;
                 if (!P.keep_all) done = true;
             }
-            // R rows of this pair at M
+            // R rows of this pair at M. R_sel order: pairs by the first
+            // appearance of their F rows in F_top order (bits desc, index
+            // asc), then R_top order; `before` = the R_sel rows of the pairs
+            // whose first F_top row precedes this pair's (the same for every
+            // R row of the pair: computed once, by direct (bits, index)
+            // comparisons -- O(fcnt^2) per pair, not a rank per comparison)
+            auto precedes = [&](uint32_t x, uint32_t y) {
+                const int bx = H[foff + x].bits10, by = H[foff + y].bits10;
+                return bx > by || (bx == by && x < y);
+            };
+            uint64_t before = 0;
+            bool have_before = false;
             for (uint32_t j = 0; j < rcnt && !done; j++) {
                 if (!r_sel(j) || H[roff + j].bits10 != M) continue;
                 const DHsp &r = H[roff + j];
                 if (pass) {
-                    // R_sel order: pairs by first appearance in F_top order, then R_top order
-                    uint64_t before = 0;
-                    // F_top rank of this pair's first F row
-                    uint32_t myfirst = 0xFFFFFFFFu;
-                    for (uint32_t i = 0; i < fcnt; i++) {
-                        const DHsp &f = H[foff + i];
-                        if (f.bits10 >= fthr && P.tx_gene[f.s_tx] == a) {
-                            const uint32_t rk = desc_rank(H, foff, fcnt, i, [&](uint32_t jj) {
-                                return H[foff + jj].bits10 >= fthr;
-                            });
-                            myfirst = min(myfirst, rk);
+                    if (!have_before) {
+                        have_before = true;
+                        uint32_t afirst = 0xFFFFFFFFu;   // this pair's first F_top row
+                        for (uint32_t i = 0; i < fcnt; i++)
+                            if (H[foff + i].bits10 >= fthr && P.tx_gene[H[foff + i].s_tx] == a &&
+                                (afirst == 0xFFFFFFFFu || precedes(i, afirst)))
+                                afirst = i;
+                        for (uint32_t i = 0; i < fcnt; i++) {
+                            const DHsp &f = H[foff + i];
+                            if (f.bits10 < fthr) continue;
+                            const uint32_t a2 = P.tx_gene[f.s_tx];
+                            if (a2 == a || precedes(afirst, i)) continue;
+                            // is f the first F_top row of pair a2?
+                            bool firstrow = true;
+                            for (uint32_t i2 = 0; i2 < fcnt && firstrow; i2++)
+                                if (i2 != i && H[foff + i2].bits10 >= fthr && P.tx_gene[H[foff + i2].s_tx] == a2 &&
+                                    precedes(i2, i))
+                                    firstrow = false;
+                            if (!firstrow) continue;
+                            const size_t g2 = grp_index(a2, B, P.n_genes);
+                            const uint32_t o2 = P.grp_off[g2], c2 = P.grp_cnt[g2];
+                            const int t2 = group_thr(H, o2, c2, P.top_n);
+                            for (uint32_t k2 = 0; k2 < c2; k2++)
+                                if (H[o2 + k2].bits10 >= t2 && P.tx_gene[H[o2 + k2].s_tx] == b) before++;
                         }
-                    }
-                    // R rows of pairs whose first F_top row precedes ours
-                    for (uint32_t i = 0; i < fcnt; i++) {
-                        const DHsp &f = H[foff + i];
-                        if (f.bits10 < fthr) continue;
-                        const uint32_t a2 = P.tx_gene[f.s_tx];
-                        if (a2 == a) continue;
-                        // is f the first F_top row of pair a2?
-                        const uint32_t rk = desc_rank(H, foff, fcnt, i, [&](uint32_t jj) {
-                            return H[foff + jj].bits10 >= fthr;
-                        });
-                        bool firstrow = true;
-                        for (uint32_t i2 = 0; i2 < fcnt; i2++) {
-                            if (i2 == i) continue;
-                            const DHsp &f2 = H[foff + i2];
-                            if (f2.bits10 < fthr || P.tx_gene[f2.s_tx] != a2) continue;
-                            const uint32_t rk2 = desc_rank(H, foff, fcnt, i2, [&](uint32_t jj) {
-                                return H[foff + jj].bits10 >= fthr;
-                            });
-                            if (rk2 < rk) firstrow = false;
-                        }
-                        if (!firstrow || rk > myfirst) continue;
-                        const size_t g2 = grp_index(a2, B, P.n_genes);
-                        const uint32_t o2 = P.grp_off[g2], c2 = P.grp_cnt[g2];
-                        const int t2 = group_thr(H, o2, c2, P.top_n);
-                        for (uint32_t k2 = 0; k2 < c2; k2++)
-                            if (H[o2 + k2].bits10 >= t2 && P.tx_gene[H[o2 + k2].s_tx] == b) before++;
                     }
                     const uint32_t rk = desc_rank(H, roff, rcnt, j, r_sel);
                     DRow row;

@@ -68,3 +68,42 @@ def match_table_similarity(table: pd.DataFrame) -> Fraction:
     """Fraction(sum nident, sum length - sum gaps) over a whole table
     (find_homologs.py:355-362)."""
     return Fraction(int(table["nident"].sum()), int(table["length"].sum() - table["gaps"].sum()))
+
+
+def main(argv=None):
+    """The find_homologs command (find_homologs.py:327-363): one sample pair's
+    gene matches, then the pair's distance as a Fraction (or a float with -f):
+    prints the deduplicated (qgene, sgene) matches unless -q, "Found N
+    matches." on stderr. `python -m rna_clique_amd.find_homologs T1 T2`."""
+    import argparse
+    import sys
+    from .transcripts import TranscriptIDParseError, default_gene_re
+    ap = argparse.ArgumentParser(description="Compute a genetic distance for one pair of samples.")
+    ap.add_argument("--transcript-id-regex", default=default_gene_re.pattern,
+                    help="regex with the gene and isoform groups of a transcript ID")
+    ap.add_argument("--evalue", type=float, default=1e-99)
+    ap.add_argument("--top-matches", type=int, default=1)
+    ap.add_argument("--keep-all", type=lambda v: str(v).lower() in ("1", "true", "yes"), default=True)
+    ap.add_argument("transcripts1", type=Path, help="path to the (top n) transcripts for the first sample")
+    ap.add_argument("transcripts2", type=Path, help="path to the (top n) transcripts for the second sample")
+    ap.add_argument("-q", "--quiet", action="store_true", help="hide the matches found")
+    ap.add_argument("-f", "--report-float", action="store_true", help="report float instead of fraction")
+    args = ap.parse_args(argv)
+    finder = HomologFinder(TranscriptID.parser_from_re(args.transcript_id_regex), args.top_matches,
+                           args.evalue, args.keep_all)
+    try:
+        best = finder.get_match_table(args.transcripts1, args.transcripts2)
+    except TranscriptIDParseError:
+        print(f"Could not parse a transcript ID with the regex {args.transcript_id_regex!r}.", file=sys.stderr)
+        raise
+    dedup = finder.without_duplicates(best)
+    if not args.quiet:
+        for match in dedup.itertuples(index=False):
+            print(*match)
+    print(f"Found {len(dedup)} matches.", file=sys.stderr)
+    dist = match_table_similarity(best)
+    print(float(dist) if args.report_float else dist)
+
+
+if __name__ == "__main__":
+    main()

@@ -334,6 +334,19 @@ def test_homolog_finder_single_pair(native, tmp_path):
     dedup = HomologFinder.without_duplicates(table)
     assert list(dedup.columns) == ["qgene", "sgene"] and len(dedup) <= len(table)
     eng.close()
+    # the find_homologs command: matches, then the Fraction (or a float with -f)
+    import contextlib
+    import io
+    from rna_clique_amd.find_homologs import main
+    for extra, want in (([], str(Fraction(int(num[0, 1]), int(den[0, 1])))),
+                        (["-q", "-f"], str(float(Fraction(int(num[0, 1]), int(den[0, 1])))))):
+        out, err = io.StringIO(), io.StringIO()
+        with contextlib.redirect_stdout(out), contextlib.redirect_stderr(err):
+            main([*extra, str(paths[0]), str(paths[1])])
+        lines = out.getvalue().splitlines()
+        assert lines[-1] == want
+        assert len(lines) == (1 if extra else len(dedup) + 1)
+        assert err.getvalue().strip() == f"Found {len(dedup)} matches."
 
 
 def test_repeat_runs_identical(native):
@@ -348,3 +361,4 @@ def test_repeat_runs_identical(native):
     _, m2 = eng.distance()
     assert all(np.array_equal(a, b) for a, b in zip(h1, h2))
     assert np.array_equal(m1, m2)
+
