@@ -108,10 +108,21 @@ def all_gather_records(local, record_size, process_group=None, device=None):
     mx = max(counts) * record_size
     if mx == 0:
         return torch.zeros(0, dtype=torch.uint8, device=dev), 0
-    send = torch.zeros(mx, dtype=torch.uint8, device=dev)
-    send[:local.numel()] = local
-    recv = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(W)]
-    dist.all_gather(recv, send, group=process_group)
+    if local.numel() == mx:
+        send = local
+    else:
+        send = torch.zeros(mx, dtype=torch.uint8, device=dev)
+        send[:local.numel()] = local
+    if dist.get_backend(process_group) == "gloo":
+        recv = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(W)]
+        dist.all_gather(recv, send, group=process_group)
+    else:
+        # RCCL: one receive buffer (no per-rank tensors), views into it
+        buf = torch.empty(W * mx, dtype=torch.uint8, device=dev)
+        dist.all_gather_into_tensor(buf, send, group=process_group)
+        recv = list(buf.view(W, mx))
+        if all(c * record_size == mx for c in counts):
+            return buf, sum(counts)   # no padding anywhere: the buffer is the result
     out = torch.cat([r[:c * record_size] for r, c in zip(recv, counts)])
     return out, sum(counts)
 
