@@ -78,8 +78,11 @@ __device__ __forceinline__ uint64_t even_bits(uint64_t x)
     return (x | (x >> 16)) & 0x00000000FFFFFFFFull;
 }
 
+#ifndef RC_DUST_MINW
+#define RC_DUST_MINW 7   // waves per SIMD the registers must allow: 7 measured best (21.4 ms at 5 waves, 20.1 at 7, 21.1 at 8)
+#endif
 template <bool AMB>
-__global__ __launch_bounds__(DW) void dust_kernel(uint64_t total, uint64_t nwords, const uint64_t *__restrict__ F,
+__global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t total, uint64_t nwords, const uint64_t *__restrict__ F,
                                                   const uint64_t *__restrict__ AF,
                                                   const uint64_t *__restrict__ txstart, int T, int W,
                                                   uint64_t *__restrict__ evs, uint32_t *__restrict__ scratch,

@@ -1284,7 +1284,7 @@ static int align_tile(rc_engine *e, int ti)
     // started with the fill, both ran at a third of their speed
     // (RC_DUST_EARLY=1 restores that order for A/B runs).
     auto start_dust = [&]() -> int {
-        const uint32_t dblocks = 256 * 20;   // at least the resident waves of the chunk kernel: their scratch
+        const uint32_t dblocks = 256 * 28;   // at least the resident waves of the chunk kernel (7 per SIMD): their scratch
         CHK(e->d_dust_scratch.ensure(dust_scratch_words(dblocks)));
         CHK(e->d_dust_events.ensure(dust_event_words(dblocks)));
         const char *dwv = getenv("RC_DUST_WAVES");
