@@ -43,13 +43,32 @@ def blast_pident(nident, length):
     return np.char.mod("%.3f", u).astype(np.float64)[inv].reshape(p.shape)
 
 
+_UNSIGNED = (np.uint8, np.uint16, np.uint32, np.uint64)
+_SIGNED = (np.int8, np.int16, np.int32, np.int64)
+
+
+def downcast_int(a: np.ndarray) -> np.ndarray:
+    """pd.to_numeric(pd.to_numeric(a, downcast="integer"), downcast="unsigned")
+    for a non-empty integer array, from its min and max: the smallest signed
+    type holding the values, then the smallest unsigned one if none is
+    negative -- i.e. the smallest unsigned type when all are >= 0."""
+    mn, mx = int(a.min()), int(a.max())
+    for t in (_UNSIGNED if mn >= 0 else _SIGNED):
+        i = np.iinfo(t)
+        if i.min <= mn and mx <= i.max:
+            return a.astype(t, copy=False)
+    return a
+
+
 def shrink_df(df: pd.DataFrame) -> pd.DataFrame:
     """Downcast integer columns (find_homologs.py:58-80)."""
     df = df.copy()
     for col in df.columns:
         if issubclass(df[col].dtype.type, numbers.Integral):
-            df[col] = pd.to_numeric(pd.to_numeric(df[col], downcast="integer"),
-                                    downcast="unsigned")
+            if len(df):
+                df[col] = downcast_int(df[col].to_numpy())
+            else:
+                df[col] = pd.to_numeric(pd.to_numeric(df[col], downcast="integer"), downcast="unsigned")
     return df
 
 

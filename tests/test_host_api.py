@@ -305,3 +305,27 @@ def test_plan_shards_partitions_pairs(native, n, shards):
                             + 11 * sum(bases[b] for b in {b for _, b in own}))
         loads = [cost(pairs[first[r]:first[r + 1]]) for r in range(shards)]
         assert max(loads) <= 2 * sum(bases[a] + bases[b] for a, b in pairs) / shards + 16 * max(bases) * n
+
+
+def test_downcast_int_matches_pandas():
+    """tables.downcast_int (shrink_df's fast path) gives pandas' double
+    to_numeric downcast (find_homologs.py:58-80) dtype and values."""
+    import numpy as np
+    import pandas as pd
+    from rna_clique_amd.tables import downcast_int
+    rng = np.random.default_rng(0)
+    cases = [np.array([0]), np.array([-1]), np.array([127, 128]), np.array([255]), np.array([256]),
+             np.array([-129, 5]), np.array([65535]), np.array([65536, 0]), np.array([-32769]),
+             np.array([2 ** 31]), np.array([-(2 ** 31) - 1]), np.array([2 ** 63 - 1])]
+    for dt in (np.int32, np.int64, np.uint32):
+        for hi in (2, 200, 70000, 5_000_000_000):
+            a = rng.integers(0, hi, 50)
+            if dt != np.uint32 and hi < 2 ** 31:
+                cases.append((a - hi // 3).astype(dt))
+            if hi < np.iinfo(dt).max:
+                cases.append(a.astype(dt))
+    for a in cases:
+        want = pd.to_numeric(pd.to_numeric(pd.Series(a), downcast="integer"), downcast="unsigned")
+        got = downcast_int(a)
+        assert got.dtype == want.dtype, (a, got.dtype, want.dtype)
+        assert (got == want.to_numpy()).all()
