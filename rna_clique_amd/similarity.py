@@ -194,6 +194,22 @@ class SampleSimilarity:
                     yield a, b, r["sgene"], r["qgene"]
             write_graph_pickle(path, tables(), self.labels)
             return
+        if self._graph is None:
+            # a sharded run holds every edge but only its own pairs' rows: the
+            # edges, per pair in pair order (a table of its distinct edges
+            # each), through the same writer -- the same nodes and edges as
+            # `graph`, without building it in Python
+            import numpy as np
+            from .tables import write_graph_pickle
+            e = self.engine.edges()
+            o = np.lexsort((e["sample_b"], e["sample_a"]))   # stable: record order inside a pair
+            e = e[o]
+            key = e["sample_a"].astype(np.int64) * (1 << 32) + e["sample_b"].astype(np.int64)
+            cut = np.flatnonzero(np.diff(key)) + 1
+            runs = np.split(np.arange(len(e)), cut) if len(e) else []
+            write_graph_pickle(path, ((int(e["sample_a"][r[0]]), int(e["sample_b"][r[0]]), e["gene_a"][r],
+                                       e["gene_b"][r]) for r in runs), self.labels)
+            return
         from .filtering_step import dump_graph
         dump_graph(self.graph, path)
 

@@ -141,7 +141,7 @@ def test_matrix_h5_from_run(native, tmp_path):
     assert h.strings(f, "/matrix/axis1") == list(df.index)
 
 
-def _shard_worker(rank, world, port, q):
+def _shard_worker(rank, world, port, q, graph_dir=None):
     import os as _os
     import torch.distributed as dist
     _os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -154,14 +154,22 @@ def _shard_worker(rank, world, port, q):
         samples, _ = simulate(5, 100, seed=31, p_iso2=0.2, indel_rate=0.002)
         eng = _load(Engine(device=0, shard_rank=rank, shard_count=world), samples)
         distributed.sharded_run(eng)
-        q.put((rank, eng.distance()[1].tobytes(), eng.stats()["edges"]))
+        gfile = None
+        if graph_dir is not None:
+            # graph.pkl of a sharded run: the native writer over the exchanged edges
+            from rna_clique_amd.similarity import SampleSimilarity
+            gfile = _os.path.join(graph_dir, f"graph_{rank}.pkl")
+            SampleSimilarity.from_engine(eng).write_graph(gfile)
+        q.put((rank, eng.distance()[1].tobytes(), eng.stats()["edges"], gfile))
     finally:
         dist.destroy_process_group()
 
 
-def test_two_processes_share_the_pairs(native):
+def test_two_processes_share_the_pairs(native, tmp_path):
     """world_size 2, one engine per process on the same GPU, gloo exchange:
-    the same distances as one engine."""
+    the same distances as one engine, and each rank's graph.pkl (native
+    writer over the exchanged edges) holds the one-engine graph's nodes and
+    edges."""
     import socket
     import torch.multiprocessing as mp
     from rna_clique_amd.engine import Engine
@@ -176,16 +184,24 @@ def test_two_processes_share_the_pairs(native):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_shard_worker, args=(r, 2, port, q, str(tmp_path))) for r in range(2)]
     for p in procs:
         p.start()
     got = [q.get(timeout=300) for _ in procs]
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    for _, blob, edges in got:
+    import pickle
+    from rna_clique_amd.similarity import SampleSimilarity
+    g_ref = SampleSimilarity.from_engine(ref).graph
+    ref_edges = {frozenset(e) for e in g_ref.edges}
+    for _, blob, edges, gfile in got:
         assert np.frombuffer(blob, dtype=np.float64).reshape(want.shape).tobytes() == want.tobytes()
         assert edges == ref.stats()["edges"]
+        with open(gfile, "rb") as f:
+            g = pickle.load(f)
+        assert set(g.nodes) == set(g_ref.nodes)
+        assert {frozenset(e) for e in g.edges} == ref_edges
 
 
 # ------------------------------------------------- SampleSimilarity(graph, tables)
