@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 
 import numpy as np
 
@@ -158,6 +159,17 @@ def lib():
             raise RuntimeError(
                 f"{LIB_PATH} is missing: build the HIP engine first "
                 "(python -c 'import __graft_entry__ as g; g.build()')")
+        if "torch" in sys.modules:
+            # torch bundles its own HIP runtime: when the caller uses torch on
+            # the GPU too (torch.distributed, CUDA tensors handed to the
+            # engine), bring torch's up first -- its lazy init after this
+            # library's runtime was seen to find no device
+            try:
+                import torch
+                if torch.cuda.is_available():
+                    torch.cuda.init()
+            except Exception:
+                pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)

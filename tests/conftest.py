@@ -22,7 +22,14 @@ def gpu_available():
 
 @pytest.fixture(scope="session")
 def native():
-    """The native library, built in-tree if needed (no fallback)."""
+    """The native library, built in-tree if needed (no fallback). On a GPU
+    box torch's HIP runtime (torch bundles its own libamdhip64) is brought up
+    first: tests that hand CUDA tensors to the engine need both in one
+    process, and torch's lazy init after the engine's own runtime was seen
+    to find no device."""
+    if gpu_available():
+        import torch
+        torch.cuda.init()
     from rna_clique_amd.build import build_native
     build_native()
     from rna_clique_amd import _native
