@@ -1,4 +1,5 @@
-"""A small HDF5 writer for the distance matrix (matrix.h5) without PyTables.
+"""A small HDF5 writer and reader for matrix.h5 and the od2 gene matches
+tables without PyTables.
 
 The reference saves the matrix with `DataFrame.to_hdf(path, key="matrix")`
 (rna_clique.py:176-177, 205-206), i.e. pandas' *fixed* format written through
