@@ -1305,28 +1305,35 @@ __device__ __forceinline__ int row_max(int v)
     return v;
 }
 
-// lane rl <- rl - 1 inside the row (rl 0 gets `edge`); FIX: also at the
-// half-wave seam (needed for the frontier, not for values only read where
-// the frontier neighbour is live)
+// lane rl <- rl - 1 inside the row (rl 0 gets `edge`). Rows wider than a DPP
+// row shift the whole wave: lane 0 keeps `edge` (FIX) or reads 0, and the
+// first lane of the upper half-wave reads the last lane of the lower one.
+// The frontier (FIX) relies on that lane being dead (-1 = edge) whenever a
+// step starts: a live sub-band edge lane ends its row's extension (abort or
+// done), every extension starts with only the seed diagonal live, and a row
+// without work sets its lanes dead. Values other than the frontier are only
+// read where the frontier neighbour is live.
 template <int RW, bool FIX>
 __device__ __forceinline__ int rw_from_lower(int v, int edge, int rl)
 {
     if constexpr (RW == 16) {
         return __builtin_amdgcn_update_dpp(edge, v, 0x111, 0xF, 0xF, false);   // row_shr:1
-    } else {   // wave_shr:1, lane 0 reads 0 (bound_ctrl); FIX puts `edge` at the row starts
-        const int x = __builtin_amdgcn_mov_dpp(v, 0x138, 0xF, 0xF, true);
-        return FIX ? (rl == 0 ? edge : x) : x;   // without FIX, edge is 0
+    } else if constexpr (FIX) {
+        return __builtin_amdgcn_update_dpp(edge, v, 0x138, 0xF, 0xF, false);   // wave_shr:1
+    } else {
+        return __builtin_amdgcn_mov_dpp(v, 0x138, 0xF, 0xF, true);             // edge is 0
     }
 }
-// lane rl <- rl + 1 inside the row (rl RW - 1 gets `edge`)
+// lane rl <- rl + 1 inside the row (rl RW - 1 gets `edge`; as above)
 template <int RW, bool FIX>
 __device__ __forceinline__ int rw_from_upper(int v, int edge, int rl)
 {
     if constexpr (RW == 16) {
         return __builtin_amdgcn_update_dpp(edge, v, 0x101, 0xF, 0xF, false);   // row_shl:1
-    } else {   // wave_shl:1, lane 63 reads 0 (bound_ctrl); FIX puts `edge` at the row ends
-        const int x = __builtin_amdgcn_mov_dpp(v, 0x130, 0xF, 0xF, true);
-        return FIX ? (rl == RW - 1 ? edge : x) : x;   // without FIX, edge is 0
+    } else if constexpr (FIX) {
+        return __builtin_amdgcn_update_dpp(edge, v, 0x130, 0xF, 0xF, false);   // wave_shl:1
+    } else {
+        return __builtin_amdgcn_mov_dpp(v, 0x130, 0xF, 0xF, true);             // edge is 0
     }
 }
 // max over the row, in every lane of the row
@@ -1371,6 +1378,13 @@ __device__ __forceinline__ uint32_t s_nonzero(uint32_t x)
     asm volatile("s_cmp_lg_u32 %1, 0\n\ts_cselect_b32 %0, -1, 0" : "=s"(r) : "s"(x) : "scc");
     return r;
 }
+// lowest set bit of a wave-uniform value (-1 for 0), one scalar instruction
+__device__ __forceinline__ int s_ff1(uint32_t x)
+{
+    int r;
+    asm volatile("s_ff1_i32_b32 %0, %1" : "=s"(r) : "s"(x));
+    return r;
+}
 // lane masks of single compares (one v_cmp each, combined in scalar registers)
 __device__ __forceinline__ uint64_t m_gt(int a, int b) { return __builtin_amdgcn_ballot_w64(a > b); }
 __device__ __forceinline__ uint64_t m_ge(int a, int b) { return __builtin_amdgcn_ballot_w64(a >= b); }
@@ -1404,20 +1418,73 @@ __device__ __forceinline__ int lane_sel(uint64_t m, int a, int b)
     return r;
 }
 
-// Matching bases from (pa, pb) forward, at most maxn; positions index one LDS
-// dword array (16 bases per dword); masks (AMB) sit `moff` bases further on.
+// 32-base windows of the row kernel's staging at absolute LDS base positions
+// (4 bases per byte of LDS address): three dword reads and two v_alignbit
+// each. The reads are one asm block so that the address is the position's
+// dword and nothing else (through a pointer the compiler adds the staging's
+// LDS symbol to every address); the block waits for its own reads.
+__device__ __forceinline__ uint64_t lds_join(uint64_t w01, uint32_t w2, uint32_t p)
+{
+    const uint32_t w0 = (uint32_t)w01, w1 = (uint32_t)(w01 >> 32);
+    const uint32_t lo = __builtin_amdgcn_alignbit(w1, w0, p * 2u), hi = __builtin_amdgcn_alignbit(w2, w1, p * 2u);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ void lds_win2(uint32_t pa, uint32_t pb, uint64_t &wa, uint64_t &wb)
+{
+    const uint32_t aa = (pa >> 2) & ~3u, ab = (pb >> 2) & ~3u;
+    uint64_t a01, b01;
+    uint32_t a2, b2;
+    asm volatile("ds_read2_b32 %0, %4 offset1:1\n\t"
+                 "ds_read_b32 %1, %4 offset:8\n\t"
+                 "ds_read2_b32 %2, %5 offset1:1\n\t"
+                 "ds_read_b32 %3, %5 offset:8\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(a01), "=&v"(a2), "=&v"(b01), "=&v"(b2)
+                 : "v"(aa), "v"(ab));
+    wa = lds_join(a01, a2, pa);
+    wb = lds_join(b01, b2, pb);
+}
+__device__ __forceinline__ uint64_t lds_win1(uint32_t p)
+{
+    const uint32_t a = (p >> 2) & ~3u;
+    uint64_t w01;
+    uint32_t w2;
+    asm volatile("ds_read2_b32 %0, %2 offset1:1\n\t"
+                 "ds_read_b32 %1, %2 offset:8\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(w01), "=&v"(w2)
+                 : "v"(a));
+    return lds_join(w01, w2, p);
+}
+__device__ __forceinline__ uint64_t lds_diff(uint32_t pa, uint32_t pb)
+{
+    uint64_t a, b;
+    lds_win2(pa, pb, a, b);
+    return a ^ b;
+}
+
+// Matching bases from (pa, pb) forward, at most maxn; positions are absolute
+// LDS base positions (lds_win2); masks (AMB) sit `moff` bases further on.
 template <bool AMB>
-__device__ __forceinline__ int slide_fwd(const uint32_t *S, uint32_t pa, uint32_t pb, int maxn, uint32_t moff)
+__device__ __forceinline__ int slide_fwd(uint32_t pa, uint32_t pb, int maxn, uint32_t moff)
 {
     // the first window outside any loop (a mismatch within 32 bases is the
     // common case); lanes on a run of 32+ matches continue in the loop
-    uint64_t x = win3(S, pa) ^ win3(S, pb);
-    if (AMB) x |= win3(S, pa + moff) | win3(S, pb + moff);
+    uint64_t x = lds_diff(pa, pb);
+    if (AMB) {
+        uint64_t ma, mb;
+        lds_win2(pa + moff, pb + moff, ma, mb);
+        x |= ma | mb;
+    }
     int n = x ? (int)(__builtin_ctzll(x) >> 1) : 32;
     if (n == 32 && maxn > 32) {
         for (;;) {
-            x = win3(S, pa + (uint32_t)n) ^ win3(S, pb + (uint32_t)n);
-            if (AMB) x |= win3(S, pa + (uint32_t)n + moff) | win3(S, pb + (uint32_t)n + moff);
+            x = lds_diff(pa + (uint32_t)n, pb + (uint32_t)n);
+            if (AMB) {
+                uint64_t ma, mb;
+                lds_win2(pa + (uint32_t)n + moff, pb + (uint32_t)n + moff, ma, mb);
+                x |= ma | mb;
+            }
             if (x) {
                 n += (int)(__builtin_ctzll(x) >> 1);
                 break;
@@ -1444,81 +1511,123 @@ enum { A_FETCH, A_UNUSED, A_RDONE, A_LDONE, A_ABORT, A_DONE, A_STEP_R, A_STEP_L 
 // right (score, i, j, d, gap state), left (same)
 enum { FX_STATUS = 0, FX_R = 1, FX_L = 6 };
 
+// The row kernel's arguments, one struct so that the kernarg segment is laid
+// out as it.
+struct RowArgs {
+    Db db;
+    ExtParams P;
+};
+using RowArgsK = const __attribute__((address_space(4))) RowArgs *;
+// The kernarg pointer behind an opaque copy: the fields read through it are
+// loaded (s_load, scalar cache) where the transitions use them instead of
+// being held in SGPRs across the step loop, where ~30 SGPRs of pointers
+// spilled into VGPR lanes and cost readlane/writelane pairs every step.
+__device__ __forceinline__ RowArgsK row_args()
+{
+    RowArgsK p = (RowArgsK)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
+// per-row state that only transitions touch (row kernel LDS)
+struct RowLds {
+    int meta[RM_N];
+    int st[RS_N];
+};
+// LDS of a row-kernel block: staging (2 guard words + rows x arrays x sw
+// words), shard prefix, rows' bookkeeping, 8 block counters
+__host__ __device__ constexpr size_t row_lds_bytes(int rw, int na, int sw)
+{
+    return ((size_t)(EBLOCK / rw) * na * sw + 2) * 8 + (NSHARD + 1) * 8 + (size_t)(EBLOCK / rw) * sizeof(RowLds) + 32;
+}
+
 // Extension of every candidate's FIRST seed (its smallest (x, y): always
 // extended, RC-megablast spec 3) to the right and to the left. Anything
 // further -- the other seeds' containment, more HSPs, purge, e-values -- is
 // first_finish_kernel's; a candidate that needs more than its first seed goes
 // to extend_kernel whole, as does one whose frontier reaches the sub-band edge.
 template <bool AMB, int RW, int MINW>
-__global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtParams P)
+__global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
 {
     constexpr int RROWS = EBLOCK / RW;   // rows per block
     constexpr int RC0 = RW / 2;          // row lane of diagonal 0
     constexpr int NA = AMB ? 8 : 4;      // staged arrays per row: Q, T (raw words), Qrev, Trev (+ masks)
     constexpr int EBIT = 26, OBIT = 13;
-    extern __shared__ uint64_t rstg[];                    // [RROWS][NA][sw]
-    __shared__ unsigned long long sprefix[NSHARD + 1];
-    // per-row state that only transitions touch lives in LDS
-    struct RowLds {
-        int meta[RM_N];
-        int st[RS_N];
-    };
-    __shared__ RowLds rows_lds[RROWS];
-    __shared__ unsigned int rcnt[4];                      // extensions, candidates, overflows
-    if (threadIdx.x < 4) rcnt[threadIdx.x] = 0;
-    for (int i = threadIdx.x; i <= NSHARD; i += EBLOCK) sprefix[i] = P.shard_prefix[i];
+    // All of the block's LDS is the dynamic allocation, staging first, so
+    // that the staging starts at LDS address 0 and the step loop's window
+    // addresses carry no base: [2 guard words][RROWS][NA][sw] staging, then
+    // the shard prefix, the rows' bookkeeping and the block counters.
+    extern __shared__ uint64_t rstg[];
+    const int sw = row_args()->P.dsw;                     // u64 words per staged array
+    unsigned long long *const sprefix = reinterpret_cast<unsigned long long *>(rstg + 2 + (size_t)RROWS * NA * sw);
+    RowLds *const rows_lds = reinterpret_cast<RowLds *>(sprefix + NSHARD + 1);
+    uint32_t *const rcnt = reinterpret_cast<uint32_t *>(rows_lds + RROWS);   // extensions, candidates, overflows
+    uint32_t &s_ncand = rcnt[4];
+    {
+        const RowArgsK K = row_args();
+        if (threadIdx.x < 4) rcnt[threadIdx.x] = 0;
+        for (int i = threadIdx.x; i <= NSHARD; i += EBLOCK) sprefix[i] = K->P.shard_prefix[i];
+        // list mode: the candidates are P.list[0, *P.list_n) (a previous row
+        // kernel's deferrals), else the linear index space over the shards
+        if (threadIdx.x == 0) s_ncand = K->P.list ? (uint32_t)*K->P.list_n : (uint32_t)K->P.n_cand;
+    }
     __syncthreads();
 
     const int lane = threadIdx.x & 63, rl = lane & (RW - 1), row = lane / RW;
     const int rs = threadIdx.x / RW;                      // row slot in the block
     const int k = rl - RC0;                               // this lane's diagonal
-    const int sw = P.dsw;                                 // u64 words per staged array
-    const uint32_t *S = reinterpret_cast<const uint32_t *>(rstg);
     // two guard words in front: reversed staging reads up to 31 bases before an array
     uint64_t *stg = rstg + 2 + (size_t)rs * NA * sw;      // Q, T, Qr, Tr, [QM, TM, QMr, TMr]
-    const uint32_t base0 = (uint32_t)(2 + rs * NA * sw) * 32u;   // base position of the row's Q array
+    // absolute LDS base position of the row's Q array (the staging's LDS
+    // offset: the low half of its generic address)
+    const uint32_t base0 = 4u * (uint32_t)reinterpret_cast<uintptr_t>(rstg) + (uint32_t)(2 + rs * NA * sw) * 32u;
     const uint32_t bqr = base0 + 64u * (uint32_t)sw, btr = bqr + 32u * (uint32_t)sw;
     const uint32_t moff = 128u * (uint32_t)sw;
     RowLds &RL = rows_lds[rs];
     int *meta = RL.meta;
-    const int X = P.xdrop;
+    const int X = row_args()->P.xdrop;
     // candidates come in chunks from a global counter (P.chunk >= 1); the
     // record of the next one is prefetched (one dword per lane) while the
     // current one is extended
-    const uint32_t chunk = (uint32_t)max(P.chunk, 1);
-    // list mode: the candidates are P.list[0, *P.list_n) (a previous row
-    // kernel's deferrals), else the linear index space over the shards
-    const uint32_t ncand = P.list ? (uint32_t)*P.list_n : (uint32_t)P.n_cand;
+    auto chunk = []() { return (uint32_t)max(row_args()->P.chunk, 1); };
     uint32_t lnx = 0;
     auto grab = [&]() {
+        const uint32_t ncand = s_ncand, ch = chunk();
         unsigned long long b = 0;
-        if (rl == 0) b = atomicAdd(P.work, (unsigned long long)chunk);
+        if (rl == 0) b = atomicAdd(row_args()->P.work, (unsigned long long)ch);
         b = (unsigned long long)__shfl((long long)b, RW * row);
         lnx = b < ncand ? (uint32_t)b : ncand;
-        if (rl == 0) RL.st[RS_LEND] = (int)(lnx + chunk);
+        if (rl == 0) RL.st[RS_LEND] = (int)(lnx + ch);
     };
     // candidate slot of linear index l; the shard cursor (in LDS) only advances
     auto slot = [&](uint32_t l, int which) -> uint64_t {
         int sh = RL.st[which];
         while (sh + 1 < NSHARD && sprefix[sh + 1] <= l) sh++;
         if (rl == 0) RL.st[which] = sh;
-        return (uint64_t)sh * P.cand_cap + (l - sprefix[sh]);
+        return (uint64_t)sh * row_args()->P.cand_cap + (l - sprefix[sh]);
     };
-    auto cslot = [&](uint32_t l, int which) -> uint64_t { return P.list ? (uint64_t)P.list[l] : slot(l, which); };
+    auto cslot = [&](uint32_t l, int which) -> uint64_t {
+        const uint32_t *list = row_args()->P.list;
+        return list ? (uint64_t)list[l] : slot(l, which);
+    };
     auto load_rec = [&](uint32_t l) -> int {
-        if (l >= ncand || rl >= CAND_DWORDS) return 0;
-        return reinterpret_cast<const int *>(P.cands + cslot(l, RS_SHN))[rl];
+        if (l >= s_ncand || rl >= CAND_DWORDS) return 0;
+        return reinterpret_cast<const int *>(row_args()->P.cands + cslot(l, RS_SHN))[rl];
     };
     // this pass's first-seed results (shared searches: pass 1 -> cand_box,
     // pass 2 over list2 -> cand_box2)
-    int32_t *const box_out = P.which ? P.cand_box2 : P.cand_box;
+    auto box_out = []() {
+        const RowArgsK K = row_args();
+        return K->P.which ? K->P.cand_box2 : K->P.cand_box;
+    };
     auto defer = [&](uint64_t ci) {   // row-uniform; extend_kernel takes the candidate whole
         if (rl == 0) {
-            if (!P.share) {   // shared searches: first_finish_kernel lists each search on its own
-                const unsigned long long di = atomicAdd(P.defer_count, 1ull);
-                P.defer[di] = (uint32_t)ci;
+            const RowArgsK K = row_args();
+            if (!K->P.share) {   // shared searches: first_finish_kernel lists each search on its own
+                const unsigned long long di = atomicAdd(K->P.defer_count, 1ull);
+                K->P.defer[di] = (uint32_t)ci;
             }
-            box_out[ci * BOX_REC + FX_STATUS] = -1;
+            box_out()[ci * BOX_REC + FX_STATUS] = -1;
         }
     };
     if (rl == 0) {
@@ -1538,7 +1647,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
 
     auto ext_init = [&](int done_act) {
         int r0 = 0;
-        if (rl == RC0) r0 = slide_fwd<AMB>(S, pa, pb, min(alen, blen), moff);
+        if (rl == RC0) r0 = slide_fwd<AMB>(pa, pb, min(alen, blen), moff);
         r0 = __shfl(r0, RW * row + RC0);
         best = 2 * r0;
         bl = RC0;
@@ -1559,7 +1668,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
         const int nw = (L >> 5) + 3;
         for (int w = rl; w < nw; w += RW) {
             const int fp = L - 32 * (w + 1);
-            dst[w] = fp > -32 ? rev2(win3(S, (uint32_t)((int)fb + fp))) : 0ull;
+            dst[w] = fp > -32 ? rev2(lds_win1((uint32_t)((int)fb + fp))) : 0ull;
         }
     };
 
@@ -1573,7 +1682,10 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
         // ---------------- transitions ----------------
         while (act < A_DONE) {
             if (act == A_FETCH) {
-                if (lnx >= ncand) {
+                if (lnx >= s_ncand) {
+                    // no work left: the row's lanes go dead for good (the
+                    // other row's steps shift this row's edge lanes in)
+                    R = -1;
                     act = A_DONE;
                     continue;
                 }
@@ -1601,11 +1713,13 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                     continue;
                 }
                 // raw words of query and subject, and the first seed: one round trip
-                const uint64_t *QA = strand ? db.RC : db.F;
-                const uint64_t *qw = QA + (q0 >> 5), *tw = db.F + (s0 >> 5);
+                const RowArgsK K = row_args();
+                const uint64_t *QA = strand ? K->db.RC : K->db.F;
+                const uint64_t *qw = QA + (q0 >> 5), *tw = K->db.F + (s0 >> 5);
                 {
                     const uint32_t e01 = (uint32_t)meta[RM_REC + RC_E01];
-                    const GSeed g0 = P.seeds[(uint32_t)meta[RM_REC + RC_SOFF] + (P.which ? e01 >> 16 : e01 & 0xFFFFu)];
+                    const GSeed g0 =
+                        K->P.seeds[(uint32_t)meta[RM_REC + RC_SOFF] + (K->P.which ? e01 >> 16 : e01 & 0xFFFFu)];
                     const uint64_t a0 = rl < nwq ? qw[rl] : 0ull, a1 = rl + RW < nwq ? qw[rl + RW] : 0ull;
                     const uint64_t b0 = rl < nwt ? tw[rl] : 0ull, b1 = rl + RW < nwt ? tw[rl + RW] : 0ull;
                     if (rl < nwq) stg[rl] = a0;
@@ -1621,7 +1735,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                 for (int w = rl + 2 * RW; w < nwq; w += RW) stg[w] = qw[w];
                 for (int w = rl + 2 * RW; w < nwt; w += RW) stg[sw + w] = tw[w];
                 if (AMB) {
-                    const uint64_t *qm = (strand ? db.ARC : db.AF) + (q0 >> 5), *tm = db.AF + (s0 >> 5);
+                    const uint64_t *qm = (strand ? K->db.ARC : K->db.AF) + (q0 >> 5), *tm = K->db.AF + (s0 >> 5);
                     for (int w = rl; w < nwq; w += RW) stg[4 * sw + w] = qm[w];
                     for (int w = rl; w < nwt; w += RW) stg[5 * sw + w] = tm[w];
                 }
@@ -1693,7 +1807,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                     if (rl == FX_L + 2) v = ej;
                     if (rl == FX_L + 3) v = ed;
                     if (rl == FX_L + 4) v = ego;
-                    if (rl < BOX_REC) box_out[ci * BOX_REC + rl] = v;
+                    if (rl < BOX_REC) box_out()[ci * BOX_REC + rl] = v;
                     act = A_FETCH;
                 }
             } else {   // A_ABORT: the sub-band overflowed
@@ -1733,7 +1847,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
             if (ni >= 0) {
                 const int ja = ni - k;
                 const int m = min(alen - ni, blen - ja);
-                const int s = slide_fwd<AMB>(S, pa + (uint32_t)ni, pb + (uint32_t)ja, m, moff);
+                const int s = slide_fwd<AMB>(pa + (uint32_t)ni, pb + (uint32_t)ja, m, moff);
                 ni += s;
                 if (s > 0) ng &= ~(3 << EBIT);
                 score = 2 * ni - k - d6;
@@ -1755,7 +1869,8 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
                 if (RW == 32 && !(lo & (lo - 1)) && !(hi & (hi - 1))) {
                     // at most one improving lane per row (the usual case): it is
                     // the row's new best, read out directly, no row reduction
-                    const int a = lo ? __builtin_ctz(lo) : 0, b = hi ? __builtin_ctz(hi) : 0;
+                    // (a row without an improving lane reads an unused lane)
+                    const int a = s_ff1(lo) & 31, b = s_ff1(hi) & 31;
                     const int s0 = __builtin_amdgcn_readlane(score, a), s1 = __builtin_amdgcn_readlane(score, 32 + b);
                     constexpr uint64_t ROW0 = 0xFFFFFFFFull;
                     best = lane_sel(mimp & ROW0, s0, lane_sel(mimp & ~ROW0, s1, best));
@@ -1784,14 +1899,16 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(Db db, ExtPar
 #endif
     }
 #ifdef RC_ROW_TIMING
-    if (lane == 0 && P.counters) {
-        atomicAdd(&P.counters[8], t_tr);
-        atomicAdd(&P.counters[9], t_st);
+    unsigned long long *const counters = row_args()->P.counters;
+    if (lane == 0 && counters) {
+        atomicAdd(&counters[8], t_tr);
+        atomicAdd(&counters[9], t_st);
     }
 #endif
-    if (lane == 0 && P.counters) atomicAdd(&P.counters[0], steps);
+    unsigned long long *const ctr = row_args()->P.counters;
+    if (lane == 0 && ctr) atomicAdd(&ctr[0], steps);
     __syncthreads();
-    if (threadIdx.x < 3 && P.counters) atomicAdd(&P.counters[1 + threadIdx.x], (unsigned long long)rcnt[threadIdx.x]);
+    if (threadIdx.x < 3 && ctr) atomicAdd(&ctr[1 + threadIdx.x], (unsigned long long)rcnt[threadIdx.x]);
 }
 
 // The candidates' first-seed extensions -> box; the other seeds of the
@@ -2086,12 +2203,12 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
     W.list = nullptr;
     W.list_n = nullptr;
     const int rw = row_width == 16 ? 16 : 32;
-    auto lds_of = [&](int w) { return ((size_t)(EBLOCK / w) * (amb ? 8 : 4) * (size_t)P.dsw + 2) * 8; };
+    auto lds_of = [&](int w) { return row_lds_bytes(w, amb ? 8 : 4, P.dsw); };
 #define RC_LAUNCH_ROWS(A, RWV, MW, PRM)                                                                   \
     do {                                                                                                  \
         auto kern = extend_rows_kernel<A, RWV, MW>;                                                       \
         const size_t lds = lds_of(RWV);                                                                   \
-        hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, lds)), dim3(EBLOCK), lds, st, db, PRM);       \
+        hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, lds)), dim3(EBLOCK), lds, st, RowArgs{db, PRM});\
     } while (0)
     const char *mwv = getenv("RC_ROW_WAVES");
     const int mw = mwv ? atoi(mwv) : ROW_MIN_WAVES;
