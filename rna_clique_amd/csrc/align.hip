@@ -1642,6 +1642,10 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
     int R = -1, goe = 0, wi = 0, wg = 0, wd = 0, best = 0, bl = RC0, d6 = 0;   // d6 = 6 x greedy step
     uint32_t pa = 0, pb = 0;
     int alen = 0, blen = 0;
+    // per-lane forms the step uses (k folded in once per extension):
+    // pb - k (b position of diagonal k at a offset 0), blen + k, -(k + d6)
+    uint32_t pbk = 0;
+    int blk = 0, nkd = 0;
     bool swap = false;                                    // spec 4b: query = the higher-numbered sample
     unsigned long long steps = 0;                         // row steps (wave-uniform count)
 
@@ -1659,6 +1663,9 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
         R = rl == RC0 ? r0 : -1;
         goe = 0;
         d6 = 0;
+        pbk = pb - (uint32_t)k;
+        blk = blen + k;
+        nkd = -k;
         if (rl == 0) atomicAdd(&rcnt[0], 1u);
         act = (min(alen, blen) - r0 <= 0) ? done_act : done_act + (A_STEP_R - A_RDONE);
     };
@@ -1828,14 +1835,16 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
         // ---------------- one greedy step of every extending row ----------------
         if (ext) {
             d6 += 6;
+            nkd -= 6;
             const int Rl = rw_from_lower<RW, true>(R, -1, rl), Rr = rw_from_upper<RW, true>(R, -1, rl);
             const int gl = rw_from_lower<RW, false>(goe, 0, rl), gr = rw_from_upper<RW, false>(goe, 0, rl);
             // candidates; ties prefer mismatch, then insertion, then deletion (a
             // frontier value R >= 0 has j = R - k >= 0, so unsigned compares
             // carry the lower bounds)
-            const int cm = ((uint32_t)R < (uint32_t)alen && (uint32_t)(R - k) < (uint32_t)blen) ? R + 1 : -1;
+            // (j = R - k < blen  <=>  R < blk;  j + 1 = Rr - k < blen + 1  <=>  Rr <= blk)
+            const int cm = ((uint32_t)R < (uint32_t)alen && R < blk) ? R + 1 : -1;
             const int cil = ((uint32_t)Rl < (uint32_t)alen) ? Rl + 1 : -1;
-            const int cd = (Rr >= 0 && Rr - (k + 1) < blen) ? Rr : -1;
+            const int cd = (Rr >= 0 && Rr <= blk) ? Rr : -1;
             int ni = max(max(cm, cil), cd);
             const bool fm = ni >= 0 && cm == ni, fi = !fm && cil == ni;
             // gap state of the chosen move: G | O << 13 | E << 26 (E: 1 insertion, 2 deletion)
@@ -1845,12 +1854,11 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
             int ng = (src & ~(3 << EBIT)) + (fm ? 0 : 1 + (pe == e ? 0 : (1 << OBIT)) + (e << EBIT));
             int score = INT_MIN, bound = INT_MIN;
             if (ni >= 0) {
-                const int ja = ni - k;
-                const int m = min(alen - ni, blen - ja);
-                const int s = slide_fwd<AMB>(pa + (uint32_t)ni, pb + (uint32_t)ja, m, moff);
+                const int m = min(alen - ni, blk - ni);
+                const int s = slide_fwd<AMB>(pa + (uint32_t)ni, pbk + (uint32_t)ni, m, moff);
                 ni += s;
                 if (s > 0) ng &= ~(3 << EBIT);
-                score = 2 * ni - k - d6;
+                score = 2 * ni + nkd;   // 2 ni - k - d6
                 if (score < best - X) ni = -1;
                 bound = score + 2 * (m - s);
             }
