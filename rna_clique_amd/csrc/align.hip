@@ -1721,8 +1721,14 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 }
                 // raw words of query and subject, and the first seed: one round trip
                 const RowArgsK K = row_args();
-                const uint64_t *QA = strand ? K->db.RC : K->db.F;
-                const uint64_t *qw = QA + (q0 >> 5), *tw = K->db.F + (s0 >> 5);
+                // both strands' pointers as scalars, selected per lane (an
+                // indexed read of the kernarg segment would be a vector load,
+                // one more round trip in front of the staging loads)
+                using GW = const __attribute__((address_space(1))) uint64_t *;
+                GW dF = (GW)K->db.F, dRC = (GW)K->db.RC;
+                asm volatile("" : "+s"(dF), "+s"(dRC));
+                const GW QA = strand ? dRC : dF;
+                const GW qw = QA + (q0 >> 5), tw = dF + (s0 >> 5);
                 {
                     const uint32_t e01 = (uint32_t)meta[RM_REC + RC_E01];
                     const GSeed g0 =
@@ -1742,7 +1748,9 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 for (int w = rl + 2 * RW; w < nwq; w += RW) stg[w] = qw[w];
                 for (int w = rl + 2 * RW; w < nwt; w += RW) stg[sw + w] = tw[w];
                 if (AMB) {
-                    const uint64_t *qm = (strand ? K->db.ARC : K->db.AF) + (q0 >> 5), *tm = K->db.AF + (s0 >> 5);
+                    GW dAF = (GW)K->db.AF, dARC = (GW)K->db.ARC;
+                    asm volatile("" : "+s"(dAF), "+s"(dARC));
+                    const GW qm = (strand ? dARC : dAF) + (q0 >> 5), tm = dAF + (s0 >> 5);
                     for (int w = rl; w < nwq; w += RW) stg[4 * sw + w] = qm[w];
                     for (int w = rl; w < nwt; w += RW) stg[5 * sw + w] = tm[w];
                 }
