@@ -1463,6 +1463,15 @@ __device__ __forceinline__ uint64_t lds_diff(uint32_t pa, uint32_t pb)
     return a ^ b;
 }
 
+// lane in mask ? K : b, K an inline constant (no register for it)
+template <int K>
+__device__ __forceinline__ int lane_sel_k(uint64_t m, int b)
+{
+    int r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "i"(K), "s"(m));
+    return r;
+}
+
 // Matching bases from (pa, pb) forward, at most maxn; positions are absolute
 // LDS base positions (lds_win2); masks (AMB) sit `moff` bases further on.
 template <bool AMB>
@@ -1646,6 +1655,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
     // pb - k (b position of diagonal k at a offset 0), blen + k, -(k + d6)
     uint32_t pbk = 0;
     int blk = 0, nkd = 0;
+    int score = 0, bound = 0;                             // of the last step
     bool swap = false;                                    // spec 4b: query = the higher-numbered sample
     unsigned long long steps = 0;                         // row steps (wave-uniform count)
 
@@ -1860,7 +1870,9 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
             const int e = fm ? 0 : (fi ? 1 : 2);
             const int pe = (src >> EBIT) & 3;
             int ng = (src & ~(3 << EBIT)) + (fm ? 0 : 1 + (pe == e ? 0 : (1 << OBIT)) + (e << EBIT));
-            int score = INT_MIN, bound = INT_MIN;
+            // score and bound of the lanes dead before the step keep stale
+            // values (loop-carried: nothing to materialize), never read
+            // unmasked (mi and mcont are ANDed with the live lanes)
             if (ni >= 0) {
                 const int m = min(alen - ni, blk - ni);
                 const int s = slide_fwd<AMB>(pa + (uint32_t)ni, pbk + (uint32_t)ni, m, moff);
@@ -1874,10 +1886,9 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
             goe = ng;
             const bool live = ni >= 0;
             // row-wide decisions as lane masks (scalar), applied with v_cndmask.
-            // A lane X-dropped this step has score < best, a dead one INT_MIN:
-            // score > best implies live.
+            // A lane X-dropped this step has score < best.
             const uint64_t mlive = m_ge(ni, 0);
-            const uint64_t mi = m_gt(score, best);
+            const uint64_t mi = m_gt(score, best) & mlive;
             const uint64_t mimp = rw_spread<RW>(mi);
             if (mimp) {
                 uint64_t mwin;
@@ -1908,7 +1919,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
             constexpr uint64_t EDGES = RW == 64 ? 0ull : (RW == 32 ? 0x8000000180000001ull : 0x8001800180018001ull);
             const uint64_t mcont = rw_spread<RW>(mlive & m_gt(bound, best)) & m_lt(d6, 6 * DMAX);
             const uint64_t medge = RW == 64 ? 0ull : rw_spread<RW>(mlive & EDGES);
-            act = lane_sel(mcont, lane_sel(medge, (int)A_ABORT, act), act - (A_STEP_R - A_RDONE));
+            act = lane_sel(mcont, lane_sel_k<A_ABORT>(medge, act), act - (A_STEP_R - A_RDONE));
         }
 #ifdef RC_ROW_TIMING
         t_st += __builtin_readcyclecounter() - c1t;
