@@ -44,7 +44,29 @@ def parse_args():
                          "default 2 x the worker count)")
     ap.add_argument("--cpu-workers", type=int, default=0,
                     help="CPU baseline processes (default: the usable cores, at most 16)")
+    ap.add_argument("--shard", default=None, metavar="R/S",
+                    help="emulate rank R of an S-GPU run on this one GPU: only that rank's samples are "
+                         "generated and resident, its pairs aligned (align + RBH timed); prints a "
+                         "shard_emulation line (C5 on a 1-GPU box)")
     return ap.parse_args()
+
+
+def launch_ranks(args):
+    """`--gpus N` without an outer launcher: run N ranks of this script under
+    torch.distributed.run as a CHILD process (nothing here has touched the
+    GPU; no exec) and pass rank 0's JSON line through. Returns the exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4"))
+    proc = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    for line in proc.stdout.splitlines():
+        print(line, flush=True)
+    return proc.returncode
 
 
 def src_hash():
@@ -198,23 +220,99 @@ def e2e_wall_clock(samples, genes, rank, world, dist, ref):
                     "tables + graph.pkl + matrix.h5 (every output the reference writes)"}
 
 
+def shard_samples(config, shard_count, rank):
+    """(samples, needed sample set, pair plan) of rank `rank` of a
+    `shard_count`-GPU run of `config`: with the config's per-node random
+    streams only the rank's own samples are generated (C5: ~17 of 33 Gbp),
+    the others come back as metadata (seq None)."""
+    from rna_clique_amd import distributed
+    from rna_clique_amd.simulate import simulate, CONFIGS
+    cfg = dict(CONFIGS[config])
+    if cfg.get("node_rng"):
+        meta, _ = simulate(only=[], **cfg)
+        bases = [int(s.tx_offsets[-1]) for s in meta]
+        need = distributed.needed_samples(bases, shard_count, rank)
+        del meta
+        samples, _ = simulate(only=sorted(need), **cfg)
+    else:
+        samples, _ = simulate(**cfg)
+        bases = [int(s.tx_offsets[-1]) for s in samples]
+        need = distributed.needed_samples(bases, shard_count, rank)
+    return samples, need, distributed.plan_pairs(bases, shard_count)
+
+
+def shard_emulation(args):
+    """--shard R/S: rank R's share of an S-GPU run on this one GPU (the pool
+    gives one GPU per box; the driver runs the real S-GPU bench). Only the
+    rank's samples are generated and resident; its pairs are aligned and go
+    through top-N / reciprocal best hits (align + finish: the rank's whole
+    data-parallel work), timed; then the graph phase runs on the rank's own
+    edges. Prints one shard_emulation JSON line: the rank's pairs/s, tiles,
+    measured HBM use vs distributed.hbm_footprint's model."""
+    R, S = (int(x) for x in args.shard.split("/"))
+    from rna_clique_amd import distributed
+    t_gen = time.perf_counter()
+    samples, need, (order, first) = shard_samples(args.config, S, R)
+    t_gen = time.perf_counter() - t_gen
+    bases = [int(s.tx_offsets[-1]) for s in samples]
+    genes = [len(set(s.gene.tolist())) for s in samples]
+    model = distributed.hbm_footprint(bases, genes, S)
+    my_pairs = int(first[R + 1] - first[R])
+    import torch
+    free0, total = torch.cuda.mem_get_info(0)
+    from rna_clique_amd.engine import Engine
+    eng = Engine(device=0, shard_rank=R, shard_count=S)
+    for i, s in enumerate(samples):
+        eng.add_sample(s.name, s.seq if i in need else None, s.tx_offsets, s.gene, s.iso)
+    del samples
+    eng.upload()
+    for _ in range(args.warmup):
+        eng.align()
+        eng.finish()
+    times = []
+    for _ in range(args.steps):
+        t0 = time.perf_counter()
+        eng.align()
+        eng.finish()
+        times.append(time.perf_counter() - t0)
+    tm = eng.timings()
+    free1, _ = torch.cuda.mem_get_info(0)
+    t0 = time.perf_counter()
+    eng.import_edges(eng.export_edges())   # the graph phase on this rank's own edges
+    t_graph = time.perf_counter() - t0
+    st = eng.stats()
+    dt = sum(times) / len(times)
+    line = {"metric": "shard_emulation: one rank's sample pairs/s (align + top-N/RBH of its pairs)",
+            "config": args.config, "rank": R, "shard_count": S, "pairs": my_pairs,
+            "total_pairs": len(order), "resident_samples": len(need),
+            "resident_bases": int(sum(bases[i] for i in need)),
+            "value": round(my_pairs / dt, 3), "unit": "sample-pairs/s", "s_per_step": round(dt, 3),
+            "steps": args.steps, "warmup": args.warmup,
+            "projected_job_pairs_per_s_if_balanced": round(len(order) / dt, 1),
+            "hbm_used_gb": round((free0 - free1) / 1e9, 2), "hbm_total_gb": round(total / 1e9, 1),
+            "hbm_model_gb": round(model[R] / 1e9, 2), "hbm_model_max_rank_gb": round(max(model) / 1e9, 2),
+            "graph_own_edges_s": round(t_graph, 3), "gen_s": round(t_gen, 1),
+            "phases_ms": {k: round(v, 3) for k, v in tm.items()},
+            "graph": {k: st[k] for k in ("seeds", "candidates", "hsps", "table_rows", "edges", "components",
+                                         "ideal_components")}}
+    print(json.dumps(line), flush=True)
+    eng.close()
+    return 0
+
+
 def main():
     args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if args.shard:
+        sys.exit(shard_emulation(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch as _t
-    ndev = max(1, _t.cuda.device_count())
-    device = local_rank % ndev   # one GPU per rank; ranks share a GPU only in rehearsals
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     import numpy as np
-    import torch
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(device)
-        dist.init_process_group(args.backend)
     from rna_clique_amd import distributed
-    from rna_clique_amd.engine import Engine
     from rna_clique_amd.simulate import simulate, CONFIGS
     cfg = CONFIGS[args.config]
     t_gen = time.perf_counter()
@@ -225,6 +323,7 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         # the CPU port on this host's cores, before anything touches the GPU
+        # (the device count below included: the pool's workers are forked)
         from oracle.parity import oracle_threads
         workers = args.cpu_workers or oracle_threads()
         n_cpu = args.cpu_pairs or 2 * workers
@@ -234,9 +333,21 @@ def main():
                "sample": f"{done} of {pairs} {args.config} sample pairs (both directed searches with DUST "
                          f"+ reciprocal best hits / table each, one pair per process, {workers} processes) "
                          f"in {secs:.1f} s; pairs/s extrapolated to the whole workload"}
+    import torch
+    ndev = max(1, torch.cuda.device_count())
+    device = local_rank % ndev   # one GPU per rank; ranks share a GPU only in rehearsals
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(device)
+        dist.init_process_group(args.backend)
+    from rna_clique_amd.engine import Engine
     eng = Engine(device=device, shard_rank=rank, shard_count=world)
-    for s in samples:
-        eng.add_sample(s.name, s.seq, s.tx_offsets, s.gene, s.iso)
+    # a rank holds the sequences of its own pairs' samples only
+    need = distributed.needed_samples([int(s.tx_offsets[-1]) for s in samples], world, rank) \
+        if world > 1 else set(range(n))
+    for i, s in enumerate(samples):
+        eng.add_sample(s.name, s.seq if i in need else None, s.tx_offsets, s.gene, s.iso)
     eng.upload()   # inputs resident in HBM before timing (H2D excluded)
 
     def step():
@@ -285,9 +396,14 @@ def main():
     bytes_launch = algorithmic_bytes(samples, hsps) * (1.0 / world)
     achieved = bytes_launch / (avg_k * 1e-3) / 1e9
     prof = pmc_profile(args.config, world)
+    traffic = prof.get("traffic_bytes_seed_extend") if prof else None
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": prof.get("traffic_bytes_seed_extend") if prof else None,
+            "traffic": traffic,
+            # the counters' bytes over the same kernel time: the HBM bandwidth
+            # actually moved (achieved/frac above use the byte model, per contract)
+            "measured_gbs": round(traffic / (avg_k * 1e-3) / 1e9, 1) if traffic else None,
+            "measured_frac": round(traffic / (avg_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
             "traffic_source": prof["file"] if prof else "no PMC profile of these sources (src_hash "
                                                        f"{src_hash()})",
             "kernel": "seed_kernel + extension kernels", "kernel_ms": round(avg_k, 3),

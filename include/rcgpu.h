@@ -136,7 +136,12 @@ const char *rc_last_error(void);
 /* Add one sample: `seq` holds all transcripts concatenated (ASCII; A/C/G/T
  * any case, anything else is an ambiguous base), tx_offsets[n_tx + 1] their
  * boundaries; gene / iso the parsed TranscriptID fields (transcripts.py:60-126).
- * `label` is the sample string used in tables and matrix order. */
+ * `label` is the sample string used in tables and matrix order.
+ * seq == NULL (with tx_offsets, gene, iso as usual): a sample this engine does
+ * not align -- in a sharded run, one no pair of this shard touches. Its
+ * transcripts and genes still count (graph nodes, the e-value search space of
+ * searches against it); its bases are not copied to the device. rc_align
+ * fails with RC_E_STATE if a pair of this shard has such a sample. */
 int rc_add_sample(rc_engine *eng, const char *label, const char *seq,
                   const uint64_t *tx_offsets, const int32_t *gene,
                   const int32_t *iso, uint32_t n_tx, int32_t *sample_id);
@@ -154,9 +159,13 @@ int rc_upload(rc_engine *eng);
 /* Phases. rc_run = rc_align + rc_finish (single shard).
  *
  * Sharded use (shard_count > 1, one engine per GPU, every engine given the
- * same samples): the C(N,2) sample pairs, in combinations order, are cut into
- * shard_count contiguous ranges of about equal sequence length; rc_align runs
- * seed-and-extend for this shard's pairs only, and rc_finish the top-N and
+ * same samples in the same order -- with their sequences only where this
+ * shard needs them, seq == NULL for the others; see rc_add_sample): the C(N,2)
+ * sample pairs are cut by rc_plan_pairs into one rectangle [a0, a1) x [b0, b1)
+ * of the pair triangle per shard, so a shard's resident samples are
+ * [a0, a1) u [b0, b1) (rna_clique_amd.distributed.needed_samples); rc_align
+ * runs seed-and-extend for this shard's pairs only (in alignment tiles of
+ * < 2^32 bases when its samples do not fit one pass), and rc_finish the top-N and
  * reciprocal-best-hit step for them, producing this shard's gene matches
  * tables and graph edges. The gene matches graph and the ideal-clique filter
  * are global, so the edges are then exchanged (one all-gather) and every shard
@@ -224,6 +233,10 @@ int rc_pair_sums_unfiltered(rc_engine *eng, int64_t *num, int64_t *den);
 /* order[n]: sample ids in output order; out: n x n row-major distances.
  * Returns RC_E_NO_IDEAL when some pair has no ideal rows. */
 int rc_distance(rc_engine *eng, const int32_t *order, double *out);
+/* The same for n distinct samples: order[n], out n x n (the matrix of the
+ * samples a SampleSimilarity built from tables knows, filtered_distance.py:
+ * 162-169 / similarity_computer.py:216-226: samples = the tables' keys). */
+int rc_distance_subset(rc_engine *eng, const int32_t *order, int32_t n, double *out);
 int rc_timings(rc_engine *eng, rc_timing *t);
 /* The DUST mask of sample `s` after rc_run / rc_align: one byte per base of
  * its concatenated transcripts (1 = masked query base, spec 1b of the oracle);

@@ -127,6 +127,7 @@ SIGNATURES = {
     "rc_pair_sums": (ctypes.c_int, [VP, VP, VP]),
     "rc_pair_sums_unfiltered": (ctypes.c_int, [VP, VP, VP]),
     "rc_distance": (ctypes.c_int, [VP, VP, VP]),
+    "rc_distance_subset": (ctypes.c_int, [VP, VP, ctypes.c_int32, VP]),
     "rc_timings": (ctypes.c_int, [VP, P(RcTiming)]),
     "rc_dust_mask": (ctypes.c_int, [VP, ctypes.c_int32, VP, ctypes.c_uint64, P(ctypes.c_uint64)]),
     "rc_fasta_open": (ctypes.c_int, [ctypes.c_char_p, P(VP)]),

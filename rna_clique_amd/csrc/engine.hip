@@ -50,7 +50,7 @@ void launch_cc(const DEdge *, uint64_t, uint32_t, const int32_t *, int, int, uin
 void launch_pair_sums(const DEdge *, uint64_t, const uint32_t *, const uint8_t *, unsigned long long *,
                       unsigned long long *, unsigned long long *, unsigned long long *, hipStream_t);
 void launch_distance(const unsigned long long *, const unsigned long long *, const int32_t *, const int32_t *,
-                     int, double *, unsigned int *, hipStream_t);
+                     int, int, double *, unsigned int *, hipStream_t);
 }  // namespace rcg
 
 using namespace rcg;
@@ -470,7 +470,7 @@ int rc_add_sample(rc_engine *e, const char *label, const char *seq, const uint64
         s.abase = align_up(e->ascii_used);
         const uint64_t need = align_up(s.abase + nb) + 64;
         if (need > e->d_ascii.cap) {
-            const size_t cap = std::max<size_t>({(size_t)need, 2 * e->d_ascii.cap, (size_t)1 << 28});
+            const size_t cap = std::max<size_t>({(size_t)need, e->d_ascii.cap + e->d_ascii.cap / 4, (size_t)1 << 28});
             uint8_t *np = nullptr;
             if (hipMalloc((void **)&np, cap) != hipSuccess) {
                 (void)hipGetLastError();
@@ -2135,29 +2135,38 @@ int rc_pair_sums_unfiltered(rc_engine *e, int64_t *num, int64_t *den)
     return RC_OK;
 }
 
-int rc_distance(rc_engine *e, const int32_t *order, double *out)
+int rc_distance_subset(rc_engine *e, const int32_t *order, int32_t n, double *out)
 {
-    if (!e || !order || !out) return fail(RC_E_ARG, "null argument");
+    if (!e || (n && (!order || !out))) return fail(RC_E_ARG, "null argument");
     if (!e->finished) return fail(RC_E_STATE, "no results yet");
     const int N = (int)e->samples.size();
+    if (n < 0 || n > N) return fail(RC_E_ARG, "bad sample count");
     std::vector<int> seen(N, 0);
-    for (int i = 0; i < N; i++) {
-        if (order[i] < 0 || order[i] >= N || seen[order[i]]) return fail(RC_E_ARG, "order must be a permutation");
+    for (int i = 0; i < n; i++) {
+        if (order[i] < 0 || order[i] >= N || seen[order[i]]) return fail(RC_E_ARG, "order must hold distinct sample ids");
         seen[order[i]] = 1;
     }
+    if (!n) return RC_OK;
     CHK(set_device(e));
-    CHK(e->d_order.ensure(N));
-    CHK(e->d_dist.ensure((size_t)N * N));
-    HIPCHK(hipMemcpyAsync(e->d_order.p, order, N * 4, hipMemcpyHostToDevice, e->st));
+    CHK(e->d_order.ensure(n));
+    CHK(e->d_dist.ensure((size_t)n * n));
+    HIPCHK(hipMemcpyAsync(e->d_order.p, order, n * 4, hipMemcpyHostToDevice, e->st));
     HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
-    launch_distance(e->d_num.p, e->d_den.p, e->d_pair_index.p, e->d_order.p, N, e->d_dist.p, e->d_status.p, e->st);
+    launch_distance(e->d_num.p, e->d_den.p, e->d_pair_index.p, e->d_order.p, N, n, e->d_dist.p, e->d_status.p,
+                    e->st);
     HIPCHK(hipGetLastError());
     unsigned int status = 0;
-    HIPCHK(hipMemcpyAsync(out, e->d_dist.p, (size_t)N * N * 8, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipMemcpyAsync(out, e->d_dist.p, (size_t)n * n * 8, hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipMemcpyAsync(&status, e->d_status.p, 4, hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
     if (status & 4u) return fail(RC_E_NO_IDEAL, "No ideal components found. Cannot report distances!");
     return RC_OK;
+}
+
+int rc_distance(rc_engine *e, const int32_t *order, double *out)
+{
+    if (!e) return fail(RC_E_ARG, "null argument");
+    return rc_distance_subset(e, order, (int32_t)e->samples.size(), out);
 }
 
 int rc_dust_mask(rc_engine *e, int32_t s, uint8_t *buf, uint64_t cap, uint64_t *n)

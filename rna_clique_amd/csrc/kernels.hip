@@ -670,12 +670,12 @@ __global__ void pair_sums_kernel(const DEdge *edges, uint64_t n_edges, const uin
 
 // d = float(1 - Fraction(num, den)) = correctly rounded (den - num) / den
 __global__ void distance_kernel(const unsigned long long *num, const unsigned long long *den,
-                                const int32_t *pair_index, const int32_t *order, int N, double *out,
+                                const int32_t *pair_index, const int32_t *order, int N, int M, double *out,
                                 unsigned int *status)
 {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= N * N) return;
-    const int i = t / N, j = t % N;
+    if (t >= M * M) return;
+    const int i = t / M, j = t % M;
     const int a = order[i], b = order[j];
     if (a == b) {
         out[t] = 0.0;
@@ -900,12 +900,12 @@ void launch_pair_sums(const DEdge *edges, uint64_t n_edges, const uint32_t *pare
 }
 
 void launch_distance(const unsigned long long *num, const unsigned long long *den, const int32_t *pair_index,
-                     const int32_t *order, int N, double *out, unsigned int *status, hipStream_t st)
+                     const int32_t *order, int N, int M, double *out, unsigned int *status, hipStream_t st)
 {
-    const int n = N * N;
+    const int n = M * M;
     if (!n) return;
     hipLaunchKernelGGL(distance_kernel, dim3((n + 255) / 256), dim3(256), 0, st, num, den, pair_index, order, N,
-                       out, status);
+                       M, out, status);
 }
 
 void launch_gather_rows(const DHsp *hsp, const DRow *rows, uint64_t n, DHsp *out, hipStream_t st)

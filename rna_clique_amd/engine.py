@@ -218,16 +218,18 @@ class Engine:
         return num, den
 
     def distance(self, order=None):
-        """N x N distances with rows/columns in `order` (default: sorted labels,
-        similarity_computer.py:220). Raises NativeError(RC_E_NO_IDEAL) when a
-        pair has no ideal rows."""
+        """Distances with rows/columns in `order` (default: every sample in
+        sorted label order, similarity_computer.py:220; a subset of the
+        samples gives their matrix only). Raises NativeError(RC_E_NO_IDEAL)
+        when a pair has no ideal rows."""
         n = len(self.labels)
         if order is None:
             order = sorted(range(n), key=lambda i: self.labels[i])
         order = np.ascontiguousarray(order, dtype=np.int32)
-        out = np.zeros((n, n), dtype=np.float64)
-        nat.check(nat.lib().rc_distance(self._h, order.ctypes.data_as(ctypes.c_void_p),
-                                        out.ctypes.data_as(ctypes.c_void_p)))
+        m = len(order)
+        out = np.zeros((m, m), dtype=np.float64)
+        nat.check(nat.lib().rc_distance_subset(self._h, order.ctypes.data_as(ctypes.c_void_p), m,
+                                               out.ctypes.data_as(ctypes.c_void_p)))
         return [self.labels[i] for i in order], out
 
     def dust_mask(self, s):

@@ -72,8 +72,9 @@ def find_all_pairs(inputs: Iterable[Path], output_dir: Path, cache_dir: Optional
         for a, b in itertools.combinations(range(len(inputs)), 2):
             if (a, b) in out_paths:
                 yield pair_table(eng, a, b)
-    paths = map(lambda x: make_output_path(output_dir, *x, path_to_sample=path_to_sample, extension=ext),
-                itertools.combinations(inputs, 2))
+    # the table files in combinations order; a sharded run (rank of a
+    # torch.distributed group) returns the pairs it owns and wrote only
+    paths = (out_paths[ab] for ab in itertools.combinations(range(len(inputs)), 2) if ab in out_paths)
     return tables(), paths, math.comb(len(inputs), 2)
 
 

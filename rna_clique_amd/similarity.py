@@ -84,6 +84,13 @@ class SampleSimilarity:
         self.engine = _graph_engine(graph, list(self._stored.items()), sample_count, device)
         self.labels = list(self.engine.labels)
         self._sample_count = self.engine.stats()["sample_count"]
+        # the similarities are those of the given tables' pairs, and the
+        # matrix's samples the tables' samples (similarity_computer.py:216-226:
+        # samples = key elements of the similarities); a sample known only
+        # from graph nodes is no row of the matrix
+        idx = {lab: i for i, lab in enumerate(self.labels)}
+        self._sim_pairs = sorted({tuple(sorted((idx[str(a)], idx[str(b)])))
+                                  for a, b in self._stored.keys() if str(a) != str(b)})
         self._samples = None
 
     @classmethod
@@ -95,6 +102,7 @@ class SampleSimilarity:
         self._sample_count = engine.stats()["sample_count"]
         self._graph = None
         self._stored = PairDict(self._table_iter()) if store_dfs else None
+        self._sim_pairs = None   # every pair of the run
         self._samples = None
         return self
 
@@ -102,7 +110,11 @@ class SampleSimilarity:
     def mapping_from_dfs(cls, dfs):
         """(pair, table) from each table's own qsample/ssample columns
         (similarity_computer.py:90-115; the first row rather than label 0,
-        see SURVEY.md Q1)."""
+        see SURVEY.md Q1). An empty table names no samples: the reference
+        fails on it (KeyError from df["qsample"][0], Q1/Q3); here it is
+        skipped, so its pair is not among the similarities (and its samples
+        are in the matrix only if another table names them) --
+        tests/test_gpu_api.py::test_sample_similarity_matrix_samples_from_tables."""
         for df in dfs:
             if len(df):
                 yield frozenset((str(df["qsample"].iloc[0]), str(df["ssample"].iloc[0]))), df
@@ -245,11 +257,14 @@ class SampleSimilarity:
         """(num, den) int64 N x N: restricted sums of nident and length - gaps."""
         return self.engine.pair_sums()
 
+    def _sim_pair_iter(self):
+        return self._sim_pairs if getattr(self, "_sim_pairs", None) is not None else self._pairs()
+
     @cached_property
     def similarities(self) -> PairDict:
         num, den = self.pair_sums()
         res = PairDict()
-        for a, b in self._pairs():
+        for a, b in self._sim_pair_iter():
             if den[a, b] == 0:
                 raise NoIdealComponentsError()
             res[(self.labels[a], self.labels[b])] = Fraction(int(num[a, b]), int(den[a, b]))
@@ -272,7 +287,10 @@ class SampleSimilarity:
     @property
     def samples(self):
         if self._samples is None:
-            self._samples = sorted(set(self.labels)) if len(self.labels) > 1 else []
+            if getattr(self, "_sim_pairs", None) is not None:
+                self._samples = sorted({self.labels[i] for p in self._sim_pairs for i in p})
+            else:
+                self._samples = sorted(set(self.labels)) if len(self.labels) > 1 else []
         return self._samples
 
     def _order(self):

@@ -121,6 +121,31 @@ def _hky85_mutate(seq, expected_subs, rng, kappa=2.0):
     return out
 
 
+def _hky85_mutate_sparse(seq, expected_subs, rng, kappa=2.0, inplace=False):
+    """_hky85_mutate for long sequences: site draws with replacement, repeats
+    dropped (k^2 / 2n of k sites, ~0.2 % at C5), so no O(n) choice; inplace
+    reuses `seq` (its last use)."""
+    n = seq.size
+    k = rng.binomial(n, 1.0 - math.exp(-expected_subs))
+    if k == 0:
+        return seq
+    pos = np.unique(rng.integers(0, n, size=k))
+    r = rng.random(pos.size) * (kappa + 2.0)
+    old = seq[pos]
+    new = np.where(r < kappa, old ^ 2, np.where(r < kappa + 1.0, old ^ 1, old ^ 3))
+    out = seq if inplace else seq.copy()
+    out[pos] = new.astype(np.uint8)
+    return out
+
+
+_ASCII_TABLE = bytes(_BASES.tolist()) + bytes(252)
+
+
+def _ascii(codes):
+    """uint8 codes 0..3 -> ASCII bases (bytes.translate: ~10x a fancy index)."""
+    return np.frombuffer(codes.tobytes().translate(_ASCII_TABLE), dtype=np.uint8)
+
+
 def _indels(gene_seqs, rate, rng):
     """Short insertions/deletions (1-6 bp) at `rate` per base."""
     out = []
@@ -148,12 +173,25 @@ def _revcomp(codes):
 def simulate(taxa, genes, seed=487, len_loc=1950, len_n=1000, len_p=0.1,
              len_uniform=None, mutation_rate=0.01, p_iso2=0.0, indel_rate=0.0,
              permute_genes=True, prefix="T", p_revcomp=0.0, p_paralog=0.0,
-             rich_genes=0, rich_iso=1, polya=None):
+             rich_genes=0, rich_iso=1, polya=None, node_rng=False, only=None):
     """Simulate `taxa` transcriptomes with `genes` orthologous genes each.
 
     len_uniform=(lo, hi) draws lengths uniformly instead of loc + Binomial.
+    node_rng: every tree node's substitutions and every leaf's own draws come
+    from their own seeded stream (default_rng([seed, 2, node]) and
+    default_rng([seed, 3, leaf index])), so any subset of the leaves can be
+    generated alone with the same bases -- the C5 mode (33 Gbp; a shard needs
+    only its own samples).
+    only: with node_rng, the leaf indices whose sequences are generated; the
+    other samples come back with seq None and their metadata (transcript
+    offsets, gene and isoform ids, coverage), as a shard that does not align
+    them adds them (rc_add_sample with seq NULL).
     Returns (samples, tree) where tree = (parent, branch_length, leaves).
     """
+    plain = (p_iso2 == 0 and indel_rate == 0 and p_revcomp == 0 and p_paralog == 0
+             and not rich_genes and polya is None)
+    if only is not None and not (node_rng and plain):
+        raise ValueError("only= needs node_rng=True and no per-gene extras")
     rng = np.random.default_rng(seed)
     parent, blen, leaves = birth_death_tree(taxa, rng)
     if len_uniform is not None:
@@ -163,11 +201,22 @@ def simulate(taxa, genes, seed=487, len_loc=1950, len_n=1000, len_p=0.1,
     total = int(lengths.sum())
     offs = np.zeros(genes + 1, dtype=np.int64)
     offs[1:] = np.cumsum(lengths)
-    root = rng.integers(0, 4, size=total, dtype=np.uint8)
     children = {}
     for v, p in enumerate(parent):
         if p >= 0:
             children.setdefault(int(p), []).append(v)
+    wanted = set(range(len(leaves))) if only is None else {int(i) for i in only}
+    # nodes on the way to a wanted leaf (node_rng: the other subtrees are skipped)
+    live = set()
+    for li in wanted:
+        v = int(leaves[li])
+        while v >= 0 and v not in live:
+            live.add(v)
+            v = int(parent[v])
+    if node_rng:
+        root = np.random.default_rng([seed, 1]).integers(0, 4, size=total, dtype=np.uint8)
+    else:
+        root = rng.integers(0, 4, size=total, dtype=np.uint8)
     # depth-first, keeping only the sequences still needed
     seqs = {0: root}
     leaf_seq = {}
@@ -179,9 +228,17 @@ def simulate(taxa, genes, seed=487, len_loc=1950, len_n=1000, len_p=0.1,
         if not kids:
             leaf_seq[v] = s
             continue
+        live_kids = [c for c in kids if c in live]
         for c in kids:
-            seqs[c] = _hky85_mutate(s, mutation_rate * blen[c], rng)
-            stack.append(c)
+            if node_rng:
+                if c in live:
+                    seqs[c] = _hky85_mutate_sparse(s, mutation_rate * blen[c], np.random.default_rng([seed, 2, c]),
+                                                   inplace=c == live_kids[-1])
+                    stack.append(c)
+            else:
+                seqs[c] = _hky85_mutate(s, mutation_rate * blen[c], rng)
+                stack.append(c)
+        del s
     iso2 = rng.random(genes) < p_iso2
     rich = set(rng.choice(genes, size=min(rich_genes, genes), replace=False).tolist()) if rich_genes else set()
     # skipped segments of the isoform-rich genes, shared by every taxon
@@ -197,6 +254,20 @@ def simulate(taxa, genes, seed=487, len_loc=1950, len_n=1000, len_p=0.1,
     cov = rng.uniform(0, 10000, size=genes)
     samples = []
     for li, leaf in enumerate(leaves):
+        lrng = np.random.default_rng([seed, 3, li]) if node_rng else rng
+        if plain:
+            # one isoform per gene in gene order: the transcripts are the leaf
+            # sequence itself (the same data the per-gene loop below builds)
+            gid = (lrng.permutation(genes) if permute_genes else np.arange(genes)) + 1
+            tcov = cov * lrng.uniform(0.9, 1.1, size=genes)
+            s = leaf_seq.pop(leaf, None)
+            samples.append(Sample(
+                name=f"{prefix}{li}", seq=None if s is None else _ascii(s),
+                tx_offsets=offs.astype(np.uint64), gene=gid.astype(np.int32),
+                iso=np.ones(genes, dtype=np.int32), cov=tcov.astype(np.float64)))
+            del s
+            continue
+        rng = lrng
         s = leaf_seq[leaf]
         gseqs = [s[offs[g]:offs[g + 1]] for g in range(genes)]
         if indel_rate > 0:
@@ -247,7 +318,8 @@ CONFIGS = {
     "C2": dict(taxa=8, genes=10000, seed=488),
     "C3": dict(taxa=32, genes=50000, seed=489, len_loc=950, len_n=100, len_p=0.5),
     "C4": dict(taxa=64, genes=50000, seed=490, len_loc=950, len_n=100, len_p=0.5),
-    "C5": dict(taxa=128, genes=100000, seed=491, len_uniform=(200, 5000)),
+    # C5 uses per-node random streams: one shard's samples can be generated alone
+    "C5": dict(taxa=128, genes=100000, seed=491, len_uniform=(200, 5000), node_rng=True),
     # C3 with the features of real transcriptomes (correctness variant of the
     # GPU tests; a bench workload too): 10 % two-isoform genes, indels, half the
     # genes on the minus strand, 2 % recent paralogs, poly-A tails on 20 %

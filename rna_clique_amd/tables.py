@@ -14,6 +14,7 @@ when a caller asks (store_dfs, od2 files, graph.pkl):
 from __future__ import annotations
 
 import numbers
+import threading
 from pathlib import Path
 
 import numpy as np
@@ -100,11 +101,18 @@ def pair_table(engine, a: int, b: int, labels=None) -> pd.DataFrame:
     return rows_to_table(engine.pair_rows(a, b), labels[a], labels[b])
 
 
+# PyTables and a default (non-thread-safe) HDF5 build must not be entered from
+# two threads at once, and PyTables releases the GIL around HDF5 calls: every
+# to_hdf / read_hdf of this module holds this lock (write_pair_tables writes
+# tables from a thread pool)
+_HDF5_LOCK = threading.Lock()
+
+
 def write_table(df: pd.DataFrame, path: Path):
     """gene_matches_tables.py:42-56: .pkl via pandas; .h5 in pandas' table
-    format under key "gene_matches" -- through PyTables when it is importable,
-    else written directly (h5.write_frame_table; read back by PyTables in
-    tests/test_h5_pytables.py)."""
+    format under key "gene_matches" -- through PyTables when it is importable
+    (serialised by _HDF5_LOCK), else written directly (h5.write_frame_table;
+    read back by PyTables in tests/test_h5_pytables.py)."""
     path = Path(path)
     if path.suffix == ".pkl":
         df.to_pickle(path)
@@ -115,7 +123,8 @@ def write_table(df: pd.DataFrame, path: Path):
             from .h5 import write_frame_table
             write_frame_table(path, df, key="gene_matches")
         else:
-            df.to_hdf(path, key="gene_matches", format="table")
+            with _HDF5_LOCK:
+                df.to_hdf(path, key="gene_matches", format="table")
     else:
         raise ValueError(f"Could not determine file type for extension {path.suffix}.")
 
@@ -133,7 +142,8 @@ def read_table(path: Path) -> pd.DataFrame:
         except ImportError:
             from .h5 import read_frame_table
             return read_frame_table(path, key="gene_matches")
-        return pd.read_hdf(path, key="gene_matches")
+        with _HDF5_LOCK:
+            return pd.read_hdf(path, key="gene_matches")
     raise ValueError(f"Could not determine file type for extension {path.suffix}.")
 
 

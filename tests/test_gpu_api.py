@@ -286,6 +286,32 @@ def test_sample_similarity_arbitrary_graph(native):
         assert (int(num[a, b]), int(den[a, b])) == want
 
 
+def test_sample_similarity_matrix_samples_from_tables(native):
+    """The matrix's samples are the tables' samples (similarity_computer.py:
+    216-226: sorted key elements of the similarities), not the graph's: a
+    sample known only from graph nodes -- with an explicit sample_count, so
+    the ideal filter is unchanged -- is no row of the matrix, and the matrix
+    is the reference's golden one. An empty table is skipped
+    (mapping_from_dfs; the reference fails on it)."""
+    import json
+    from rna_clique_amd.similarity import SampleSimilarity
+    d = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "post_alignment.json")))
+    fx = next(f for f in d["fixtures"] if not f["expected"]["errors"] and f["expected"]["matrix"])
+    exp = fx["expected"]
+    g, dfs = _golden_inputs(fx, d["columns"])
+    g.add_node(("zzz_graph_only", 7))
+    g.add_edge(("zzz_graph_only", 8), ("zzz_graph_only2", 9))
+    sim = SampleSimilarity(g, dfs, sample_count=exp["sample_count"])
+    assert "zzz_graph_only" in sim.labels
+    df = sim.get_dissimilarity_df()
+    assert list(df.index) == exp["matrix"]["labels"] == list(df.columns)
+    assert np.array_equal(df.to_numpy(), np.array(exp["matrix"]["values"]))
+    assert set(sim.get_similarities().key_elements()) == set(exp["matrix"]["labels"])
+    empty = dfs[0][1].iloc[0:0]
+    kept = list(SampleSimilarity.mapping_from_dfs([empty] + [t for _, t in dfs]))
+    assert len(kept) == len(dfs)
+
+
 def test_tables_and_graph_reload(native, tmp_path):
     """The resume path (CS3): rna_clique() writes od2 tables and graph.pkl,
     SampleSimilarity.from_filenames reads them back and gives the same

@@ -1,0 +1,156 @@
+"""GPU: the sharded path at BASELINE configuration scale.
+
+* C4 (64 x 50 000, BASELINE configs[3]) cut into the 8 shards of an 8-GPU
+  run, the shard engines run one after another on the one GPU of the box,
+  each holding only its own pairs' samples and closed after exporting its
+  edges; the concatenated edges imported into a graph-only engine give the
+  unsharded run's distances, sums, edges and ideal nodes bit for bit, and
+  every shard's tables equal the unsharded tables of the same pairs
+  (find_all_pairs.py:224-228 runs the pairs independently).
+* C5 (128 x 100 000, 200 bp - 5 kb, BASELINE configs[4]): rank 2 of 8 -- the
+  largest modelled HBM footprint -- alone on the GPU with only its 65 of 128
+  samples generated and resident, cut into alignment tiles: whole-shard
+  properties, determinism, two owned pairs bit-exact vs the oracle, and the
+  measured HBM use against distributed.hbm_footprint's model.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle.parity import check_pairs
+
+pytestmark = pytest.mark.gpu
+
+
+def _edge_digest(rec):
+    """(count, order-independent 64-bit digests) of fixed-size records, an
+    (n, record bytes) uint8 array (records are unique, so equal digests mean
+    equal sets up to hash collisions)."""
+    n, rs = rec.shape
+    if rs % 8:
+        rec = np.concatenate([rec, np.zeros((n, 8 - rs % 8), np.uint8)], axis=1)
+    u = np.ascontiguousarray(rec).view(np.uint64)
+    h = np.zeros(n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        for c in range(u.shape[1]):
+            x = (u[:, c] + np.uint64(0x9E3779B97F4A7C15) * np.uint64(c + 1)) ^ h
+            x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            h = x ^ (x >> np.uint64(31))
+        return n, int(h.sum(dtype=np.uint64)), int(np.bitwise_xor.reduce(h)) if n else 0
+
+
+def _records(arr, rs):
+    return np.ascontiguousarray(arr).view(np.uint8).reshape(-1, rs)
+
+
+def _record(name, obj):
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(os.path.join("gpurun_out", f"{name}.json"), "w") as f:
+        json.dump(obj, f, indent=1)
+
+
+def test_C4_eight_shards_match_unsharded(native):
+    from rna_clique_amd import distributed
+    from rna_clique_amd.engine import Engine
+    from rna_clique_amd.simulate import CONFIGS, simulate
+    samples, _ = simulate(**CONFIGS["C4"])
+    N, S = len(samples), 8
+    bases = [int(s.tx_offsets[-1]) for s in samples]
+    ref = Engine(device=0)
+    for s in samples:
+        ref.add_sample(s.name, s.seq, s.tx_offsets, s.gene, s.iso)
+    ref.run()
+    want = {"distance": ref.distance()[1], "sums": ref.pair_sums(), "usums": ref.pair_sums(unfiltered=True),
+            "edges": _edge_digest(_records(ref.edges(), 16)), "ideal": sorted(zip(*ref.ideal_nodes())), "stats": ref.stats()}
+    order, first = distributed.plan_pairs(bases, S)
+    # six pairs of every shard: first, last and four spread between
+    check = {}
+    for r in range(S):
+        own = order[int(first[r]):int(first[r + 1])]
+        for k in sorted({0, len(own) - 1, *(len(own) * j // 5 for j in range(1, 5))}):
+            check[own[k]] = ref.pair_rows(*own[k]).tobytes()
+    ref.close()
+    parts, resident = [], []
+    for r in range(S):
+        need = distributed.needed_samples(bases, S, r)
+        resident.append(len(need))
+        e = Engine(device=0, shard_rank=r, shard_count=S)
+        for i, s in enumerate(samples):
+            e.add_sample(s.name, s.seq if i in need else None, s.tx_offsets, s.gene, s.iso)
+        e.align()
+        e.finish()
+        assert e.owned_pairs() == order[int(first[r]):int(first[r + 1])]
+        for p in e.owned_pairs():
+            if p in check:
+                assert e.pair_rows(*p).tobytes() == check[p], (r, p)
+        parts.append(e.export_edges())
+        e.close()
+    assert max(resident) < N
+    g = Engine(device=0)   # graph-only: every shard's edges, as each rank has after the all-gather
+    for s in samples:
+        g.add_sample(s.name, None, s.tx_offsets, s.gene, s.iso)
+    g.import_edges(np.concatenate(parts))
+    assert np.array_equal(g.distance()[1], want["distance"])
+    for got, exp in ((g.pair_sums(), want["sums"]), (g.pair_sums(unfiltered=True), want["usums"])):
+        assert np.array_equal(got[0], exp[0]) and np.array_equal(got[1], exp[1])
+    assert _edge_digest(_records(g.edges(), 16)) == want["edges"]
+    assert sorted(zip(*g.ideal_nodes())) == want["ideal"]
+    st = g.stats()
+    for k in ("edges", "components", "ideal_components", "ideal_nodes", "sample_count"):
+        assert st[k] == want["stats"][k], k
+    _record("C4_shards", {"resident_samples": resident, "edges": st["edges"], "checked_pairs": len(check)})
+    g.close()
+
+
+def test_C5_one_rank_shard(native):
+    import torch
+    from bench import shard_samples
+    from rna_clique_amd import distributed
+    from rna_clique_amd.engine import Engine
+    S = 8
+    # the rank with the largest modelled footprint (rank 2 at C5)
+    samples, need, (order, first) = shard_samples("C5", S, 2)
+    bases = [int(s.tx_offsets[-1]) for s in samples]
+    genes = [len(np.unique(s.gene)) for s in samples]
+    model = distributed.hbm_footprint(bases, genes, S)
+    R = int(np.argmax(model))
+    assert R == 2
+    assert len(need) < len(samples) and all((samples[i].seq is None) == (i not in need) for i in range(128))
+    free0, _ = torch.cuda.mem_get_info(0)
+    eng = Engine(device=0, shard_rank=R, shard_count=S)
+    for i, s in enumerate(samples):
+        eng.add_sample(s.name, s.seq if i in need else None, s.tx_offsets, s.gene, s.iso)
+    eng.align()
+    eng.finish()
+    tm = eng.timings()
+    assert tm["tiles"] > 1
+    free1, _ = torch.cuda.mem_get_info(0)
+    own = eng.owned_pairs()
+    assert own == order[int(first[R]):int(first[R + 1])] and len(own) > 900
+    edges = eng.export_edges()
+    # determinism: the rank's whole pass again gives the same edges
+    eng.align()
+    eng.finish()
+    again = eng.export_edges()
+    rs = Engine.edge_record_size()
+    assert _edge_digest(_records(again, rs)) == _edge_digest(_records(edges, rs))
+    eng.import_edges(edges)   # the graph phase over this rank's own edges
+    st = eng.stats()
+    num, den = eng.pair_sums()
+    unum, uden = eng.pair_sums(unfiltered=True)
+    assert np.array_equal(unum, unum.T) and np.array_equal(uden, uden.T)
+    for a, b in own:
+        assert 0 < unum[a, b] <= uden[a, b]
+        assert 0 <= num[a, b] <= unum[a, b] and 0 <= den[a, b] <= uden[a, b]
+    _record("C5_shard", {"rank": R, "pairs": len(own), "resident_samples": len(need),
+                         "hbm_used_gb": (free0 - free1) / 1e9, "hbm_model_gb": model[R] / 1e9,
+                         "timings": tm, "stats": st})
+    assert (free0 - free1) < 1.25 * model[R]
+    # two owned pairs against the oracle (both directed searches, table, sums)
+    picks = [own[0], own[len(own) // 2]]
+    msgs = check_pairs(eng, samples, picks)
+    assert not msgs, "\n".join(msgs[:10])
+    eng.close()
