@@ -243,6 +243,18 @@ int rc_timings(rc_engine *eng, rc_timing *t);
  * all zero when DUST is off. buf == NULL queries the size. */
 int rc_dust_mask(rc_engine *eng, int32_t s, uint8_t *buf, uint64_t cap, uint64_t *n);
 
+/* ---- outputs next to matrix.h5 (od2 tables, graph.pkl) -------------------
+ * rc_write_outputs: the gene matches table files of pairs (s1[i], s2[i]) at
+ * table_paths[i] (pandas table format, key "gene_matches": write_table,
+ * gene_matches_tables.py:42-56; NULL = none) and graph.pkl at graph_path
+ * (build_graph over the pairs in the given order + pickle.dump, build_graph.py:
+ * 40-68, filtering_step.py:158-159; NULL = none; single-shard engines), each
+ * pair's rows fetched once, the files written by `threads` host threads.
+ * rc_table_write_rows: one table file from rc_row records (host only). */
+int rc_write_outputs(rc_engine *eng, int32_t n_pairs, const int32_t *s1, const int32_t *s2,
+                     const char *const *table_paths, const char *graph_path, int32_t threads);
+int rc_table_write_rows(const rc_row *rows, uint64_t n, const char *ssample, const char *qsample, const char *path);
+
 /* ---- FASTA input (host only; fasta.cpp) ----------------------------------
  * Replaces the Bio.SeqIO passes of TopGeneSelector (select_top_genes.py:108-127)
  * and the Bio.SeqIO.write of select_top_and_save (select_top_genes_all.py:12-46).

@@ -7,10 +7,11 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "librcgpu.so")
-SOURCES = ["kernels.hip", "align.hip", "dust.hip", "engine.hip", "fasta.cpp", "graph_pickle.cpp"]
+SOURCES = ["kernels.hip", "align.hip", "dust.hip", "engine.hip", "fasta.cpp", "graph_pickle.cpp",
+           "od2_tables.cpp"]
 HEADERS = ["device.h", os.path.join("..", "..", "include", "rcgpu.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread",
          "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
 
 

@@ -25,7 +25,7 @@ constexpr int SBLOCK = 256;
 #define RC_SEED_CAP 1024
 #endif
 #ifndef RC_SEED_WAVES
-#define RC_SEED_WAVES 1
+#define RC_SEED_WAVES 4   // min blocks per CU: 4 waves/SIMD (what the LDS allows), <= 128 VGPRs
 #endif
 constexpr int SEED_CAP = RC_SEED_CAP;   // seeds of one pass in LDS (a power of two: the bitonic sort pads to one)
 static_assert((SEED_CAP & (SEED_CAP - 1)) == 0, "RC_SEED_CAP must be a power of two");
@@ -149,8 +149,9 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
     __shared__ uint32_t hq_pos[SBLOCK / 64][64 * HBATCH];   // per-wave queue of hits for the full test
     __shared__ uint8_t hq_k[SBLOCK / 64][64 * HBATCH];
     __shared__ uint64_t it_qlw[SBLOCK], it_qlm[AMB ? SBLOCK : 1];
-    __shared__ uint64_t iso_start[MAX_ISO];
-    __shared__ uint32_t iso_len[MAX_ISO], iso_gtx[MAX_ISO], iso_pre[MAX_ISO + 1];
+    __shared__ uint64_t iso_start[ISO_LDS];
+    __shared__ uint32_t iso_len[ISO_LDS], iso_gtx[ISO_LDS], iso_pre[ISO_LDS + 1];
+    __shared__ uint16_t it_iso[SBLOCK];   // isoform of each word item (it_info: p | strand << 24)
     __shared__ uint32_t tcnt[MAX_SAMPLES], tpre[MAX_SAMPLES + 1];
     __shared__ uint32_t wsum[SBLOCK / 64];
     __shared__ uint32_t sh_nseed, sh_flags, sh_rs0, sh_rs1;
@@ -171,25 +172,36 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
         if (tid == 0) atomicOr(P.status, 2u);
         return;
     }
-    for (uint32_t i = tid; i < niso; i += SBLOCK) {
-        const uint32_t gtx = db.gene_tx[t0 + i];
-        const TxInfo ti = db.tx[gtx];
-        iso_gtx[i] = gtx;
-        iso_start[i] = ti.start;
-        iso_len[i] = ti.len;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t pre = 0;
-        for (uint32_t i = 0; i < niso; i++) {
-            iso_pre[i] = pre;
-            const int L = (int)iso_len[i];
-            pre += (L >= W16) ? 2u * (uint32_t)((L - W16) / stride + 1) : 0u;
+    // a gene's isoform tables: in LDS, or -- more than ISO_LDS isoforms (rare:
+    // real assemblies have genes with hundreds) -- read from HBM (transcript
+    // table and the host's word-item prefix); a block-uniform branch
+    const bool isog = niso > (uint32_t)ISO_LDS;
+    if (!isog) {
+        for (uint32_t i = tid; i < niso; i += SBLOCK) {
+            const uint32_t gtx = db.gene_tx[t0 + i];
+            const TxInfo ti = db.tx[gtx];
+            iso_gtx[i] = gtx;
+            iso_start[i] = ti.start;
+            iso_len[i] = ti.len;
         }
-        iso_pre[niso] = pre;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t pre = 0;
+            for (uint32_t i = 0; i < niso; i++) {
+                iso_pre[i] = pre;
+                const int L = (int)iso_len[i];
+                pre += (L >= W16) ? 2u * (uint32_t)((L - W16) / stride + 1) : 0u;
+            }
+            iso_pre[niso] = pre;
+        }
+        __syncthreads();
     }
-    __syncthreads();
-    const uint32_t n_items = iso_pre[niso];
+    const uint32_t *const gpre = P.iso_pre_g + t0 + g;
+    auto I_gtx = [&](uint32_t i) -> uint32_t { return isog ? db.gene_tx[t0 + i] : iso_gtx[i]; };
+    auto I_start = [&](uint32_t i) -> uint64_t { return isog ? db.tx[db.gene_tx[t0 + i]].start : iso_start[i]; };
+    auto I_len = [&](uint32_t i) -> int { return isog ? (int)db.tx[db.gene_tx[t0 + i]].len : (int)iso_len[i]; };
+    auto I_pre = [&](uint32_t i) -> uint32_t { return isog ? gpre[i] : iso_pre[i]; };
+    const uint32_t n_items = I_pre(niso);
 #ifdef RC_ROW_TIMING
     unsigned long long tph[6] = {0, 0, 0, 0, 0, 0};
     unsigned long long tc = __builtin_readcyclecounter();
@@ -255,7 +267,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
             // with a subject in this pass's samples
             for (uint32_t i = sh_rs0 + (uint32_t)tid; i < sh_rs1; i += SBLOCK) {
                 const LSeed sd = P.rs_rec[P.rs_idx[i]];
-                const int T = db.tx[(uint32_t)(sd.k1 >> 24)].sample;
+                const int T = db.tx[key_gtx(sd.k1)].sample;
                 if (T < T0 || T >= T1 || !((tm[T >> 6] >> (T & 63)) & 1)) continue;
                 const uint32_t slot = atomicAdd(&sh_nseed, 1u);
                 if (slot < cap) seeds[slot] = sd;
@@ -279,13 +291,23 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
             int p = 0, strand = 0;
             uint32_t ii = 0;
             if (it < n_items) {
-                while (ii + 1 < niso && iso_pre[ii + 1] <= it) ii++;
-                const uint32_t rem = it - iso_pre[ii];
-                const uint32_t ns = (iso_pre[ii + 1] - iso_pre[ii]) >> 1;
+                if (!isog) {
+                    while (ii + 1 < niso && iso_pre[ii + 1] <= it) ii++;
+                } else {
+                    uint32_t lo2 = 0, hi2 = niso;   // last isoform with pre <= it
+                    while (hi2 - lo2 > 1) {
+                        const uint32_t mid = (lo2 + hi2) >> 1;
+                        if (gpre[mid] <= it) lo2 = mid; else hi2 = mid;
+                    }
+                    ii = lo2;
+                }
+                const uint32_t pre0 = I_pre(ii);
+                const uint32_t rem = it - pre0;
+                const uint32_t ns = (I_pre(ii + 1) - pre0) >> 1;
                 strand = rem >= ns ? 1 : 0;
                 p = (int)(rem - (strand ? ns : 0)) * stride;
-                info = ii | ((uint32_t)strand << 7) | ((uint32_t)p << 8);
-                ok = word_usable<AMB>(db, iso_start[ii], (int)iso_len[ii], strand, p, total);
+                info = (uint32_t)p | ((uint32_t)strand << 24);
+                ok = word_usable<AMB>(db, I_start(ii), I_len(ii), strand, p, total);
             }
             // D(p): the previous usable word of the same isoform and strand is
             // item it - k (p - k s), in this batch's LDS or looked up again
@@ -295,7 +317,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
             if (ok) {
                 for (int k = 1; p - k * stride >= 0; k++) {
                     const bool u = tid - k >= 0 ? it_d[tid - k] != 0
-                                                : word_usable<AMB>(db, iso_start[ii], (int)iso_len[ii], strand,
+                                                : word_usable<AMB>(db, I_start(ii), I_len(ii), strand,
                                                                    p - k * stride, total);
                     if (u) {
                         D = (uint32_t)(k * stride);
@@ -306,7 +328,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
             __syncthreads();
             it_d[tid] = D;
             if (it < n_items) {
-                QGeo qg = {iso_start[ii], (int)iso_len[ii]};
+                QGeo qg = {I_start(ii), I_len(ii)};
                 const uint64_t qp = qfwd_pos(qg, strand, total, p);
                 const uint64_t *QA = strand ? db.RC : db.F;
                 if (ok) {
@@ -344,6 +366,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
             it_lo[tid] = lo;
             it_cnt[tid] = cnt;
             it_info[tid] = info;
+            it_iso[tid] = (uint16_t)ii;
             it_key[tid] = key;
             it_qlw[tid] = qlw;
             if (AMB) it_qlm[tid] = qlm;
@@ -400,7 +423,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     hsw[j] = hsm[j] = hbw[j] = 0;
                     bool decided = false;
                     if (lpre && live[j] && hk[j] > 0 && it_d[hk[j]] == (uint32_t)stride &&
-                        (int)(it_info[hk[j]] >> 8) >= stride) {
+                        (int)(it_info[hk[j]] & 0xFFFFFFu) >= stride) {
                         const uint32_t a = it_pre[hk[j] - 1], b = it_pre[hk[j]];
                         if (a >= hb0 && b <= hb0 + HCHUNK) {
                             const uint32_t tgt = pos - (uint32_t)stride;
@@ -421,7 +444,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     }
                     if (decided) {
                     } else if (live[j] && fast && it_d[hk[j]] == (uint32_t)stride &&
-                               (int)(it_info[hk[j]] >> 8) >= stride) {
+                               (int)(it_info[hk[j]] & 0xFFFFFFu) >= stride) {
                         hsw[j] = win_s(db.F, (int64_t)pos - 32) ^ it_qlw[hk[j]];
                         if (AMB) hsm[j] = win_s(db.AF, (int64_t)pos - 32) | it_qlm[hk[j]];
                         hbw[j] = win_bits(db.txstart, (int64_t)pos - 63);
@@ -450,10 +473,10 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     const uint32_t pos = wqp[q];
                     const int k = wqk[q];
                     const uint32_t inf = it_info[k];
-                    const int p = (int)(inf >> 8);
-                    const uint32_t ii = inf & 127;
-                    const int strand = (inf >> 7) & 1;
-                    QGeo qg = {iso_start[ii], (int)iso_len[ii]};
+                    const int p = (int)(inf & 0xFFFFFFu);
+                    const uint32_t ii = it_iso[k];
+                    const int strand = (int)(inf >> 24);
+                    QGeo qg = {I_start(ii), I_len(ii)};
                     const uint64_t *QA = strand ? db.RC : db.F;
                     const uint64_t *QAM = strand ? db.ARC : db.AF;
                     const uint64_t qp = qfwd_pos(qg, strand, total, p);
@@ -511,8 +534,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                             fwd = word_usable<AMB>(db, st.start, La, strand, u, total);
                         if (fwd) continue;
                         LSeed sd;
-                        sd.k1 = ((uint64_t)P.tx_pos[stx] << 57) | ((uint64_t)strand << 56) |
-                                ((uint64_t)iso_gtx[ii] << 24) | (uint64_t)(uint32_t)xa;
+                        sd.k1 = seed_key(P.tx_pos[stx], (uint32_t)strand, I_gtx(ii), (uint32_t)xa);
                         sd.y = (uint32_t)(strand ? qg.Lq - pb - len : pb);
                         sd.len = (uint32_t)len | SEED_R;
                         const unsigned long long k = atomicAdd(P.rseed_n, 1ull);
@@ -545,8 +567,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     const uint32_t slot = atomicAdd(&sh_nseed, 1u);
                     if (slot < cap) {
                         LSeed sd;
-                        sd.k1 = ((uint64_t)ii << 57) | ((uint64_t)strand << 56) | ((uint64_t)stx << 24) |
-                                (uint64_t)(uint32_t)(p - l);
+                        sd.k1 = seed_key(ii, (uint32_t)strand, stx, (uint32_t)(p - l));
                         sd.y = (uint32_t)(off - l);
                         sd.len = (uint32_t)len | dfl;
                         seeds[slot] = sd;
@@ -701,7 +722,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
         for (int T = tid; T < N; T += SBLOCK) tcnt[T] = 0;
         __syncthreads();
         for (uint32_t sg = tid; sg < nseg; sg += SBLOCK) {
-            const uint32_t gtx = (uint32_t)(seeds[seg_begin[sg]].k1 >> 24);
+            const uint32_t gtx = key_gtx(seeds[seg_begin[sg]].k1);
             const int T = db.tx[gtx].sample;
             seg_T[sg] = (uint8_t)T;
             atomicAdd(&tcnt[T], 1u);
@@ -725,7 +746,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
         if (room) {
             for (uint32_t i = tid; i < nseed; i += SBLOCK) {
                 GSeed gs;
-                gs.x = (uint32_t)(seeds[i].k1 & 0xFFFFFFull);
+                gs.x = key_x(seeds[i].k1);
                 gs.y = seeds[i].y;
                 gs.len = seeds[i].len;
                 P.seeds[sbase + i] = gs;
@@ -738,20 +759,20 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                 if (sg < nseg) {
                     const uint32_t b0 = seg_begin[sg], b1 = seg_begin[sg + 1];
                     const uint64_t k1 = seeds[b0].k1;
-                    const uint32_t gtx = (uint32_t)(k1 >> 24);
+                    const uint32_t gtx = key_gtx(k1);
                     const int T = seg_T[sg];
                     uint32_t rk = 0;   // rank among earlier candidates of the same sample
                     if (T1 - T0 == 1)
                         rk = sg;
                     else
                         for (uint32_t s2 = 0; s2 < sg; s2++) rk += seg_T[s2] == T;
-                    if (b1 - b0 > 0xFFFFu) atomicOr(P.status, 16u);   // seed_cnt is 16 bits
                     Cand c;
                     c.seed_off = (uint32_t)(sbase + b0);
-                    c.q_gtx = iso_gtx[(uint32_t)(k1 >> 57)];
+                    c.q_gtx = I_gtx(key_iso(k1));
                     c.s_gtx = gtx;
-                    c.seed_cnt = (uint16_t)(b1 - b0);
-                    c.strand = (uint8_t)((k1 >> 56) & 1);
+                    c.seed_lo = (uint16_t)(b1 - b0);
+                    c.seed_hi = (uint16_t)((b1 - b0) >> 16);
+                    c.strand = (uint8_t)key_strand(k1);
                     c.dflags = 1;
                     c.e0 = 0;
                     c.e1 = SEED_NONE;
@@ -766,7 +787,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                             const uint32_t sl = seeds[i].len;
                             if ((sl & SEED_F) && fF < 0) fF = (int)(i - b0);
                             if (sl & SEED_R) {
-                                const uint32_t sx = (uint32_t)(seeds[i].k1 & 0xFFFFFFull), sy = seeds[i].y, ln = sl & SEED_LEN;
+                                const uint32_t sx = key_x(seeds[i].k1), sy = seeds[i].y, ln = sl & SEED_LEN;
                                 const uint64_t key = c.strand ? ((uint64_t)~(sy + ln) << 32) | (uint32_t)~(sx + ln)
                                                               : ((uint64_t)sy << 32) | sx;
                                 if (key < bk) {
@@ -775,19 +796,23 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                                 }
                             }
                         }
+                        // e0 / e1 are 16-bit seed indices (SEED_NONE reserved)
+                        if (fF >= (int)SEED_NONE || fR >= (int)SEED_NONE) atomicOr(P.status, 16u);
                         c.dflags = (uint8_t)((fF >= 0 ? 1 : 0) | (fR >= 0 ? 2 : 0));
                         c.e0 = (uint16_t)(fF >= 0 ? fF : fR);
                         c.e1 = (fF >= 0 && fR >= 0 && fR != fF) ? (uint16_t)fR : SEED_NONE;
                         want = c.e1 != SEED_NONE ? 1u : 0u;
                     }
-                    const uint32_t qi = (uint32_t)(k1 >> 57);
-                    c.q0 = c.strand ? total - iso_start[qi] - (uint64_t)iso_len[qi] : iso_start[qi];
+                    const uint32_t qi = key_iso(k1);
+                    const uint64_t qstart = I_start(qi);
+                    const int qlen = I_len(qi);
+                    c.q0 = c.strand ? total - qstart - (uint64_t)qlen : qstart;
                     const TxInfo st = db.tx[gtx];
                     c.s0 = st.start;
-                    c.Lq = (int32_t)iso_len[qi];
+                    c.Lq = (int32_t)qlen;
                     c.Lt = (int32_t)st.len;
-                    c.qsam = (uint16_t)Q;
-                    c.ssam = (uint16_t)st.sample;
+                    c.qsam = (uint8_t)Q;
+                    c.ssam = (uint8_t)st.sample;
                     cslot = cbase + tpre[T] + rk;
                     P.cands[cslot] = c;
                 }
@@ -1154,7 +1179,7 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
         const TxInfo qt = txs[cd.q_gtx], st = txs[cd.s_gtx];
         const int Lq = (int)qt.len, Lt = (int)st.len;
         const int strand = cd.strand;
-        const int ns = cd.seed_cnt;
+        const int ns = (int)cand_seeds(cd);
         const GSeed *sd = P.seeds + cd.seed_off;
         ncands++;
         int bqa = 0, bqb = 0, bsa = 0, bsb = 0, bsc = 0, bd = 0, bg = 0, bo = 0, bni = 0, nh = 0;
@@ -1783,7 +1808,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 // right extension from the seed's end
                 const int x = meta[RM_X], y = meta[RM_Y], len = meta[RM_LEN];
                 const uint32_t sams = (uint32_t)meta[RM_REC + RC_SAMS];
-                swap = (sams & 0xFFFFu) > (sams >> 16);
+                swap = (sams & 0xFFu) > ((sams >> 8) & 0xFFu);
                 pa = qb + (uint32_t)(x + len);
                 alen = Lq - (x + len);
                 pb = tb + (uint32_t)(y + len);
@@ -1988,7 +2013,7 @@ __global__ __launch_bounds__(256) void first_finish_kernel(ExtParams P)
             const int lg = lgo & GMASK, lo2 = (lgo >> OBIT) & GMASK, rg = rgo & GMASK, ro = (rgo >> OBIT) & GMASK;
             const int bqa = x - lI, bqb = x + len + ri, bsa = y - lJ, bsb = y + len + rj;
             bool all_in = true;
-            for (uint32_t i = 0; i < cd.seed_cnt && all_in; i++) {
+            for (uint32_t i = 0, ns = cand_seeds(cd); i < ns && all_in; i++) {
                 if (i == e) continue;
                 const GSeed s = P.seeds[cd.seed_off + i];
                 if (dbit && !(s.len & dbit)) continue;
@@ -2135,8 +2160,11 @@ __global__ void mirror_scatter_kernel(GroupParams P, int pass)
     }
 }
 
-// sort each mirrored group by its order keys (groups are small) and fill the
-// group table
+// sort each mirrored group by its order keys and fill the group table:
+// groups of up to MSORT_SMALL entries (nearly all) by one thread's insertion
+// sort; larger ones -- an isoform-rich gene against an isoform-rich ortholog
+// holds tens of thousands -- go on a list for mirror_sort_big_kernel
+constexpr uint32_t MSORT_SMALL = 32;
 __global__ void mirror_sort_kernel(GroupParams P)
 {
     const uint64_t n = (uint64_t)P.n_genes * (uint64_t)P.N;
@@ -2147,6 +2175,11 @@ __global__ void mirror_sort_kernel(GroupParams P)
         const uint64_t b = P.mscan[gi];
         P.grp_off[gi] = (uint32_t)(P.mbase + b);
         P.grp_cnt[gi] = c;
+        if (c > MSORT_SMALL) {
+            const unsigned long long k = atomicAdd(P.mbig_n, 1ull);
+            P.mbig[k] = gi;   // capacity: nm / (MSORT_SMALL + 1) + 1 entries
+            continue;
+        }
         for (uint32_t i = 1; i < c; i++) {
             const uint64_t k1 = P.mkey[2 * (b + i)], k2 = P.mkey[2 * (b + i) + 1];
             const DHsp h = P.out[P.mbase + b + i];
@@ -2162,6 +2195,52 @@ __global__ void mirror_sort_kernel(GroupParams P)
             P.mkey[2 * (b + j)] = k1;
             P.mkey[2 * (b + j) + 1] = k2;
             P.out[P.mbase + b + j] = h;
+        }
+    }
+}
+
+// One workgroup per large mirrored group (persistent over the list): an
+// in-place bitonic network over the group's c entries, ascending in every
+// merge (the first stage of each merge compares mirrored positions), so the
+// virtual +inf padding past c never moves and its comparators are skipped.
+// Keys are unique per group: (isoform position, strand, subject tx, index).
+__global__ __launch_bounds__(256) void mirror_sort_big_kernel(GroupParams P)
+{
+    const uint64_t nb = *P.mbig_n;
+    for (uint64_t q = blockIdx.x; q < nb; q += gridDim.x) {
+        const uint64_t gi = P.mbig[q];
+        const uint32_t c = P.mcnt[gi];
+        const uint64_t b = P.mscan[gi];
+        uint64_t *K = P.mkey + 2 * b;
+        DHsp *H = P.out + P.mbase + b;
+        uint32_t np2 = 1;
+        while (np2 < c) np2 <<= 1;
+        auto cmpx = [&](uint32_t i, uint32_t j) {   // i < j: the smaller key to i
+            if (j >= c) return;
+            const uint64_t a1 = K[2 * i], a2 = K[2 * i + 1], b1 = K[2 * j], b2 = K[2 * j + 1];
+            if (a1 > b1 || (a1 == b1 && a2 > b2)) {
+                K[2 * i] = b1; K[2 * i + 1] = b2; K[2 * j] = a1; K[2 * j + 1] = a2;
+                const DHsp t = H[i];
+                H[i] = H[j];
+                H[j] = t;
+            }
+        };
+        for (uint32_t kk = 2; kk <= np2; kk <<= 1) {
+            // flip stage: i in the lower half of a kk-block against its mirror
+            for (uint32_t t = threadIdx.x; t < np2 / 2; t += blockDim.x) {
+                const uint32_t blk = t / (kk / 2), off = t % (kk / 2);
+                const uint32_t i = blk * kk + off, j = blk * kk + kk - 1 - off;
+                cmpx(i, j);
+            }
+            __syncthreads();
+            for (uint32_t j2 = kk / 4; j2 > 0; j2 >>= 1) {   // half-cleaners
+                for (uint32_t t = threadIdx.x; t < np2 / 2; t += blockDim.x) {
+                    const uint32_t blk = t / j2, off = t % j2;
+                    const uint32_t i = blk * 2 * j2 + off;
+                    cmpx(i, i + j2);
+                }
+                __syncthreads();
+            }
         }
     }
 }
@@ -2340,8 +2419,10 @@ void launch_group(const GroupParams &P, int pass, hipStream_t st)
         hipLaunchKernelGGL(group_write_kernel, dim3((unsigned)g), dim3(256), 0, st, P);
     else if (pass == 2 || pass == 3)
         hipLaunchKernelGGL(mirror_scatter_kernel, dim3((unsigned)g), dim3(256), 0, st, P, pass - 2);
-    else
+    else {
         hipLaunchKernelGGL(mirror_sort_kernel, dim3((unsigned)g), dim3(256), 0, st, P);
+        hipLaunchKernelGGL(mirror_sort_big_kernel, dim3(1024), dim3(256), 0, st, P);
+    }
 }
 
 }  // namespace rcg

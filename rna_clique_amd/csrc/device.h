@@ -10,7 +10,9 @@ constexpr int BAND = 64;        // greedy band: one diagonal per lane of a wave
 constexpr int BAND_LO = -32;    // diagonal of lane 0
 constexpr int MAX_HSP = 8;      // HSPs per (query tx, strand, subject tx)
 constexpr int DMAX = 4096;      // greedy differences cap
-constexpr int MAX_ISO = 127;    // transcripts per gene (7-bit field of the seed key)
+constexpr int MAX_ISO = 4095;   // transcripts per gene (12-bit field of the seed key)
+constexpr int ISO_LDS = 128;    // a gene's isoform tables the seed kernel keeps in LDS (more: read from HBM)
+constexpr uint64_t MAX_TX = 1ull << 27;   // transcripts per engine (27-bit field of the seed key)
 
 // Transcript record (16 B, one load).
 struct TxInfo {
@@ -111,27 +113,38 @@ constexpr uint16_t SEED_NONE = 0xFFFFu;
 struct Cand {
     uint32_t seed_off;     // absolute index of its first seed (sorted by (x, y))
     uint32_t q_gtx, s_gtx;
-    uint16_t seed_cnt;
+    uint16_t seed_lo;      // seed count, low 16 bits (cand_seeds())
     uint8_t strand;
     uint8_t dflags;        // shared searches: bit 0 the forward search has seeds, bit 1 the reverse one
     uint64_t q0;           // first base of the oriented query: in F (strand 0) or RC (strand 1)
     uint64_t s0;           // first base of the subject in F
     int32_t Lq, Lt;        // transcript lengths
-    uint16_t qsam, ssam;   // samples of query and subject
+    uint8_t qsam, ssam;    // samples of query and subject (< 256)
+    uint16_t seed_hi;      // seed count, high 16 bits
     // seeds (indices in the candidate) the row kernel extends first: e0 into
     // cand_box (the forward search's first seed, or the reverse one's when the
     // forward search has none), e1 into cand_box2 (the reverse search's first
     // seed when it is another seed; SEED_NONE otherwise)
     uint16_t e0, e1;
 };
+__host__ __device__ __forceinline__ uint32_t cand_seeds(const Cand &c) { return c.seed_lo | ((uint32_t)c.seed_hi << 16); }
 constexpr int CAND_DWORDS = (int)(sizeof(Cand) / 4);
 static_assert(sizeof(Cand) == 48, "Cand is read as 12 dwords");
 
-// A seed of the seed kernel before sorting: k1 = iso:7 | strand:1 | gtx:32 | x:24
+// A seed of the seed kernel before sorting: k1 = iso:12 | strand:1 | gtx:27 | x:24
+// (sorted by k1, then y; k1 >> 24 is the candidate: isoform, strand, subject tx)
 struct LSeed {
     uint64_t k1;
     uint32_t y, len;
 };
+__host__ __device__ __forceinline__ uint64_t seed_key(uint32_t iso, uint32_t strand, uint32_t gtx, uint32_t x)
+{
+    return ((uint64_t)iso << 52) | ((uint64_t)strand << 51) | ((uint64_t)gtx << 24) | (uint64_t)x;
+}
+__host__ __device__ __forceinline__ uint32_t key_iso(uint64_t k) { return (uint32_t)(k >> 52); }
+__host__ __device__ __forceinline__ uint32_t key_strand(uint64_t k) { return (uint32_t)(k >> 51) & 1u; }
+__host__ __device__ __forceinline__ uint32_t key_gtx(uint64_t k) { return (uint32_t)(k >> 24) & (uint32_t)(MAX_TX - 1); }
+__host__ __device__ __forceinline__ uint32_t key_x(uint64_t k) { return (uint32_t)k & 0xFFFFFFu; }
 
 // seed_kernel: per query gene, lookups -> canonical seeds -> candidates.
 struct SeedParams {
@@ -149,6 +162,9 @@ struct SeedParams {
     // rs_idx = the permutation, rs_n entries.
     int32_t rev;
     const uint32_t *tx_pos;       // isoform index of a transcript in its gene
+    // genes with more than ISO_LDS isoforms: the word-item prefix of each
+    // isoform, at gene_tx_off[g] + g + i (i = 0..niso; stride P.stride)
+    const uint32_t *iso_pre_g;
     LSeed *rseeds;
     uint32_t *rseed_gene;
     uint64_t rseed_cap;
@@ -167,7 +183,7 @@ struct SeedParams {
     unsigned long long *cand_count;  // [NSHARD]
     uint32_t *gc_off, *gc_cnt;    // [(g - gene_begin) * N + T] candidates of (gene, sample)
     const uint64_t *tmask;        // [n_samples][4] subject samples (> query sample) of this shard
-    unsigned int *status;         // bit 0 overflow, bit 1 gene limit, bit 3 big list full, bit 4 seed_cnt > 16 bits
+    unsigned int *status;         // bit 0 overflow, bit 1 gene limit, bit 3 big list full, bit 4 seed index > 16 bits
     unsigned long long *prof;     // RC_ROW_TIMING builds: block cycles per phase
     // (gene, sample) passes whose seeds overflow LDS: ((gene - gene_begin) << 8) | sample
     uint64_t *big_out;            // the LDS kernel appends here
@@ -269,6 +285,8 @@ struct GroupParams {
     uint32_t *mcur;               // scatter cursors [gene * N + T]
     uint64_t mbase;               // first output slot of the mirrored region
     uint64_t *mkey;               // order keys of the mirrored region (parallel to out)
+    uint64_t *mbig;               // mirrored groups too large for one thread's sort (mirror_sort_big_kernel)
+    unsigned long long *mbig_n;
     uint32_t n_genes;
 };
 

@@ -17,11 +17,20 @@
 #include <cstdlib>
 #include <cstring>
 #include <array>
+#include <condition_variable>
+#include <deque>
 #include <functional>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
+
+// od2_tables.cpp: one pair's gene matches table file
+int od2_write_table(const rc_row *rows, uint64_t n, const std::string &ssample, const std::string &qsample,
+                    const std::string &path);
 
 namespace rcg {
 void launch_pack(const uint8_t *, uint64_t, uint64_t, uint64_t *, uint64_t *, uint64_t *, uint64_t *, hipStream_t);
@@ -322,8 +331,8 @@ struct rc_engine {
     DBuf<DRow> d_rows_tmp;
     DBuf<DEdge> d_edges_tmp;
     DBuf<uint32_t> d_cand_ovf, d_gc_off, d_gc_cnt, d_gcount, d_defer, d_defer2;
-    DBuf<uint64_t> d_gscan, d_mscan, d_mkey, d_tmask;
-    DBuf<uint32_t> d_mcnt, d_mcur, d_tx_pos;
+    DBuf<uint64_t> d_gscan, d_mscan, d_mkey, d_tmask, d_mbig;
+    DBuf<uint32_t> d_mcnt, d_mcur, d_tx_pos, d_iso_pre;
     DBuf<unsigned long long> d_shard_cnt, d_shard_prefix;
     uint64_t seed_cap = 0, cand_cap = 0, ovf_cap = 0;   // per-shard / total capacities
     // (gene, sample) seed passes too big for LDS, and their global scratch
@@ -352,6 +361,7 @@ struct rc_engine {
 
     // host results
     std::vector<unsigned long long> h_num, h_den, h_num_all, h_den_all, h_stats;
+    std::vector<double> h_ss;   // search space of a query of length L against sample T: [T][L]
     rc_timing tm{};
     hipEvent_t ev[16] = {};
     hipEvent_t evd[3] = {};   // DUST start / end on st2, its start condition on st
@@ -634,6 +644,7 @@ static int upload(rc_engine *e)
     const int N = (int)e->samples.size();
     if (N < 2) return fail(RC_E_ARG, "need at least two samples");
     if (N > 256) return fail(RC_E_LIMIT, "more than 256 samples per engine");
+    if (e->tx_sample.size() >= MAX_TX) return fail(RC_E_LIMIT, "more than 2^27 transcripts per engine");
     const uint32_t n_tx = (uint32_t)e->tx_sample.size();
     // genes: per sample distinct gene ids ascending; a gene's transcripts in input order
     e->tx_gene.assign(n_tx, 0);
@@ -680,7 +691,8 @@ static int upload(rc_engine *e)
     const uint32_t n_genes = (uint32_t)e->gene_sample.size();
     for (uint32_t g = 0; g < n_genes; g++)
         if (e->gene_tx_off[g + 1] - e->gene_tx_off[g] > (uint32_t)MAX_ISO)
-            return fail(RC_E_LIMIT, "gene " + std::to_string(e->gene_id[g]) + " has more than 127 transcripts");
+            return fail(RC_E_LIMIT, "gene " + std::to_string(e->gene_id[g]) + " has more than " +
+                                        std::to_string(MAX_ISO) + " transcripts");
     // pairs (a < b) in the shard plan's order (plan::plan_pairs): every
     // shard a rectangle [a0, a1) x [b0, b1) of the pair triangle; items =
     // (pair, gene of b). (Outputs are per pair and do not depend on this.)
@@ -728,6 +740,25 @@ static int upload(rc_engine *e)
     for (uint32_t g = 0; g < n_genes; g++)
         for (uint32_t i = e->gene_tx_off[g]; i < e->gene_tx_off[g + 1]; i++) tx_pos[e->gene_tx[i]] = i - e->gene_tx_off[g];
     CHK(up(e->d_tx_pos, tx_pos));
+    {
+        // word-item prefix of every gene's isoforms (the seed kernel reads it
+        // for genes with more than ISO_LDS isoforms): gene g's entries at
+        // gene_tx_off[g] + g + i, i = 0..niso
+        const int stride = e->o.word_size - W16 + 1;
+        std::vector<uint32_t> ipre((size_t)n_tx + n_genes + 1, 0);
+        for (uint32_t g = 0; g < n_genes; g++) {
+            uint32_t pre = 0;
+            const uint32_t b = e->gene_tx_off[g], n = e->gene_tx_off[g + 1] - b;
+            for (uint32_t i = 0; i <= n; i++) {
+                ipre[(size_t)b + g + i] = pre;
+                if (i < n) {
+                    const int64_t L = (int64_t)e->h_tx[e->gene_tx[b + i]].len;
+                    pre += L >= W16 ? 2u * (uint32_t)((L - W16) / stride + 1) : 0u;
+                }
+            }
+        }
+        CHK(up(e->d_iso_pre, ipre));
+    }
     CHK(up(e->d_gene_tx_off, e->gene_tx_off));
     CHK(up(e->d_gene_tx, e->gene_tx));
     CHK(up(e->d_gene_sample, e->gene_sample));
@@ -739,10 +770,13 @@ static int upload(rc_engine *e)
     CHK(up(e->d_pair_index, e->pair_index));
     // statistics tables
     std::vector<int32_t> thr((size_t)N * (e->max_len + 1));
+    e->h_ss.assign((size_t)N * (e->max_len + 1), 0.0);
     for (int T = 0; T < N; T++)
-        for (int32_t L = 0; L <= e->max_len; L++)
-            thr[(size_t)T * (e->max_len + 1) + L] =
-                L ? stats::threshold(stats::search_space(L, e->db_len[T], e->db_n[T]), e->o.evalue) : (1 << 26);
+        for (int32_t L = 0; L <= e->max_len; L++) {
+            const size_t k = (size_t)T * (e->max_len + 1) + L;
+            e->h_ss[k] = stats::search_space(L, e->db_len[T], e->db_n[T]);
+            thr[k] = L ? stats::threshold(e->h_ss[k], e->o.evalue) : (1 << 26);
+        }
     std::vector<int32_t> b10((size_t)2 * e->max_len + 2);
     for (size_t sc = 0; sc < b10.size(); sc++) b10[sc] = stats::bits10((int32_t)sc);
     CHK(up(e->d_thr, thr));
@@ -1149,6 +1183,7 @@ static int reverse_pass(rc_engine *e, int ti, const Db &db, const Index &ixm, ui
             S.pre_mode = pm ? atoi(pm) : 1;
             S.rev = 1;
             S.tx_pos = e->d_tx_pos.p;
+            S.iso_pre_g = e->d_iso_pre.p;
             S.rseeds = e->d_rseeds.p;
             S.rseed_gene = e->d_rseed_gene.p;
             S.rseed_cap = e->rseed_cap;
@@ -1167,7 +1202,7 @@ static int reverse_pass(rc_engine *e, int ti, const Db &db, const Index &ixm, ui
         HIPCHK(hipMemcpyAsync(&cnt, e->d_rctr.p + 1, sizeof cnt, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipStreamSynchronize(e->st));
-        if (status & 2u) return fail(RC_E_LIMIT, "a query gene has more than 127 isoforms");
+        if (status & 2u) return fail(RC_E_LIMIT, "a query gene has more than " + std::to_string(MAX_ISO) + " isoforms");
         if (cnt <= e->rseed_cap) break;
         e->rseed_cap = cnt + cnt / 4 + 1024;
     }
@@ -1398,6 +1433,7 @@ static int align_tile(rc_engine *e, int ti)
             S.sym = e->o.symmetric;
             S.share = e->share ? 1 : 0;
             S.tx_pos = e->d_tx_pos.p;
+            S.iso_pre_g = e->d_iso_pre.p;
             S.rs_rec = e->d_rseeds.p;
             S.rs_key = e->d_rs_key.p;
             S.rs_idx = e->d_rs_idx.p;
@@ -1428,7 +1464,9 @@ static int align_tile(rc_engine *e, int ti)
             HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
             HIPCHK(hipMemcpyAsync(&nb, big_n, sizeof nb, hipMemcpyDeviceToHost, e->st));
             HIPCHK(hipStreamSynchronize(e->st));
-            if (status & 2u) return fail(RC_E_LIMIT, "a query gene has more than 127 isoforms");
+            if (status & 2u) return fail(RC_E_LIMIT, "a query gene has more than " + std::to_string(MAX_ISO) + " isoforms");
+            if (status & 16u)
+                return fail(RC_E_LIMIT, "a candidate's first seed of a directed search is past seed 65534");
             if (status & 8u) {   // the big-pass list itself overflowed
                 e->big_list_cap = std::max<uint64_t>(4 * e->big_list_cap, nb + 1024);
                 again = true;
@@ -1469,7 +1507,8 @@ static int align_tile(rc_engine *e, int ti)
                 HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
                 HIPCHK(hipMemcpyAsync(&nr, big_retry_n, sizeof nr, hipMemcpyDeviceToHost, e->st));
                 HIPCHK(hipStreamSynchronize(e->st));
-                if (status & 16u) return fail(RC_E_LIMIT, "a candidate has more than 65535 seeds");
+                if (status & 16u)
+                    return fail(RC_E_LIMIT, "a candidate's first seed of a directed search is past seed 65534");
                 again = (status & 1u) != 0;
                 nb = nr;
                 // the retry entries become the next list (buffers swapped, not copied)
@@ -1687,10 +1726,14 @@ static int align_tile(rc_engine *e, int ti)
     }
     if (mirror) {
         CHK(e->d_mkey.ensure(2 * nm + 2));
+        CHK(e->d_mbig.ensure(nm / 33 + 2));
+        HIPCHK(hipMemsetAsync(e->d_count.p + 19, 0, sizeof(unsigned long long), e->st));
         G.mscan = e->d_mscan.p;
         G.out = e->d_hsp.p;
         G.mbase = base;
         G.mkey = e->d_mkey.p;
+        G.mbig = e->d_mbig.p;
+        G.mbig_n = e->d_count.p + 19;
         launch_group(G, 3, e->st);
         launch_group(G, 4, e->st);
     }
@@ -1897,7 +1940,7 @@ static int do_finish(rc_engine *e)
 // results
 // ------------------------------------------------------------------------
 
-static rc_hsp to_rc_hsp(rc_engine *e, const DHsp &d, int qs_, int ss_)
+static rc_hsp to_rc_hsp(const rc_engine *e, const DHsp &d, int qs_, int ss_)
 {
     rc_hsp h;
     h.q_tx = d.q_tx - e->samples[qs_].tx_begin;
@@ -1906,7 +1949,9 @@ static rc_hsp to_rc_hsp(rc_engine *e, const DHsp &d, int qs_, int ss_)
     h.length = d.length; h.nident = d.nident; h.mismatch = d.mismatch; h.gaps = d.gaps;
     h.gapopen = d.gapopen; h.score_half = d.score_half; h.bits10 = d.bits10; h.strand = d.strand & 1;
     const int64_t qlen = (int64_t)(e->tx_start[d.q_tx + 1] - e->tx_start[d.q_tx]);
-    h.evalue = stats::evalue(stats::search_space(qlen, e->db_len[ss_], e->db_n[ss_]), d.score_half);
+    const double ss = qlen <= e->max_len ? e->h_ss[(size_t)ss_ * (e->max_len + 1) + (size_t)qlen]
+                                         : stats::search_space(qlen, e->db_len[ss_], e->db_n[ss_]);
+    h.evalue = stats::evalue(ss, d.score_half);
     return h;
 }
 
@@ -1985,9 +2030,16 @@ int rc_hsps(rc_engine *e, int32_t q, int32_t s, rc_hsp *buf, uint64_t cap, uint6
     return RC_OK;
 }
 
-int rc_pair_rows(rc_engine *e, int32_t s1, int32_t s2, rc_row *buf, uint64_t cap, uint64_t *n)
+// A pair's rows on the host: its table rows (DRow) and their HSPs, fetched
+// from the device (the engine's stream; one caller at a time).
+struct PairRaw {
+    int32_t s1 = 0, s2 = 0;
+    std::vector<DRow> rows;
+    std::vector<DHsp> hs;
+};
+
+static int pair_row_range(rc_engine *e, int32_t s1, int32_t s2, uint64_t &r0, uint64_t &r1)
 {
-    if (!e || !n) return fail(RC_E_ARG, "null argument");
     if (!e->rbh_done || e->graph_only) return fail(RC_E_STATE, "no gene matches tables on this engine");
     const int N = (int)e->samples.size();
     if (s1 < 0 || s1 >= N || s2 < 0 || s2 >= N || s1 >= s2) return fail(RC_E_ARG, "need s1 < s2 (input order)");
@@ -1995,22 +2047,38 @@ int rc_pair_rows(rc_engine *e, int32_t s1, int32_t s2, rc_row *buf, uint64_t cap
     const uint64_t p = (uint64_t)e->pair_index[s1 * N + s2];
     if (p < e->pair0 || p >= e->pair1) return fail(RC_E_ARG, "pair belongs to another shard");
     const uint64_t ib = e->pair_item_begin[p] - e->item0, ie = e->pair_item_begin[p + 1] - e->item0;
-    uint64_t r0 = 0, r1 = 0;
     HIPCHK(hipMemcpy(&r0, e->d_off4.p + ib, 8, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(&r1, e->d_off4.p + ie, 8, hipMemcpyDeviceToHost));
+    return RC_OK;
+}
+
+static int fetch_pair(rc_engine *e, int32_t s1, int32_t s2, PairRaw &out)
+{
+    uint64_t r0 = 0, r1 = 0;
+    CHK(pair_row_range(e, s1, s2, r0, r1));
     const uint64_t nr = r1 - r0;
-    *n = nr;
-    if (!buf) return RC_OK;
-    if (cap < nr) return fail(RC_E_CAPACITY, "buffer too small");
+    out.s1 = s1;
+    out.s2 = s2;
+    out.rows.resize(nr);
+    out.hs.resize(nr);
     if (!nr) return RC_OK;
-    std::vector<DRow> rows(nr);
-    std::vector<DHsp> hs(nr);
     CHK(e->d_gather.ensure(nr));
     launch_gather_rows(e->d_hsp.p, e->d_rows.p + r0, nr, e->d_gather.p, e->st);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(rows.data(), e->d_rows.p + r0, nr * sizeof(DRow), hipMemcpyDeviceToHost, e->st));
-    HIPCHK(hipMemcpyAsync(hs.data(), e->d_gather.p, nr * sizeof(DHsp), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipMemcpyAsync(out.rows.data(), e->d_rows.p + r0, nr * sizeof(DRow), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipMemcpyAsync(out.hs.data(), e->d_gather.p, nr * sizeof(DHsp), hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
+    return RC_OK;
+}
+
+// rc_row records of fetched rows (host only: thread-safe, the engine's host
+// tables are read only)
+static void convert_rows(const rc_engine *e, const PairRaw &raw, rc_row *buf)
+{
+    const int32_t s1 = raw.s1, s2 = raw.s2;
+    const uint64_t nr = raw.rows.size();
+    const std::vector<DRow> &rows = raw.rows;
+    const std::vector<DHsp> &hs = raw.hs;
     for (uint64_t i = 0; i < nr; i++) {
         const DHsp &d = hs[i];
         rc_row &r = buf[i];
@@ -2029,6 +2097,20 @@ int rc_pair_rows(rc_engine *e, int32_t s1, int32_t s2, rc_row *buf, uint64_t cap
         r.reverse = rev ? 1 : 0;
         r.label = rows[i].label;
     }
+}
+
+int rc_pair_rows(rc_engine *e, int32_t s1, int32_t s2, rc_row *buf, uint64_t cap, uint64_t *n)
+{
+    if (!e || !n) return fail(RC_E_ARG, "null argument");
+    uint64_t r0 = 0, r1 = 0;
+    CHK(pair_row_range(e, s1, s2, r0, r1));
+    *n = r1 - r0;
+    if (!buf) return RC_OK;
+    if (cap < r1 - r0) return fail(RC_E_CAPACITY, "buffer too small");
+    if (r1 == r0) return RC_OK;
+    PairRaw raw;
+    CHK(fetch_pair(e, s1, s2, raw));
+    convert_rows(e, raw, buf);
     return RC_OK;
 }
 
@@ -2294,6 +2376,138 @@ int rc_shard_pairs(rc_engine *e, int64_t *first, int64_t *last)
     CHK(upload(e));
     *first = (int64_t)e->pair0;
     *last = (int64_t)e->pair1;
+    return RC_OK;
+}
+
+// The outputs a run writes next to matrix.h5: the od2 gene matches tables of
+// the given pairs (paths[i] for pair (s1[i], s2[i]), table_paths may be NULL)
+// and graph.pkl (graph_path, may be NULL; build_graph's graph over the pairs
+// in the given order -- every pair of a single-shard engine, in combinations
+// order). Each pair's rows leave the device once; the calling thread fetches
+// them in order, `threads` workers convert and write the tables (od2_tables.
+// cpp), one more thread builds and writes the pickle (graph_pickle.cpp) --
+// all outside the Python interpreter.
+int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int32_t *s2,
+                     const char *const *table_paths, const char *graph_path, int32_t threads)
+{
+    if (!e || n_pairs < 0 || (n_pairs && (!s1 || !s2))) return fail(RC_E_ARG, "null argument");
+    if (!table_paths && !graph_path) return RC_OK;
+    if (graph_path && e->o.shard_count != 1)
+        return fail(RC_E_STATE, "a sharded engine holds only its own pairs' rows: graph.pkl comes from the edges");
+    const int nt = std::max(1, std::min(64, (int)threads));
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::pair<int, std::shared_ptr<PairRaw>>> tq, gq;
+    bool closed = false;
+    int in_flight = 0, err = RC_OK;
+    std::string err_msg;
+    auto set_err = [&](int code) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (err == RC_OK) {
+            err = code;
+            err_msg = rc_last_error();
+        }
+    };
+    auto worker = [&]() {
+        std::vector<rc_row> buf;
+        for (;;) {
+            std::pair<int, std::shared_ptr<PairRaw>> job;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return !tq.empty() || closed; });
+                if (tq.empty()) return;
+                job = std::move(tq.front());
+                tq.pop_front();
+            }
+            const PairRaw &raw = *job.second;
+            buf.resize(raw.rows.size());
+            convert_rows(e, raw, buf.data());
+            const int rc = od2_write_table(buf.data(), buf.size(), e->samples[raw.s1].label, e->samples[raw.s2].label,
+                                           table_paths[job.first]);
+            if (rc != RC_OK) set_err(rc);
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                in_flight--;
+            }
+            cv.notify_all();
+        }
+    };
+    auto grapher = [&]() {
+        rc_gpickle *g = nullptr;
+        if (rc_graph_pickle_begin(&g) != RC_OK) {
+            set_err(RC_E_NOMEM);
+            return;
+        }
+        std::vector<int64_t> sg, qg;
+        bool ok = true;
+        for (;;) {
+            std::pair<int, std::shared_ptr<PairRaw>> job;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return !gq.empty() || closed; });
+                if (gq.empty()) break;
+                job = std::move(gq.front());
+                gq.pop_front();
+            }
+            const PairRaw &raw = *job.second;
+            const size_t n = raw.rows.size();
+            sg.resize(n);
+            qg.resize(n);
+            for (size_t i = 0; i < n; i++) {
+                const DHsp &d = raw.hs[i];
+                const bool rev = raw.rows[i].reverse != 0;
+                qg[i] = e->tx_gene_id[rev ? d.s_tx : d.q_tx];   // qgene: the transcript of s2
+                sg[i] = e->tx_gene_id[rev ? d.q_tx : d.s_tx];
+            }
+            if (ok && rc_graph_pickle_add(g, raw.s1, raw.s2, sg.data(), qg.data(), n) != RC_OK) {
+                set_err(RC_E_LIMIT);
+                ok = false;
+            }
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                in_flight--;
+            }
+            cv.notify_all();
+        }
+        if (ok) {
+            std::vector<const char *> names;
+            for (const SampleRec &s : e->samples) names.push_back(s.label.c_str());
+            if (rc_graph_pickle_write(g, graph_path, (int32_t)names.size(), names.data()) != RC_OK) set_err(RC_E_IO);
+        }
+        rc_graph_pickle_free(g);
+    };
+    std::vector<std::thread> pool;
+    if (table_paths)
+        for (int i = 0; i < nt; i++) pool.emplace_back(worker);
+    if (graph_path) pool.emplace_back(grapher);
+    const int per_job = (table_paths ? 1 : 0) + (graph_path ? 1 : 0);
+    const int max_flight = 4 * nt + 4;
+    int rc = RC_OK;
+    for (int i = 0; i < n_pairs && rc == RC_OK; i++) {
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return in_flight < max_flight * per_job || err != RC_OK; });
+            if (err != RC_OK) break;
+        }
+        auto raw = std::make_shared<PairRaw>();
+        rc = fetch_pair(e, s1[i], s2[i], *raw);
+        if (rc != RC_OK) break;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            if (table_paths) tq.push_back({i, raw});
+            if (graph_path) gq.push_back({i, raw});
+            in_flight += per_job;
+        }
+        cv.notify_all();
+    }
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        closed = true;
+    }
+    cv.notify_all();
+    for (std::thread &t : pool) t.join();
+    if (rc != RC_OK) return rc;
+    if (err != RC_OK) return fail(err, err_msg);
     return RC_OK;
 }
 

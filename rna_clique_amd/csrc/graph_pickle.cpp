@@ -204,11 +204,25 @@ int rc_graph_pickle_write(rc_gpickle *g, const char *path, int32_t n_names, cons
     const std::string tmp = std::string(path) + ".tmp";
     FILE *f = fopen(tmp.c_str(), "wb");
     if (!f) return rcg_fail(RC_E_IO, "cannot open " + tmp);
-    std::vector<char> buf(1 << 22);
-    setvbuf(f, buf.data(), _IOFBF, buf.size());
+    // the stream is built in a 16 MiB block and written a block at a time
+    // (per-opcode stdio calls, each taking the FILE lock, ran at ~38 MB/s)
+    std::vector<uint8_t> blk;
+    blk.reserve(1 << 24);
+    bool werr = false;
+    auto flush = [&]() {
+        if (!blk.empty() && fwrite(blk.data(), 1, blk.size(), f) != blk.size()) werr = true;
+        blk.clear();
+    };
     uint32_t memo = 0;
-    auto put = [&](const void *p, size_t n) { fwrite(p, 1, n, f); };
-    auto op = [&](uint8_t c) { fputc(c, f); };
+    auto put = [&](const void *p, size_t n) {
+        const uint8_t *b = static_cast<const uint8_t *>(p);
+        blk.insert(blk.end(), b, b + n);
+        if (blk.size() >= (1u << 24) - 64) flush();
+    };
+    auto op = [&](uint8_t c) {
+        blk.push_back(c);
+        if (blk.size() >= (1u << 24) - 64) flush();
+    };
     auto u32 = [&](uint32_t v) { put(&v, 4); };
     auto memoize = [&]() { op(0x94); return memo++; };
     auto get = [&](uint32_t m) { op('j'); u32(m); };   // LONG_BINGET
@@ -318,7 +332,8 @@ int rc_graph_pickle_write(rc_gpickle *g, const char *path, int32_t n_names, cons
     op('u');    // SETITEMS of the state dict
     op('b');    // BUILD
     op('.');    // STOP
-    const bool bad = ferror(f) != 0;
+    flush();
+    const bool bad = werr || ferror(f) != 0;
     if (fclose(f) != 0 || bad) {
         remove(tmp.c_str());
         return rcg_fail(RC_E_IO, "write failed: " + tmp);

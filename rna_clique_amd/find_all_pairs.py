@@ -78,8 +78,11 @@ def find_all_pairs(inputs: Iterable[Path], output_dir: Path, cache_dir: Optional
     return tables(), paths, math.comb(len(inputs), 2)
 
 
-def write_pair_tables(eng, inputs, output_dir, path_to_sample, ext, jobs: int = 8) -> dict:
-    """Write the tables of the pairs this engine owns; {(a, b): path}."""
+def write_pair_tables(eng, inputs, output_dir, path_to_sample, ext, jobs: int = 8, graph_path=None) -> dict:
+    """Write the tables of the pairs this engine owns; {(a, b): path}. .h5
+    tables (and graph.pkl when `graph_path` is given: build_graph over every
+    pair, a single-shard engine) are written natively in one pass
+    (tables.write_engine_outputs); .pkl tables through pandas."""
     output_dir = Path(output_dir)
     output_dir.mkdir(parents=True, exist_ok=True)
     own = set(eng.owned_pairs())
@@ -87,6 +90,12 @@ def write_pair_tables(eng, inputs, output_dir, path_to_sample, ext, jobs: int = 
     for a, b in itertools.combinations(range(len(inputs)), 2):
         if (a, b) in own:
             out[(a, b)] = make_output_path(output_dir, inputs[a], inputs[b], path_to_sample, ext)
+    if ext == "h5":
+        from .tables import write_engine_outputs
+        write_engine_outputs(eng, list(out), [out[p] for p in out], graph_path, max(1, jobs))
+        return out
+    if graph_path is not None:
+        raise ValueError("graph_path is written with .h5 tables only")
     labels = eng.labels
     lock = threading.Lock()
 

@@ -101,13 +101,19 @@ def rna_clique(
     sim = SampleSimilarity.from_engine(eng, store_dfs=store_dfs)
     from . import distributed
     writer = distributed.world(process_group)[1] == 0
+    graph_done = False
     if out_dir_2 is not None and table_format != "none":
-        # every rank writes the tables of the pairs it owns (all of them on one GPU)
+        # every rank writes the tables of the pairs it owns (all of them on one
+        # GPU); on one GPU, graph.pkl is written in the same native pass
         from .find_all_pairs import table_extension, write_pair_tables
-        write_pair_tables(eng, [s.path for s in samples], out_dir_2, pts.__getitem__,
-                          table_format or table_extension(), max(1, jobs))
+        ext = table_format or table_extension()
+        gpath = output_graph if (writer and output_graph is not None and ext == "h5"
+                                 and eng.shard_count == 1) else None
+        write_pair_tables(eng, [s.path for s in samples], out_dir_2, pts.__getitem__, ext, max(1, jobs),
+                          graph_path=gpath)
+        graph_done = gpath is not None
     t3 = time.perf_counter()
-    if writer and output_graph is not None:
+    if writer and output_graph is not None and not graph_done:
         sim.write_graph(output_graph)
     t4 = time.perf_counter()
     if writer and output_matrix is not None:

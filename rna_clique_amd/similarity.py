@@ -198,13 +198,8 @@ class SampleSimilarity:
         streams the pairs' rows (tables.write_graph_pickle: the same Graph on
         pickle.load, without per-edge Python inserts)."""
         if self._graph is None and getattr(self.engine, "shard_count", 1) == 1:
-            from .tables import write_graph_pickle
-
-            def tables():
-                for a, b in self._pairs():
-                    r = self.engine.pair_rows(a, b)
-                    yield a, b, r["sgene"], r["qgene"]
-            write_graph_pickle(path, tables(), self.labels)
+            from .tables import write_engine_outputs
+            write_engine_outputs(self.engine, list(self._pairs()), None, path)
             return
         if self._graph is None:
             # a sharded run holds every edge but only its own pairs' rows: the

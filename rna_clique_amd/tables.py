@@ -170,6 +170,31 @@ def build_graph(tables):
     return g
 
 
+def write_engine_outputs(engine, pairs, table_paths=None, graph_path=None, threads=8):
+    """The od2 table files (`table_paths[i]` for `pairs[i]` = (a, b), a < b)
+    and/or graph.pkl of an engine run, natively (rc_write_outputs): each
+    pair's rows leave the GPU once; table files are written by `threads` host
+    threads in pandas' table format -- the bytes h5.write_frame_table writes
+    for pair_table(engine, a, b), tests/test_od2_native.py -- and the graph
+    pickle (build_graph over `pairs` in order, then pickle.dump) beside them,
+    all outside the interpreter (the GIL is released for the whole call)."""
+    import ctypes
+    from . import _native
+    n = len(pairs)
+    a = np.ascontiguousarray([p[0] for p in pairs], dtype=np.int32)
+    b = np.ascontiguousarray([p[1] for p in pairs], dtype=np.int32)
+    tp = None
+    if table_paths is not None:
+        enc = [str(x).encode() for x in table_paths]
+        if len(enc) != n:
+            raise ValueError("one table path per pair")
+        tp = (ctypes.c_char_p * max(n, 1))(*enc)
+    _native.check(_native.lib().rc_write_outputs(
+        engine._h, n, a.ctypes.data_as(ctypes.c_void_p), b.ctypes.data_as(ctypes.c_void_p),
+        ctypes.cast(tp, ctypes.c_void_p) if tp is not None else None,
+        str(graph_path).encode() if graph_path is not None else None, int(threads)))
+
+
 def write_graph_pickle(path, tables, names):
     """graph.pkl of the graph build_graph would make from `tables` -- an
     iterable of (ssample index, qsample index, sgene array, qgene array), in

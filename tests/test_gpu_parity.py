@@ -128,6 +128,25 @@ def test_isoform_rich_genes_and_repeats(native):
         eng.close()
 
 
+def test_gene_with_201_isoforms(native):
+    """A gene with 201 transcripts in both samples (more than the seed
+    kernel's LDS isoform tables, ISO_LDS = 128, and than round 2's limit of
+    127): the seed kernel reads that gene's isoform tables from HBM, its
+    (gene, sample) passes run from global memory, and every HSP, table row,
+    edge and distance is bit-exact vs the oracle. The reference keeps every
+    isoform of a top gene (select_top_genes.py:121-127) and groups by qgene
+    with no bound (find_homologs.py:130)."""
+    import numpy as np
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(2, 30, seed=31, len_loc=1200, len_n=400, len_p=0.5, rich_genes=1, rich_iso=201)
+    assert all(np.bincount(s.gene).max() == 201 for s in samples)
+    eng = _run_sim(samples)
+    msgs, summary = full_check(eng, samples)
+    assert not msgs, "\n".join(msgs[:10])
+    assert summary["hsps"] > 100000 and eng.timings()["big_passes"] > 0
+    eng.close()
+
+
 def test_simulated_parity_variants(native):
     """Minus-strand transcripts, recent paralogs (reciprocal-best-hit ties,
     non-ideal components), isoforms and indels together."""

@@ -46,6 +46,31 @@ def _records(arr, rs):
     return np.ascontiguousarray(arr).view(np.uint8).reshape(-1, rs)
 
 
+class _heartbeat:
+    """Prints a line every 30 s while a long step runs (GPU runs are killed
+    after 3 minutes without output; pytest -s shows these)."""
+
+    def __init__(self, what):
+        import threading
+        self.what, self.stop = what, threading.Event()
+        self.t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        import time
+        t0 = time.time()
+        while not self.stop.wait(30):
+            print(f"  ... {self.what}: {time.time() - t0:.0f} s", flush=True)
+
+    def __enter__(self):
+        print(f"  {self.what}", flush=True)
+        self.t.start()
+        return self
+
+    def __exit__(self, *a):
+        self.stop.set()
+        self.t.join()
+
+
 def _record(name, obj):
     os.makedirs("gpurun_out", exist_ok=True)
     with open(os.path.join("gpurun_out", f"{name}.json"), "w") as f:
@@ -56,7 +81,8 @@ def test_C4_eight_shards_match_unsharded(native):
     from rna_clique_amd import distributed
     from rna_clique_amd.engine import Engine
     from rna_clique_amd.simulate import CONFIGS, simulate
-    samples, _ = simulate(**CONFIGS["C4"])
+    with _heartbeat("C4: simulate"):
+        samples, _ = simulate(**CONFIGS["C4"])
     N, S = len(samples), 8
     bases = [int(s.tx_offsets[-1]) for s in samples]
     ref = Engine(device=0)
@@ -75,6 +101,7 @@ def test_C4_eight_shards_match_unsharded(native):
     ref.close()
     parts, resident = [], []
     for r in range(S):
+        print(f"  C4 shard {r}", flush=True)
         need = distributed.needed_samples(bases, S, r)
         resident.append(len(need))
         e = Engine(device=0, shard_rank=r, shard_count=S)
@@ -112,7 +139,8 @@ def test_C5_one_rank_shard(native):
     from rna_clique_amd.engine import Engine
     S = 8
     # the rank with the largest modelled footprint (rank 2 at C5)
-    samples, need, (order, first) = shard_samples("C5", S, 2)
+    with _heartbeat("C5: generate rank 2's samples"):
+        samples, need, (order, first) = shard_samples("C5", S, 2)
     bases = [int(s.tx_offsets[-1]) for s in samples]
     genes = [len(np.unique(s.gene)) for s in samples]
     model = distributed.hbm_footprint(bases, genes, S)
@@ -123,9 +151,11 @@ def test_C5_one_rank_shard(native):
     eng = Engine(device=0, shard_rank=R, shard_count=S)
     for i, s in enumerate(samples):
         eng.add_sample(s.name, s.seq if i in need else None, s.tx_offsets, s.gene, s.iso)
-    eng.align()
-    eng.finish()
+    with _heartbeat("C5: align + finish"):
+        eng.align()
+        eng.finish()
     tm = eng.timings()
+    print(f"  C5 rank 2: {tm['tiles']:.0f} tiles, {tm['total_ms']:.0f} ms", flush=True)
     assert tm["tiles"] > 1
     free1, _ = torch.cuda.mem_get_info(0)
     own = eng.owned_pairs()
@@ -151,6 +181,7 @@ def test_C5_one_rank_shard(native):
     assert (free0 - free1) < 1.25 * model[R]
     # two owned pairs against the oracle (both directed searches, table, sums)
     picks = [own[0], own[len(own) // 2]]
-    msgs = check_pairs(eng, samples, picks)
+    with _heartbeat(f"C5: oracle on pairs {picks}"):
+        msgs = check_pairs(eng, samples, picks)
     assert not msgs, "\n".join(msgs[:10])
     eng.close()

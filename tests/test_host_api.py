@@ -333,16 +333,19 @@ def test_downcast_int_matches_pandas():
 
 def test_pytables_branch_is_serialised(tmp_path, monkeypatch):
     """When PyTables is importable, write_table goes through df.to_hdf, which
-    is not thread-safe (PyTables releases the GIL around HDF5): the table
-    thread pool of write_pair_tables must never be inside it twice at once."""
+    is not thread-safe (PyTables releases the GIL around HDF5): callers on
+    several threads must never be inside it twice at once. (The engine's own
+    od2 tables are written natively, rc_write_outputs; write_table is the
+    reference's entry point for any DataFrame.)"""
     import sys
     import threading
     import time
     import types
+    from concurrent.futures import ThreadPoolExecutor
     import numpy as np
     import pandas as pd
     from rna_clique_amd import _native
-    from rna_clique_amd.find_all_pairs import write_pair_tables
+    from rna_clique_amd.tables import rows_to_table, write_table
     monkeypatch.setitem(sys.modules, "tables", types.ModuleType("tables"))
     state = {"in": 0, "max": 0, "calls": 0}
     guard = threading.Lock()
@@ -357,19 +360,11 @@ def test_pytables_branch_is_serialised(tmp_path, monkeypatch):
         with guard:
             state["in"] -= 1
     monkeypatch.setattr(pd.DataFrame, "to_hdf", fake_to_hdf)
-
-    class FakeEngine:
-        labels = ["od1/A_top.fasta", "od1/B_top.fasta", "od1/C_top.fasta", "od1/D_top.fasta"]
-
-        def owned_pairs(self):
-            return [(a, b) for b in range(4) for a in range(b)]
-
-        def pair_rows(self, a, b):
-            r = np.zeros(3, dtype=_native.ROW_DTYPE)
-            r["qgene"], r["sgene"], r["label"] = [1, 2, 3], [4, 5, 6], [0, 1, 2]
-            r["hsp"]["length"], r["hsp"]["nident"], r["hsp"]["bits10"] = 100, 99, 1800
-            return r
-    out = write_pair_tables(FakeEngine(), [f"od1/{c}_top.fasta" for c in "ABCD"], tmp_path,
-                            lambda p: p.split("/")[1][0], "h5", jobs=6)
-    assert len(out) == 6 and state["calls"] == 6
+    r = np.zeros(3, dtype=_native.ROW_DTYPE)
+    r["qgene"], r["sgene"], r["label"] = [1, 2, 3], [4, 5, 6], [0, 1, 2]
+    r["hsp"]["length"], r["hsp"]["nident"], r["hsp"]["bits10"] = 100, 99, 1800
+    df = rows_to_table(r, "od1/A_top.fasta", "od1/B_top.fasta")
+    with ThreadPoolExecutor(6) as ex:
+        list(ex.map(lambda i: write_table(df, tmp_path / f"t{i}.h5"), range(6)))
+    assert state["calls"] == 6
     assert state["max"] == 1
