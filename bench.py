@@ -64,8 +64,10 @@ def launch_ranks(args):
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
     env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4"))
     proc = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    # rank 0's JSON line on stdout; anything else the ranks printed there
+    # (gloo / RCCL banners) goes to stderr
     for line in proc.stdout.splitlines():
-        print(line, flush=True)
+        print(line, file=sys.stdout if line.startswith("{") else sys.stderr, flush=True)
     return proc.returncode
 
 
@@ -250,6 +252,10 @@ def shard_emulation(args):
     edges. Prints one shard_emulation JSON line: the rank's pairs/s, tiles,
     measured HBM use vs distributed.hbm_footprint's model."""
     R, S = (int(x) for x in args.shard.split("/"))
+    # torch's HIP runtime first, then librcgpu.so (the shard plan below loads
+    # it): the other order leaves the engine's runtime without a device
+    import torch
+    torch.cuda.init()
     from rna_clique_amd import distributed
     t_gen = time.perf_counter()
     samples, need, (order, first) = shard_samples(args.config, S, R)
@@ -258,7 +264,6 @@ def shard_emulation(args):
     genes = [len(set(s.gene.tolist())) for s in samples]
     model = distributed.hbm_footprint(bases, genes, S)
     my_pairs = int(first[R + 1] - first[R])
-    import torch
     free0, total = torch.cuda.mem_get_info(0)
     from rna_clique_amd.engine import Engine
     eng = Engine(device=0, shard_rank=R, shard_count=S)
@@ -290,6 +295,7 @@ def shard_emulation(args):
             "steps": args.steps, "warmup": args.warmup,
             "projected_job_pairs_per_s_if_balanced": round(len(order) / dt, 1),
             "hbm_used_gb": round((free0 - free1) / 1e9, 2), "hbm_total_gb": round(total / 1e9, 1),
+            "engine_peak_gb": round(tm["dev_peak_bytes"] / 1e9, 2),
             "hbm_model_gb": round(model[R] / 1e9, 2), "hbm_model_max_rank_gb": round(max(model) / 1e9, 2),
             "graph_own_edges_s": round(t_graph, 3), "gen_s": round(t_gen, 1),
             "phases_ms": {k: round(v, 3) for k, v in tm.items()},

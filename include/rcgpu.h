@@ -125,6 +125,8 @@ typedef struct rc_timing {
                                  (a second first-seed extension) */
     double near_index;        /* shared searches with DUST: entries of the reverse pass's near-mask index */
     double reverse_seeds;     /* shared searches with DUST: reverse-search seeds only the reverse pass finds */
+    double dev_bytes;         /* device memory the engines of this process hold now (bytes) */
+    double dev_peak_bytes;    /* ... and the most they held at once */
 } rc_timing;
 
 void rc_default_opts(rc_opts *opts);

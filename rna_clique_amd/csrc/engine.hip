@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <array>
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -90,6 +91,17 @@ int rcg_fail(int code, const std::string &msg)
         if (r_ != RC_OK) return r_; \
     } while (0)
 
+// Device bytes the engines of this process hold (now and at most), for the
+// HBM footprint checks (rc_timing.dev_bytes / dev_peak_bytes)
+static std::atomic<long long> g_dev_bytes{0}, g_dev_peak{0};
+static void dev_account(long long b)
+{
+    const long long v = g_dev_bytes.fetch_add(b) + b;
+    long long pk = g_dev_peak.load();
+    while (v > pk && !g_dev_peak.compare_exchange_weak(pk, v)) {
+    }
+}
+
 // Device buffer that only grows (no allocation once sized: reruns are alloc-free).
 template <class T>
 struct DBuf {
@@ -98,21 +110,37 @@ struct DBuf {
     int ensure(size_t n)
     {
         if (n <= cap && p) return RC_OK;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
+        release();
         size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
         if (hipMalloc((void **)&p, bytes) != hipSuccess) {
             (void)hipGetLastError();
+            p = nullptr;
             return fail(RC_E_NOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
         }
         cap = std::max<size_t>(n, 1);
+        dev_account((long long)(cap * sizeof(T)));
         return RC_OK;
+    }
+    // a buffer allocated elsewhere (the growth paths that keep contents)
+    void adopt(T *np, size_t ncap)
+    {
+        dev_account((long long)(ncap * sizeof(T)));   // both are held until the old one goes
+        T *op = p;
+        const size_t oc = cap;
+        p = np;
+        cap = ncap;
+        if (op) {
+            (void)hipFree(op);
+            dev_account(-(long long)(oc * sizeof(T)));
+        }
     }
     ~DBuf() { release(); }
     void release()
     {
-        if (p) (void)hipFree(p);
+        if (p) {
+            (void)hipFree(p);
+            dev_account(-(long long)(cap * sizeof(T)));
+        }
         p = nullptr;
         cap = 0;
     }
@@ -489,9 +517,7 @@ int rc_add_sample(rc_engine *e, const char *label, const char *seq, const uint64
             if (e->ascii_used)
                 HIPCHK(hipMemcpyAsync(np, e->d_ascii.p, e->ascii_used, hipMemcpyDeviceToDevice, e->st));
             HIPCHK(hipStreamSynchronize(e->st));
-            e->d_ascii.release();
-            e->d_ascii.p = np;
-            e->d_ascii.cap = cap;
+            e->d_ascii.adopt(np, cap);
         }
         HIPCHK(hipMemsetAsync(e->d_ascii.p + e->ascii_used, 'A', need - e->ascii_used, e->st));
         HIPCHK(hipMemcpyAsync(e->d_ascii.p + s.abase, seq, nb, hipMemcpyHostToDevice, e->st));
@@ -713,12 +739,6 @@ static int upload(rc_engine *e)
     }
     e->n_items = items;
     shard_pairs(e);
-    // the samples of this shard's pairs must be on this GPU
-    for (uint64_t p = e->pair0; p < e->pair1; p++)
-        for (int s : {(int)e->pair_a[p], (int)e->pair_b[p]})
-            if (!e->samples[s].resident)
-                return fail(RC_E_STATE, "sample " + e->samples[s].label +
-                                            " is aligned by this shard but was added without its sequence");
 
     // device copies of what does not change between runs
     auto up = [&](auto &buf, const auto &vec) -> int {
@@ -1271,9 +1291,7 @@ static int grow_hsp(rc_engine *e, uint64_t n)
     }
     if (e->hsp_used) HIPCHK(hipMemcpyAsync(np, e->d_hsp.p, e->hsp_used * sizeof(DHsp), hipMemcpyDeviceToDevice, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
-    e->d_hsp.release();
-    e->d_hsp.p = np;
-    e->d_hsp.cap = cap;
+    e->d_hsp.adopt(np, cap);
     return RC_OK;
 }
 
@@ -1769,6 +1787,13 @@ static int do_align(rc_engine *e)
         return RC_OK;
     }
     const int N = (int)e->samples.size();
+    // the samples of this shard's pairs must be on this GPU (a graph-only
+    // engine, rc_import_edges on a fresh engine, aligns nothing and needs none)
+    for (uint64_t p = e->pair0; p < e->pair1; p++)
+        for (int s : {(int)e->pair_a[p], (int)e->pair_b[p]})
+            if (!e->samples[s].resident)
+                return fail(RC_E_STATE, "sample " + e->samples[s].label +
+                                            " is aligned by this shard but was added without its sequence");
     const size_t ngrp = (size_t)e->gene_sample.size() * N;
     CHK(e->d_grp_off.ensure(ngrp));
     CHK(e->d_grp_cnt.ensure(ngrp));
@@ -2286,6 +2311,8 @@ int rc_timings(rc_engine *e, rc_timing *t)
 {
     if (!e || !t) return fail(RC_E_ARG, "null argument");
     *t = e->tm;
+    t->dev_bytes = (double)g_dev_bytes.load();
+    t->dev_peak_bytes = (double)g_dev_peak.load();
     return RC_OK;
 }
 

@@ -66,13 +66,21 @@ def needed_samples(sample_bases, shard_count, rank):
 
 def hbm_footprint(sample_bases, sample_genes, shard_count, tile_bases=(1 << 32) - (1 << 24),
                   hsps_per_gene=1.0):
-    """Modelled HBM bytes of every rank (a planning aid: bench and tests check
-    that a configuration fits 288 GB per GPU before running it). Per rank:
-    its samples' bases (1 B each, resident), one tile's working set (packed
-    forward + reverse complement 0.5 B/base, the 16-mer index and its sort
-    buffer 16 B/base, seeds and candidates ~ 3 B/base, DUST mask), its HSP
-    store (56 B per HSP, both directed searches of every pair) and the
-    (gene, sample) group table and graph arrays over all genes."""
+    """Modelled device bytes of every rank (a planning aid: bench and tests
+    check that a configuration fits 288 GB per GPU before running it; the
+    engine reports what it actually holds, rc_timing.dev_peak_bytes). Per rank:
+    * its samples' bases, resident (1 B/base; the array grows by 1.25x);
+    * the largest alignment tile's working set: the 16-mer index and its sort
+      buffer (16 B/base), the tile's gathered copy (1), packed forward + reverse
+      complement (0.5), transcript-start and DUST bit arrays (0.25), the
+      near-mask index (0.5), seeds and candidates (~3), plus the 2^28-bucket
+      table (1 GiB);
+    * its HSP store (56 B per HSP, both directed searches of every pair; the
+      store grows by 1.5x) and table rows (16 B each);
+    * the (gene, sample) group tables over all genes x samples (24 B: offset,
+      count, mirror count, cursor, mirror scan);
+    * per (pair, gene) RBH item 100 B (row and edge slots, counts, offsets)
+      and the edge records (20 B) of all ranks after the exchange."""
     import math
     order, first = plan_pairs(sample_bases, shard_count)
     n = len(sample_bases)
@@ -83,11 +91,13 @@ def hbm_footprint(sample_bases, sample_genes, shard_count, tile_bases=(1 << 32) 
         samples = {s for p in pairs for s in p}
         resident = sum(sample_bases[s] for s in samples)
         tile = min(resident, tile_bases)
-        work = tile * (0.5 + 16 + 3 + 0.25) + (1 << 30) * 4   # + bucket table (2^28 x 4 B) and slack
-        hsps = sum(sample_genes[a] + sample_genes[b] for a, b in pairs) * hsps_per_gene * 56
-        groups = genes * n * 8 + genes * 32
-        edges = sum(min(sample_genes[a], sample_genes[b]) for a, b in pairs) * 20 * shard_count
-        out.append(int(resident + work + hsps + groups + edges + math.comb(n, 2) * 64))
+        work = tile * (16 + 1 + 0.5 + 0.25 + 0.5 + 3) + (1 << 30)
+        nh = sum(sample_genes[a] + sample_genes[b] for a, b in pairs) * hsps_per_gene
+        items = sum(sample_genes[b] for a, b in pairs)
+        groups = genes * n * 24
+        edges = sum(min(sample_genes[a], sample_genes[b]) for a, b in order) * 20
+        out.append(int(1.25 * resident + work + nh * (56 * 1.5 + 16) + items * 100 + groups + edges
+                       + math.comb(n, 2) * 64))
     return out
 
 

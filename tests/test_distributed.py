@@ -111,13 +111,15 @@ def test_c5_fits_hbm_per_rank():
     ~33 Gbp) on 8 GPUs: every rank's modelled HBM footprint (resident samples,
     one tile's working set, its HSP store, the group table) is within the
     288 GB of an MI355X, and within it with room to spare at the configuration's
-    mean transcript length."""
+    mean transcript length. (The model is calibrated on the engine's own
+    device-memory peak of rank 2 at C5, tests/test_gpu_scale.py: 202 GB
+    measured device-wide in r03.)"""
     from rna_clique_amd import distributed
     n, genes, mean_len = 128, 100_000, 2600
     bases = [genes * mean_len] * n
     fp = distributed.hbm_footprint(bases, [genes] * n, 8)
     assert max(fp) < 288e9, [f / 1e9 for f in fp]
-    assert max(fp) < 0.6 * 288e9
+    assert max(fp) < 0.72 * 288e9
     # sharding divides the resident bases and the HSP store
     one = distributed.hbm_footprint(bases, [genes] * n, 1)[0]
     assert max(fp) < 0.65 * one
