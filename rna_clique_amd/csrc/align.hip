@@ -127,11 +127,15 @@ __device__ __forceinline__ bool word_usable(const Db &db, uint64_t qs, int Lq, i
 // BIG = true: one workgroup per big_list entry, that single pass with its
 // seeds in global scratch (P.big_cap per workgroup); an entry that overflows
 // even that goes to P.big_retry (the host doubles big_cap).
-template <bool AMB, bool BIG>
+// ISOG (with BIG = false): one workgroup per gene of P.iso_list -- the genes
+// with more than ISO_LDS isoforms, whose isoform tables are read from HBM; the
+// plain launch leaves them to it (so its own code has no such path).
+template <bool AMB, bool BIG, bool ISOG>
 __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Index ix, SeedParams P)
 {
     const uint64_t big_e = BIG ? P.big_list[blockIdx.x] : 0ull;
-    const uint32_t g = BIG ? P.gene_begin + (uint32_t)(big_e >> 8) : P.gene_begin + blockIdx.x;
+    const uint32_t g = BIG ? P.gene_begin + (uint32_t)(big_e >> 8)
+                           : (ISOG ? P.iso_list[blockIdx.x] : P.gene_begin + blockIdx.x);
     if (g >= P.gene_end) return;
     const int tid = threadIdx.x;
 
@@ -175,7 +179,8 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
     // a gene's isoform tables: in LDS, or -- more than ISO_LDS isoforms (rare:
     // real assemblies have genes with hundreds) -- read from HBM (transcript
     // table and the host's word-item prefix); a block-uniform branch
-    const bool isog = niso > (uint32_t)ISO_LDS;
+    const bool isog = BIG ? niso > (uint32_t)ISO_LDS : ISOG;
+    if (!BIG && !ISOG && niso > (uint32_t)ISO_LDS) return;   // the ISOG launch takes this gene
     if (!isog) {
         for (uint32_t i = tid; i < niso; i += SBLOCK) {
             const uint32_t gtx = db.gene_tx[t0 + i];
@@ -2254,9 +2259,15 @@ void launch_seed(bool amb, const Db &db, const Index &ix, const SeedParams &P, h
     const uint32_t n = P.gene_end - P.gene_begin;
     if (n == 0) return;
     if (amb)
-        hipLaunchKernelGGL((seed_kernel<true, false>), dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
+        hipLaunchKernelGGL((seed_kernel<true, false, false>), dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
     else
-        hipLaunchKernelGGL((seed_kernel<false, false>), dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
+        hipLaunchKernelGGL((seed_kernel<false, false, false>), dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
+    if (P.iso_n) {   // the run's genes with more than ISO_LDS isoforms
+        if (amb)
+            hipLaunchKernelGGL((seed_kernel<true, false, true>), dim3(P.iso_n), dim3(SBLOCK), 0, st, db, ix, P);
+        else
+            hipLaunchKernelGGL((seed_kernel<false, false, true>), dim3(P.iso_n), dim3(SBLOCK), 0, st, db, ix, P);
+    }
 }
 
 // the global-memory passes of the (gene, sample) entries P.big_list[0, n)
@@ -2264,9 +2275,9 @@ void launch_seed_big(bool amb, const Db &db, const Index &ix, const SeedParams &
 {
     if (n == 0) return;
     if (amb)
-        hipLaunchKernelGGL((seed_kernel<true, true>), dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
+        hipLaunchKernelGGL((seed_kernel<true, true, false>), dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
     else
-        hipLaunchKernelGGL((seed_kernel<false, true>), dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
+        hipLaunchKernelGGL((seed_kernel<false, true, false>), dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
 }
 
 void launch_extend(bool amb, const Db &db, const ExtParams &P, hipStream_t st)

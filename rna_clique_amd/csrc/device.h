@@ -165,6 +165,8 @@ struct SeedParams {
     // genes with more than ISO_LDS isoforms: the word-item prefix of each
     // isoform, at gene_tx_off[g] + g + i (i = 0..niso; stride P.stride)
     const uint32_t *iso_pre_g;
+    const uint32_t *iso_list;     // ... those genes of [gene_begin, gene_end) (the ISOG launch)
+    uint32_t iso_n;
     LSeed *rseeds;
     uint32_t *rseed_gene;
     uint64_t rseed_cap;

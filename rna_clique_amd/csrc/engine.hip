@@ -360,7 +360,7 @@ struct rc_engine {
     DBuf<DEdge> d_edges_tmp;
     DBuf<uint32_t> d_cand_ovf, d_gc_off, d_gc_cnt, d_gcount, d_defer, d_defer2;
     DBuf<uint64_t> d_gscan, d_mscan, d_mkey, d_tmask, d_mbig;
-    DBuf<uint32_t> d_mcnt, d_mcur, d_tx_pos, d_iso_pre;
+    DBuf<uint32_t> d_mcnt, d_mcur, d_tx_pos, d_iso_pre, d_iso_list, d_iso_list_r;
     DBuf<unsigned long long> d_shard_cnt, d_shard_prefix;
     uint64_t seed_cap = 0, cand_cap = 0, ovf_cap = 0;   // per-shard / total capacities
     // (gene, sample) seed passes too big for LDS, and their global scratch
@@ -1099,6 +1099,19 @@ static int build_masked_index(rc_engine *e)
     return RC_OK;
 }
 
+// Genes of [g0, g1) with more than ISO_LDS isoforms (the seed kernel's ISOG
+// launch), appended to `list`; returns their count
+static uint32_t iso_genes(const rc_engine *e, uint32_t g0, uint32_t g1, std::vector<uint32_t> &list)
+{
+    uint32_t n = 0;
+    for (uint32_t g = g0; g < g1; g++)
+        if (e->gene_tx_off[g + 1] - e->gene_tx_off[g] > (uint32_t)ISO_LDS) {
+            list.push_back(g);
+            n++;
+        }
+    return n;
+}
+
 static Db make_db(rc_engine *e)
 {
     Db db;
@@ -1186,6 +1199,12 @@ static int reverse_pass(rc_engine *e, int ti, const Db &db, const Index &ixm, ui
     }
     CHK(e->d_rtmask.ensure(rmask.size()));
     HIPCHK(hipMemcpyAsync(e->d_rtmask.p, rmask.data(), rmask.size() * 8, hipMemcpyHostToDevice, e->st));
+    std::vector<uint32_t> ilist, ioff(1, 0);
+    for (auto &r : runs) ioff.push_back(ioff.back() + iso_genes(e, e->sample_gene_begin[r.first],
+                                                                 e->sample_gene_begin[r.second], ilist));
+    CHK(e->d_iso_list_r.ensure(std::max<size_t>(ilist.size(), 1)));
+    if (!ilist.empty())
+        HIPCHK(hipMemcpyAsync(e->d_iso_list_r.p, ilist.data(), ilist.size() * 4, hipMemcpyHostToDevice, e->st));
     CHK(e->d_rctr.ensure(4));
     CHK(e->d_big_out.ensure(std::max<uint64_t>(e->big_list_cap, 1)));
     if (!e->rseed_cap) e->rseed_cap = 1u << 20;
@@ -1195,8 +1214,11 @@ static int reverse_pass(rc_engine *e, int ti, const Db &db, const Index &ixm, ui
         CHK(e->d_rseed_gene.ensure(e->rseed_cap));
         HIPCHK(hipMemsetAsync(e->d_rctr.p + 1, 0, 2 * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
-        for (auto &r : runs) {
+        for (size_t ri = 0; ri < runs.size(); ri++) {
+            const auto &r = runs[ri];
             SeedParams S{};
+            S.iso_list = e->d_iso_list_r.p + ioff[ri];
+            S.iso_n = ioff[ri + 1] - ioff[ri];
             S.word = e->o.word_size;
             S.stride = e->o.word_size - W16 + 1;
             const char *pm = getenv("RC_SEED_PRE");
@@ -1379,13 +1401,18 @@ static int align_tile(rc_engine *e, int ti)
     HIPCHK(hipMemcpyAsync(e->d_tmask.p, tmask.data(), tmask.size() * 8, hipMemcpyHostToDevice, e->st));
     // per run: its genes [g0, g1) and its slice of the (gene, sample) arrays
     std::vector<uint32_t> rg0(RT), rg1(RT);
+    std::vector<uint32_t> ilist, ioff(1, 0);
     std::vector<size_t> gcb(RT + 1, 0), cnb(R + 1, 0);
     for (size_t r = 0; r < RT; r++) {
         rg0[r] = e->sample_gene_begin[runs[r].first];
         rg1[r] = e->sample_gene_begin[runs[r].second];
         gcb[r + 1] = gcb[r] + (size_t)(rg1[r] - rg0[r]) * N;
         if (r < R) cnb[r + 1] = cnb[r] + (size_t)(rg1[r] - rg0[r]) * N + 1;
+        ioff.push_back(ioff.back() + iso_genes(e, rg0[r], rg1[r], ilist));
     }
+    CHK(e->d_iso_list.ensure(std::max<size_t>(ilist.size(), 1)));
+    if (!ilist.empty())
+        HIPCHK(hipMemcpyAsync(e->d_iso_list.p, ilist.data(), ilist.size() * 4, hipMemcpyHostToDevice, e->st));
     CHK(e->d_gc_off.ensure(std::max<size_t>(gcb[RT], 1)));
     CHK(e->d_gc_cnt.ensure(std::max<size_t>(gcb[RT], 1)));
     CHK(e->d_gcount.ensure(std::max<size_t>(cnb[R], 1)));
@@ -1460,6 +1487,8 @@ static int align_tile(rc_engine *e, int ti)
             S.list2_n = e->d_count.p + 16;
             S.gene_begin = rg0[r];
             S.gene_end = rg1[r];
+            S.iso_list = e->d_iso_list.p + ioff[r];
+            S.iso_n = ioff[r + 1] - ioff[r];
             S.seeds = e->d_seeds.p;
             S.seed_cap = e->seed_cap;
             S.seed_count = e->d_shard_cnt.p;
