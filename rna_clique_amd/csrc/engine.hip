@@ -18,6 +18,7 @@
 #include <cstring>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -2451,6 +2452,15 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
     if (graph_path && e->o.shard_count != 1)
         return fail(RC_E_STATE, "a sharded engine holds only its own pairs' rows: graph.pkl comes from the edges");
     const int nt = std::max(1, std::min(64, (int)threads));
+    // RC_OUT_TIMING=1: where the time goes (stderr)
+    const char *otv = getenv("RC_OUT_TIMING");
+    const bool otime = otv && atoi(otv);
+    std::atomic<long long> t_fetch{0}, t_conv{0}, t_write{0}, t_gadd{0}, t_gwrite{0};
+    auto now_ns = []() {
+        return (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    };
+    const long long t_start = now_ns();
     std::mutex mu;
     std::condition_variable cv;
     std::deque<std::pair<int, std::shared_ptr<PairRaw>>> tq, gq;
@@ -2476,10 +2486,14 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
                 tq.pop_front();
             }
             const PairRaw &raw = *job.second;
+            const long long c0 = now_ns();
             buf.resize(raw.rows.size());
             convert_rows(e, raw, buf.data());
+            const long long c1 = now_ns();
             const int rc = od2_write_table(buf.data(), buf.size(), e->samples[raw.s1].label, e->samples[raw.s2].label,
                                            table_paths[job.first]);
+            t_conv += c1 - c0;
+            t_write += now_ns() - c1;
             if (rc != RC_OK) set_err(rc);
             {
                 std::lock_guard<std::mutex> lk(mu);
@@ -2506,6 +2520,7 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
                 gq.pop_front();
             }
             const PairRaw &raw = *job.second;
+            const long long a0 = now_ns();
             const size_t n = raw.rows.size();
             sg.resize(n);
             qg.resize(n);
@@ -2519,6 +2534,7 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
                 set_err(RC_E_LIMIT);
                 ok = false;
             }
+            t_gadd += now_ns() - a0;
             {
                 std::lock_guard<std::mutex> lk(mu);
                 in_flight--;
@@ -2526,9 +2542,11 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
             cv.notify_all();
         }
         if (ok) {
+            const long long w0 = now_ns();
             std::vector<const char *> names;
             for (const SampleRec &s : e->samples) names.push_back(s.label.c_str());
             if (rc_graph_pickle_write(g, graph_path, (int32_t)names.size(), names.data()) != RC_OK) set_err(RC_E_IO);
+            t_gwrite += now_ns() - w0;
         }
         rc_graph_pickle_free(g);
     };
@@ -2546,7 +2564,9 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
             if (err != RC_OK) break;
         }
         auto raw = std::make_shared<PairRaw>();
+        const long long f0 = now_ns();
         rc = fetch_pair(e, s1[i], s2[i], *raw);
+        t_fetch += now_ns() - f0;
         if (rc != RC_OK) break;
         {
             std::lock_guard<std::mutex> lk(mu);
@@ -2562,6 +2582,10 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
     }
     cv.notify_all();
     for (std::thread &t : pool) t.join();
+    if (otime)
+        fprintf(stderr, "rc_write_outputs: %.3f s wall; fetch %.3f s, convert %.3f, table write %.3f (thread-s, %d threads), "
+                        "graph add %.3f, graph write %.3f\n", (now_ns() - t_start) * 1e-9, t_fetch * 1e-9, t_conv * 1e-9,
+                t_write * 1e-9, nt, t_gadd * 1e-9, t_gwrite * 1e-9);
     if (rc != RC_OK) return rc;
     if (err != RC_OK) return fail(err, err_msg);
     return RC_OK;

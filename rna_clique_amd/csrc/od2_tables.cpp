@@ -24,6 +24,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 int rcg_fail(int code, const std::string &msg);
@@ -753,11 +754,27 @@ int od2_write_table(const rc_row *rows, uint64_t n, const std::string &ssample, 
     t.n = n;
     t.pident.resize(n);
     t.evalue.resize(n);
+    // a table holds few distinct (nident, length) pairs and e-values: print
+    // and parse each once (as tables.py does with np.unique)
+    std::unordered_map<uint64_t, double> pmemo, ememo;
     for (uint64_t i = 0; i < n; i++) {
         const rc_hsp &h = rows[i].hsp;
-        const double L = (double)(h.length > 1 ? h.length : 1);
-        t.pident[i] = od2::printed("%.3f", 100.0 * (double)h.nident / L);
-        t.evalue[i] = h.evalue < 1.0e-180 ? 0.0 : od2::printed("%.2e", h.evalue);
+        const uint64_t pk = ((uint64_t)(uint32_t)h.nident << 32) | (uint32_t)h.length;
+        auto pi = pmemo.find(pk);
+        if (pi == pmemo.end()) {
+            const double L = (double)(h.length > 1 ? h.length : 1);
+            pi = pmemo.emplace(pk, od2::printed("%.3f", 100.0 * (double)h.nident / L)).first;
+        }
+        t.pident[i] = pi->second;
+        if (h.evalue < 1.0e-180) {
+            t.evalue[i] = 0.0;
+        } else {
+            uint64_t ek;
+            std::memcpy(&ek, &h.evalue, 8);
+            auto ei = ememo.find(ek);
+            if (ei == ememo.end()) ei = ememo.emplace(ek, od2::printed("%.2e", h.evalue)).first;
+            t.evalue[i] = ei->second;
+        }
     }
     const std::string file = od2::build_table_file(t, ssample, qsample);
     const std::string tmp = path + ".tmp";
