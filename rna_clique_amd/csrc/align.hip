@@ -25,7 +25,7 @@ constexpr int SBLOCK = 256;
 #define RC_SEED_CAP 1024
 #endif
 #ifndef RC_SEED_WAVES
-#define RC_SEED_WAVES 4   // min blocks per CU: 4 waves/SIMD (what the LDS allows), <= 128 VGPRs
+#define RC_SEED_WAVES 1   // measured: a 4-wave bound (<= 128 VGPRs, more SGPR spills) is 7 % slower
 #endif
 constexpr int SEED_CAP = RC_SEED_CAP;   // seeds of one pass in LDS (a power of two: the bitonic sort pads to one)
 static_assert((SEED_CAP & (SEED_CAP - 1)) == 0, "RC_SEED_CAP must be a power of two");

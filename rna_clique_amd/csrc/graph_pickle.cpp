@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <algorithm>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -126,7 +127,10 @@ struct rc_gpickle {
     std::vector<std::vector<uint32_t>> dense;      // per sample: gene -> node id + 1
     static constexpr int64_t DENSE = 1 << 26;
     std::vector<NodeKey> node;                     // insertion order
-    EdgeMap emap;
+    // an edge joins two samples' genes, so only tables of the same sample pair
+    // can repeat it: one small edge set per (unordered) sample pair, not one
+    // set of every edge (random probes into a 25 M-entry table at C3)
+    std::map<std::pair<int32_t, int32_t>, EdgeMap> emap;
     std::vector<std::pair<uint32_t, uint32_t>> edge;   // insertion order
 };
 
@@ -165,10 +169,11 @@ int rc_graph_pickle_add(rc_gpickle *g, int32_t ssample, int32_t qsample, const i
     };
     for (uint64_t i = 0; i < n; i++) su[i] = node_id(ssample, sgene[i]);
     for (uint64_t i = 0; i < n; i++) qu[i] = node_id(qsample, qgene[i]);
+    EdgeMap &em = g->emap[{std::min(ssample, qsample), std::max(ssample, qsample)}];
     for (uint64_t i = 0; i < n; i++) {
         const uint32_t a = su[i], b = qu[i];
         const uint64_t k = a < b ? ((uint64_t)a << 32 | b) : ((uint64_t)b << 32 | a);
-        if (g->emap.add(k)) g->edge.push_back({a, b});
+        if (em.add(k)) g->edge.push_back({a, b});
     }
     if (g->node.size() >= 0x7FFFFFFFull || g->edge.size() >= 0x7FFFFFFFull)
         return rcg_fail(RC_E_LIMIT, "graph too large for the pickle writer");
@@ -206,22 +211,30 @@ int rc_graph_pickle_write(rc_gpickle *g, const char *path, int32_t n_names, cons
     if (!f) return rcg_fail(RC_E_IO, "cannot open " + tmp);
     // the stream is built in a 16 MiB block and written a block at a time
     // (per-opcode stdio calls, each taking the FILE lock, ran at ~38 MB/s)
-    std::vector<uint8_t> blk;
-    blk.reserve(1 << 24);
+    const size_t BLK = 1u << 24;
+    std::vector<uint8_t> blk(BLK + 4096);
+    uint8_t *w = blk.data();
+    uint8_t *const wend = blk.data() + BLK;
     bool werr = false;
     auto flush = [&]() {
-        if (!blk.empty() && fwrite(blk.data(), 1, blk.size(), f) != blk.size()) werr = true;
-        blk.clear();
+        const size_t n = (size_t)(w - blk.data());
+        if (n && fwrite(blk.data(), 1, n, f) != n) werr = true;
+        w = blk.data();
     };
     uint32_t memo = 0;
     auto put = [&](const void *p, size_t n) {
-        const uint8_t *b = static_cast<const uint8_t *>(p);
-        blk.insert(blk.end(), b, b + n);
-        if (blk.size() >= (1u << 24) - 64) flush();
+        if (n > 4096) {   // a long sample name
+            flush();
+            if (fwrite(p, 1, n, f) != n) werr = true;
+            return;
+        }
+        std::memcpy(w, p, n);
+        w += n;
+        if (w >= wend) flush();
     };
     auto op = [&](uint8_t c) {
-        blk.push_back(c);
-        if (blk.size() >= (1u << 24) - 64) flush();
+        *w++ = c;
+        if (w >= wend) flush();
     };
     auto u32 = [&](uint32_t v) { put(&v, 4); };
     auto memoize = [&]() { op(0x94); return memo++; };
