@@ -1538,14 +1538,20 @@ __device__ __forceinline__ int slide_fwd(uint32_t pa, uint32_t pb, int maxn, uin
 
 // per-row bookkeeping in LDS: the candidate record (CAND_DWORDS dwords) and state
 enum { RM_REC = 0, RM_CLO = CAND_DWORDS, RM_CHI, RM_QB, RM_TB, RM_X, RM_Y, RM_LEN,
-       RM_RSC, RM_RI, RM_RJ, RM_RD, RM_RGO, RM_N };
+       RM_RSC, RM_RI, RM_RJ, RM_RD, RM_RGO,
+       RM_PHASE,                                  // the running extension's done action (A_RDONE / A_LDONE)
+       RM_KOF,                                    // the window's diagonal offset (sliding sub-band)
+       RM_PWI, RM_PWG, RM_PWD, RM_PK,             // the row's best record parked by a window slide, its diagonal
+       RM_N };
 // fields of the record (dword offsets, layout of Cand)
 enum { RC_SOFF = 0, RC_QTX = 1, RC_STX = 2, RC_CNT_STRAND = 3, RC_Q0 = 4, RC_S0 = 6, RC_LQ = 8, RC_LT = 9,
        RC_SAMS = 10, RC_E01 = 11 };
 // work cursors of a row
 enum { RS_LEND, RS_SHARD, RS_SHN, RS_N };
 // row actions (transition actions < A_DONE; extending: A_STEP_R / A_STEP_L = their done action + 4)
-enum { A_FETCH, A_UNUSED, A_RDONE, A_LDONE, A_ABORT, A_DONE, A_STEP_R, A_STEP_L };
+enum { A_FETCH, A_SLIDE, A_RDONE, A_LDONE, A_ABORT, A_DONE, A_STEP_R, A_STEP_L };
+// bl of a row whose best record is parked in its LDS bookkeeping (a window slide)
+constexpr int BL_PARKED = -64;
 // cand_box record of a first-seed extension: status (0 done, -1 deferred),
 // right (score, i, j, d, gap state), left (same)
 enum { FX_STATUS = 0, FX_R = 1, FX_L = 6 };
@@ -1584,7 +1590,17 @@ __host__ __device__ constexpr size_t row_lds_bytes(int rw, int na, int sw)
 // extended, RC-megablast spec 3) to the right and to the left. Anything
 // further -- the other seeds' containment, more HSPs, purge, e-values -- is
 // first_finish_kernel's; a candidate that needs more than its first seed goes
-// to extend_kernel whole, as does one whose frontier reaches the sub-band edge.
+// to extend_kernel whole.
+// Sliding sub-band: a row's RW lanes are the diagonals [kof - RW/2, kof +
+// RW/2 - 1] of the spec's 64-diagonal band, kof = 0 when an extension starts.
+// When a live lane reaches the window's edge, the window slides so that the
+// live diagonals are centred (|kof| <= 31 - RW/2: its edges never meet the
+// band's, so the edge lanes stay dead at every step start, as the half-wave
+// seam of the frontier shifts needs); the lanes entering it are diagonals no
+// live lane has reached (an outside diagonal can only come alive from a live
+// edge lane, which slides first), so the extension stays exact. Only a live
+// span wider than the window, or one reaching past the band's +-31, goes to
+// the one-wave full-band kernel (indels: C3v).
 template <bool AMB, int RW, int MINW>
 __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
 {
@@ -1706,7 +1722,11 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
         pbk = pb - (uint32_t)k;
         blk = blen + k;
         nkd = -k;
-        if (rl == 0) atomicAdd(&rcnt[0], 1u);
+        if (rl == 0) {
+            atomicAdd(&rcnt[0], 1u);
+            meta[RM_PHASE] = done_act;
+            meta[RM_KOF] = 0;
+        }
         act = (min(alen, blen) - r0 <= 0) ? done_act : done_act + (A_STEP_R - A_RDONE);
     };
     // reversed copy of a staged array: word w holds bases L - 1 - 32 w down to
@@ -1823,11 +1843,61 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                     const int u = alen; alen = blen; blen = u;
                 }
                 ext_init(A_RDONE);
+            } else if (act == A_SLIDE) {
+                // a live lane at the window's edge: centre the live diagonals
+                const uint32_t livem = rw_mask<RW>(ballot(R >= 0), row);
+                const int kof = meta[RM_KOF];
+                const int lmin = __builtin_ctz(livem), lmax = 31 - __builtin_clz(livem);
+                constexpr int KMAX = 31 - RW / 2;
+                const int kn = max(-KMAX, min(KMAX, kof + ((lmin + lmax + 1) >> 1) - RC0));
+                const int s = kn - kof;
+                if (s == 0 || lmin - s < 1 || lmax - s > RW - 2) {
+                    act = A_ABORT;   // wider than the window, or at the band's edge
+                    continue;
+                }
+                if (bl != BL_PARKED) {
+                    // the row's best record leaves its lane's hands (that lane may leave the window)
+                    const int bsrc = RW * row + bl;
+                    const int pwi = __shfl(wi, bsrc), pwg = __shfl(wg, bsrc), pwd = __shfl(wd, bsrc);
+                    if (rl == 0) {
+                        meta[RM_PWI] = pwi;
+                        meta[RM_PWG] = pwg;
+                        meta[RM_PWD] = pwd;
+                        meta[RM_PK] = bl - RC0 + kof;
+                    }
+                    bl = BL_PARKED;
+                }
+                const int from = rl + s;
+                const bool in = from >= 0 && from < RW;
+                const int nR = __shfl(R, RW * row + (in ? from : rl)), ng = __shfl(goe, RW * row + (in ? from : rl));
+                R = in ? nR : -1;
+                goe = in ? ng : 0;
+                const int kk = k + kn;    // this lane's diagonal now
+                pbk = pb - (uint32_t)kk;
+                blk = blen + kk;
+                nkd = -(kk + d6);
+                if (rl == 0) {
+                    meta[RM_KOF] = kn;
+                    atomicAdd(&rcnt[3], 1u);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                act = meta[RM_PHASE] + (A_STEP_R - A_RDONE);
             } else if (act == A_RDONE || act == A_LDONE) {
-                const int src = RW * row + bl;
-                int ei = __shfl(wi, src);
-                const int ed = __shfl(wd, src) / 6, ego = __shfl(wg, src);
-                int ej = ei - (bl - RC0);
+                int ei, ed, ego, kb;   // the best record and its diagonal
+                if (bl == BL_PARKED) {
+                    ei = meta[RM_PWI];
+                    ed = meta[RM_PWD] / 6;
+                    ego = meta[RM_PWG];
+                    kb = meta[RM_PK];
+                } else {
+                    const int src = RW * row + bl;
+                    ei = __shfl(wi, src);
+                    ed = __shfl(wd, src) / 6;
+                    ego = __shfl(wg, src);
+                    kb = bl - RC0 + meta[RM_KOF];
+                }
+                int ej = ei - kb;
                 if (swap) {
                     const int t = ei; ei = ej; ej = t;
                 }
@@ -1949,7 +2019,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
             constexpr uint64_t EDGES = RW == 64 ? 0ull : (RW == 32 ? 0x8000000180000001ull : 0x8001800180018001ull);
             const uint64_t mcont = rw_spread<RW>(mlive & m_gt(bound, best)) & m_lt(d6, 6 * DMAX);
             const uint64_t medge = RW == 64 ? 0ull : rw_spread<RW>(mlive & EDGES);
-            act = lane_sel(mcont, lane_sel_k<A_ABORT>(medge, act), act - (A_STEP_R - A_RDONE));
+            act = lane_sel(mcont, lane_sel_k<A_SLIDE>(medge, act), act - (A_STEP_R - A_RDONE));
         }
 #ifdef RC_ROW_TIMING
         t_st += __builtin_readcyclecounter() - c1t;
@@ -1965,7 +2035,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
     unsigned long long *const ctr = row_args()->P.counters;
     if (lane == 0 && ctr) atomicAdd(&ctr[0], steps);
     __syncthreads();
-    if (threadIdx.x < 3 && ctr) atomicAdd(&ctr[1 + threadIdx.x], (unsigned long long)rcnt[threadIdx.x]);
+    if (threadIdx.x < 4 && ctr) atomicAdd(&ctr[1 + threadIdx.x], (unsigned long long)rcnt[threadIdx.x]);   // [4]: slides
 }
 
 // The candidates' first-seed extensions -> box; the other seeds of the

@@ -1685,6 +1685,7 @@ static int align_tile(rc_engine *e, int ti)
             e->tm.ext_deferred += (double)ctr[5] + (double)ndr;
             e->tm.ext_second += e->share ? (double)nl2 : 0.0;
             e->tm.band_bound += (double)ctr[7];
+            e->tm.ext_slides += (double)ctr[4];
             e->tm.maxhsp_bound += (double)ctr[10];
             break;
         }
