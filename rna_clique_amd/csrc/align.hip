@@ -1872,10 +1872,11 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 const int nR = __shfl(R, RW * row + (in ? from : rl)), ng = __shfl(goe, RW * row + (in ? from : rl));
                 R = in ? nR : -1;
                 goe = in ? ng : 0;
-                const int kk = k + kn;    // this lane's diagonal now
-                pbk = pb - (uint32_t)kk;
-                blk = blen + kk;
-                nkd = -(kk + d6);
+                // this lane's diagonal was k + kof and is k + kn: refold it
+                // into the per-lane constants (pb and blen are not kept)
+                pbk -= (uint32_t)s;
+                blk += s;
+                nkd -= s;
                 if (rl == 0) {
                     meta[RM_KOF] = kn;
                     atomicAdd(&rcnt[3], 1u);
