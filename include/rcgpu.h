@@ -126,6 +126,8 @@ typedef struct rc_timing {
     double near_index;        /* shared searches with DUST: entries of the reverse pass's near-mask index */
     double reverse_seeds;     /* shared searches with DUST: reverse-search seeds only the reverse pass finds */
     double ext_slides;        /* row-kernel window slides (the sliding 32-diagonal sub-band) */
+    double ext_wide;          /* first-seed extensions whose live diagonals outgrew the sliding sub-band,
+                                 redone on 64-lane rows (the spec's whole band) */
     double dev_bytes;         /* device memory the engines of this process hold now (bytes) */
     double dev_peak_bytes;    /* ... and the most they held at once */
 } rc_timing;

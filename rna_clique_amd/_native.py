@@ -86,7 +86,7 @@ class RcTiming(ctypes.Structure):
         "pack_ms", "index_ms", "align_ms", "topn_ms", "rbh_ms", "graph_ms",
         "reduce_ms", "total_ms", "seed_kernel_ms", "align_kernel_ms", "ext_steps",
         "ext_calls", "ext_fullband", "ext_deferred", "big_passes", "tiles", "dust_ms",
-        "band_bound", "maxhsp_bound", "ext_second", "near_index", "reverse_seeds", "ext_slides", "dev_bytes",
+        "band_bound", "maxhsp_bound", "ext_second", "near_index", "reverse_seeds", "ext_slides", "ext_wide", "dev_bytes",
         "dev_peak_bytes")]
 
 

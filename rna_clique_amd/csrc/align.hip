@@ -1675,12 +1675,17 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
         const RowArgsK K = row_args();
         return K->P.which ? K->P.cand_box2 : K->P.cand_box;
     };
-    auto defer = [&](uint64_t ci) {   // row-uniform; extend_kernel takes the candidate whole
+    // row-uniform; extend_kernel takes the candidate whole -- or, shared
+    // searches, a sub-band overflow (wide) the 64-lane pass over P.wide next
+    auto defer = [&](uint64_t ci, bool wide) {
         if (rl == 0) {
             const RowArgsK K = row_args();
             if (!K->P.share) {   // shared searches: first_finish_kernel lists each search on its own
                 const unsigned long long di = atomicAdd(K->P.defer_count, 1ull);
                 K->P.defer[di] = (uint32_t)ci;
+            } else if (wide && K->P.wide) {
+                const unsigned long long wi2 = atomicAdd(K->P.wide_n, 1ull);
+                K->P.wide[wi2] = (uint32_t)ci;
             }
             box_out()[ci * BOX_REC + FX_STATUS] = -1;
         }
@@ -1776,7 +1781,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 const int nwq = (int)(((q0 & 31) + (uint64_t)Lq) >> 5) + 3;
                 const int nwt = (int)(((s0 & 31) + (uint64_t)Lt) >> 5) + 3;
                 if (nwq > sw || nwt > sw || (Lq >> 5) + 3 > sw || (Lt >> 5) + 3 > sw) {
-                    defer(ci);
+                    defer(ci, false);
                     continue;
                 }
                 // raw words of query and subject, and the first seed: one round trip
@@ -1938,7 +1943,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 }
             } else {   // A_ABORT: the sub-band overflowed
                 const uint64_t ci = (uint64_t)(uint32_t)meta[RM_CLO] | ((uint64_t)(uint32_t)meta[RM_CHI] << 32);
-                defer(ci);
+                defer(ci, true);
                 if (rl == 0) atomicAdd(&rcnt[2], 1u);
                 act = A_FETCH;
             }
@@ -2404,14 +2409,36 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
         // shared searches: first seeds e0 over every candidate, then e1 over
         // list2 (reverse searches whose first seed is another seed), then each
         // directed search checked (or listed for extend_kernel) on its own
+        // each 32-lane pass is followed by a 64-lane pass (the spec's whole
+        // band) over the candidates whose live diagonals outgrew the sliding
+        // sub-band (RC_WIDE=0: they go to the one-wave kernel instead)
+        const char *wv = getenv("RC_WIDE");
+        const bool widep = !(wv && atoi(wv) == 0) && P.wide0;
+        auto wide_pass = [&](const ExtParams &B, uint32_t *lst, unsigned long long *lst_n, unsigned long long *wk) {
+            ExtParams V = B;
+            V.list = lst;
+            V.list_n = lst_n;
+            V.work = wk;
+            V.wide = nullptr;
+            V.wide_n = nullptr;
+            if (amb) RC_LAUNCH_ROWS(true, 64, ROW_MIN_WAVES, V); else RC_LAUNCH_ROWS(false, 64, ROW_MIN_WAVES, V);
+        };
         W.which = 0;
+        W.wide = widep ? P.wide0 : nullptr;
+        W.wide_n = P.wide0_n;
         if (amb) RC_LAUNCH_ROWS(true, 32, ROW_MIN_WAVES, W); else RC_LAUNCH_ROWS(false, 32, ROW_MIN_WAVES, W);
+        if (widep) wide_pass(W, P.wide0, P.wide0_n, P.work_w0);
         ExtParams W2 = W;
         W2.which = 1;
         W2.list = P.list2;
         W2.list_n = P.list2_n;
         W2.work = P.work3;
+        W2.wide = widep ? P.wide1 : nullptr;
+        W2.wide_n = P.wide1_n;
         if (amb) RC_LAUNCH_ROWS(true, 32, ROW_MIN_WAVES, W2); else RC_LAUNCH_ROWS(false, 32, ROW_MIN_WAVES, W2);
+        if (widep) wide_pass(W2, P.wide1, P.wide1_n, P.work_w1);
+        W.list = nullptr;
+        W.list_n = nullptr;
         uint64_t g = (P.n_cand + 255) / 256;
         if (g > 65536) g = 65536;
         hipLaunchKernelGGL(first_finish_kernel, dim3((unsigned)g), dim3(256), 0, st, W);

@@ -248,6 +248,12 @@ struct ExtParams {
     const uint32_t *list2;              // candidates with e1 != SEED_NONE (the seed kernel's list)
     const unsigned long long *list2_n;
     unsigned long long *work3;          // work counter of the row kernel's pass over list2
+    // shared searches: candidates whose live diagonals outgrew the 32-lane
+    // sliding sub-band, for the 64-lane pass after each 32-lane pass
+    uint32_t *wide;                     // the list the running pass appends to (null: none)
+    unsigned long long *wide_n;
+    uint32_t *wide0, *wide1;            // the e0 pass's and the e1 pass's lists
+    unsigned long long *wide0_n, *wide1_n, *work_w0, *work_w1;
 };
 
 // DHsp.strand carries, besides the strand (bit 0), the direction flags of a

@@ -355,7 +355,7 @@ struct rc_engine {
     // shared searches (RC_SHARE, default): the reverse search's HSPs per candidate
     DBuf<DHsp> d_cand_hsp_r;
     DBuf<uint8_t> d_cand_nh_r;
-    DBuf<uint32_t> d_cand_ovf_r, d_defer_r, d_list2;
+    DBuf<uint32_t> d_cand_ovf_r, d_defer_r, d_list2, d_wide0, d_wide1;
     bool share = false;
     DBuf<DRow> d_rows_tmp;
     DBuf<DEdge> d_edges_tmp;
@@ -1445,7 +1445,7 @@ static int align_tile(rc_engine *e, int ti)
     ixm.bits = e->mindex_bits;
     // --- seeds ---
     std::vector<unsigned long long> shard_cnt(2 * NSHARD);
-    CHK(e->d_count.ensure(24));
+    CHK(e->d_count.ensure(32));
     unsigned long long *big_n = e->d_count.p + 12, *big_retry_n = e->d_count.p + 13;
     uint64_t n_big = 0;
     HIPCHK(hipEventRecord(e->ev[3], e->st));
@@ -1597,6 +1597,8 @@ static int align_tile(rc_engine *e, int ti)
         CHK(e->d_cand_nh_r.ensure(slots));
         CHK(e->d_cand_ovf_r.ensure(slots));
         CHK(e->d_defer_r.ensure(std::max<uint64_t>(n_cand, 1)));
+        CHK(e->d_wide0.ensure(std::max<uint64_t>(n_cand, 1)));
+        CHK(e->d_wide1.ensure(std::max<uint64_t>(n_cand, 1)));
     }
     CHK(e->d_defer.ensure(std::max<uint64_t>(n_cand, 1)));
     CHK(e->d_defer2.ensure(std::max<uint64_t>(n_cand, 1)));
@@ -1606,6 +1608,7 @@ static int align_tile(rc_engine *e, int ti)
         HIPCHK(hipMemsetAsync(e->d_count.p, 0, 12 * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_count.p + 14, 0, 2 * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_count.p + 17, 0, 2 * sizeof(unsigned long long), e->st));
+        HIPCHK(hipMemsetAsync(e->d_count.p + 20, 0, 4 * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
         ExtParams X{};
         X.xdrop = e->o.xdrop_half;
@@ -1646,6 +1649,12 @@ static int align_tile(rc_engine *e, int ti)
         X.list2 = e->d_list2.p;
         X.list2_n = e->d_count.p + 16;
         X.work3 = e->d_count.p + 18;
+        X.wide0 = e->share ? e->d_wide0.p : nullptr;
+        X.wide1 = e->d_wide1.p;
+        X.wide0_n = e->d_count.p + 20;
+        X.wide1_n = e->d_count.p + 21;
+        X.work_w0 = e->d_count.p + 22;
+        X.work_w1 = e->d_count.p + 23;
         {
             const char *cv = getenv("RC_ROW_CHUNK");
             X.chunk = cv ? atoi(cv) : 8;
@@ -1661,6 +1670,8 @@ static int align_tile(rc_engine *e, int ti)
         HIPCHK(hipEventRecord(e->ev[11], e->st));
         unsigned long long ovn = 0, ctr[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, nfull = 0;
         HIPCHK(hipMemcpyAsync(&nfull, e->d_count.p + 14, sizeof nfull, hipMemcpyDeviceToHost, e->st));
+        unsigned long long nwide[2] = {0, 0};   // shared searches: candidates the 64-lane passes took
+        HIPCHK(hipMemcpyAsync(nwide, e->d_count.p + 20, sizeof nwide, hipMemcpyDeviceToHost, e->st));
         unsigned long long ndr = 0, nl2 = 0;   // shared searches: reverse searches redone whole, second first seeds
         HIPCHK(hipMemcpyAsync(&ndr, e->d_count.p + 17, sizeof ndr, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipMemcpyAsync(&nl2, e->d_count.p + 16, sizeof nl2, hipMemcpyDeviceToHost, e->st));
@@ -1686,6 +1697,7 @@ static int align_tile(rc_engine *e, int ti)
             e->tm.ext_second += e->share ? (double)nl2 : 0.0;
             e->tm.band_bound += (double)ctr[7];
             e->tm.ext_slides += (double)ctr[4];
+            e->tm.ext_wide += (double)(nwide[0] + nwide[1]);
             e->tm.maxhsp_bound += (double)ctr[10];
             break;
         }
