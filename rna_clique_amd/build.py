@@ -7,7 +7,7 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "librcgpu.so")
-SOURCES = ["kernels.hip", "align.hip", "dust.hip", "engine.hip", "fasta.cpp", "graph_pickle.cpp",
+SOURCES = ["kernels.hip", "sort.hip", "align.hip", "dust.hip", "engine.hip", "fasta.cpp", "graph_pickle.cpp",
            "od2_tables.cpp"]
 HEADERS = ["device.h", os.path.join("..", "..", "include", "rcgpu.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -40,6 +40,10 @@ void launch_kmer_count(const TxInfo *, uint32_t, const uint64_t *, uint64_t *, h
 void launch_kmer_fill(bool, const TxInfo *, uint32_t, const uint64_t *, const uint64_t *, const uint64_t *,
                       uint64_t *, hipStream_t);
 void launch_bucket_fill(const uint64_t *, uint64_t, int, uint32_t *, hipStream_t);
+uint64_t os_status_words(uint64_t n);
+uint64_t os_scratch_words(uint64_t n);
+bool os_sort_keys(uint64_t *keys, uint64_t *alt, uint64_t n, int bb, uint32_t *scratch, uint64_t *status,
+                  uint32_t &epoch, hipStream_t st);
 void launch_tx_masked(const TxInfo *, uint32_t, const uint64_t *, uint8_t *, hipStream_t);
 void launch_near_fill(bool, const TxInfo *, uint32_t, const uint8_t *, const uint64_t *, const uint64_t *,
                       const uint64_t *, uint64_t *, uint64_t, unsigned long long *, hipStream_t);
@@ -339,6 +343,11 @@ struct rc_engine {
     DBuf<uint64_t> d_rtmask;
     uint64_t rseed_cap = 0, n_rseeds = 0;
     DBuf<uint64_t> d_ent, d_ent2;   // (k-mer << 32 | position), unsorted / sorted
+    // the index sort's scratch (sort.hip): digit histograms + tile counters,
+    // the look-back table (zeroed when allocated; tagged by pass epoch)
+    DBuf<uint32_t> d_sort_scratch;
+    DBuf<uint64_t> d_sort_status;
+    uint32_t sort_epoch = 0;
     DBuf<uint32_t> d_bucket, d_pos_tx;
     DBuf<uint64_t> d_sample_pos, d_txstart, d_kpos_rel, d_dmask;
     DBuf<uint32_t> d_dust_scratch;
@@ -1007,10 +1016,34 @@ static int load_tile(rc_engine *e, int ti)
 static int sort_index(rc_engine *e, DBuf<uint64_t> &ent, DBuf<uint64_t> &ent2, uint64_t npos, unsigned bb, int extra,
                       DBuf<uint32_t> &bucket, int &bits_out)
 {
-    size_t tmp = 0;
-    HIPCHK(rocprim::radix_sort_keys(nullptr, tmp, ent.p, ent2.p, (size_t)npos, bb, 64u, e->st));
-    CHK(e->d_tmp.ensure(tmp));
-    HIPCHK(rocprim::radix_sort_keys(e->d_tmp.p, tmp, ent.p, ent2.p, (size_t)npos, bb, 64u, e->st));
+    static const bool lib = getenv("RC_SORT") && !strcmp(getenv("RC_SORT"), "rocprim");
+    if (lib) {   // A/B only: rocPRIM's onesweep
+        // (rocPRIM sorts up to 2^20 items with a merge sort that did not keep
+        // the input order for a partial bit range: there, all 64 bits -- the
+        // same result, positions are unique)
+        const unsigned lb = bb == 32 && npos <= (1ull << 20) ? 0u : bb;
+        size_t tmp = 0;
+        HIPCHK(rocprim::radix_sort_keys(nullptr, tmp, ent.p, ent2.p, (size_t)npos, lb, 64u, e->st));
+        CHK(e->d_tmp.ensure(tmp));
+        HIPCHK(rocprim::radix_sort_keys(e->d_tmp.p, tmp, ent.p, ent2.p, (size_t)npos, lb, 64u, e->st));
+    } else if (npos) {
+        // sort.hip: 8-bit LSD passes ping-ponging between the two buffers;
+        // the result must end in ent2
+        if (npos > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "more than 2^32 index entries");
+        CHK(e->d_sort_scratch.ensure(os_scratch_words(npos)));
+        const uint64_t words = os_status_words(npos);
+        if (e->d_sort_status.cap < words) {
+            CHK(e->d_sort_status.ensure(words));
+            HIPCHK(hipMemsetAsync(e->d_sort_status.p, 0, words * sizeof(uint64_t), e->st));
+        }
+        const bool in_alt = os_sort_keys(ent.p, ent2.p, npos, (int)bb, e->d_sort_scratch.p, e->d_sort_status.p,
+                                         e->sort_epoch, e->st);
+        HIPCHK(hipGetLastError());
+        if (!in_alt) {
+            std::swap(ent.p, ent2.p);
+            std::swap(ent.cap, ent2.cap);
+        }
+    }
     const char *ibv = getenv("RC_INDEX_BITS_MAX");
     const int bmax = ibv ? std::max(16, std::min(30, atoi(ibv))) : 28;
     int bits = 16;
@@ -1050,11 +1083,8 @@ static int build_index_of(rc_engine *e, const TxInfo *txl, uint32_t n_tx, uint64
                                offs, ent.p, e->st);
     if (after_fill) CHK(after_fill());
     // sort on the k-mer (bits 32..63); the fill order is position order and the
-    // onesweep radix sort is stable, so positions stay ascending per k-mer.
-    // rocPRIM sorts up to 2^20 items with a merge sort that did not keep that
-    // order for a partial bit range: there, sort all 64 bits (same result,
-    // positions are unique).
-    CHK(sort_index(e, ent, ent2, npos, npos <= (1ull << 20) ? 0u : 32u, 0, bucket, bits_out));
+    // radix sort is stable, so positions stay ascending per k-mer.
+    CHK(sort_index(e, ent, ent2, npos, 32u, 0, bucket, bits_out));
     n_out = npos;
     return RC_OK;
 }
