@@ -1013,6 +1013,10 @@ __device__ __forceinline__ void extend_seed(const uint32_t *QO, const uint32_t *
     }
 }
 
+// cand_box record of a first-seed extension: status (0 done, -1 deferred),
+// right (score, i, j, d, gap state), left (same)
+enum { FX_STATUS = 0, FX_R = 1, FX_L = 6 };
+
 // Shared searches: one directed search of a candidate on one wave, in the
 // forward search's coordinates (query = the lower sample, which is also the
 // first role of spec 4b). The search's seeds (dbit) are taken in ITS order
@@ -1026,9 +1030,25 @@ __device__ __forceinline__ void process_search(const uint32_t *QO, const uint32_
                                                int X, int lane, uint32_t dbit, int strand, int &bqa, int &bqb,
                                                int &bsa, int &bsb, int &bsc, int &bd, int &bg, int &bo, int &bni,
                                                int &nh, uint32_t &steps, uint32_t &exts, uint32_t &edges,
-                                               uint32_t &capped, bool swap)
+                                               uint32_t &capped, bool swap, const int *fx = nullptr, int e = -1)
 {
     nh = 0;
+    if (fx) {
+        // the search's first seed (always extended, spec 3) was extended by
+        // the row kernel: its HSP as first_finish_kernel builds it
+        constexpr int OBIT = 13, GMASK = 8191;
+        const GSeed s0 = sd[e];
+        const int x = (int)s0.x, y = (int)s0.y, len = (int)(s0.len & SEED_LEN);
+        const int rsc = fx[FX_R], ri = fx[FX_R + 1], rj = fx[FX_R + 2], rd = fx[FX_R + 3], rgo = fx[FX_R + 4];
+        const int lsc = fx[FX_L], lI = fx[FX_L + 1], lJ = fx[FX_L + 2], ld = fx[FX_L + 3], lgo = fx[FX_L + 4];
+        if (lane == 0) {
+            bqa = x - lI; bqb = x + len + ri; bsa = y - lJ; bsb = y + len + rj;
+            bsc = lsc + 2 * len + rsc;
+            bd = ld + rd; bg = (lgo & GMASK) + (rgo & GMASK); bo = ((lgo >> OBIT) & GMASK) + ((rgo >> OBIT) & GMASK);
+            bni = len + (lI + lJ - 2 * ld + (lgo & GMASK)) / 2 + (ri + rj - 2 * rd + (rgo & GMASK)) / 2;
+        }
+        nh = 1;
+    }
     for (;;) {
         unsigned long long bk = ~0ull;
         int bi = 0;
@@ -1196,6 +1216,19 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
         const bool swap = qt.sample > st.sample;
         // shared searches: this work item is one directed search of the candidate
         const uint32_t dbit = P.dir ? SEED_R : SEED_F;
+        // its first seed's extension from the row kernel, when that finished
+        // (a search deferred for a seed outside the first box, not for a
+        // sub-band overflow): the search starts with that HSP
+        const int *fx0 = nullptr;
+        int e0 = -1;
+        if (P.share && P.reuse_first) {
+            const bool second = P.dir == 1 && cd.e1 != SEED_NONE;
+            const int *fx = (second ? P.cand_box2 : P.cand_box) + ci * BOX_REC;
+            if (fx[FX_STATUS] >= 0) {
+                fx0 = fx;
+                e0 = (int)(second ? cd.e1 : cd.e0);
+            }
+        }
         if (Lq + SPAD <= STAGE_BASES && Lt + SPAD <= STAGE_BASES) {
             uint64_t *QO = stg[wid][0], *TF = stg[wid][1];
             stage_seq(QO, QA, q0, Lq, lane);
@@ -1213,7 +1246,7 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
                 process_search<AMB, uint32_t>(reinterpret_cast<const uint32_t *>(QO), QOM, (uint32_t)SPAD,
                                               reinterpret_cast<const uint32_t *>(TF), TFM, (uint32_t)SPAD, Lq, Lt,
                                               sd, ns, P.xdrop, lane, dbit, strand, bqa, bqb, bsa, bsb, bsc, bd, bg,
-                                              bo, bni, nh, steps, exts, edges, capped, swap);
+                                              bo, bni, nh, steps, exts, edges, capped, swap, fx0, e0);
             else
                 process_candidate<AMB, uint32_t>(reinterpret_cast<const uint32_t *>(QO), QOM, (uint32_t)SPAD,
                                                  reinterpret_cast<const uint32_t *>(TF), TFM, (uint32_t)SPAD, Lq, Lt,
@@ -1225,7 +1258,7 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
                                          reinterpret_cast<const uint32_t *>(db.F),
                                          reinterpret_cast<const uint32_t *>(db.AF), (int64_t)st.start, Lq, Lt, sd,
                                          ns, P.xdrop, lane, dbit, strand, bqa, bqb, bsa, bsb, bsc, bd, bg, bo, bni,
-                                         nh, steps, exts, edges, capped, swap);
+                                         nh, steps, exts, edges, capped, swap, fx0, e0);
         } else {
             // global arrays carry two zero words in front, so backward windows
             // of the first transcript stay in bounds (positions may go to -32)
@@ -1552,10 +1585,6 @@ enum { RS_LEND, RS_SHARD, RS_SHN, RS_N };
 enum { A_FETCH, A_SLIDE, A_RDONE, A_LDONE, A_ABORT, A_DONE, A_STEP_R, A_STEP_L };
 // bl of a row whose best record is parked in its LDS bookkeeping (a window slide)
 constexpr int BL_PARKED = -64;
-// cand_box record of a first-seed extension: status (0 done, -1 deferred),
-// right (score, i, j, d, gap state), left (same)
-enum { FX_STATUS = 0, FX_R = 1, FX_L = 6 };
-
 // The row kernel's arguments, one struct so that the kernarg segment is laid
 // out as it.
 struct RowArgs {
@@ -2411,12 +2440,12 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
         // directed search checked (or listed for extend_kernel) on its own
         // each 32-lane pass is followed by a 64-lane pass (the spec's whole
         // band) over the candidates whose live diagonals outgrew the sliding
-        // sub-band, RC_WIDE=1 (else they go to the one-wave kernel)
-        // (measured at C3v: 987 vs 903 ms per step -- most of the overflowing
-        // candidates have seeds outside the first box and go to the one-wave
-        // kernel anyway -- so off unless RC_WIDE=1)
+        // sub-band (RC_WIDE=0: they go to the one-wave kernel whole). Most of
+        // them also have seeds outside the first box; extend_kernel starts
+        // those searches from the first seed's HSP (P.reuse_first), so the
+        // 64-lane pass is not redone: C3v 806 vs 875 ms per step.
         const char *wv = getenv("RC_WIDE");
-        const bool widep = wv && atoi(wv) == 1 && P.wide0;
+        const bool widep = !(wv && atoi(wv) == 0) && P.wide0;
         auto wide_pass = [&](const ExtParams &B, uint32_t *lst, unsigned long long *lst_n, unsigned long long *wk) {
             ExtParams V = B;
             V.list = lst;

@@ -254,6 +254,9 @@ struct ExtParams {
     unsigned long long *wide_n;
     uint32_t *wide0, *wide1;            // the e0 pass's and the e1 pass's lists
     unsigned long long *wide0_n, *wide1_n, *work_w0, *work_w1;
+    // extend_kernel (shared searches): start a search from its first seed's
+    // row-kernel result (cand_box / cand_box2) when it has one
+    int32_t reuse_first;
 };
 
 // DHsp.strand carries, besides the strand (bit 0), the direction flags of a

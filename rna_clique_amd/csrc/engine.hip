@@ -1688,6 +1688,8 @@ static int align_tile(rc_engine *e, int ti)
         {
             const char *cv = getenv("RC_ROW_CHUNK");
             X.chunk = cv ? atoi(cv) : 8;
+            const char *rv = getenv("RC_REUSE");   // 0: extend_kernel redoes every search's first seed
+            X.reuse_first = rv ? atoi(rv) : 1;
         }
         HIPCHK(hipEventRecord(e->ev[10], e->st));
         {

@@ -8,3 +8,5 @@ mkdir -p bin
   scripts/micro/dust_micro.hip rna_clique_amd/csrc/dust.hip
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fgpu-rdc -DRC_DUST_PROF -DRC_DUST_NO_B -o bin/dust_micro_noB \
   scripts/micro/dust_micro.hip rna_clique_amd/csrc/dust.hip
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fgpu-rdc -o bin/dust_micro_plain \
+  scripts/micro/dust_micro.hip rna_clique_amd/csrc/dust.hip

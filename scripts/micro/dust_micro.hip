@@ -23,6 +23,14 @@ int main(int argc, char **argv)
     for (auto &v : h) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; v = x; }
     std::vector<uint64_t> tb((total >> 6) + 4, 0);
     for (uint64_t p = 0; p < total; p += 1000) { const uint64_t q = p + 64; tb[q >> 6] |= 1ull << (q & 63); }
+    // argv[3]: fraction of the 1000-base transcripts ending in a 30-base poly-A tail (as C3v)
+    const double pa = argc > 3 ? atof(argv[3]) : 0.0;
+    uint64_t y = 12345;
+    for (uint64_t p = 64; p + 1000 <= total; p += 1000) {
+        y ^= y << 13; y ^= y >> 7; y ^= y << 17;
+        if ((double)(y % 1000000) / 1e6 >= pa) continue;
+        for (uint64_t u = p + 1000 - 30; u < p + 1000; u++) h[u >> 5] &= ~(3ull << (2 * (u & 31)));
+    }
     uint64_t *F, *TB, *M, *E; uint32_t *S;
     hipMalloc(&F, nw * 8); hipMalloc(&TB, tb.size() * 8); hipMalloc(&M, tb.size() * 8);
     const uint32_t blocks = argc > 2 ? (uint32_t)atoi(argv[2]) : 256 * 10;
