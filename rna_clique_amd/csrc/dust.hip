@@ -37,11 +37,8 @@ namespace rcg {
 constexpr int DW = 64;          // lanes per block (one wave)
 constexpr int DCHUNK = 256;     // bases per lane
 constexpr int DWIN_MAX = 64;    // longest DUST window the kernel supports
-constexpr int DEVCAP = 32;  // events a lane holds before it runs them (phase B) in the middle of its scan
+constexpr int DEVCAP = 64;  // events a lane holds (phase B runs between scan blocks when one nears this)
 
-#ifdef RC_DUST_PROF
-__device__ unsigned long long g_dust_prof[4];   // cycles of phase A, phase B; events; B iterations (microbenchmarks)
-#endif
 
 __device__ __forceinline__ void dust_mark(uint64_t *mask, uint64_t a, uint64_t b)
 {
@@ -79,8 +76,39 @@ __device__ __forceinline__ uint64_t even_bits(uint64_t x)
 }
 
 #ifndef RC_DUST_MINW
-#define RC_DUST_MINW 7   // waves per SIMD the registers must allow: 7 measured best (21.4 ms at 5 waves, 20.1 at 7, 21.1 at 8)
+#define RC_DUST_MINW 5   // waves per SIMD the registers must allow (r03: 22.7 ms at 5, 24.7 at 6, 25.5 at 7 on 1.6 Gbp random)
 #endif
+#ifndef RC_DUST_HEAVY
+#define RC_DUST_HEAVY 12   // an event whose suffix loop runs more starts than this goes to the whole wave
+#endif
+
+// wave-uniform 64-bit lane read
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l)
+{
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+
+// the number of triplets ending 0 .. a - 1 bases before j that equal the one
+// ending a back, from the window's bit planes (bit e: the base e back)
+__device__ __forceinline__ int dust_later(uint64_t Q0, uint64_t Q1, int a)
+{
+    const uint64_t t0 = Q0 >> a, t1 = Q1 >> a;
+    const int bl = (int)((t0 & 1) | ((t1 & 1) << 1)), bm = (int)(((t0 >> 1) & 1) | (t1 & 2)),
+              bf = (int)(((t0 >> 2) & 1) | ((t1 >> 1) & 2));
+    const uint64_t eq = (base_eq(Q0, Q1, bf) >> 2) & (base_eq(Q0, Q1, bm) >> 1) & base_eq(Q0, Q1, bl);
+    return a ? __builtin_popcountll(eq & bit_range(0, a - 1)) : 0;
+}
+
+// (n, d) <- the larger ratio of (n, d) and (m, e) (ties keep (n, d))
+__device__ __forceinline__ void ratio_max(int &n, int &d, int m, int e)
+{
+    if (m * d > n * e) {
+        n = m;
+        d = e;
+    }
+}
+
 template <bool AMB>
 __global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t total, uint64_t nwords, const uint64_t *__restrict__ F,
                                                   const uint64_t *__restrict__ AF,
@@ -90,18 +118,26 @@ __global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t total, 
 {
     const int lane = threadIdx.x;
     const int need = (2 * T) / 10;   // occurrences before a new one that break the L-suffix bound
-    uint32_t *slot = scratch + ((size_t)blockIdx.x * DW + lane) * DWIN_MAX;   // [run offset of the start & 63]
+    uint32_t *const slot0 = scratch + (size_t)blockIdx.x * DW * DWIN_MAX;   // [lane][run offset of a start & 63]
+    uint32_t *const slot = slot0 + lane * DWIN_MAX;
+    // the lane's triplet counts over the window (64 bytes, lane stride 68:
+    // spread over the LDS banks): the window score moves by the counts of the
+    // entering and the leaving triplet, so the bit-plane match of a triplet
+    // is only needed where the L-suffix bound may move
+    __shared__ uint32_t cnt_lds[DW * 17];
+    uint8_t *const C = reinterpret_cast<uint8_t *>(cnt_lds + 17 * lane);
     uint64_t *ev = evs + (size_t)blockIdx.x * DEVCAP * 3 * DW + lane;         // [event][field][lane]
     const uint64_t nchunk = (total + DCHUNK - 1) / DCHUNK;
     auto word = [&](uint64_t w) -> uint64_t { return w < nwords ? F[w] : 0ull; };
     auto aword = [&](uint64_t w) -> uint64_t { return AMB && w < nwords ? AF[w] : 0ull; };
-    for (uint64_t ch = (uint64_t)blockIdx.x * DW + lane; ch < nchunk; ch += (uint64_t)gridDim.x * DW) {
-        const uint64_t c0 = ch * DCHUNK, c1 = min(c0 + DCHUNK, total);
-        const uint64_t lim = min(c1 + (uint64_t)W, total);   // the scan's reach
-        // ---------------- B: the lane's events, in order (state kept across runs of B) ----------------
-#ifdef RC_DUST_PROF
-        unsigned long long its = 0, tb = 0;
-#endif
+    // wave-uniform chunk rounds (the whole wave meets in phase B); a lane past
+    // the last chunk scans nothing
+    for (uint64_t chb = (uint64_t)blockIdx.x * DW; chb < nchunk; chb += (uint64_t)gridDim.x * DW) {
+        const uint64_t ch = chb + (uint64_t)lane;
+        const bool have = ch < nchunk;
+        const uint64_t c0 = have ? ch * DCHUNK : total, c1 = have ? min(c0 + DCHUNK, total) : total;
+        const uint64_t lim = have ? min(c1 + (uint64_t)W, total) : total;   // the scan's reach
+        // ---------------- B: the events, in order per lane (state kept across runs of B) ----------------
         uint64_t set = 0, prs = ~0ull;   // slots holding a perfect interval; their run's start
         int pw = 0;                      // window start (run offset) of the previous event
         auto finalize = [&](uint64_t keep_from) {   // the perfect intervals starting before keep_from (run offset) are final
@@ -116,20 +152,12 @@ __global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t total, 
                 set &= ~(1ull << k);
             }
         };
-        int nev = 0;
-        auto run_events = [&]() {
-#ifdef RC_DUST_PROF
-        const unsigned long long tq = __builtin_readcyclecounter();
-#endif
-        // an event: (j, rw, L, rel) and the bit planes of its window
-        uint64_t nx = nev ? ev[0] : 0ull, nq0 = nev ? ev[DW] : 0ull, nq1 = nev ? ev[2 * DW] : 0ull;
-        for (int e = 0; e < nev; e++) {
-            const uint64_t x = nx, Q0 = nq0, Q1 = nq1;
-            if (e + 1 < nev) {   // the next event's loads in flight meanwhile
-                nx = ev[(size_t)(3 * e + 3) * DW];
-                nq0 = ev[(size_t)(3 * e + 4) * DW];
-                nq1 = ev[(size_t)(3 * e + 5) * DW];
-            }
+        // an event: x = j | rw << 15 | L << 9 | rel (fields below), the bit
+        // planes Q0/Q1 of its window (bit a = the base a positions before j).
+        // The suffixes longer than the L-suffix, shortest first, against the
+        // best ratio of the perfect intervals they contain (align_oracle.c
+        // dust_run). One lane on its own event:
+        auto light_event = [&](uint64_t x, uint64_t Q0, uint64_t Q1) {
             const int rel = (int)(x & 0x1FF), Lq = (int)((x >> 9) & 63), rwe = (int)((x >> 15) & 0x7FF);
             const int32_t j = (int32_t)(x >> 26), pt = j - 2, wstart = max(j + 1 - W, 0), Lst = pt + 1 - Lq;
             const uint64_t r0 = c0 + (uint64_t)rel - (uint64_t)j;   // the run's start
@@ -140,21 +168,8 @@ __global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t total, 
                 finalize((uint64_t)wstart);
             }
             pw = wstart;
-            // Q0/Q1: bit a = the base a positions before j. The triplet starting
-            // at st ends pt - st back; those starting later in (st, pt] end
-            // 0 .. pt - st - 1 back.
-            auto later = [&](int32_t st) -> int {
-                const int a = pt - st;   // the triplet's last base is a back, its first a + 2
-                const uint64_t t0 = Q0 >> a, t1 = Q1 >> a;
-                const int bl = (int)((t0 & 1) | ((t1 & 1) << 1)), bm = (int)(((t0 >> 1) & 1) | (t1 & 2)),
-                          bf = (int)(((t0 >> 2) & 1) | ((t1 >> 1) & 2));
-                // bit e: the triplet ending e back equals it (masks from the codes:
-                // a select among precomputed masks would be an indexed array, i.e. scratch)
-                const uint64_t eq = (base_eq(Q0, Q1, bf) >> 2) & (base_eq(Q0, Q1, bm) >> 1) & base_eq(Q0, Q1, bl);
-                return a ? __builtin_popcountll(eq & bit_range(0, a - 1)) : 0;
-            };
             int r = 0;
-            for (int32_t st = Lst; st <= pt; st++) r += later(st);   // the L-suffix's score
+            for (int32_t st = Lst; st <= pt; st++) r += dust_later(Q0, Q1, pt - st);   // the L-suffix's score
             int mr = 0, ml = 0;
             {   // best ratio of the perfect intervals inside the L-suffix
                 uint64_t m = set;
@@ -170,10 +185,7 @@ __global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t total, 
             for (int32_t st = Lst - 1; st >= wstart; st--) {
                 const int l = pt - st;
                 if (T * l >= 10 * rwe) break;   // no longer suffix can pass the level
-#ifdef RC_DUST_PROF
-                its++;
-#endif
-                r += later(st);
+                r += dust_later(Q0, Q1, l);
                 const int k = st & 63;
                 const bool has = (set >> k) & 1ull;
                 const uint32_t s = has ? slot[k] : 0u;
@@ -190,124 +202,232 @@ __global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t total, 
                     ml = l;
                 }
             }
-#ifdef RC_DUST_PROF
-            its += (unsigned long long)Lq;
-#endif
-        }
-        nev = 0;
-#ifdef RC_DUST_PROF
-        tb += __builtin_readcyclecounter() - tq;
-#endif
+        };
+        // The whole wave on lane o's event (wave-uniform x, Q0, Q1): lane k
+        // holds the owner's slot k; lane i tries the suffix starting at
+        // Lst - 1 - i. Its score is a prefix sum over the lanes; the best ratio
+        // it is compared with -- the L-suffix's perfect intervals, then every
+        // shorter suffix's slot and every shorter suffix that passes the
+        // level (a passing one that does not beat the running best leaves it
+        // unchanged) -- is an exclusive max-scan: the sequential loop's
+        // result, without its walk over up to 62 starts.
+        auto coop_event = [&](int o, uint64_t x, uint64_t Q0, uint64_t Q1) {
+            const int rel = (int)(x & 0x1FF), Lq = (int)((x >> 9) & 63), rwe = (int)((x >> 15) & 0x7FF);
+            const int32_t j = (int32_t)(x >> 26), pt = j - 2, wstart = max(j + 1 - W, 0), Lst = pt + 1 - Lq;
+            const uint64_t oc0 = rl64(c0, o), oc1 = rl64(c1, o);
+            uint64_t oset = rl64(set, o), oprs = rl64(prs, o);
+            const int opw = __builtin_amdgcn_readlane(pw, o);
+            uint32_t *const os = slot0 + o * DWIN_MAX;
+            const uint64_t r0 = oc0 + (uint64_t)rel - (uint64_t)j;
+            bool mine = (oset >> lane) & 1ull;
+            uint32_t sv = mine ? os[lane] : 0u;
+            // finalize: the owner's intervals that start before the window (all
+            // of them on a new run)
+            if (mine) {
+                const uint64_t a = (uint64_t)opw + (uint64_t)((lane - opw) & 63);
+                if (r0 != oprs || a < (uint64_t)wstart) {
+                    if (oprs + a < oc1) dust_mark(mask, oprs + a, oprs + a + ((sv >> 20) & 0x1FFu));
+                    mine = false;
+                }
+            }
+            oset = __ballot(mine);
+            oprs = r0;
+            // the L-suffix's score: triplets ending a = 0 .. Lq - 1 back
+            int v = lane < Lq ? dust_later(Q0, Q1, lane) : 0;
+#pragma unroll
+            for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d);
+            const int rL = v;
+            // the best ratio inside the L-suffix (slots starting at or after Lst)
+            int mn = 0, md = 1;
+            {
+                const int startk = wstart + ((lane - wstart) & 63);
+                int n = 0, dd = 1;
+                if (mine && startk >= Lst) {
+                    n = (int)(sv & 0xFFF);
+                    dd = (int)((sv >> 12) & 0xFF);
+                }
+#pragma unroll
+                for (int d = 32; d; d >>= 1) {
+                    const int n2 = __shfl_xor(n, d), d2 = __shfl_xor(dd, d);
+                    ratio_max(n, dd, n2, d2);
+                }
+                mn = n;
+                md = dd;
+            }
+            // lane i: the suffix starting at st = Lst - 1 - i, l = pt - st
+            const int32_t st = Lst - 1 - lane;
+            const int l = Lq + lane;
+            const bool act = st >= wstart && T * l < 10 * rwe;   // a prefix of the lanes (the loop's break)
+            int r = act ? dust_later(Q0, Q1, l) : 0;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int y = __shfl_up(r, d);
+                if (lane >= d) r += y;
+            }
+            r += rL;
+            const int ki = st & 63;
+            const uint32_t si = (uint32_t)__shfl((int)sv, ki);
+            const bool has = act && ((oset >> ki) & 1ull);
+            const int sr = (int)(si & 0xFFF), sl = (int)((si >> 12) & 0xFF);
+            const bool pass = act && r * 10 > T * l;
+            int vn = 0, vd = 1;
+            if (has) { vn = sr; vd = sl; }
+            if (pass) ratio_max(vn, vd, r, l);
+            // exclusive max-scan of (vn, vd), seeded with the L-suffix's best
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int n2 = __shfl_up(vn, d), d2 = __shfl_up(vd, d);
+                if (lane >= d) ratio_max(vn, vd, n2, d2);
+            }
+            int en = __shfl_up(vn, 1), ed = __shfl_up(vd, 1);
+            if (lane == 0) { en = 0; ed = 1; }
+            ratio_max(en, ed, mn, md);
+            if (has) ratio_max(en, ed, sr, sl);
+            const bool perfect = pass && r * ed >= en * l;
+            if (perfect) {
+                const int end = j + 1 - st;
+                int nr = r, nl = l;
+                if (has && !(r * sl > sr * l)) { nr = sr; nl = sl; }
+                const int ne = has ? max(end, (int)((si >> 20) & 0x1FF)) : end;
+                os[ki] = ((uint32_t)ne << 20) | ((uint32_t)nl << 12) | (uint32_t)nr;
+            }
+            // lane i's slot is (Lst - 1 - i) & 63: the ballot reversed, rotated by Lst
+            const uint64_t rv = __builtin_bitreverse64(__ballot(perfect));
+            const int sh = Lst & 63;
+            oset |= sh ? (rv << sh) | (rv >> (64 - sh)) : rv;
+            if (lane == o) {
+                set = oset;
+                prs = oprs;
+                pw = wstart;
+            }
+        };
+        int nev = 0;
+        // every lane's events (wave-uniform call): round e runs each lane's
+        // event e -- alone when short, by the whole wave one owner at a time
+        // when its suffix loop is long (low-complexity runs: poly-A tails)
+        auto run_events = [&]() {
+            for (int e = 0;; e++) {
+                const bool pend = e < nev;
+                if (!__ballot(pend)) break;
+                uint64_t x = 0, Q0 = 0, Q1 = 0;
+                bool heavy = false;
+                if (pend) {
+                    x = ev[(size_t)(3 * e) * DW];
+                    Q0 = ev[(size_t)(3 * e + 1) * DW];
+                    Q1 = ev[(size_t)(3 * e + 2) * DW];
+                    const int Lq = (int)((x >> 9) & 63), rwe = (int)((x >> 15) & 0x7FF);
+                    const int32_t j = (int32_t)(x >> 26), wstart = max(j + 1 - W, 0), Lst = j - 1 - Lq;
+                    const int lbrk = (10 * rwe + T - 1) / T;   // the first l the loop breaks at
+                    heavy = min(Lst - wstart, lbrk - Lq) > RC_DUST_HEAVY;
+                }
+                if (pend && !heavy) light_event(x, Q0, Q1);
+                for (uint64_t hm = __ballot(pend && heavy); hm; hm &= hm - 1) {
+                    const int o = __builtin_ctzll(hm);
+                    coop_event(o, rl64(x, o), rl64(Q0, o), rl64(Q1, o));
+                }
+            }
+            nev = 0;
         };
         // ---------------- A: the window scan over [c0, lim) ----------------
-#ifdef RC_DUST_PROF
-        const unsigned long long tp0 = __builtin_readcyclecounter();
-#endif
         // The scan goes a packed word (32 bases) at a time: the words of the
         // next block are loaded at the top of a block and only rotated in at
         // its end, so their latency hides behind 32 steps (a load rotated per
-        // step would make every step wait for it).
+        // step would make every step wait for it). Blocks are wave-uniform
+        // rounds, so phase B can run between them when a lane's events near
+        // the buffer's capacity.
         const uint64_t w0 = c0 >> 5;   // c0 is a multiple of 64
         const uint64_t t0i = c0 >> 6, tmax = (total >> 6) + 1;
-        uint64_t wpp = 0, wp = 0, wc = word(w0), ac = aword(w0), tc = txstart[t0i];
+        uint64_t wpp = 0, wp = 0, wc = have ? word(w0) : 0ull, ac = have ? aword(w0) : 0ull,
+                 tc = have ? txstart[t0i] : 0ull;
         const int o = 66 - W;   // the trailing cursor's first base in the 96-base window (wpp, wp, wc)
         uint64_t P0 = 0, P1 = 0;   // bit planes of the last 64 bases, bit a = a bases back
-        bool in_run = false, done = false;
+        bool in_run = false, done = !have;
         int nb = 0, tri = 0, tri2 = 0, rw = 0, Lst = 0;
-        for (uint64_t k = 0; !done && c0 + 32 * k < lim; k++) {
-            const uint64_t wn = word(w0 + k + 1), an = aword(w0 + k + 1);
-            const uint64_t ti = t0i + ((k + 1) >> 1);
-            const uint64_t tn = ti <= tmax ? txstart[ti] : 0ull;
-            // the trailing bases of this block (32 k + i - W + 2) and its transcript-start bits
-            const uint64_t tw = o < 32 ? (wpp >> (2 * o)) | (wp << (64 - 2 * o))
-                                       : (o == 32 ? wp : (wp >> (2 * (o - 32))) | (wc << (64 - 2 * (o - 32))));
-            const uint32_t txb = (uint32_t)(tc >> (32 * (k & 1)));
-            for (int i = 0; i < 32; i++) {
-                const uint64_t rel = 32 * k + (uint64_t)i;
-                const uint64_t u = c0 + rel;
-                if (u >= lim) {
-                    done = true;
-                    break;
-                }
-                const bool amb = AMB && ((ac >> (2 * i)) & 3u);
-                const int b = (int)((wc >> (2 * i)) & 3u);
-                // the trailing cursor: the triplet that leaves the window starts at u - W
-                if ((int64_t)rel - W + 2 >= 0) tri2 = ((tri2 << 2) | (int)((tw >> (2 * i)) & 3u)) & 63;
-                if (in_run && (amb || ((txb >> i) & 1u))) in_run = false;   // ambiguous base or next transcript
-                if (amb) {
-                    if (u >= c1) {
+        for (uint64_t k = 0;; k++) {
+            if (!done && c0 + 32 * k >= lim) done = true;
+            if (!__ballot(!done)) break;
+            if (!done) {
+                const uint64_t wn = word(w0 + k + 1), an = aword(w0 + k + 1);
+                const uint64_t ti = t0i + ((k + 1) >> 1);
+                const uint64_t tn = ti <= tmax ? txstart[ti] : 0ull;
+                // the trailing bases of this block (32 k + i - W + 2) and its transcript-start bits
+                const uint64_t tw = o < 32 ? (wpp >> (2 * o)) | (wp << (64 - 2 * o))
+                                           : (o == 32 ? wp : (wp >> (2 * (o - 32))) | (wc << (64 - 2 * (o - 32))));
+                const uint32_t txb = (uint32_t)(tc >> (32 * (k & 1)));
+                for (int i = 0; i < 32; i++) {
+                    const uint64_t rel = 32 * k + (uint64_t)i;
+                    const uint64_t u = c0 + rel;
+                    if (u >= lim) {
                         done = true;
                         break;
                     }
-                    continue;
-                }
-                if (!in_run) {
-                    if (u >= c1) {   // runs starting past the chunk are the next lane's
-                        done = true;
-                        break;
+                    const bool amb = AMB && ((ac >> (2 * i)) & 3u);
+                    const int b = (int)((wc >> (2 * i)) & 3u);
+                    // the trailing cursor: the triplet that leaves the window starts at u - W
+                    if ((int64_t)rel - W + 2 >= 0) tri2 = ((tri2 << 2) | (int)((tw >> (2 * i)) & 3u)) & 63;
+                    if (in_run && (amb || ((txb >> i) & 1u))) in_run = false;   // ambiguous base or next transcript
+                    if (amb) {
+                        if (u >= c1) {
+                            done = true;
+                            break;
+                        }
+                        continue;
                     }
-                    in_run = true;
-                    nb = rw = Lst = 0;
+                    if (!in_run) {
+                        if (u >= c1) {   // runs starting past the chunk are the next lane's
+                            done = true;
+                            break;
+                        }
+                        in_run = true;
+                        nb = rw = Lst = 0;
+                        for (int q = 0; q < 16; q++) cnt_lds[17 * lane + q] = 0u;
+                    }
+                    nb++;
+                    tri = ((tri << 2) | b) & 63;
+                    P0 = (P0 << 1) | (uint64_t)(b & 1);
+                    P1 = (P1 << 1) | (uint64_t)(b >> 1);
+                    if (nb < 3) continue;
+                    const int32_t j = nb - 1;        // run offset of u
+                    const int32_t pt = j - 2;        // start of the new triplet
+                    const int32_t wstart = max(j + 1 - W, 0);
+                    if (j >= W) {   // the leaving triplet (start j - W): its partners are its other copies
+                        const int c2 = (int)C[tri2] - 1;
+                        C[tri2] = (uint8_t)c2;
+                        rw -= c2;
+                    }
+                    const int cw = (int)C[tri];   // the new triplet's copies in the window
+                    C[tri] = (uint8_t)(cw + 1);
+                    rw += cw;
+                    Lst = max(Lst, wstart);
+                    if (cw >= need) {   // the need-th previous occurrence (need-th lowest bit) is in the window
+                        // the window without the new triplet: the triplets ending
+                        // 1 .. W - 3 bases back that start in the run; bit e: the
+                        // triplet ending e back is the new one
+                        const uint64_t wm = bit_range(1, min(W - 3, j - 2));
+                        uint64_t m = (base_eq(P0, P1, tri >> 4) >> 2) & (base_eq(P0, P1, (tri >> 2) & 3) >> 1) &
+                                     base_eq(P0, P1, tri & 3) & wm;
+                        for (int q = 1; q < need; q++) m &= m - 1;
+                        const int p = need ? pt - (int)__builtin_ctzll(m) : pt;
+                        if (p >= Lst) Lst = p + 1;
+                    }
+                    if (rw * 10 <= (pt - Lst + 1) * T) continue;
+                    // rare: B tries the longer suffixes; event = j | rw | L | rel
+                    ev[(size_t)(3 * nev) * DW] = ((uint64_t)j << 26) | ((uint64_t)rw << 15) | ((uint64_t)(pt - Lst + 1) << 9) | rel;
+                    ev[(size_t)(3 * nev + 1) * DW] = P0;
+                    ev[(size_t)(3 * nev + 2) * DW] = P1;
+                    nev++;
                 }
-                nb++;
-                tri = ((tri << 2) | b) & 63;
-                P0 = (P0 << 1) | (uint64_t)(b & 1);
-                P1 = (P1 << 1) | (uint64_t)(b >> 1);
-                if (nb < 3) continue;
-                const int32_t j = nb - 1;        // run offset of u
-                const int32_t pt = j - 2;        // start of the new triplet
-                const int32_t wstart = max(j + 1 - W, 0);
-                // the window without the new triplet, after the leaving one (start
-                // j - W) is gone: the triplets ending 1 .. W - 3 bases back that
-                // start in the run. Bit e of trip(v): the triplet ending e back is v.
-                const uint64_t wm = bit_range(1, min(W - 3, j - 2));
-                auto trip = [&](int v) -> uint64_t {
-                    return (base_eq(P0, P1, v >> 4) >> 2) & (base_eq(P0, P1, (v >> 2) & 3) >> 1) & base_eq(P0, P1, v & 3);
-                };
-                if (j >= W) rw -= __builtin_popcountll(trip(tri2) & wm);   // its partners in the window
-                const uint64_t e3 = trip(tri) & wm;
-                const int cw = __builtin_popcountll(e3);
-                rw += cw;
-                Lst = max(Lst, wstart);
-                if (cw >= need) {   // the need-th previous occurrence (need-th lowest bit) is in the window
-                    uint64_t m = e3;
-                    for (int q = 1; q < need; q++) m &= m - 1;
-                    const int p = need ? pt - (int)__builtin_ctzll(m) : pt;
-                    if (p >= Lst) Lst = p + 1;
-                }
-                if (rw * 10 <= (pt - Lst + 1) * T) continue;
-                // rare: B tries the longer suffixes; event = j | rw | L | rel
-#ifndef RC_DUST_NO_B
-                ev[(size_t)(3 * nev) * DW] = ((uint64_t)j << 26) | ((uint64_t)rw << 15) | ((uint64_t)(pt - Lst + 1) << 9) | rel;
-                ev[(size_t)(3 * nev + 1) * DW] = P0;
-                ev[(size_t)(3 * nev + 2) * DW] = P1;
-                if (++nev == DEVCAP) run_events();
-#else
-                nev++;
-#endif
+                wpp = wp;
+                wp = wc;
+                wc = wn;
+                ac = an;
+                if (k & 1) tc = tn;
             }
-            wpp = wp;
-            wp = wc;
-            wc = wn;
-            ac = an;
-            if (k & 1) tc = tn;
+            // a block adds at most 32 events per lane
+            if (__ballot(nev > DEVCAP - 32)) run_events();
         }
-#ifdef RC_DUST_PROF
-        const unsigned long long tp1 = __builtin_readcyclecounter();
-#endif
-#ifndef RC_DUST_NO_B
         run_events();
-#endif
         finalize(~0ull);   // the last run's intervals (its end, or the scan's reach)
-#ifdef RC_DUST_PROF
-        const unsigned long long tp2 = __builtin_readcyclecounter();
-        if (lane == 0) {
-            atomicAdd(&g_dust_prof[0], tp1 - tp0);   // the scan (with any runs of B in it)
-            atomicAdd(&g_dust_prof[1], tp2 - tp1);   // the last run of B
-        }
-        atomicAdd(&g_dust_prof[3], its);
-        atomicAdd(&g_dust_prof[2], (unsigned long long)nev);
-#endif
     }
 }
 

@@ -9,9 +9,6 @@ void launch_dust(bool, uint64_t, const uint64_t *, const uint64_t *, const uint6
                  int, int, uint32_t *, uint64_t *, uint32_t, int, uint64_t *, hipStream_t);
 uint32_t dust_scratch_words(uint32_t);
 uint64_t dust_event_words(uint32_t);
-#ifdef RC_DUST_PROF
-extern __device__ unsigned long long g_dust_prof[4];
-#endif
 }
 using namespace rcg;
 int main(int argc, char **argv)
@@ -42,19 +39,11 @@ int main(int argc, char **argv)
     for (int it = 0; it < 3; it++) {
         hipMemset(M, 0, tb.size() * 8);
         hipEventRecord(a, 0);
-#ifdef RC_DUST_PROF
-        unsigned long long z[4] = {0, 0, 0, 0};
-        hipMemcpyToSymbol(HIP_SYMBOL(g_dust_prof), z, sizeof z);
-#endif
         launch_dust(false, total, F, nullptr, TB + 1, nullptr, 0, 20, 64, 1, S, E, blocks, 0, M + 1, 0);
         hipEventRecord(b, 0);
         hipEventSynchronize(b);
         float ms; hipEventElapsedTime(&ms, a, b);
         printf("dust %.3f ms (%s)\n", ms, hipGetErrorString(hipGetLastError()));
-#ifdef RC_DUST_PROF
-        hipMemcpyFromSymbol(z, HIP_SYMBOL(g_dust_prof), sizeof z);
-        printf("  wave-cycles A %.3g B %.3g  events %llu  iterations %llu\n", (double)z[0], (double)z[1], z[2], z[3]);
-#endif
     }
     std::vector<uint64_t> m(tb.size());
     hipMemcpy(m.data(), M, m.size() * 8, hipMemcpyDeviceToHost);
