@@ -2458,7 +2458,15 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
         W.which = 0;
         W.wide = widep ? P.wide0 : nullptr;
         W.wide_n = P.wide0_n;
-        if (amb) RC_LAUNCH_ROWS(true, 32, ROW_MIN_WAVES, W); else RC_LAUNCH_ROWS(false, 32, ROW_MIN_WAVES, W);
+        // RC_ROW_WIDTH=16: the sliding sub-band on 16-lane rows (4 candidates per wave)
+        auto rows_pass = [&](const ExtParams &B) {
+            if (rw == 16) {
+                if (amb) RC_LAUNCH_ROWS(true, 16, ROW_MIN_WAVES, B); else RC_LAUNCH_ROWS(false, 16, ROW_MIN_WAVES, B);
+            } else {
+                if (amb) RC_LAUNCH_ROWS(true, 32, ROW_MIN_WAVES, B); else RC_LAUNCH_ROWS(false, 32, ROW_MIN_WAVES, B);
+            }
+        };
+        rows_pass(W);
         if (widep) wide_pass(W, P.wide0, P.wide0_n, P.work_w0);
         ExtParams W2 = W;
         W2.which = 1;
@@ -2467,7 +2475,7 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
         W2.work = P.work3;
         W2.wide = widep ? P.wide1 : nullptr;
         W2.wide_n = P.wide1_n;
-        if (amb) RC_LAUNCH_ROWS(true, 32, ROW_MIN_WAVES, W2); else RC_LAUNCH_ROWS(false, 32, ROW_MIN_WAVES, W2);
+        rows_pass(W2);
         if (widep) wide_pass(W2, P.wide1, P.wide1_n, P.work_w1);
         W.list = nullptr;
         W.list_n = nullptr;
