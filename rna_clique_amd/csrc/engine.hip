@@ -43,7 +43,9 @@ void launch_bucket_fill(const uint64_t *, uint64_t, int, uint32_t *, hipStream_t
 uint64_t os_status_words(uint64_t n);
 uint64_t os_scratch_words(uint64_t n);
 bool os_sort_keys(uint64_t *keys, uint64_t *alt, uint64_t n, int bb, uint32_t *scratch, uint64_t *status,
-                  uint32_t &epoch, hipStream_t st);
+                  uint32_t &epoch, hipStream_t st, const std::function<void()> &after_prep, bool counted);
+void os_fill_hist(const TxInfo *tx, uint32_t n_tx, const uint64_t *F, const uint64_t *koff, uint64_t *ent,
+                  uint64_t n, uint32_t *scratch, hipStream_t st);
 void launch_tx_masked(const TxInfo *, uint32_t, const uint64_t *, uint8_t *, hipStream_t);
 void launch_near_fill(bool, const TxInfo *, uint32_t, const uint8_t *, const uint64_t *, const uint64_t *,
                       const uint64_t *, uint64_t *, uint64_t, unsigned long long *, hipStream_t);
@@ -1014,14 +1016,18 @@ static int load_tile(rc_engine *e, int ti)
 // 2^extra), at most 2^28 (RC_INDEX_BITS_MAX; 28 measured best at C3 -- a 1 GiB
 // table instead of 4 GiB, same seed-kernel time)
 static int sort_index(rc_engine *e, DBuf<uint64_t> &ent, DBuf<uint64_t> &ent2, uint64_t npos, unsigned bb, int extra,
-                      DBuf<uint32_t> &bucket, int &bits_out)
+                      DBuf<uint32_t> &bucket, int &bits_out, const std::function<int()> &after_prep = nullptr,
+                      bool counted = false)
 {
     static const bool lib = getenv("RC_SORT") && !strcmp(getenv("RC_SORT"), "rocprim");
+    bool prepped = false;   // after_prep runs exactly once, also for an empty index
     if (lib) {   // A/B only: rocPRIM's onesweep
         // (rocPRIM sorts up to 2^20 items with a merge sort that did not keep
         // the input order for a partial bit range: there, all 64 bits -- the
         // same result, positions are unique)
         const unsigned lb = bb == 32 && npos <= (1ull << 20) ? 0u : bb;
+        prepped = true;
+        if (after_prep) CHK(after_prep());
         size_t tmp = 0;
         HIPCHK(rocprim::radix_sort_keys(nullptr, tmp, ent.p, ent2.p, (size_t)npos, lb, 64u, e->st));
         CHK(e->d_tmp.ensure(tmp));
@@ -1036,14 +1042,20 @@ static int sort_index(rc_engine *e, DBuf<uint64_t> &ent, DBuf<uint64_t> &ent2, u
             CHK(e->d_sort_status.ensure(words));
             HIPCHK(hipMemsetAsync(e->d_sort_status.p, 0, words * sizeof(uint64_t), e->st));
         }
+        int prc = RC_OK;
         const bool in_alt = os_sort_keys(ent.p, ent2.p, npos, (int)bb, e->d_sort_scratch.p, e->d_sort_status.p,
-                                         e->sort_epoch, e->st);
+                                         e->sort_epoch, e->st, [&]() {
+                                             prepped = true;
+                                             if (after_prep) prc = after_prep();
+                                         }, counted);
+        CHK(prc);
         HIPCHK(hipGetLastError());
         if (!in_alt) {
             std::swap(ent.p, ent2.p);
             std::swap(ent.cap, ent2.cap);
         }
     }
+    if (!prepped && after_prep) CHK(after_prep());
     const char *ibv = getenv("RC_INDEX_BITS_MAX");
     const int bmax = ibv ? std::max(16, std::min(30, atoi(ibv))) : 28;
     int bits = 16;
@@ -1079,12 +1091,22 @@ static int build_index_of(rc_engine *e, const TxInfo *txl, uint32_t n_tx, uint64
     }
     CHK(ent.ensure(std::max<uint64_t>(npos, 1)));
     CHK(ent2.ensure(std::max<uint64_t>(npos, 1)));
-    if (n_tx) launch_kmer_fill(amb, txl, n_tx, e->d_F.p + FRONT_PAD, amb ? e->d_AF.p + FRONT_PAD : nullptr,
-                               offs, ent.p, e->st);
-    if (after_fill) CHK(after_fill());
+    // without ambiguity codes the fill also counts the sort's segment
+    // histograms (sort.hip), so the sort does not read the keys to count them
+    static const bool lib = getenv("RC_SORT") && !strcmp(getenv("RC_SORT"), "rocprim");
+    const bool counted = !amb && !lib && npos > 0 && npos <= 0xFFFFFFFFull;
+    if (counted) {
+        CHK(e->d_sort_scratch.ensure(os_scratch_words(npos)));
+        os_fill_hist(txl, n_tx, e->d_F.p + FRONT_PAD, offs, ent.p, npos, e->d_sort_scratch.p, e->st);
+    } else if (n_tx) {
+        launch_kmer_fill(amb, txl, n_tx, e->d_F.p + FRONT_PAD, amb ? e->d_AF.p + FRONT_PAD : nullptr, offs, ent.p,
+                         e->st);
+    }
     // sort on the k-mer (bits 32..63); the fill order is position order and the
-    // radix sort is stable, so positions stay ascending per k-mer.
-    CHK(sort_index(e, ent, ent2, npos, 32u, 0, bucket, bits_out));
+    // radix sort is stable, so positions stay ascending per k-mer. after_fill
+    // (DUST on the second stream) starts once the sort's one-block table
+    // kernels are queued: beside DUST's waves they crawled (4.2 ms vs 14 us).
+    CHK(sort_index(e, ent, ent2, npos, 32u, 0, bucket, bits_out, after_fill, counted));
     n_out = npos;
     return RC_OK;
 }

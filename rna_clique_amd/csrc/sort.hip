@@ -29,11 +29,10 @@
 //     to a tile whose inclusive prefix is published;
 //   * the keys go to LDS in digit order and leave in runs per digit, each run
 //     to consecutive global slots.
-#include <hip/hip_runtime.h>
-
-#include <stdint.h>
+#include "device.h"
 
 #include <algorithm>
+#include <functional>
 #include <utility>
 
 namespace rcg {
@@ -185,6 +184,51 @@ __global__ void tile_order_kernel(const uint32_t *scratch, int p, uint32_t *orde
         pos += std::min(nt, j) + (q < sg && nt > j ? 1u : 0u);
     }
     order[pos] = g;
+}
+
+// The index fill (kernels.hip kmer_fill_kernel, no ambiguity codes: entry
+// koff[t] + o is window o of transcript t) with the sort's segment
+// histograms counted on the way, so the sort does not read the keys to count
+// them. Wave per transcript, grid-stride; per-block LDS tables.
+__global__ __launch_bounds__(256) void kmer_fill_hist_kernel(const TxInfo *__restrict__ tx, uint32_t n_tx,
+                                                             const uint64_t *__restrict__ F,
+                                                             const uint64_t *__restrict__ out_off,
+                                                             uint64_t *__restrict__ ent, int np, uint64_t segsize,
+                                                             uint32_t *scratch)
+{
+    extern __shared__ uint32_t h[];
+    const int tab = OS_SEG * RADIX;
+    for (int i = threadIdx.x; i < np * tab; i += 256) h[i] = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const uint32_t nwave = gridDim.x * 4u;
+    for (uint32_t t = blockIdx.x * 4u + (threadIdx.x >> 6); t < n_tx; t += nwave) {
+        const TxInfo ti = tx[t];
+        const int64_t nwin = (int64_t)ti.len - W16 + 1;
+        const uint64_t base = out_off[t];
+        for (int64_t o0 = 0; o0 < nwin; o0 += 64) {
+            // the segment of the 64 entries: one division per wave (a segment
+            // holds at least 64 entries once n >= 64 OS_SEG)
+            const uint64_t i0 = base + (uint64_t)o0;
+            const uint32_t s0 = (uint32_t)(i0 / segsize);
+            const uint64_t nb = (uint64_t)(s0 + 1) * segsize;
+            const int64_t o = o0 + lane;
+            if (o >= nwin) continue;
+            const uint64_t p = ti.start + (uint64_t)o;
+            const uint32_t key = (uint32_t)win(F, p);
+            const uint64_t i = base + (uint64_t)o;
+            ent[i] = ((uint64_t)key << 32) | p;
+            uint32_t prev = segsize >= 64 ? s0 + (i >= nb ? 1u : 0u) : (uint32_t)(i / segsize);
+            for (int q = 0; q < np; q++) {
+                const uint32_t d = (key >> (8 * q)) & 255u;
+                atomicAdd(&h[q * tab + (q ? (prev >> OS_GSH) : prev) * RADIX + d], 1u);
+                prev = d;
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < np * tab; i += 256)
+        if (h[i]) atomicAdd(&pass_tab(scratch, i / tab).H[i % tab], h[i]);
 }
 
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m)
@@ -365,23 +409,44 @@ __global__ __launch_bounds__(OS_BLOCK, OS_MINB * OS_WAVES / 4) void onesweep_ker
 uint64_t os_status_words(uint64_t n) { return ((n + OS_TILE - 1) / OS_TILE + OS_SEG) * (uint64_t)RADIX; }
 uint64_t os_scratch_words(uint64_t n) { return OS_FIXED_WORDS + (n + OS_TILE - 1) / OS_TILE + OS_SEG; }
 
+// after_prep (optional) runs once the tables and the first pass's claim order
+// are queued, before the first pass: work for another stream that should not
+// starve those one-block kernels (the engine starts DUST there).
+// The index fill and the segment histograms of a 32-bit-key sort (bb = 32)
+// in one kernel (transcripts without ambiguity codes; koff: first entry of
+// each transcript); os_sort_keys(..., counted = true) then skips its count.
+void os_fill_hist(const TxInfo *tx, uint32_t n_tx, const uint64_t *F, const uint64_t *koff, uint64_t *ent,
+                  uint64_t n, uint32_t *scratch, hipStream_t st)
+{
+    (void)hipMemsetAsync(scratch, 0, OS_FIXED_WORDS * sizeof(uint32_t), st);
+    if (!n_tx || !n) return;
+    const int np = 4;
+    const uint64_t segsize = (n + OS_SEG - 1) / OS_SEG;
+    const dim3 g(std::min<uint32_t>((n_tx + 3) / 4, 256 * 8));
+    hipLaunchKernelGGL(kmer_fill_hist_kernel, g, dim3(256), (size_t)np * OS_SEG * RADIX * sizeof(uint32_t), st, tx,
+                       n_tx, F, koff, ent, np, segsize, scratch);
+}
+
 bool os_sort_keys(uint64_t *keys, uint64_t *alt, uint64_t n, int bb, uint32_t *scratch, uint64_t *status,
-                  uint32_t &epoch, hipStream_t st)
+                  uint32_t &epoch, hipStream_t st, const std::function<void()> &after_prep, bool counted)
 {
     const int np = (64 - bb + 7) / 8;
     if (n == 0) return false;
     uint32_t *ctr = scratch + HIST_MAXP * OS_PASS_WORDS, *order = ctr + HIST_MAXP;
-    (void)hipMemsetAsync(scratch, 0, OS_FIXED_WORDS * sizeof(uint32_t), st);
     const uint64_t segsize = (n + OS_SEG - 1) / OS_SEG;
-    const uint64_t hb = std::min<uint64_t>((n + HIST_BLOCK * 8 - 1) / (HIST_BLOCK * 8), 1024);
-    hipLaunchKernelGGL(seg_hist_kernel, dim3((unsigned)hb), dim3(HIST_BLOCK),
-                       (size_t)np * OS_SEG * RADIX * sizeof(uint32_t), st, keys, n, bb, np, segsize, scratch);
+    if (!counted) {
+        (void)hipMemsetAsync(scratch, 0, OS_FIXED_WORDS * sizeof(uint32_t), st);
+        const uint64_t hb = std::min<uint64_t>((n + HIST_BLOCK * 8 - 1) / (HIST_BLOCK * 8), 1024);
+        hipLaunchKernelGGL(seg_hist_kernel, dim3((unsigned)hb), dim3(HIST_BLOCK),
+                           (size_t)np * OS_SEG * RADIX * sizeof(uint32_t), st, keys, n, bb, np, segsize, scratch);
+    }
     hipLaunchKernelGGL(seg_scan_kernel, dim3(1), dim3(RADIX), 0, st, scratch, np, n, segsize);
     const uint32_t tmax = (uint32_t)((n + OS_TILE - 1) / OS_TILE + OS_SEG);
     const unsigned grid = tmax;   // tiles beyond a pass's count exit at once
     uint64_t *src = keys, *dst = alt;
     for (int p = 0; p < np; p++) {
         hipLaunchKernelGGL(tile_order_kernel, dim3((tmax + 255) / 256), dim3(256), 0, st, scratch, p, order, tmax);
+        if (p == 0 && after_prep) after_prep();
         ++epoch;
         hipLaunchKernelGGL(onesweep_kernel, dim3(grid), dim3(OS_BLOCK), 0, st, src, dst, bb + 8 * p, scratch, p,
                            order, (gu64 *)status, epoch, ctr + p, n);
