@@ -1575,7 +1575,18 @@ enum { RM_REC = 0, RM_CLO = CAND_DWORDS, RM_CHI, RM_QB, RM_TB, RM_X, RM_Y, RM_LE
        RM_PHASE,                                  // the running extension's done action (A_RDONE / A_LDONE)
        RM_KOF,                                    // the window's diagonal offset (sliding sub-band)
        RM_PWI, RM_PWG, RM_PWD, RM_PK,             // the row's best record parked by a window slide, its diagonal
-       RM_N };
+       RM_N };   // (its size is part of the row kernel's tuning: 3 more fields cost 4 VGPR spills)
+// the step count and best score of an extension that outgrew the window, kept
+// (SAVE kernel) where the candidate record's start positions were (only read
+// while the candidate is staged)
+enum { RM_AD6 = RM_REC + 4, RM_ABEST = RM_REC + 5 };
+// a saved extension (ExtParams::resume, RES_REC ints): the bookkeeping
+// RM_RSC .. RM_PK, the step count, the best score, then the window's frontier
+// R and gap states
+enum { RES_RSC = 0, RES_PHASE = RM_PHASE - RM_RSC, RES_KOF = RM_KOF - RM_RSC, RES_PWI = RM_PWI - RM_RSC,
+       RES_PWG = RM_PWG - RM_RSC, RES_PWD = RM_PWD - RM_RSC, RES_PK = RM_PK - RM_RSC, RES_D6 = RES_PK + 1,
+       RES_BEST = RES_PK + 2, RES_R = 16, RES_G = 48 };
+static_assert(RES_BEST < RES_R && RES_G + 32 <= RES_REC, "resume record layout");
 // fields of the record (dword offsets, layout of Cand)
 enum { RC_SOFF = 0, RC_QTX = 1, RC_STX = 2, RC_CNT_STRAND = 3, RC_Q0 = 4, RC_S0 = 6, RC_LQ = 8, RC_LT = 9,
        RC_SAMS = 10, RC_E01 = 11 };
@@ -1630,7 +1641,10 @@ __host__ __device__ constexpr size_t row_lds_bytes(int rw, int na, int sw)
 // edge lane, which slides first), so the extension stays exact. Only a live
 // span wider than the window, or one reaching past the band's +-31, goes to
 // the one-wave full-band kernel (indels: C3v).
-template <bool AMB, int RW, int MINW>
+// SAVE (32-lane rows): an extension that outgrows the window is saved for the
+// 64-lane pass to continue (a separate instantiation: the save code's
+// registers cost the plain kernel 7 % at C3, where nearly nothing overflows).
+template <bool AMB, int RW, int MINW, bool SAVE = false>
 __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
 {
     constexpr int RROWS = EBLOCK / RW;   // rows per block
@@ -1706,18 +1720,22 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
     };
     // row-uniform; extend_kernel takes the candidate whole -- or, shared
     // searches, a sub-band overflow (wide) the 64-lane pass over P.wide next
-    auto defer = [&](uint64_t ci, bool wide) {
+    // (returns the wide-list entry, row-uniform; ~0 when not listed)
+    auto defer = [&](uint64_t ci, bool wide) -> unsigned long long {
+        unsigned long long wi2 = ~0ull;
         if (rl == 0) {
             const RowArgsK K = row_args();
             if (!K->P.share) {   // shared searches: first_finish_kernel lists each search on its own
                 const unsigned long long di = atomicAdd(K->P.defer_count, 1ull);
                 K->P.defer[di] = (uint32_t)ci;
             } else if (wide && K->P.wide) {
-                const unsigned long long wi2 = atomicAdd(K->P.wide_n, 1ull);
+                wi2 = atomicAdd(K->P.wide_n, 1ull);
                 K->P.wide[wi2] = (uint32_t)ci;
             }
             box_out()[ci * BOX_REC + FX_STATUS] = -1;
         }
+        if constexpr (SAVE) return (unsigned long long)__shfl((long long)wi2, RW * row);
+        return wi2;
     };
     if (rl == 0) {
         RL.st[RS_SHARD] = 0;
@@ -1796,6 +1814,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                     meta[RM_CLO] = (int)(uint32_t)ci;
                     meta[RM_CHI] = (int)(uint32_t)(ci >> 32);
                 }
+                const uint32_t lidx = lnx;   // list index (the 64-lane pass's resume record)
                 // prefetch the next record
                 if (++lnx >= (uint32_t)RL.st[RS_LEND]) grab();
                 recv = load_rec(lnx);
@@ -1876,6 +1895,50 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                     const uint32_t t = pa; pa = pb; pb = t;
                     const int u = alen; alen = blen; blen = u;
                 }
+                if constexpr (RW == 64) {
+                    // a 32-lane extension that outgrew its window: continue it
+                    // from the saved state (the diagonals outside the window
+                    // were never reached, so the full band's state is it)
+                    if (K->P.resume && K->P.list && lidx < K->P.res_cap) {
+                        const int *rec = K->P.resume + (size_t)lidx * RES_REC;
+                        const int phase = rec[RES_PHASE], kof = rec[RES_KOF];
+                        if (phase == A_LDONE) {
+                            if (rl < 5) meta[RM_RSC + rl] = rec[RES_RSC + rl];
+                            // left extension: forward from reversed position L - x
+                            pa = bqr + (uint32_t)(Lq - x);
+                            alen = x;
+                            pb = btr + (uint32_t)(Lt - y);
+                            blen = y;
+                            if (swap) {
+                                const uint32_t t = pa; pa = pb; pb = t;
+                                const int u = alen; alen = blen; blen = u;
+                            }
+                        }
+                        d6 = rec[RES_D6];
+                        best = rec[RES_BEST];
+                        const int kb = rec[RES_PK];
+                        bl = kb + RC0;
+                        const int w = rl - RC0 - kof + 16;   // this diagonal's lane in the saved window
+                        const bool inw = w >= 0 && w < 32;
+                        R = inw ? rec[RES_R + (inw ? w : 0)] : -1;
+                        goe = inw ? rec[RES_G + (inw ? w : 0)] : 0;
+                        if (rl == bl) {
+                            wi = rec[RES_PWI];
+                            wg = rec[RES_PWG];
+                            wd = rec[RES_PWD];
+                        }
+                        pbk = pb - (uint32_t)k;
+                        blk = blen + k;
+                        nkd = -(k + d6);
+                        if (rl == 0) {
+                            atomicAdd(&rcnt[0], 1u);
+                            meta[RM_PHASE] = phase;
+                            meta[RM_KOF] = 0;
+                        }
+                        act = phase + (A_STEP_R - A_RDONE);
+                        continue;
+                    }
+                }
                 ext_init(A_RDONE);
             } else if (act == A_SLIDE) {
                 // a live lane at the window's edge: centre the live diagonals
@@ -1887,6 +1950,25 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 const int s = kn - kof;
                 if (s == 0 || lmin - s < 1 || lmax - s > RW - 2) {
                     act = A_ABORT;   // wider than the window, or at the band's edge
+                    if constexpr (SAVE && RW == 32) {
+                        // what the 64-lane pass needs to continue it (A_ABORT
+                        // saves it with the frontier): the best record parked
+                        // as a slide parks it, the step count, the best score
+                        if (bl != BL_PARKED) {
+                            const int bsrc = RW * row + bl;
+                            const int pwi = __shfl(wi, bsrc), pwg = __shfl(wg, bsrc), pwd = __shfl(wd, bsrc);
+                            if (rl == 0) {
+                                meta[RM_PWI] = pwi;
+                                meta[RM_PWG] = pwg;
+                                meta[RM_PWD] = pwd;
+                                meta[RM_PK] = bl - RC0 + kof;
+                            }
+                        }
+                        if (rl == 0) {
+                            meta[RM_AD6] = d6;
+                            meta[RM_ABEST] = best;
+                        }
+                    }
                     continue;
                 }
                 if (bl != BL_PARKED) {
@@ -1972,7 +2054,24 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 }
             } else {   // A_ABORT: the sub-band overflowed
                 const uint64_t ci = (uint64_t)(uint32_t)meta[RM_CLO] | ((uint64_t)(uint32_t)meta[RM_CHI] << 32);
-                defer(ci, true);
+                const unsigned long long wi2 = defer(ci, true);
+                if constexpr (SAVE && RW == 32) {
+                    // the wide pass continues from here: the window's frontier
+                    // and the header A_SLIDE left in the bookkeeping
+                    if (wi2 != ~0ull) {
+                        const RowArgsK K = row_args();
+                        if (K->P.resume && wi2 < K->P.res_cap) {
+                            int *rec = K->P.resume + (size_t)wi2 * RES_REC;
+                            rec[RES_R + rl] = R;
+                            rec[RES_G + rl] = goe;
+                            // the bookkeeping from the right results to the best
+                            // record, the step count, the best score
+                            if (rl <= RES_PK) rec[rl] = meta[RM_RSC + rl];
+                            if (rl == RES_D6) rec[rl] = meta[RM_AD6];
+                            if (rl == RES_BEST) rec[rl] = meta[RM_ABEST];
+                        }
+                    }
+                }
                 if (rl == 0) atomicAdd(&rcnt[2], 1u);
                 act = A_FETCH;
             }
@@ -2424,14 +2523,18 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
     ExtParams W = P;
     W.list = nullptr;
     W.list_n = nullptr;
+    // saved extension states: only the shared-search 32-lane passes write
+    // them and only their 64-lane passes read them
+    W.resume = nullptr;
     const int rw = row_width == 16 ? 16 : 32;
     auto lds_of = [&](int w) { return row_lds_bytes(w, amb ? 8 : 4, P.dsw); };
-#define RC_LAUNCH_ROWS(A, RWV, MW, PRM)                                                                   \
+#define RC_LAUNCH_ROWS_S(A, RWV, MW, SV, PRM)                                                             \
     do {                                                                                                  \
-        auto kern = extend_rows_kernel<A, RWV, MW>;                                                       \
+        auto kern = extend_rows_kernel<A, RWV, MW, SV>;                                                   \
         const size_t lds = lds_of(RWV);                                                                   \
         hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, lds)), dim3(EBLOCK), lds, st, RowArgs{db, PRM});\
     } while (0)
+#define RC_LAUNCH_ROWS(A, RWV, MW, PRM) RC_LAUNCH_ROWS_S(A, RWV, MW, false, PRM)
     const char *mwv = getenv("RC_ROW_WAVES");
     const int mw = mwv ? atoi(mwv) : ROW_MIN_WAVES;
     if (P.share) {
@@ -2458,10 +2561,14 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
         W.which = 0;
         W.wide = widep ? P.wide0 : nullptr;
         W.wide_n = P.wide0_n;
+        W.resume = widep && rw == 32 ? P.resume : nullptr;
         // RC_ROW_WIDTH=16: the sliding sub-band on 16-lane rows (4 candidates per wave)
         auto rows_pass = [&](const ExtParams &B) {
             if (rw == 16) {
                 if (amb) RC_LAUNCH_ROWS(true, 16, ROW_MIN_WAVES, B); else RC_LAUNCH_ROWS(false, 16, ROW_MIN_WAVES, B);
+            } else if (B.resume) {
+                if (amb) RC_LAUNCH_ROWS_S(true, 32, ROW_MIN_WAVES, true, B);
+                else RC_LAUNCH_ROWS_S(false, 32, ROW_MIN_WAVES, true, B);
             } else {
                 if (amb) RC_LAUNCH_ROWS(true, 32, ROW_MIN_WAVES, B); else RC_LAUNCH_ROWS(false, 32, ROW_MIN_WAVES, B);
             }
@@ -2538,6 +2645,7 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
     W2.work = P.work2;
     if (amb) RC_LAUNCH_ROWS(true, 64, ROW_MIN_WAVES, W2); else RC_LAUNCH_ROWS(false, 64, ROW_MIN_WAVES, W2);
 #undef RC_LAUNCH_ROWS
+#undef RC_LAUNCH_ROWS_S
     uint64_t g = (P.n_cand + 255) / 256;
     if (g > 65536) g = 65536;
     ExtParams W3 = W;

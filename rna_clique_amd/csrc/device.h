@@ -257,7 +257,13 @@ struct ExtParams {
     // extend_kernel (shared searches): start a search from its first seed's
     // row-kernel result (cand_box / cand_box2) when it has one
     int32_t reuse_first;
+    // shared searches: the state of a 32-lane extension that outgrew its
+    // window, saved per wide-list entry (the first res_cap entries), so the
+    // 64-lane pass continues it instead of starting over (RES_REC ints each)
+    int32_t *resume;
+    uint32_t res_cap;
 };
+constexpr int RES_REC = 80;   // phase, kof, d6, best, best record (i, gap, d6, diagonal), right results, R[32], goe[32]
 
 // DHsp.strand carries, besides the strand (bit 0), the direction flags of a
 // freshly extended HSP (bit 1: passes the query->subject e-value cut, bit 2:

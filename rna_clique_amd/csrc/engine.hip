@@ -344,6 +344,10 @@ struct rc_engine {
     DBuf<unsigned long long> d_rctr;   // [0] near-index entries, [1] reverse-only seeds
     DBuf<uint64_t> d_rtmask;
     uint64_t rseed_cap = 0, n_rseeds = 0;
+    uint32_t res_cap = 0;
+    // fraction of the last run's candidates whose first-seed extension
+    // outgrew the 32-lane window (selects the saving row kernel, RC_RESUME)
+    double ovf_frac = 0.0;
     DBuf<uint64_t> d_ent, d_ent2;   // (k-mer << 32 | position), unsorted / sorted
     // the index sort's scratch (sort.hip): digit histograms + tile counters,
     // the look-back table (zeroed when allocated; tagged by pass epoch)
@@ -367,6 +371,7 @@ struct rc_engine {
     DBuf<DHsp> d_cand_hsp_r;
     DBuf<uint8_t> d_cand_nh_r;
     DBuf<uint32_t> d_cand_ovf_r, d_defer_r, d_list2, d_wide0, d_wide1;
+    DBuf<int32_t> d_resume;   // saved 32-lane extension states for the 64-lane pass (RES_REC ints each)
     bool share = false;
     DBuf<DRow> d_rows_tmp;
     DBuf<DEdge> d_edges_tmp;
@@ -1651,6 +1656,14 @@ static int align_tile(rc_engine *e, int ti)
         CHK(e->d_defer_r.ensure(std::max<uint64_t>(n_cand, 1)));
         CHK(e->d_wide0.ensure(std::max<uint64_t>(n_cand, 1)));
         CHK(e->d_wide1.ensure(std::max<uint64_t>(n_cand, 1)));
+        {
+            // room to continue the first 12 M overflowing extensions of a pass
+            // (3.8 GB); later ones start over in the 64-lane pass
+            const char *rv = getenv("RC_RESUME");
+            e->res_cap = (rv && atoi(rv) == 0) ? 0u : (uint32_t)std::min<uint64_t>(n_cand, 12u << 20);
+            if (!(rv && atoi(rv) == 1) && e->ovf_frac <= 0.02) e->res_cap = 0;   // not needed: no buffer
+            if (e->res_cap) CHK(e->d_resume.ensure((size_t)e->res_cap * RES_REC));
+        }
     }
     CHK(e->d_defer.ensure(std::max<uint64_t>(n_cand, 1)));
     CHK(e->d_defer2.ensure(std::max<uint64_t>(n_cand, 1)));
@@ -1705,6 +1718,15 @@ static int align_tile(rc_engine *e, int ti)
         X.wide1 = e->d_wide1.p;
         X.wide0_n = e->d_count.p + 20;
         X.wide1_n = e->d_count.p + 21;
+        {
+            // save overflowing extensions for the 64-lane pass when the last
+            // run had many (C3v: 39 %, C3: 0.002 %): the saving kernel costs
+            // the plain one 7 % (RC_RESUME=1 always, 0 never)
+            const char *rv = getenv("RC_RESUME");
+            const bool on = rv ? atoi(rv) == 1 : e->ovf_frac > 0.02;
+            X.resume = e->res_cap && on ? e->d_resume.p : nullptr;
+            X.res_cap = e->res_cap;
+        }
         X.work_w0 = e->d_count.p + 22;
         X.work_w1 = e->d_count.p + 23;
         {
@@ -1747,6 +1769,7 @@ static int align_tile(rc_engine *e, int ti)
             // candidates the one-wave kernel took (the 64-lane pass's list, or the row kernel's)
             const char *r64 = getenv("RC_ROW64");
             e->tm.ext_fullband += (r64 && atoi(r64)) ? (double)nfull : (double)ctr[3];
+            e->ovf_frac = n_cand ? (double)ctr[3] / (double)n_cand : 0.0;
             e->tm.ext_deferred += (double)ctr[5] + (double)ndr;
             e->tm.ext_second += e->share ? (double)nl2 : 0.0;
             e->tm.band_bound += (double)ctr[7];
