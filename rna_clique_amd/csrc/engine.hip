@@ -1413,11 +1413,11 @@ static int align_tile(rc_engine *e, int ti)
     HIPCHK(hipEventRecord(e->ev[1], e->st));
     // DUST masks of the tile's transcripts (the query side), bit per base, on
     // the second stream: a compute-bound scan beside the HBM-bound index
-    // build. It starts once the k-mer fill is done (beside the radix sort):
-    // started with the fill, both ran at a third of their speed
-    // (RC_DUST_EARLY=1 restores that order for A/B runs).
+    // build, started with the fill (r03, hand-written sort and DUST: index
+    // phase 55.7 vs 58.1 ms at C3 when started after the sort's table kernels;
+    // RC_DUST_EARLY=0 starts it there).
     auto start_dust = [&]() -> int {
-        const uint32_t dblocks = 256 * 28;   // at least the resident waves of the chunk kernel (7 per SIMD): their scratch
+        const uint32_t dblocks = 256 * 28;   // at least the resident waves of the chunk kernel (<= 7 per SIMD): their scratch
         CHK(e->d_dust_scratch.ensure(dust_scratch_words(dblocks)));
         CHK(e->d_dust_events.ensure(dust_event_words(dblocks)));
         const char *dwv = getenv("RC_DUST_WAVES");
@@ -1434,7 +1434,7 @@ static int align_tile(rc_engine *e, int ti)
         return RC_OK;
     };
     const char *dev = getenv("RC_DUST_EARLY");
-    const bool dust_early = dev && atoi(dev);
+    const bool dust_early = !(dev && atoi(dev) == 0);
     if (dust && dust_early) CHK(start_dust());
     CHK(build_index(e, dust && !dust_early ? std::function<int()>(start_dust) : nullptr));
     HIPCHK(hipGetLastError());
