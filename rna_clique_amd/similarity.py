@@ -172,25 +172,35 @@ class SampleSimilarity:
         """The gene matches graph (networkx): the one given, or the one
         build_graph.py:40-68 makes from an engine run's tables. A sharded
         engine holds only its own pairs' tables, but every shard has all
-        graph edges after the exchange: the graph is built from those (same
-        nodes and edges; insertion order by pair, then edge)."""
+        graph edges after the exchange, per pair in pair order and in the
+        order of each pair's rows: build_graph over those per-pair edge
+        tables gives the same graph, node and neighbour order included."""
         if self._graph is not None:
             return self._graph
         if getattr(self.engine, "shard_count", 1) > 1:
-            import networkx as nx
-            e = self.engine.edges()
-            g = nx.Graph()
-            la = [self.labels[i] for i in e["sample_a"].tolist()]
-            lb = [self.labels[i] for i in e["sample_b"].tolist()]
-            g.add_edges_from(zip(zip(la, e["gene_a"].tolist()), zip(lb, e["gene_b"].tolist())))
-            self._graph = g
-            return g
+            self._graph = build_graph(
+                (self.labels[sa], self.labels[qa], {"sgene": sg, "qgene": qg})
+                for sa, qa, sg, qg in self._edge_tables())
+            return self._graph
 
         def rows():
             for a, b in self._pairs():
                 yield self.labels[a], self.labels[b], self.engine.pair_rows(a, b)
         self._graph = build_graph(rows())
         return self._graph
+
+    def _edge_tables(self):
+        """A sharded engine's exchanged edges as per-pair tables (ssample,
+        qsample, sgene array, qgene array) in pair order, each in its rows'
+        order (the record order inside a pair is kept)."""
+        import numpy as np
+        e = self.engine.edges()
+        o = np.lexsort((e["sample_b"], e["sample_a"]))   # stable: record order inside a pair
+        e = e[o]
+        key = e["sample_a"].astype(np.int64) * (1 << 32) + e["sample_b"].astype(np.int64)
+        cut = np.flatnonzero(np.diff(key)) + 1
+        for r in (np.split(np.arange(len(e)), cut) if len(e) else []):
+            yield int(e["sample_a"][r[0]]), int(e["sample_b"][r[0]]), e["gene_a"][r], e["gene_b"][r]
 
     def write_graph(self, path):
         """graph.pkl (filtering_step.py:158-159): the pickle of `graph`. For an
@@ -203,19 +213,9 @@ class SampleSimilarity:
             return
         if self._graph is None:
             # a sharded run holds every edge but only its own pairs' rows: the
-            # edges, per pair in pair order (a table of its distinct edges
-            # each), through the same writer -- the same nodes and edges as
-            # `graph`, without building it in Python
-            import numpy as np
+            # exchanged edges as per-pair tables through the same writer
             from .tables import write_graph_pickle
-            e = self.engine.edges()
-            o = np.lexsort((e["sample_b"], e["sample_a"]))   # stable: record order inside a pair
-            e = e[o]
-            key = e["sample_a"].astype(np.int64) * (1 << 32) + e["sample_b"].astype(np.int64)
-            cut = np.flatnonzero(np.diff(key)) + 1
-            runs = np.split(np.arange(len(e)), cut) if len(e) else []
-            write_graph_pickle(path, ((int(e["sample_a"][r[0]]), int(e["sample_b"][r[0]]), e["gene_a"][r],
-                                       e["gene_b"][r]) for r in runs), self.labels)
+            write_graph_pickle(path, self._edge_tables(), self.labels)
             return
         from .filtering_step import dump_graph
         dump_graph(self.graph, path)

@@ -56,6 +56,11 @@ def test_sharded_engines_match_unsharded(native, shards):
         st, rst = e.stats(), ref.stats()
         for k in ("edges", "components", "ideal_components", "ideal_nodes", "sample_count"):
             assert st[k] == rst[k], k
+        # the graph from the exchanged edges is build_graph's, orders included
+        from rna_clique_amd.similarity import SampleSimilarity
+        g, g_ref = SampleSimilarity.from_engine(e).graph, SampleSimilarity.from_engine(ref).graph
+        assert list(g.nodes) == list(g_ref.nodes)
+        assert all(list(g.adj[n]) == list(g_ref.adj[n]) for n in g_ref.nodes)
 
 
 def _top_select(sample, top):
@@ -168,8 +173,9 @@ def _shard_worker(rank, world, port, q, graph_dir=None):
 def test_two_processes_share_the_pairs(native, tmp_path):
     """world_size 2, one engine per process on the same GPU, gloo exchange:
     the same distances as one engine, and each rank's graph.pkl (native
-    writer over the exchanged edges) holds the one-engine graph's nodes and
-    edges."""
+    writer over the exchanged edges) is build_graph's graph: its nodes and
+    edges, in its node order and neighbour order (the exchanged edges come
+    per pair in pair order, in the order of each pair's rows)."""
     import socket
     import torch.multiprocessing as mp
     from rna_clique_amd.engine import Engine
@@ -202,6 +208,8 @@ def test_two_processes_share_the_pairs(native, tmp_path):
             g = pickle.load(f)
         assert set(g.nodes) == set(g_ref.nodes)
         assert {frozenset(e) for e in g.edges} == ref_edges
+        assert list(g.nodes) == list(g_ref.nodes)
+        assert all(list(g.adj[n]) == list(g_ref.adj[n]) for n in g_ref.nodes)
 
 
 # ------------------------------------------------- SampleSimilarity(graph, tables)
