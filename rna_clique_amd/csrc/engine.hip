@@ -43,7 +43,10 @@ void launch_bucket_fill(const uint64_t *, uint64_t, int, uint32_t *, hipStream_t
 uint64_t os_status_words(uint64_t n);
 uint64_t os_scratch_words(uint64_t n);
 bool os_sort_keys(uint64_t *keys, uint64_t *alt, uint64_t n, int bb, uint32_t *scratch, uint64_t *status,
-                  uint32_t &epoch, hipStream_t st, const std::function<void()> &after_prep, bool counted);
+                  uint32_t &epoch, hipStream_t st, const std::function<void()> &after_prep, bool counted,
+                  const TxInfo *gen_tx, const uint64_t *gen_koff, const uint64_t *gen_F, uint32_t gen_ntx,
+                  uint32_t *gen_tile);
+uint64_t os_gen_tile_words(uint64_t n);
 void os_fill_hist(const TxInfo *tx, uint32_t n_tx, const uint64_t *F, const uint64_t *koff, uint64_t *ent,
                   uint64_t n, uint32_t *scratch, hipStream_t st);
 void launch_tx_masked(const TxInfo *, uint32_t, const uint64_t *, uint8_t *, hipStream_t);
@@ -351,7 +354,7 @@ struct rc_engine {
     DBuf<uint64_t> d_ent, d_ent2;   // (k-mer << 32 | position), unsorted / sorted
     // the index sort's scratch (sort.hip): digit histograms + tile counters,
     // the look-back table (zeroed when allocated; tagged by pass epoch)
-    DBuf<uint32_t> d_sort_scratch;
+    DBuf<uint32_t> d_sort_scratch, d_gen_tile;
     DBuf<uint64_t> d_sort_status;
     uint32_t sort_epoch = 0;
     DBuf<uint32_t> d_bucket, d_pos_tx;
@@ -1020,9 +1023,17 @@ static int load_tile(rc_engine *e, int ti)
 // bucket table over the top k-mer bits: about one bucket per entry (times
 // 2^extra), at most 2^28 (RC_INDEX_BITS_MAX; 28 measured best at C3 -- a 1 GiB
 // table instead of 4 GiB, same seed-kernel time)
+// the first pass's key generator (sort.hip KeyGen): keys from the packed
+// sequence instead of the fill's entry array
+struct GenArgs {
+    const TxInfo *tx;
+    const uint64_t *koff;
+    const uint64_t *F;
+    uint32_t n_tx;
+};
 static int sort_index(rc_engine *e, DBuf<uint64_t> &ent, DBuf<uint64_t> &ent2, uint64_t npos, unsigned bb, int extra,
                       DBuf<uint32_t> &bucket, int &bits_out, const std::function<int()> &after_prep = nullptr,
-                      bool counted = false)
+                      bool counted = false, const GenArgs *gen = nullptr)
 {
     static const bool lib = getenv("RC_SORT") && !strcmp(getenv("RC_SORT"), "rocprim");
     bool prepped = false;   // after_prep runs exactly once, also for an empty index
@@ -1048,11 +1059,14 @@ static int sort_index(rc_engine *e, DBuf<uint64_t> &ent, DBuf<uint64_t> &ent2, u
             HIPCHK(hipMemsetAsync(e->d_sort_status.p, 0, words * sizeof(uint64_t), e->st));
         }
         int prc = RC_OK;
+        if (gen) CHK(e->d_gen_tile.ensure(os_gen_tile_words(npos)));
         const bool in_alt = os_sort_keys(ent.p, ent2.p, npos, (int)bb, e->d_sort_scratch.p, e->d_sort_status.p,
                                          e->sort_epoch, e->st, [&]() {
                                              prepped = true;
                                              if (after_prep) prc = after_prep();
-                                         }, counted);
+                                         }, counted, gen ? gen->tx : nullptr, gen ? gen->koff : nullptr,
+                                         gen ? gen->F : nullptr, gen ? gen->n_tx : 0u,
+                                         gen ? e->d_gen_tile.p : nullptr);
         CHK(prc);
         HIPCHK(hipGetLastError());
         if (!in_alt) {
@@ -1100,9 +1114,16 @@ static int build_index_of(rc_engine *e, const TxInfo *txl, uint32_t n_tx, uint64
     // histograms (sort.hip), so the sort does not read the keys to count them
     static const bool lib = getenv("RC_SORT") && !strcmp(getenv("RC_SORT"), "rocprim");
     const bool counted = !amb && !lib && npos > 0 && npos <= 0xFFFFFFFFull;
+    // RC_GEN=1: the sort's first pass computes the keys from the sequence
+    // instead of reading the entry array the fill writes (measured slower:
+    // index phase 61.1 vs 57.9 ms at C3 -- the per-key transcript search and
+    // sequence windows cost more than the 25.6 GB of traffic they save)
+    static const bool genv = getenv("RC_GEN") && atoi(getenv("RC_GEN")) == 1;
+    const bool gen = counted && genv && n_tx;
+    const GenArgs ga{txl, offs, e->d_F.p + FRONT_PAD, n_tx};
     if (counted) {
         CHK(e->d_sort_scratch.ensure(os_scratch_words(npos)));
-        os_fill_hist(txl, n_tx, e->d_F.p + FRONT_PAD, offs, ent.p, npos, e->d_sort_scratch.p, e->st);
+        os_fill_hist(txl, n_tx, e->d_F.p + FRONT_PAD, offs, gen ? nullptr : ent.p, npos, e->d_sort_scratch.p, e->st);
     } else if (n_tx) {
         launch_kmer_fill(amb, txl, n_tx, e->d_F.p + FRONT_PAD, amb ? e->d_AF.p + FRONT_PAD : nullptr, offs, ent.p,
                          e->st);
@@ -1111,7 +1132,7 @@ static int build_index_of(rc_engine *e, const TxInfo *txl, uint32_t n_tx, uint64
     // radix sort is stable, so positions stay ascending per k-mer. after_fill
     // (DUST on the second stream) starts once the sort's one-block table
     // kernels are queued: beside DUST's waves they crawled (4.2 ms vs 14 us).
-    CHK(sort_index(e, ent, ent2, npos, 32u, 0, bucket, bits_out, after_fill, counted));
+    CHK(sort_index(e, ent, ent2, npos, 32u, 0, bucket, bits_out, after_fill, counted, gen ? &ga : nullptr));
     n_out = npos;
     return RC_OK;
 }

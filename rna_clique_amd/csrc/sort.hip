@@ -217,7 +217,7 @@ __global__ __launch_bounds__(256) void kmer_fill_hist_kernel(const TxInfo *__res
             const uint64_t p = ti.start + (uint64_t)o;
             const uint32_t key = (uint32_t)win(F, p);
             const uint64_t i = base + (uint64_t)o;
-            ent[i] = ((uint64_t)key << 32) | p;
+            if (ent) ent[i] = ((uint64_t)key << 32) | p;   // null: the first pass generates the keys itself
             uint32_t prev = segsize >= 64 ? s0 + (i >= nb ? 1u : 0u) : (uint32_t)(i / segsize);
             for (int q = 0; q < np; q++) {
                 const uint32_t d = (key >> (8 * q)) & 255u;
@@ -236,6 +236,41 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m)
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// Pass 0 without the entry array: key i of the fill order is window
+// i - koff[t] of tile transcript t (koff[t] <= i < koff[t + 1]), so the first
+// pass computes it from the packed sequence instead of reading 8 bytes the
+// fill would have written (transcripts without ambiguity codes).
+struct KeyGen {
+    const TxInfo *tx;
+    const uint64_t *koff;   // n_tx + 1 entries
+    const uint64_t *F;
+    uint32_t n_tx;
+    uint32_t *tile_tx;      // per pass-0 tile: its first transcript
+};
+
+// the transcript of entry i: last t with koff[t] <= i (binary search)
+__device__ __forceinline__ uint32_t gen_tx_of(const uint64_t *koff, uint32_t n_tx, uint64_t i)
+{
+    uint32_t lo = 0, hi = n_tx;   // koff[lo] <= i < koff[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (koff[mid] <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// the first transcript of every pass-0 tile (one thread per tile)
+__global__ void gen_tile_tx_kernel(const uint32_t *scratch, KeyGen G, uint32_t tmax)
+{
+    const PassTab T = pass_tab(const_cast<uint32_t *>(scratch), 0);
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= tmax || g >= T.tbase[OS_SEG]) return;
+    int sg = 0;
+    while (sg + 1 < OS_SEG && T.tbase[sg + 1] <= g) sg++;
+    const uint64_t t0 = (uint64_t)T.segoff[sg] + (uint64_t)(g - T.tbase[sg]) * OS_TILE;
+    G.tile_tx[g] = gen_tx_of(G.koff, G.n_tx, t0);
+}
+
 #ifdef OS_STATS
 __device__ unsigned long long os_stats[4];   // look-back loads, not-ready polls, tiles
 #endif
@@ -244,12 +279,13 @@ __device__ unsigned long long os_stats[4];   // look-back loads, not-ready polls
 // waves 0-3 then walk the look-back (one digit per thread) while waves 4-7
 // rank their keys, and rank theirs after it; the keys go to LDS in digit
 // order and out in runs.
+template <bool GEN>
 __global__ __launch_bounds__(OS_BLOCK, OS_MINB * OS_WAVES / 4) void onesweep_kernel(const uint64_t *__restrict__ in,
                                                                      uint64_t *__restrict__ out, int shift,
                                                                      const uint32_t *scratch, int p,
                                                                      const uint32_t *__restrict__ order,
                                                                      gu64 *status, uint32_t epoch, uint32_t *tile_ctr,
-                                                                     uint64_t n_all)
+                                                                     uint64_t n_all, KeyGen G)
 {
     static_assert(OS_BLOCK >= RADIX && OS_TILE <= 65536 && OS_ITEMS % 2 == 0, "one look-back thread per digit; 16-bit ranks");
     __shared__ uint64_t s_keys[OS_TILE];
@@ -259,6 +295,8 @@ __global__ __launch_bounds__(OS_BLOCK, OS_MINB * OS_WAVES / 4) void onesweep_ker
     __shared__ uint64_t s_goff[RADIX];
     __shared__ uint32_t s_wsum[RADIX / 64];
     __shared__ uint32_t s_tile;
+    constexpr int GTX = 64;   // GEN: the tile's transcripts staged (first entry, start); more: searched in HBM
+    __shared__ uint64_t s_gk[GEN ? GTX + 1 : 1], s_gs[GEN ? GTX : 1];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const PassTab T = pass_tab(const_cast<uint32_t *>(scratch), p);
     if (tid == 0) {
@@ -277,10 +315,45 @@ __global__ __launch_bounds__(OS_BLOCK, OS_MINB * OS_WAVES / 4) void onesweep_ker
     const uint64_t n = std::min<uint64_t>(t0 + OS_TILE, T.segoff[sg + 1]);   // keys [t0, n)
     const uint64_t wbase = t0 + (uint64_t)w * (64 * OS_ITEMS) + (uint64_t)lane;
     uint64_t k[OS_ITEMS];
+    if constexpr (GEN) {
+        // the tile's transcripts from its first: their first entries and starts
+        const uint32_t tf = G.tile_tx[tile];
+        for (int q = tid; q <= GTX; q += OS_BLOCK) {
+            const uint32_t t = tf + (uint32_t)q;
+            s_gk[q] = t <= G.n_tx ? G.koff[t] : ~0ull;
+            if (q < GTX) s_gs[q] = t < G.n_tx ? G.tx[t].start : 0ull;
+        }
+        __syncthreads();
 #pragma unroll
-    for (int j = 0; j < OS_ITEMS; j++) {
-        const uint64_t i = wbase + (uint64_t)j * 64;
-        k[j] = i < n ? in[i] : 0ull;
+        for (int j = 0; j < OS_ITEMS; j++) {
+            const uint64_t i = wbase + (uint64_t)j * 64;
+            uint64_t key = 0;
+            if (i < n) {
+                uint64_t st, k0;
+                if (s_gk[GTX] > i) {   // among the staged transcripts: last q with first entry <= i
+                    int lo = 0, hi = GTX;
+                    while (hi - lo > 1) {
+                        const int mid = (lo + hi) >> 1;
+                        if (s_gk[mid] <= i) lo = mid; else hi = mid;
+                    }
+                    st = s_gs[lo];
+                    k0 = s_gk[lo];
+                } else {
+                    const uint32_t t = gen_tx_of(G.koff, G.n_tx, i);
+                    st = G.tx[t].start;
+                    k0 = G.koff[t];
+                }
+                const uint64_t pos = st + (i - k0);
+                key = ((uint64_t)(uint32_t)win(G.F, pos) << 32) | pos;
+            }
+            k[j] = key;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < OS_ITEMS; j++) {
+            const uint64_t i = wbase + (uint64_t)j * 64;
+            k[j] = i < n ? in[i] : 0ull;
+        }
     }
     // the tile's digit counts
 #pragma unroll
@@ -415,6 +488,7 @@ uint64_t os_scratch_words(uint64_t n) { return OS_FIXED_WORDS + (n + OS_TILE - 1
 // The index fill and the segment histograms of a 32-bit-key sort (bb = 32)
 // in one kernel (transcripts without ambiguity codes; koff: first entry of
 // each transcript); os_sort_keys(..., counted = true) then skips its count.
+// ent == nullptr: counts only (the sort's first pass then generates the keys: os_sort_keys with gen).
 void os_fill_hist(const TxInfo *tx, uint32_t n_tx, const uint64_t *F, const uint64_t *koff, uint64_t *ent,
                   uint64_t n, uint32_t *scratch, hipStream_t st)
 {
@@ -427,8 +501,15 @@ void os_fill_hist(const TxInfo *tx, uint32_t n_tx, const uint64_t *F, const uint
                        n_tx, F, koff, ent, np, segsize, scratch);
 }
 
+// gen (bb = 32, counted): the first pass computes the keys from the packed
+// sequence F of the transcripts tx[0, n_tx) with first entries koff[0, n_tx]
+// (keys need not hold them); gen_tile: scratch of os_gen_tile_words(n) u32.
+uint64_t os_gen_tile_words(uint64_t n) { return (n + OS_TILE - 1) / OS_TILE + OS_SEG; }
+
 bool os_sort_keys(uint64_t *keys, uint64_t *alt, uint64_t n, int bb, uint32_t *scratch, uint64_t *status,
-                  uint32_t &epoch, hipStream_t st, const std::function<void()> &after_prep, bool counted)
+                  uint32_t &epoch, hipStream_t st, const std::function<void()> &after_prep, bool counted,
+                  const TxInfo *gen_tx, const uint64_t *gen_koff, const uint64_t *gen_F, uint32_t gen_ntx,
+                  uint32_t *gen_tile)
 {
     const int np = (64 - bb + 7) / 8;
     if (n == 0) return false;
@@ -444,12 +525,20 @@ bool os_sort_keys(uint64_t *keys, uint64_t *alt, uint64_t n, int bb, uint32_t *s
     const uint32_t tmax = (uint32_t)((n + OS_TILE - 1) / OS_TILE + OS_SEG);
     const unsigned grid = tmax;   // tiles beyond a pass's count exit at once
     uint64_t *src = keys, *dst = alt;
+    const bool gen = counted && gen_koff && bb == 32;
+    KeyGen G{gen_tx, gen_koff, gen_F, gen_ntx, gen_tile};
     for (int p = 0; p < np; p++) {
         hipLaunchKernelGGL(tile_order_kernel, dim3((tmax + 255) / 256), dim3(256), 0, st, scratch, p, order, tmax);
+        if (p == 0 && gen)
+            hipLaunchKernelGGL(gen_tile_tx_kernel, dim3((tmax + 255) / 256), dim3(256), 0, st, scratch, G, tmax);
         if (p == 0 && after_prep) after_prep();
         ++epoch;
-        hipLaunchKernelGGL(onesweep_kernel, dim3(grid), dim3(OS_BLOCK), 0, st, src, dst, bb + 8 * p, scratch, p,
-                           order, (gu64 *)status, epoch, ctr + p, n);
+        if (p == 0 && gen)
+            hipLaunchKernelGGL(onesweep_kernel<true>, dim3(grid), dim3(OS_BLOCK), 0, st, src, dst, bb + 8 * p, scratch,
+                               p, order, (gu64 *)status, epoch, ctr + p, n, G);
+        else
+            hipLaunchKernelGGL(onesweep_kernel<false>, dim3(grid), dim3(OS_BLOCK), 0, st, src, dst, bb + 8 * p,
+                               scratch, p, order, (gu64 *)status, epoch, ctr + p, n, G);
         std::swap(src, dst);
     }
     return src == alt;
