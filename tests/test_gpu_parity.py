@@ -381,3 +381,65 @@ def test_repeat_runs_identical(native):
     assert all(np.array_equal(a, b) for a, b in zip(h1, h2))
     assert np.array_equal(m1, m2)
 
+
+
+def _with_degenerate(s, rng, gene0, only=False):
+    """Sample s plus transcripts the index and DUST must get right at their
+    edges: 1, 15, 16 and 17 bases (no 16-mer, exactly one, two), all-N, a
+    300-base poly-A run, a dinucleotide repeat and a 16-mer flanked by N.
+    only=True keeps just those."""
+    from rna_clique_amd.simulate import Sample
+    extra = [b"A", b"ACGTACGTACGTACG", b"ACGTTGCAACGTTGCA", b"ACGTTGCAACGTTGCAT", b"N" * 300,
+             b"A" * 300, b"AC" * 150,
+             b"N" * 20 + bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), 16)) + b"N" * 20]
+    seqs = [] if only else [s.seq.tobytes()]
+    lens = [] if only else list(np.diff(s.tx_offsets.astype(np.int64)))
+    for x in extra:
+        seqs.append(x)
+        lens.append(len(x))
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    k = len(extra)
+    keep = 0 if only else s.n_tx
+    return Sample(s.name, np.frombuffer(b"".join(seqs), dtype=np.uint8).copy(), offs,
+                  np.concatenate([s.gene[:keep], np.arange(gene0, gene0 + k)]).astype(np.int32),
+                  np.concatenate([s.iso[:keep], np.ones(k)]).astype(np.int32),
+                  np.concatenate([s.cov[:keep], 1.0 + np.arange(k) / 7.0]))
+
+
+@pytest.mark.parametrize("dust", [None, False])
+def test_degenerate_transcripts(native, dust):
+    """Transcripts shorter than a 16-mer, exactly one or two 16-mers long,
+    all-N, wholly low-complexity (DUST masks every base), plus one sample made
+    of nothing else: the index fill's per-transcript slots, the sort's
+    segments and DUST's ends are where these break. Parity with the oracle
+    on every output; and a run whose index is empty (no transcript holds a
+    16-mer) ends with no HSPs and the reference's no-ideal-components error."""
+    from rna_clique_amd._native import NativeError, RC_E_NO_IDEAL
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(3, 80, seed=52, p_iso2=0.2, polya=(0.3, 10, 40))
+    rng = np.random.default_rng(52)
+    samples = [_with_degenerate(s, rng, 100000) for s in samples]
+    samples.append(_with_degenerate(samples[0], rng, 200000, only=True))
+    samples[-1].name = "only_degenerate"
+    eng = _run_sim(samples, dust=dust)
+    msgs, summary = full_check(eng, samples)
+    assert not msgs, "\n".join(msgs[:10])
+    assert summary["hsps"] > 0 and summary["ideal_nodes"] > 0
+    eng.close()
+    tiny = []
+    for i, s in enumerate(simulate(2, 10, seed=53)[0]):
+        t = _with_degenerate(s, rng, 300000, only=True)
+        keep = [j for j in range(t.n_tx) if t.tx_offsets[j + 1] - t.tx_offsets[j] < 16]
+        seq = b"".join(t.seq[t.tx_offsets[j]:t.tx_offsets[j + 1]].tobytes() for j in keep)
+        lens = [int(t.tx_offsets[j + 1] - t.tx_offsets[j]) for j in keep]
+        t.seq = np.frombuffer(seq, dtype=np.uint8).copy()
+        t.tx_offsets = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        t.gene, t.iso, t.cov = t.gene[keep], t.iso[keep], t.cov[keep]
+        tiny.append(t)
+    eng = _run_sim(tiny, dust=dust)
+    assert all(len(eng.hsps(q, s)) == 0 for q in range(2) for s in range(2) if q != s)
+    assert len(eng.edges()) == 0
+    with pytest.raises(NativeError) as ei:
+        eng.distance()
+    assert ei.value.code == RC_E_NO_IDEAL
+    eng.close()
