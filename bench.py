@@ -419,13 +419,20 @@ def main():
         # per step over its measured time vs the VALU issue peak (a wave64
         # instruction holds a 32-lane SIMD for 2 clocks)
         iss = prof["issue"]
-        t_ext = tm["align_kernel_ms"] * 1e-3
+        # the row kernel's own time (kernel trace of the same sources) when the
+        # profile has it; else every extension kernel's live time (an upper bound)
+        own = iss.get("kernel_ms")
+        t_ext = (own if own else tm["align_kernel_ms"]) * 1e-3
         peak = iss.get("valu_peak_g_per_s", 256 * 4 * 2.4 / 2)
         roof["issue_extension"] = {"bound": "valu", "unit": "G wave-VALU/s",
                                    "achieved": round(iss["valu"] / t_ext / 1e9, 1), "peak": peak,
                                    "frac": round(iss["valu"] / t_ext / 1e9 / peak, 4),
                                    "salu_g_per_s": round(iss["salu"] / t_ext / 1e9, 1),
-                                   "valu_per_wave_step": iss.get("valu_per_wave_step")}
+                                   "valu_per_wave_step": iss.get("valu_per_wave_step"),
+                                   "kernel": iss.get("kernel", "extend_rows_kernel"),
+                                   "kernel_ms": round(t_ext * 1e3, 3),
+                                   "kernel_ms_source": iss.get("kernel_ms_source") if own else
+                                   "live extension kernels (HIP events)"}
     if cpu:
         cpu["gpu_speedup"] = round(value / cpu["value"], 1)
     line = {

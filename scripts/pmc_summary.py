@@ -1,6 +1,12 @@
 """Summarise rocprofv3 PMC passes (scripts/gpu_pmc.sh) per kernel.
 
 Usage: python scripts/pmc_summary.py gpurun_out/pmc_C3 profiles/<round>/C3_pmc.json [commit]
+       [kernel_stats.csv runs]
+
+With a `rocprofv3 --kernel-trace --stats` CSV of the same sources and the
+number of bench steps it covers (warmup included), the issue entry also
+carries the row kernel's own time per step, so bench.py can price its VALU
+count against that kernel alone rather than against every extension kernel.
 
 The summary is stamped with bench.src_hash() of the sources in this tree
 (run it on the tree the profile was measured on); bench.py reports PMC
@@ -46,7 +52,17 @@ def _ext_steps(src):
     return None
 
 
-def main(src, dst, commit=None):
+def _rows_ms(stats, runs):
+    """extend_rows_kernel<..., 32, ...> (the sliding rows) ms per step from a
+    kernel-stats CSV covering `runs` steps."""
+    tot = 0.0
+    for r in csv.DictReader(open(stats)):
+        if "extend_rows_kernel" in r["Name"] and ", 32," in r["Name"]:
+            tot += float(r["TotalDurationNs"])
+    return round(tot / 1e6 / runs, 3) if tot else None
+
+
+def main(src, dst, commit=None, stats=None, runs=None):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from bench import src_hash
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -69,6 +85,9 @@ def main(src, dst, commit=None):
         out["issue"] = {"kernel": "extend_rows_kernel", "wave_instr": wi, "valu_peak_g_per_s": VALU_PEAK_G,
                         "valu": ext.get("SQ_INSTS_VALU"), "salu": ext.get("SQ_INSTS_SALU"),
                         "valu_per_wave_step": round(ext["SQ_INSTS_VALU"] / (steps / 2), 1) if steps else None}
+        if stats:
+            out["issue"]["kernel_ms"] = _rows_ms(stats, int(runs))
+            out["issue"]["kernel_ms_source"] = stats
     with open(dst, "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
     print(json.dumps({k: out["kernels"].get(k) for k in ("seed_kernel", "extend_rows_kernel")}, indent=1))
