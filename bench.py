@@ -119,6 +119,26 @@ def pmc_profile(config, world):
     return None
 
 
+def issue_roofline(iss, align_kernel_ms):
+    """The extension's issue roofline: it is bound by VALU issue, not bytes.
+    The row kernel's VALU instructions per step (PMC summary `issue`) over
+    that kernel's own time per step (kernel trace of the same sources, when
+    the summary has it; else every extension kernel's live HIP-event time, an
+    upper bound) against the VALU issue peak (a wave64 instruction holds a
+    32-lane SIMD for 2 clocks)."""
+    own = iss.get("kernel_ms")
+    t_ext = (own if own else align_kernel_ms) * 1e-3
+    peak = iss.get("valu_peak_g_per_s", 256 * 4 * 2.4 / 2)
+    return {"bound": "valu", "unit": "G wave-VALU/s",
+            "achieved": round(iss["valu"] / t_ext / 1e9, 1), "peak": peak,
+            "frac": round(iss["valu"] / t_ext / 1e9 / peak, 4),
+            "salu_g_per_s": round(iss["salu"] / t_ext / 1e9, 1),
+            "valu_per_wave_step": iss.get("valu_per_wave_step"),
+            "kernel": iss.get("kernel", "extend_rows_kernel"),
+            "kernel_ms": round(t_ext * 1e3, 3),
+            "kernel_ms_source": iss.get("kernel_ms_source") if own else "live extension kernels (HIP events)"}
+
+
 _CPU_SAMPLES = None
 
 
@@ -415,24 +435,7 @@ def main():
             "kernel": "seed_kernel + extension kernels", "kernel_ms": round(avg_k, 3),
             "bytes_per_launch": int(bytes_launch)}
     if prof and prof.get("issue"):
-        # the extension is bound by VALU issue, not bytes: its VALU instructions
-        # per step over its measured time vs the VALU issue peak (a wave64
-        # instruction holds a 32-lane SIMD for 2 clocks)
-        iss = prof["issue"]
-        # the row kernel's own time (kernel trace of the same sources) when the
-        # profile has it; else every extension kernel's live time (an upper bound)
-        own = iss.get("kernel_ms")
-        t_ext = (own if own else tm["align_kernel_ms"]) * 1e-3
-        peak = iss.get("valu_peak_g_per_s", 256 * 4 * 2.4 / 2)
-        roof["issue_extension"] = {"bound": "valu", "unit": "G wave-VALU/s",
-                                   "achieved": round(iss["valu"] / t_ext / 1e9, 1), "peak": peak,
-                                   "frac": round(iss["valu"] / t_ext / 1e9 / peak, 4),
-                                   "salu_g_per_s": round(iss["salu"] / t_ext / 1e9, 1),
-                                   "valu_per_wave_step": iss.get("valu_per_wave_step"),
-                                   "kernel": iss.get("kernel", "extend_rows_kernel"),
-                                   "kernel_ms": round(t_ext * 1e3, 3),
-                                   "kernel_ms_source": iss.get("kernel_ms_source") if own else
-                                   "live extension kernels (HIP events)"}
+        roof["issue_extension"] = issue_roofline(prof["issue"], tm["align_kernel_ms"])
     if cpu:
         cpu["gpu_speedup"] = round(value / cpu["value"], 1)
     line = {
