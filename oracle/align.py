@@ -101,14 +101,17 @@ class OracleDB:
         gene_tx_off, gene_tx, gene_sample, gene_id = [0], [], [], []
         self.tx_gene = np.zeros(len(tx_sample), dtype=np.int64)
         for si, s in enumerate(samples):
+            # genes in ascending id, each gene's transcripts in input order (a
+            # stable sort by gene id)
             g = np.asarray(s.gene)
-            for gid in np.unique(g):
-                members = np.nonzero(g == gid)[0] + self.tx_base[si]
-                self.tx_gene[members] = len(gene_sample)
-                gene_tx.extend(members.tolist())
-                gene_tx_off.append(len(gene_tx))
-                gene_sample.append(si)
-                gene_id.append(int(gid))
+            order = np.argsort(g, kind="stable")
+            gids, first, counts = np.unique(g[order], return_index=True, return_counts=True)
+            members = order + self.tx_base[si]
+            self.tx_gene[members] = len(gene_sample) + np.repeat(np.arange(len(gids)), counts)
+            gene_tx.extend(members.tolist())
+            gene_tx_off.extend((len(gene_tx) - len(members) + first + counts).tolist())
+            gene_sample.extend([si] * len(gids))
+            gene_id.extend(gids.tolist())
         self.gene_tx_off = np.array(gene_tx_off, dtype=np.uint32)
         self.gene_tx = np.array(gene_tx, dtype=np.uint32)
         self.gene_sample = np.array(gene_sample, dtype=np.int32)

@@ -175,6 +175,42 @@ def full_check(engine, samples, word_size=28, xdrop_half=108, evalue=1e-99,
     return msgs, summary
 
 
+def capture_pairs(engine, pairs):
+    """The engine's side of check_pairs, copied to the host (so that the
+    engine can be closed before the oracle finishes): per pair (a, b) both
+    directed searches' HSPs, the gene matches table rows and the unfiltered
+    sums. The engine must have its graph phase done (pair_sums)."""
+    num, den = engine.pair_sums(unfiltered=True)
+    out = {}
+    for a, b in pairs:
+        out[(a, b)] = {"hsps": {(0, 1): engine.hsps(a, b), (1, 0): engine.hsps(b, a)},
+                       "rows": engine.pair_rows(a, b), "usums": (int(num[a, b]), int(den[a, b]))}
+    return {"labels": list(engine.labels), "pairs": out,
+            "symmetric": getattr(engine, "symmetric", False), "dust": getattr(engine, "dust", None)}
+
+
+def compare_pair(cap, samples, a, b, db, ora, top_matches=1, keep_all=True):
+    """A captured pair (capture_pairs) against the oracle's two directed
+    searches of it: db = OracleDB([samples[a], samples[b]]), ora = {(0, 1):
+    db.align(0, 1, ...), (1, 0): db.align(1, 0, ...)}. HSPs bit for bit, then
+    the pair's table through the pinned post-alignment oracle and its
+    unfiltered sums. Returns messages (empty = parity)."""
+    got = cap["pairs"][(a, b)]
+    names = cap["labels"]
+    msgs = []
+    for (q, s), arr in ora.items():
+        msgs += [f"pair {a},{b}: {m}" for m in diff_hsps(got["hsps"][(q, s)], arr, db, q, s)]
+    pn = [names[a], names[b]]
+    hits = hits_for_post([samples[a], samples[b]], db, ora, pn)
+    out = post_oracle.run_pipeline(pn, hits, post_oracle.default_parse_id, top_matches, keep_all)
+    table = out["tables"][(pn[0], pn[1])]
+    msgs += diff_rows(got["rows"], table, f"pair {a},{b}")
+    want = (sum(r["nident"] for r in table), sum(r["length"] - r["gaps"] for r in table))
+    if got["usums"] != want:
+        msgs.append(f"pair {a},{b}: unfiltered sums {got['usums']} vs {want}")
+    return msgs
+
+
 def check_pairs(engine, samples, pairs, word_size=28, xdrop_half=108, evalue=1e-99,
                 top_matches=1, keep_all=True, threads=None):
     """Bit-exact check of selected sample pairs of a (large) engine run: for
@@ -183,27 +219,15 @@ def check_pairs(engine, samples, pairs, word_size=28, xdrop_half=108, evalue=1e-
     the pair's table through the pinned post-alignment oracle, and the pair's
     unfiltered sums. Returns messages (empty = parity)."""
     from concurrent.futures import ThreadPoolExecutor
-    names = list(engine.labels)
-    sym, dust = getattr(engine, "symmetric", False), getattr(engine, "dust", None)
+    cap = capture_pairs(engine, pairs)
+    sym, dust = cap["symmetric"], cap["dust"]
     dbs = {(a, b): OracleDB([samples[a], samples[b]]) for a, b in pairs}
     jobs = [(a, b, q, s) for a, b in pairs for q, s in ((0, 1), (1, 0))]
     run = lambda j: dbs[j[:2]].align(j[2], j[3], word_size, xdrop_half, evalue, sym, dust)  # noqa: E731
     with ThreadPoolExecutor(threads or oracle_threads()) as ex:
         res = dict(zip(jobs, ex.map(run, jobs)))
-    num, den = engine.pair_sums(unfiltered=True)
     msgs = []
     for a, b in pairs:
-        db = dbs[(a, b)]
         ora = {(0, 1): res[(a, b, 0, 1)], (1, 0): res[(a, b, 1, 0)]}
-        for (q, s), arr in ora.items():
-            got = engine.hsps((a, b)[q], (a, b)[s])
-            msgs += [f"pair {a},{b}: {m}" for m in diff_hsps(got, arr, db, q, s)]
-        pn = [names[a], names[b]]
-        hits = hits_for_post([samples[a], samples[b]], db, ora, pn)
-        out = post_oracle.run_pipeline(pn, hits, post_oracle.default_parse_id, top_matches, keep_all)
-        table = out["tables"][(pn[0], pn[1])]
-        msgs += diff_rows(engine.pair_rows(a, b), table, f"pair {a},{b}")
-        want = (sum(r["nident"] for r in table), sum(r["length"] - r["gaps"] for r in table))
-        if (int(num[a, b]), int(den[a, b])) != want:
-            msgs.append(f"pair {a},{b}: unfiltered sums {(int(num[a, b]), int(den[a, b]))} vs {want}")
+        msgs += compare_pair(cap, samples, a, b, dbs[(a, b)], ora, top_matches, keep_all)
     return msgs

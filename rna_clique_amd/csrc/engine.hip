@@ -2579,11 +2579,14 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
     int in_flight = 0, err = RC_OK;
     std::string err_msg;
     auto set_err = [&](int code) {
-        std::lock_guard<std::mutex> lk(mu);
-        if (err == RC_OK) {
-            err = code;
-            err_msg = rc_last_error();
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            if (err == RC_OK) {
+                err = code;
+                err_msg = rc_last_error();
+            }
         }
+        cv.notify_all();   // the fetch loop may be waiting for room
     };
     auto worker = [&]() {
         std::vector<rc_row> buf;
@@ -2615,12 +2618,14 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
     };
     auto grapher = [&]() {
         rc_gpickle *g = nullptr;
+        bool ok = true;
         if (rc_graph_pickle_begin(&g) != RC_OK) {
+            // keep draining the queue (in_flight must still go down)
             set_err(RC_E_NOMEM);
-            return;
+            g = nullptr;
+            ok = false;
         }
         std::vector<int64_t> sg, qg;
-        bool ok = true;
         for (;;) {
             std::pair<int, std::shared_ptr<PairRaw>> job;
             {

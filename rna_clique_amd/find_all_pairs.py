@@ -18,7 +18,6 @@ on a thread pool of `jobs` workers.
 from __future__ import annotations
 
 import itertools
-import math
 import multiprocessing
 import threading
 from concurrent.futures import ThreadPoolExecutor
@@ -73,9 +72,10 @@ def find_all_pairs(inputs: Iterable[Path], output_dir: Path, cache_dir: Optional
             if (a, b) in out_paths:
                 yield pair_table(eng, a, b)
     # the table files in combinations order; a sharded run (rank of a
-    # torch.distributed group) returns the pairs it owns and wrote only
+    # torch.distributed group) returns the pairs it owns and wrote only, and
+    # counts those (unsharded: all C(N, 2), the reference's count)
     paths = (out_paths[ab] for ab in itertools.combinations(range(len(inputs)), 2) if ab in out_paths)
-    return tables(), paths, math.comb(len(inputs), 2)
+    return tables(), paths, len(out_paths)
 
 
 def write_pair_tables(eng, inputs, output_dir, path_to_sample, ext, jobs: int = 8, graph_path=None) -> dict:

@@ -128,7 +128,9 @@ def _hky85_mutate_sparse(seq, expected_subs, rng, kappa=2.0, inplace=False):
     n = seq.size
     k = rng.binomial(n, 1.0 - math.exp(-expected_subs))
     if k == 0:
-        return seq
+        # a copy unless this is the parent's last use: a sibling mutated in
+        # place later must not rewrite this one
+        return seq if inplace else seq.copy()
     pos = np.unique(rng.integers(0, n, size=k))
     r = rng.random(pos.size) * (kappa + 2.0)
     old = seq[pos]

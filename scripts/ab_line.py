@@ -1,4 +1,4 @@
-"""One summary line of a bench JSON (scripts/gpu_ab.sh)."""
+"""One summary line of a bench JSON (scripts/gpu_ab_env.sh)."""
 import json
 import sys
 

@@ -134,6 +134,91 @@ def test_C4_eight_shards_match_unsharded(native):
     g.close()
 
 
+def test_graph_phase_at_C5_size(native):
+    """The graph phase alone at C5's size (build_graph.py:40-68,
+    filtered_distance.py:30-39): 128 samples x 100 000 genes (12.8 M nodes)
+    and every pair's edge of every gene family -- 8.1 x 10^8 edge records,
+    16 GB, as a graph-only engine holds them after the 8-rank all-gather.
+    Families are 128-cliques (ideal) except: f % 10 == 0 misses its (0, 1)
+    edge (not complete), f % 10 == 5 gains an edge to family f + 1 (one
+    component of 256 nodes). Components, ideal components and nodes, the
+    filtered and unfiltered sums of every pair and the matrix are known in
+    closed form."""
+    from rna_clique_amd.engine import Engine
+    N, G = 128, 100_000
+    rs = Engine.edge_record_size()
+    dt = np.dtype([("a", np.uint32), ("b", np.uint32), ("pair", np.uint32), ("nident", np.int32),
+                   ("den", np.int32)])
+    assert dt.itemsize == rs
+    f = np.arange(G, dtype=np.uint32)
+    nid = (1000 + f % 7).astype(np.int32)
+    dn = (1100 + f % 3).astype(np.int32)
+    drop = f % 10 == 0
+    extra = np.nonzero(f % 10 == 5)[0].astype(np.uint32)
+    n_pairs = N * (N - 1) // 2
+    n = n_pairs * G - int(drop.sum()) + len(extra)
+    with _heartbeat(f"graph at C5 size: {n} edge records"):
+        rec = np.zeros(n, dtype=dt)
+        w = 0
+        keep01 = f[~drop]
+        for b in range(1, N):
+            for a in range(b):
+                p = b * (b - 1) // 2 + a   # a single shard's pair order: subject-major
+                ff = keep01 if (a, b) == (0, 1) else f
+                k = len(ff)
+                sl = rec[w:w + k]
+                sl["a"] = a * G + ff
+                sl["b"] = b * G + ff
+                sl["pair"] = p
+                sl["nident"] = nid[ff]
+                sl["den"] = dn[ff]
+                w += k
+        sl = rec[w:]
+        sl["a"] = extra            # sample 0, family f
+        sl["b"] = G + extra + 1    # sample 1, family f + 1
+        sl["pair"] = 0
+        sl["nident"] = 7
+        sl["den"] = 9
+        assert w + len(extra) == n
+        g = Engine(device=0)
+        for s in range(N):
+            g.add_sample(f"S{s:03d}", None, np.arange(G + 1, dtype=np.uint64) * 1000,
+                         np.arange(1, G + 1, dtype=np.int32), np.ones(G, dtype=np.int32))
+        t0 = __import__("time").perf_counter()
+        g.import_edges(rec.view(np.uint8))
+        t_import = __import__("time").perf_counter() - t0
+        del rec, sl
+        st = g.stats()
+        ideal = (f % 10 != 0) & (f % 10 != 5) & (f % 10 != 6)
+        assert st["edges"] == n
+        assert st["nodes"] == N * G
+        assert st["components"] == G - len(extra)
+        assert st["ideal_components"] == int(ideal.sum())
+        assert st["ideal_nodes"] == int(ideal.sum()) * N
+        assert st["sample_count"] == N
+        num, den = g.pair_sums()
+        unum, uden = g.pair_sums(unfiltered=True)
+        want_n, want_d = int(nid[ideal].astype(np.int64).sum()), int(dn[ideal].astype(np.int64).sum())
+        off = ~np.eye(N, dtype=bool)
+        assert np.all(num[off] == want_n) and np.all(den[off] == want_d)
+        all_n, all_d = int(nid.astype(np.int64).sum()), int(dn.astype(np.int64).sum())
+        u01 = (all_n - int(nid[drop].astype(np.int64).sum()) + 7 * len(extra),
+               all_d - int(dn[drop].astype(np.int64).sum()) + 9 * len(extra))
+        assert (int(unum[0, 1]), int(uden[0, 1])) == u01 == (int(unum[1, 0]), int(uden[1, 0]))
+        m01 = np.zeros((N, N), dtype=bool)
+        m01[0, 1] = m01[1, 0] = True
+        assert np.all(unum[off & ~m01] == all_n) and np.all(uden[off & ~m01] == all_d)
+        labels, mat = g.distance()
+        assert labels == [f"S{s:03d}" for s in range(N)]
+        want = np.full((N, N), (want_d - want_n) / want_d)
+        np.fill_diagonal(want, 0.0)
+        assert np.array_equal(mat, want)
+        tm = g.timings()
+        _record("graph_C5_size", {"edges": n, "import_s": t_import, "graph_ms": tm["graph_ms"],
+                                  "reduce_ms": tm["reduce_ms"], "device_gb": tm["dev_bytes"] / 1e9})
+        g.close()
+
+
 def test_C5_one_rank_shard(native):
     import torch
     from bench import shard_samples
