@@ -130,6 +130,11 @@ typedef struct rc_timing {
                                  redone on 64-lane rows (the spec's whole band) */
     double dev_bytes;         /* device memory the engines of this process hold now (bytes) */
     double dev_peak_bytes;    /* ... and the most they held at once */
+    double defer_length;      /* candidates with a transcript past the row kernels' staging slot */
+    double defer_gaveup;      /* directed searches the one-wave kernel took because the row kernels gave
+                                 up on their first seed (transcript length) */
+    double defer_outside;     /* directed searches the one-wave kernel took because a seed lies outside
+                                 their first HSP's box (more than one HSP) */
 } rc_timing;
 
 void rc_default_opts(rc_opts *opts);

@@ -1829,6 +1829,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 const int nwq = (int)(((q0 & 31) + (uint64_t)Lq) >> 5) + 3;
                 const int nwt = (int)(((s0 & 31) + (uint64_t)Lt) >> 5) + 3;
                 if (nwq > sw || nwt > sw || (Lq >> 5) + 3 > sw || (Lt >> 5) + 3 > sw) {
+                    if (rl == 0 && row_args()->P.why) atomicAdd(&row_args()->P.why[0], 1ull);
                     defer(ci, false);
                     continue;
                 }
@@ -2211,6 +2212,7 @@ __global__ __launch_bounds__(256) void first_finish_kernel(ExtParams P)
                 (dir ? P.defer_r : P.defer)[di] = (uint32_t)ci;
             };
             if (fx[FX_STATUS] < 0) {   // (shared searches) the row kernel gave it up
+                if (P.why) atomicAdd(&P.why[1], 1ull);
                 defer_dir();
                 continue;
             }
@@ -2230,6 +2232,7 @@ __global__ __launch_bounds__(256) void first_finish_kernel(ExtParams P)
                 all_in = bqa <= (int)s.x && (int)s.x + sl <= bqb && bsa <= (int)s.y && (int)s.y + sl <= bsb;
             }
             if (!all_in) {
+                if (P.why) atomicAdd(&P.why[2], 1ull);
                 defer_dir();
                 continue;
             }

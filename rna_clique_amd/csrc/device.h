@@ -262,6 +262,11 @@ struct ExtParams {
     // 64-lane pass continues it instead of starting over (RES_REC ints each)
     int32_t *resume;
     uint32_t res_cap;
+    // why searches leave the row kernels: [0] a transcript past the staging
+    // slot (row kernel), [1] a directed search whose first seed the row
+    // kernels gave up on, [2] one with a seed outside its first HSP's box
+    // (first_finish_kernel)
+    unsigned long long *why;
 };
 constexpr int RES_REC = 80;   // phase, kof, d6, best, best record (i, gap, d6, diagonal), right results, R[32], goe[32]
 

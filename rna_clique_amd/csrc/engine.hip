@@ -1694,7 +1694,7 @@ static int align_tile(rc_engine *e, int ti)
         HIPCHK(hipMemsetAsync(e->d_count.p, 0, 12 * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_count.p + 14, 0, 2 * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_count.p + 17, 0, 2 * sizeof(unsigned long long), e->st));
-        HIPCHK(hipMemsetAsync(e->d_count.p + 20, 0, 4 * sizeof(unsigned long long), e->st));
+        HIPCHK(hipMemsetAsync(e->d_count.p + 20, 0, 7 * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
         ExtParams X{};
         X.xdrop = e->o.xdrop_half;
@@ -1750,6 +1750,7 @@ static int align_tile(rc_engine *e, int ti)
         }
         X.work_w0 = e->d_count.p + 22;
         X.work_w1 = e->d_count.p + 23;
+        X.why = e->d_count.p + 24;   // [24, 27): deferral causes
         {
             const char *cv = getenv("RC_ROW_CHUNK");
             X.chunk = cv ? atoi(cv) : 8;
@@ -1769,6 +1770,8 @@ static int align_tile(rc_engine *e, int ti)
         HIPCHK(hipMemcpyAsync(&nfull, e->d_count.p + 14, sizeof nfull, hipMemcpyDeviceToHost, e->st));
         unsigned long long nwide[2] = {0, 0};   // shared searches: candidates the 64-lane passes took
         HIPCHK(hipMemcpyAsync(nwide, e->d_count.p + 20, sizeof nwide, hipMemcpyDeviceToHost, e->st));
+        unsigned long long why[3] = {0, 0, 0};
+        HIPCHK(hipMemcpyAsync(why, e->d_count.p + 24, sizeof why, hipMemcpyDeviceToHost, e->st));
         unsigned long long ndr = 0, nl2 = 0;   // shared searches: reverse searches redone whole, second first seeds
         HIPCHK(hipMemcpyAsync(&ndr, e->d_count.p + 17, sizeof ndr, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipMemcpyAsync(&nl2, e->d_count.p + 16, sizeof nl2, hipMemcpyDeviceToHost, e->st));
@@ -1797,6 +1800,9 @@ static int align_tile(rc_engine *e, int ti)
             e->tm.ext_slides += (double)ctr[4];
             e->tm.ext_wide += (double)(nwide[0] + nwide[1]);
             e->tm.maxhsp_bound += (double)ctr[10];
+            e->tm.defer_length += (double)why[0];
+            e->tm.defer_gaveup += (double)why[1];
+            e->tm.defer_outside += (double)why[2];
             break;
         }
         e->ovf_cap = std::max<uint64_t>(e->ovf_cap, ovn * 5 / 4 + 1024);

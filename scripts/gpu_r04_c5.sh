@@ -14,4 +14,8 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_scale.py -k graph_phase_at_
 rc=$?; echo "graph test rc=$rc"; tail -3 gpurun_out/r04_c5/graph_test.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 780 python -u scripts/c5_full.py --config C5 --out gpurun_out/r04_c5/c5_full.json > gpurun_out/r04_c5/c5_full.log 2>&1
 rc=$?; echo "C5 full rc=$rc"; tail -4 gpurun_out/r04_c5/c5_full.log
+case $rc in 0|1) ;; *) exit $rc;; esac
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r04_c5/prof_C5s2 -o run -- python3 bench.py --config C5 --shard 2/8 --steps 1 --warmup 0 --no-cpu-baseline --no-e2e > gpurun_out/r04_c5/prof_C5s2.log 2>&1
+echo "C5 shard-2 rocprof rc=$?"
 exit $rc
