@@ -176,6 +176,32 @@ def cpu_baseline(samples, workers, n_pairs):
     return done / dt, dt, done
 
 
+def cpu_workers(samples, forced=0):
+    """(processes, how chosen) for the CPU baseline: every core this process
+    may use (affinity mask and cgroup quota, oracle.parity.usable_cores),
+    unless host memory cannot hold that many concurrent pair tasks (a task
+    holds a subject index of 24 B per seed position while it sorts it, and
+    the two samples' base codes)."""
+    import numpy as np
+    from oracle.parity import usable_cores
+    uc = usable_cores()
+    if forced:
+        return forced, dict(uc, forced=forced)
+    P = max(int(np.maximum(np.diff(s.tx_offsets.astype(np.int64)) - 15, 0).sum()) for s in samples)
+    L = max(int(s.tx_offsets[-1]) for s in samples)
+    per_task = 24 * P + 2 * L + (64 << 20)
+    try:
+        import psutil
+        avail = psutil.virtual_memory().available
+    except ImportError:
+        avail = 64 << 30
+    # the GPU box caps one command at ~270 GiB of host memory
+    budget = int(0.6 * min(avail, 250 << 30))
+    by_mem = max(1, budget // per_task)
+    n = max(1, min(uc["cores"], by_mem))
+    return n, dict(uc, memory_cap=int(by_mem), task_bytes=int(per_task))
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -350,12 +376,11 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         # the CPU port on this host's cores, before anything touches the GPU
         # (the device count below included: the pool's workers are forked)
-        from oracle.parity import oracle_threads
-        workers = args.cpu_workers or oracle_threads()
-        n_cpu = args.cpu_pairs or 2 * workers
+        workers, why = cpu_workers(samples, args.cpu_workers)
+        n_cpu = args.cpu_pairs or max(8, workers)
         v, secs, done = cpu_baseline(samples, workers, n_cpu)
         cpu = {"value": round(v, 4), "unit": "sample-pairs/s", "cores": workers, "kind": "port",
-               "cpu": cpu_model(), "extrapolated": True,
+               "cpu": cpu_model(), "extrapolated": True, "cores_how": why,
                "sample": f"{done} of {pairs} {args.config} sample pairs (both directed searches with DUST "
                          f"+ reciprocal best hits / table each, one pair per process, {workers} processes) "
                          f"in {secs:.1f} s; pairs/s extrapolated to the whole workload"}

@@ -33,14 +33,30 @@ def oracle_all_hsps(db: OracleDB, n_samples, word_size=28, xdrop_half=108,
 
 
 def oracle_threads():
-    """Worker threads for the oracle: the cores this process may use, at most
-    16 (the GPU box's CPU share; os.cpu_count() there shows the whole host)."""
+    """Worker threads for the oracle in tests: the cores this process may
+    use, at most 16 (the GPU box's CPU share for test runs)."""
+    return max(1, min(16, usable_cores()["cores"]))
+
+
+def usable_cores():
+    """The CPUs this process may run on: its affinity mask, and the cgroup
+    CPU quota when one is set (cgroup v2 cpu.max). {"cores": min of both,
+    "affinity": n, "quota": q or None}."""
+    import math
     import os
     try:
-        n = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(16, n))
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, math.ceil(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    return {"cores": max(1, min(aff, quota or aff)), "affinity": aff, "quota": quota}
 
 
 def diff_hsps(eng, ora, db: OracleDB, q, s):

@@ -30,7 +30,7 @@ constexpr int SBLOCK = 256;
 constexpr int SEED_CAP = RC_SEED_CAP;   // seeds of one pass in LDS (a power of two: the bitonic sort pads to one)
 static_assert((SEED_CAP & (SEED_CAP - 1)) == 0, "RC_SEED_CAP must be a power of two");
 constexpr int HBATCH = 4;                          // hits per lane per batch of the seed kernel
-constexpr int MAX_SAMPLES = 256;
+constexpr int PASS_SAMPLES = 256;                  // subject samples of one seed pass (per-sample counts in LDS)
 
 constexpr int EBLOCK = 256;
 constexpr int EWAVES = EBLOCK / 64;
@@ -134,7 +134,7 @@ template <bool AMB, bool BIG, bool ISOG>
 __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Index ix, SeedParams P)
 {
     const uint64_t big_e = BIG ? P.big_list[blockIdx.x] : 0ull;
-    const uint32_t g = BIG ? P.gene_begin + (uint32_t)(big_e >> 8)
+    const uint32_t g = BIG ? P.gene_begin + (uint32_t)(big_e >> 16)
                            : (ISOG ? P.iso_list[blockIdx.x] : P.gene_begin + blockIdx.x);
     if (g >= P.gene_end) return;
     const int tid = threadIdx.x;
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
     __shared__ uint64_t iso_start[ISO_LDS];
     __shared__ uint32_t iso_len[ISO_LDS], iso_gtx[ISO_LDS], iso_pre[ISO_LDS + 1];
     __shared__ uint16_t it_iso[SBLOCK];   // isoform of each word item (it_info: p | strand << 24)
-    __shared__ uint32_t tcnt[MAX_SAMPLES], tpre[MAX_SAMPLES + 1];
+    __shared__ uint32_t tcnt[PASS_SAMPLES], tpre[PASS_SAMPLES + 1];   // by subject sample - T0
     __shared__ uint32_t wsum[SBLOCK / 64];
     __shared__ uint32_t sh_nseed, sh_flags, sh_rs0, sh_rs1;
     __shared__ unsigned long long sh_sbase, sh_cbase, sh_lbase;
@@ -172,7 +172,8 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
     const uint64_t total = db.total;
     const int stride = P.stride;
     const uint32_t shard = blockIdx.x % NSHARD;
-    if (niso > (uint32_t)MAX_ISO || N > MAX_SAMPLES) {
+    const int xb = P.xbits;
+    if (niso > P.max_iso) {
         if (tid == 0) atomicOr(P.status, 2u);
         return;
     }
@@ -222,26 +223,35 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
     const uint32_t gl = g - P.gene_begin;
 
     // subject samples of this query sample in this shard (spec 5b: the
-    // higher-numbered ones only, the pair's other direction is the mirror image)
-    const uint64_t tm[4] = {P.tmask[4 * Q], P.tmask[4 * Q + 1], P.tmask[4 * Q + 2], P.tmask[4 * Q + 3]};
+    // higher-numbered ones only, the pair's other direction is the mirror
+    // image): its row of tmask; tm holds the bits of the current pass's
+    // samples [T0, T0 + PASS_SAMPLES) (pass_mask)
+    const uint64_t *const tmrow = P.tmask + (size_t)Q * (size_t)P.tmw;
+    __shared__ uint64_t tm[4];   // (in LDS: the kernel's scalar registers already spill)
+    auto pass_mask = [&](int T0) {   // the caller synchronises before tm is read
+        if (tid < 4) {
+            const int b = T0 + 64 * tid, wi = b >> 6, sh = b & 63;
+            const uint64_t lo = wi < P.tmw ? tmrow[wi] : 0ull, hi = wi + 1 < P.tmw ? tmrow[wi + 1] : 0ull;
+            tm[tid] = (lo >> sh) | ((hi << 1) << (63 - sh));
+        }
+    };
+    auto in_mask = [&](int T, int T0) { return ((tm[(T - T0) >> 6] >> ((T - T0) & 63)) & 1ull) != 0; };
     // passes run over the span [T0, Tr) of the subject samples (a contiguous
     // position range, so hits are filtered by position; the query's own
     // sample, inside the span when both directions are searched, is filtered
     // out by position too), halved [T0, T1) while their seeds overflow the
     // pass capacity; the seed test drops any other sample outside the mask
-    int T0 = N, Tr = 0;
+    int T0, Tr;
     if (BIG) {
-        T0 = (int)(big_e & 0xFFu);
+        T0 = (int)(big_e & 0xFFFFu);
         Tr = T0 + 1;
     } else {
-        for (int w = 0; w < 4; w++)
-            if (tm[w]) {
-                T0 = min(T0, 64 * w + __builtin_ctzll(tm[w]));
-                Tr = max(Tr, 64 * w + 64 - __builtin_clzll(tm[w]));
-            }
+        T0 = P.trange[2 * Q];
+        Tr = P.trange[2 * Q + 1];
         if (P.sym || P.share) T0 = max(T0, Q + 1);
     }
-    int T1 = Tr;
+    int T1 = min(Tr, T0 + PASS_SAMPLES);
+    pass_mask(T0);
     const uint32_t qpb0 = (uint32_t)db.sample_pos_begin[Q], qpb1 = (uint32_t)db.sample_pos_begin[Q + 1];
     // the reverse pass's seeds of this gene's transcripts: [sh_rs0, sh_rs1) of rs_key
     if (P.rs_n) {
@@ -272,8 +282,8 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
             // with a subject in this pass's samples
             for (uint32_t i = sh_rs0 + (uint32_t)tid; i < sh_rs1; i += SBLOCK) {
                 const LSeed sd = P.rs_rec[P.rs_idx[i]];
-                const int T = db.tx[key_gtx(sd.k1)].sample;
-                if (T < T0 || T >= T1 || !((tm[T >> 6] >> (T & 63)) & 1)) continue;
+                const int T = db.tx[key_gtx(sd.k1, xb)].sample;
+                if (T < T0 || T >= T1 || !in_mask(T, T0)) continue;
                 const uint32_t slot = atomicAdd(&sh_nseed, 1u);
                 if (slot < cap) seeds[slot] = sd;
                 else atomicOr(&sh_flags, 1u);
@@ -499,7 +509,8 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                             xr |= win(QAM, qp + W16) | win(db.AF, (uint64_t)pos + W16);
                         }
                     }
-                    if (!((tm[st.sample >> 6] >> (st.sample & 63)) & 1)) continue;
+                    // (pos in [pb0, pb1): st.sample is in [T0, T1))
+                    if (!in_mask(st.sample, T0)) continue;
                     const int off = (int)(pos - (uint32_t)st.start);
                     const int Dp = (int)it_d[k];
                     const int maxl = min(min(p, off), Dp);
@@ -539,7 +550,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                             fwd = word_usable<AMB>(db, st.start, La, strand, u, total);
                         if (fwd) continue;
                         LSeed sd;
-                        sd.k1 = seed_key(P.tx_pos[stx], (uint32_t)strand, I_gtx(ii), (uint32_t)xa);
+                        sd.k1 = seed_key(P.tx_pos[stx], (uint32_t)strand, I_gtx(ii), (uint32_t)xa, xb);
                         sd.y = (uint32_t)(strand ? qg.Lq - pb - len : pb);
                         sd.len = (uint32_t)len | SEED_R;
                         const unsigned long long k = atomicAdd(P.rseed_n, 1ull);
@@ -572,7 +583,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     const uint32_t slot = atomicAdd(&sh_nseed, 1u);
                     if (slot < cap) {
                         LSeed sd;
-                        sd.k1 = seed_key(ii, (uint32_t)strand, stx, (uint32_t)(p - l));
+                        sd.k1 = seed_key(ii, (uint32_t)strand, stx, (uint32_t)(p - l), xb);
                         sd.y = (uint32_t)(off - l);
                         sd.len = (uint32_t)len | dfl;
                         seeds[slot] = sd;
@@ -590,13 +601,14 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                 // one subject sample alone overflows: the global-memory pass
                 // takes (gene, T0); its groups stay empty here
                 if (tid == 0) {
-                    const uint64_t e = ((uint64_t)gl << 8) | (uint64_t)T0;
+                    const uint64_t e = ((uint64_t)gl << 16) | (uint64_t)T0;
                     const unsigned long long k = atomicAdd(BIG ? P.big_retry_n : P.big_n, 1ull);
                     if (k < P.big_list_cap) (BIG ? P.big_retry : P.big_out)[k] = e;
                     else atomicOr(P.status, 8u);
                 }
                 T0 = T1;
-                T1 = Tr;
+                T1 = min(Tr, T0 + PASS_SAMPLES);
+                pass_mask(T0);
                 __syncthreads();
                 continue;
             }
@@ -717,27 +729,28 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
         uint32_t nseg = 0;
         for (uint32_t c0 = 0; c0 < nseed; c0 += SBLOCK) {
             const uint32_t i = c0 + tid;
-            const uint32_t f = (i < nseed && (i == 0 || (seeds[i].k1 >> 24) != (seeds[i - 1].k1 >> 24))) ? 1u : 0u;
+            const uint32_t f = (i < nseed && (i == 0 || (seeds[i].k1 >> xb) != (seeds[i - 1].k1 >> xb))) ? 1u : 0u;
             uint32_t tot;
             const uint32_t pos = nseg + block_exscan(f, wsum, tot);
             if (f) seg_begin[pos] = (SegIdx)i;
             nseg += tot;
         }
         if (tid == 0) seg_begin[nseg] = (SegIdx)nseed;
-        for (int T = tid; T < N; T += SBLOCK) tcnt[T] = 0;
+        const int NT = T1 - T0;   // <= PASS_SAMPLES: counts by T - T0
+        for (int T = tid; T < NT; T += SBLOCK) tcnt[T] = 0;
         __syncthreads();
         for (uint32_t sg = tid; sg < nseg; sg += SBLOCK) {
-            const uint32_t gtx = key_gtx(seeds[seg_begin[sg]].k1);
-            const int T = db.tx[gtx].sample;
+            const uint32_t gtx = key_gtx(seeds[seg_begin[sg]].k1, xb);
+            const int T = db.tx[gtx].sample - T0;
             seg_T[sg] = (uint8_t)T;
             atomicAdd(&tcnt[T], 1u);
         }
         __syncthreads();
         {
             uint32_t tot;
-            const uint32_t v = tid < N ? tcnt[tid] : 0u;
+            const uint32_t v = tid < NT ? tcnt[tid] : 0u;
             const uint32_t pre = block_exscan(v, wsum, tot);
-            if (tid < N) tpre[tid] = pre;
+            if (tid < NT) tpre[tid] = pre;
         }
         if (tid == 0) {
             sh_sbase = nseed ? atomicAdd(&P.seed_count[shard], (unsigned long long)nseed) : 0ull;
@@ -751,7 +764,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
         if (room) {
             for (uint32_t i = tid; i < nseed; i += SBLOCK) {
                 GSeed gs;
-                gs.x = key_x(seeds[i].k1);
+                gs.x = key_x(seeds[i].k1, xb);
                 gs.y = seeds[i].y;
                 gs.len = seeds[i].len;
                 P.seeds[sbase + i] = gs;
@@ -764,8 +777,8 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                 if (sg < nseg) {
                     const uint32_t b0 = seg_begin[sg], b1 = seg_begin[sg + 1];
                     const uint64_t k1 = seeds[b0].k1;
-                    const uint32_t gtx = key_gtx(k1);
-                    const int T = seg_T[sg];
+                    const uint32_t gtx = key_gtx(k1, xb);
+                    const int T = seg_T[sg];   // - T0
                     uint32_t rk = 0;   // rank among earlier candidates of the same sample
                     if (T1 - T0 == 1)
                         rk = sg;
@@ -773,11 +786,11 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                         for (uint32_t s2 = 0; s2 < sg; s2++) rk += seg_T[s2] == T;
                     Cand c;
                     c.seed_off = (uint32_t)(sbase + b0);
-                    c.q_gtx = I_gtx(key_iso(k1));
+                    c.q_gtx = I_gtx(key_iso(k1, xb));
                     c.s_gtx = gtx;
                     c.seed_lo = (uint16_t)(b1 - b0);
                     c.seed_hi = (uint16_t)((b1 - b0) >> 16);
-                    c.strand = (uint8_t)key_strand(k1);
+                    c.strand = (uint8_t)key_strand(k1, xb);
                     c.dflags = 1;
                     c.e0 = 0;
                     c.e1 = SEED_NONE;
@@ -792,7 +805,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                             const uint32_t sl = seeds[i].len;
                             if ((sl & SEED_F) && fF < 0) fF = (int)(i - b0);
                             if (sl & SEED_R) {
-                                const uint32_t sx = key_x(seeds[i].k1), sy = seeds[i].y, ln = sl & SEED_LEN;
+                                const uint32_t sx = key_x(seeds[i].k1, xb), sy = seeds[i].y, ln = sl & SEED_LEN;
                                 const uint64_t key = c.strand ? ((uint64_t)~(sy + ln) << 32) | (uint32_t)~(sx + ln)
                                                               : ((uint64_t)sy << 32) | sx;
                                 if (key < bk) {
@@ -808,16 +821,18 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                         c.e1 = (fF >= 0 && fR >= 0 && fR != fF) ? (uint16_t)fR : SEED_NONE;
                         want = c.e1 != SEED_NONE ? 1u : 0u;
                     }
-                    const uint32_t qi = key_iso(k1);
+                    const uint32_t qi = key_iso(k1, xb);
                     const uint64_t qstart = I_start(qi);
                     const int qlen = I_len(qi);
-                    c.q0 = c.strand ? total - qstart - (uint64_t)qlen : qstart;
+                    c.q0 = (uint32_t)(c.strand ? total - qstart - (uint64_t)qlen : qstart);
                     const TxInfo st = db.tx[gtx];
-                    c.s0 = st.start;
+                    c.s0 = (uint32_t)st.start;
                     c.Lq = (int32_t)qlen;
                     c.Lt = (int32_t)st.len;
-                    c.qsam = (uint8_t)Q;
-                    c.ssam = (uint8_t)st.sample;
+                    c.qsam = (uint16_t)Q;
+                    c.ssam = (uint16_t)st.sample;
+                    c.pad0 = 0;
+                    c.pad1 = 0;
                     cslot = cbase + tpre[T] + rk;
                     P.cands[cslot] = c;
                 }
@@ -835,11 +850,12 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
         }
         for (int T = T0 + tid; T < T1; T += SBLOCK) {
             const size_t gi = (size_t)gl * (size_t)N + (size_t)T;
-            P.gc_off[gi] = (uint32_t)(cbase + tpre[T]);
-            P.gc_cnt[gi] = tcnt[T];
+            P.gc_off[gi] = (uint32_t)(cbase + tpre[T - T0]);
+            P.gc_cnt[gi] = tcnt[T - T0];
         }
         T0 = T1;
-        T1 = Tr;
+        T1 = min(Tr, T0 + PASS_SAMPLES);
+        pass_mask(T0);
         __syncthreads();
         SEED_TICK(4);
     }
@@ -1577,9 +1593,9 @@ enum { RM_REC = 0, RM_CLO = CAND_DWORDS, RM_CHI, RM_QB, RM_TB, RM_X, RM_Y, RM_LE
        RM_PWI, RM_PWG, RM_PWD, RM_PK,             // the row's best record parked by a window slide, its diagonal
        RM_N };   // (its size is part of the row kernel's tuning: 3 more fields cost 4 VGPR spills)
 // the step count and best score of an extension that outgrew the window, kept
-// (SAVE kernel) where the candidate record's start positions were (only read
-// while the candidate is staged)
-enum { RM_AD6 = RM_REC + 4, RM_ABEST = RM_REC + 5 };
+// (SAVE kernel) in record fields the row kernel does not read (the seed
+// count's high half, the padding)
+enum { RM_AD6 = RM_REC + 9, RM_ABEST = RM_REC + 11 };
 // a saved extension (ExtParams::resume, RES_REC ints): the bookkeeping
 // RM_RSC .. RM_PK, the step count, the best score, then the window's frontier
 // R and gap states
@@ -1588,8 +1604,8 @@ enum { RES_RSC = 0, RES_PHASE = RM_PHASE - RM_RSC, RES_KOF = RM_KOF - RM_RSC, RE
        RES_BEST = RES_PK + 2, RES_R = 16, RES_G = 48 };
 static_assert(RES_BEST < RES_R && RES_G + 32 <= RES_REC, "resume record layout");
 // fields of the record (dword offsets, layout of Cand)
-enum { RC_SOFF = 0, RC_QTX = 1, RC_STX = 2, RC_CNT_STRAND = 3, RC_Q0 = 4, RC_S0 = 6, RC_LQ = 8, RC_LT = 9,
-       RC_SAMS = 10, RC_E01 = 11 };
+enum { RC_SOFF = 0, RC_QTX = 1, RC_STX = 2, RC_CNT_STRAND = 3, RC_Q0 = 4, RC_S0 = 5, RC_LQ = 6, RC_LT = 7,
+       RC_SAMS = 8, RC_SEEDHI = 9, RC_E01 = 10, RC_PAD1 = 11 };
 // work cursors of a row
 enum { RS_LEND, RS_SHARD, RS_SHN, RS_N };
 // row actions (transition actions < A_DONE; extending: A_STEP_R / A_STEP_L = their done action + 4)
@@ -1821,10 +1837,8 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 const int Lq = meta[RM_REC + RC_LQ], Lt = meta[RM_REC + RC_LT];
-                const uint64_t q0 = (uint64_t)(uint32_t)meta[RM_REC + RC_Q0] |
-                                    ((uint64_t)(uint32_t)meta[RM_REC + RC_Q0 + 1] << 32);
-                const uint64_t s0 = (uint64_t)(uint32_t)meta[RM_REC + RC_S0] |
-                                    ((uint64_t)(uint32_t)meta[RM_REC + RC_S0 + 1] << 32);
+                const uint64_t q0 = (uint64_t)(uint32_t)meta[RM_REC + RC_Q0];
+                const uint64_t s0 = (uint64_t)(uint32_t)meta[RM_REC + RC_S0];
                 const int strand = (meta[RM_REC + RC_CNT_STRAND] >> 16) & 1;
                 const int nwq = (int)(((q0 & 31) + (uint64_t)Lq) >> 5) + 3;
                 const int nwt = (int)(((s0 & 31) + (uint64_t)Lt) >> 5) + 3;
@@ -1887,7 +1901,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 // right extension from the seed's end
                 const int x = meta[RM_X], y = meta[RM_Y], len = meta[RM_LEN];
                 const uint32_t sams = (uint32_t)meta[RM_REC + RC_SAMS];
-                swap = (sams & 0xFFu) > ((sams >> 8) & 0xFFu);
+                swap = (sams & 0xFFFFu) > (sams >> 16);
                 pa = qb + (uint32_t)(x + len);
                 alen = Lq - (x + len);
                 pb = tb + (uint32_t)(y + len);

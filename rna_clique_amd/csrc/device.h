@@ -10,9 +10,9 @@ constexpr int BAND = 64;        // greedy band: one diagonal per lane of a wave
 constexpr int BAND_LO = -32;    // diagonal of lane 0
 constexpr int MAX_HSP = 8;      // HSPs per (query tx, strand, subject tx)
 constexpr int DMAX = 4096;      // greedy differences cap
-constexpr int MAX_ISO = 4095;   // transcripts per gene (12-bit field of the seed key)
 constexpr int ISO_LDS = 128;    // a gene's isoform tables the seed kernel keeps in LDS (more: read from HBM)
 constexpr uint64_t MAX_TX = 1ull << 27;   // transcripts per engine (27-bit field of the seed key)
+constexpr int MAX_SAMPLES = 65535;         // samples per engine (16-bit fields of Cand and the big-pass list)
 
 // Transcript record (16 B, one load).
 struct TxInfo {
@@ -109,42 +109,62 @@ constexpr uint32_t SEED_F = 1u << 30, SEED_R = 1u << 31, SEED_LEN = SEED_F - 1u;
 constexpr uint16_t SEED_NONE = 0xFFFFu;
 
 // Candidate = (query transcript, strand, subject transcript) with >= 1 seed.
-// Self-contained (48 B): the extension reads one record, no transcript table.
+// Self-contained (48 B, 12 dwords): the extension reads one record, no
+// transcript table. Positions are tile positions (a tile has < 2^32 bases).
 struct Cand {
     uint32_t seed_off;     // absolute index of its first seed (sorted by (x, y))
     uint32_t q_gtx, s_gtx;
     uint16_t seed_lo;      // seed count, low 16 bits (cand_seeds())
     uint8_t strand;
     uint8_t dflags;        // shared searches: bit 0 the forward search has seeds, bit 1 the reverse one
-    uint64_t q0;           // first base of the oriented query: in F (strand 0) or RC (strand 1)
-    uint64_t s0;           // first base of the subject in F
+    uint32_t q0;           // first base of the oriented query: in F (strand 0) or RC (strand 1)
+    uint32_t s0;           // first base of the subject in F
     int32_t Lq, Lt;        // transcript lengths
-    uint8_t qsam, ssam;    // samples of query and subject (< 256)
+    uint16_t qsam, ssam;   // samples of query and subject
     uint16_t seed_hi;      // seed count, high 16 bits
+    uint16_t pad0;
     // seeds (indices in the candidate) the row kernel extends first: e0 into
     // cand_box (the forward search's first seed, or the reverse one's when the
     // forward search has none), e1 into cand_box2 (the reverse search's first
     // seed when it is another seed; SEED_NONE otherwise)
     uint16_t e0, e1;
+    uint32_t pad1;
 };
 __host__ __device__ __forceinline__ uint32_t cand_seeds(const Cand &c) { return c.seed_lo | ((uint32_t)c.seed_hi << 16); }
 constexpr int CAND_DWORDS = (int)(sizeof(Cand) / 4);
 static_assert(sizeof(Cand) == 48, "Cand is read as 12 dwords");
 
-// A seed of the seed kernel before sorting: k1 = iso:12 | strand:1 | gtx:27 | x:24
-// (sorted by k1, then y; k1 >> 24 is the candidate: isoform, strand, subject tx)
+// A seed of the seed kernel before sorting: k1 = iso | strand:1 | gtx:27 | x:xb
+// (sorted by k1, then y; k1 >> xb is the candidate: isoform, strand, subject
+// tx). xb = SeedParams::xbits, the bits of the longest transcript length: the
+// isoform field has 36 - xb bits (engine limit: max_iso()).
 struct LSeed {
     uint64_t k1;
     uint32_t y, len;
 };
-__host__ __device__ __forceinline__ uint64_t seed_key(uint32_t iso, uint32_t strand, uint32_t gtx, uint32_t x)
+constexpr int GTX_BITS = 27;
+__host__ __device__ __forceinline__ uint64_t seed_key(uint32_t iso, uint32_t strand, uint32_t gtx, uint32_t x, int xb)
 {
-    return ((uint64_t)iso << 52) | ((uint64_t)strand << 51) | ((uint64_t)gtx << 24) | (uint64_t)x;
+    return ((uint64_t)iso << (xb + GTX_BITS + 1)) | ((uint64_t)strand << (xb + GTX_BITS)) | ((uint64_t)gtx << xb) |
+           (uint64_t)x;
 }
-__host__ __device__ __forceinline__ uint32_t key_iso(uint64_t k) { return (uint32_t)(k >> 52); }
-__host__ __device__ __forceinline__ uint32_t key_strand(uint64_t k) { return (uint32_t)(k >> 51) & 1u; }
-__host__ __device__ __forceinline__ uint32_t key_gtx(uint64_t k) { return (uint32_t)(k >> 24) & (uint32_t)(MAX_TX - 1); }
-__host__ __device__ __forceinline__ uint32_t key_x(uint64_t k) { return (uint32_t)k & 0xFFFFFFu; }
+__host__ __device__ __forceinline__ uint32_t key_iso(uint64_t k, int xb) { return (uint32_t)(k >> (xb + GTX_BITS + 1)); }
+__host__ __device__ __forceinline__ uint32_t key_strand(uint64_t k, int xb) { return (uint32_t)(k >> (xb + GTX_BITS)) & 1u; }
+__host__ __device__ __forceinline__ uint32_t key_gtx(uint64_t k, int xb) { return (uint32_t)(k >> xb) & (uint32_t)(MAX_TX - 1); }
+__host__ __device__ __forceinline__ uint32_t key_x(uint64_t k, int xb) { return (uint32_t)k & ((1u << xb) - 1u); }
+// bits of a transcript position (x < max_len) and the isoforms per gene the
+// key then holds (it_iso in the seed kernel's LDS is 16-bit: at most 65535)
+__host__ __device__ __forceinline__ int pos_bits(int64_t max_len)
+{
+    int b = 1;
+    while (b < 24 && (1ll << b) <= max_len) b++;
+    return b;
+}
+__host__ __device__ __forceinline__ uint32_t max_iso(int xb)
+{
+    const int ib = 64 - (xb + GTX_BITS + 1);
+    return ib >= 16 ? 65535u : (1u << ib) - 1u;
+}
 
 // seed_kernel: per query gene, lookups -> canonical seeds -> candidates.
 struct SeedParams {
@@ -161,6 +181,10 @@ struct SeedParams {
     // pass merges them into its candidates: rs_key = those genes sorted,
     // rs_idx = the permutation, rs_n entries.
     int32_t rev;
+    int32_t xbits;                // seed-key position bits (pos_bits(max_len)); max_iso(xbits) isoforms per gene
+    uint32_t max_iso;
+    int32_t tmw;                  // words per query sample of tmask
+    const int32_t *trange;        // [n_samples][2]: first and one-past-last subject sample of each query sample
     const uint32_t *tx_pos;       // isoform index of a transcript in its gene
     // genes with more than ISO_LDS isoforms: the word-item prefix of each
     // isoform, at gene_tx_off[g] + g + i (i = 0..niso; stride P.stride)
@@ -184,10 +208,10 @@ struct SeedParams {
     uint64_t cand_cap;            // per allocation shard
     unsigned long long *cand_count;  // [NSHARD]
     uint32_t *gc_off, *gc_cnt;    // [(g - gene_begin) * N + T] candidates of (gene, sample)
-    const uint64_t *tmask;        // [n_samples][4] subject samples (> query sample) of this shard
+    const uint64_t *tmask;        // [n_samples][tmw] subject samples (> query sample) of this shard
     unsigned int *status;         // bit 0 overflow, bit 1 gene limit, bit 3 big list full, bit 4 seed index > 16 bits
     unsigned long long *prof;     // RC_ROW_TIMING builds: block cycles per phase
-    // (gene, sample) passes whose seeds overflow LDS: ((gene - gene_begin) << 8) | sample
+    // (gene, sample) passes whose seeds overflow LDS: ((gene - gene_begin) << 16) | sample
     uint64_t *big_out;            // the LDS kernel appends here
     unsigned long long *big_n;
     const uint64_t *big_list;     // the global-memory kernel's entries (one workgroup each)

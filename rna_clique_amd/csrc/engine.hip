@@ -293,10 +293,11 @@ struct rc_engine {
     std::vector<int64_t> shard_first;   // shard r owns pairs [shard_first[r], shard_first[r + 1])
     std::vector<uint32_t> pair_item_begin;
     int32_t max_len = 0;
+    int xbits = 24;                     // seed-key position bits (pos_bits(max_len))
     uint64_t n_items = 0;
     int index_bits = 16;
     uint64_t n_index = 0;               // entries of the loaded tile's index
-    std::vector<uint64_t> h_koff;       // closed-form k-mer slot prefix per tile transcript
+    std::vector<uint64_t> h_koff;       // closed-form k-mer slot prefix per indexed tile transcript
     std::vector<TxInfo> h_tx;           // every transcript; start = position in the loaded tile
 
     // tiles of this shard (plan_tiles) and the one whose tables are loaded
@@ -310,7 +311,9 @@ struct rc_engine {
     std::vector<uint64_t> tile_pos;     // first base of each sample in the loaded tile
     uint64_t tile_total = 0;
     bool tile_direct = false;           // the loaded tile is d_ascii's layout (no gathered copy)
-    uint32_t tile_ntx = 0;
+    uint32_t tile_ntx = 0;              // the tile's transcripts (DUST, near-mask index)
+    uint32_t tile_nitx = 0;             // ... of its subject samples (the 16-mer index)
+    bool tile_share = false;            // the search mode the loaded tile's index list was built for
     uint64_t hsp_used = 0;              // HSPs appended to d_hsp by the tiles of this run
 
     // external HSPs
@@ -328,7 +331,7 @@ struct rc_engine {
 
     // device buffers
     DBuf<uint8_t> d_ascii, d_tile_ascii;
-    DBuf<TxInfo> d_tile_tx;
+    DBuf<TxInfo> d_tile_tx, d_tile_itx;
     DBuf<uint64_t> d_F, d_RC, d_AF, d_ARC;
     DBuf<TxInfo> d_tx;
     DBuf<uint32_t> d_tx_gene, d_gene_tx_off, d_gene_tx, d_sample_gene_begin, d_sample_tx_begin;
@@ -346,6 +349,7 @@ struct rc_engine {
     DBuf<uint32_t> d_rseed_gene, d_rs_key, d_rs_idx;
     DBuf<unsigned long long> d_rctr;   // [0] near-index entries, [1] reverse-only seeds
     DBuf<uint64_t> d_rtmask;
+    DBuf<int32_t> d_trange, d_rtrange;   // [N][2] subject-sample range of each query sample (tmask / rtmask)
     uint64_t rseed_cap = 0, n_rseeds = 0;
     uint32_t res_cap = 0;
     // fraction of the last run's candidates whose first-seed extension
@@ -427,6 +431,14 @@ struct rc_engine {
 
 static int set_device(rc_engine *e) { HIPCHK(hipSetDevice(e->o.device)); return RC_OK; }
 
+// Both directed searches of a pair from one candidate set (query = the lower
+// sample), unless spec 5b or RC_SHARE=0 (one after the other)
+static bool share_mode(const rc_engine *e)
+{
+    const char *sv = getenv("RC_SHARE");
+    return !e->o.symmetric && !(sv && atoi(sv) == 0);
+}
+
 extern "C" {
 
 void rc_default_opts(rc_opts *o)
@@ -502,7 +514,7 @@ int rc_add_sample(rc_engine *e, const char *label, const char *seq, const uint64
 {
     if (!e || !label || !tx_offsets || (n_tx && (!gene || !iso))) return fail(RC_E_ARG, "null argument");
     if (e->uploaded) return fail(RC_E_STATE, "samples must be added before rc_run");
-    if (e->samples.size() >= 256) return fail(RC_E_LIMIT, "at most 256 samples per engine");
+    if (e->samples.size() >= MAX_SAMPLES) return fail(RC_E_LIMIT, "at most 65535 samples per engine");
     if (tx_offsets[0] != 0) return fail(RC_E_ARG, "tx_offsets[0] must be 0");
     for (uint32_t t = 0; t < n_tx; t++) {
         if (tx_offsets[t + 1] < tx_offsets[t]) return fail(RC_E_ARG, "tx_offsets must be non-decreasing");
@@ -689,7 +701,7 @@ static int upload(rc_engine *e)
     CHK(set_device(e));
     const int N = (int)e->samples.size();
     if (N < 2) return fail(RC_E_ARG, "need at least two samples");
-    if (N > 256) return fail(RC_E_LIMIT, "more than 256 samples per engine");
+    if (N > MAX_SAMPLES) return fail(RC_E_LIMIT, "more than 65535 samples per engine");
     if (e->tx_sample.size() >= MAX_TX) return fail(RC_E_LIMIT, "more than 2^27 transcripts per engine");
     const uint32_t n_tx = (uint32_t)e->tx_sample.size();
     // genes: per sample distinct gene ids ascending; a gene's transcripts in input order
@@ -735,10 +747,13 @@ static int upload(rc_engine *e)
     e->sample_tx_begin[N] = n_tx;
     e->sample_gene_begin[N] = (uint32_t)e->gene_sample.size();
     const uint32_t n_genes = (uint32_t)e->gene_sample.size();
+    // the seed key's position field holds the longest transcript; its
+    // isoform field the rest (max_iso: 65535 unless transcripts reach 2^21)
+    e->xbits = pos_bits(e->max_len);
     for (uint32_t g = 0; g < n_genes; g++)
-        if (e->gene_tx_off[g + 1] - e->gene_tx_off[g] > (uint32_t)MAX_ISO)
+        if (e->gene_tx_off[g + 1] - e->gene_tx_off[g] > max_iso(e->xbits))
             return fail(RC_E_LIMIT, "gene " + std::to_string(e->gene_id[g]) + " has more than " +
-                                        std::to_string(MAX_ISO) + " transcripts");
+                                        std::to_string(max_iso(e->xbits)) + " transcripts");
     // pairs (a < b) in the shard plan's order (plan::plan_pairs): every
     // shard a rectangle [a0, a1) x [b0, b1) of the pair triangle; items =
     // (pair, gene of b). (Outputs are per pair and do not depend on this.)
@@ -952,7 +967,15 @@ static int load_tile(rc_engine *e, int ti)
     }
     e->tile_total = total;
     e->tile_direct = direct;
-    if (e->tile_loaded == ti) return RC_OK;
+    // the 16-mer index holds the tile's subject samples only: the b of each
+    // pair (shared searches and spec 5b: query = the lower sample), or both
+    const bool share = share_mode(e);
+    if (e->tile_loaded == ti && e->tile_share == share) return RC_OK;
+    std::vector<char> subj(N, 0);
+    for (auto &pr : T.pairs) {
+        subj[pr.second] = 1;
+        if (!share && !e->o.symmetric) subj[pr.first] = 1;
+    }
     auto up = [&](auto &buf, const auto &vec) -> int {
         using Tv = typename std::remove_reference<decltype(vec)>::type::value_type;
         CHK(buf.ensure(vec.size()));
@@ -962,7 +985,7 @@ static int load_tile(rc_engine *e, int ti)
     };
     // transcript starts in the tile; the tile's transcripts (index) with their
     // closed-form k-mer slots; blocks of positions -> transcript
-    std::vector<TxInfo> ttx;
+    std::vector<TxInfo> ttx, itx;
     std::vector<uint32_t> gid;
     std::vector<uint64_t> koff(1, 0);
     std::vector<uint32_t> pos_tx((total >> POS_TX_SHIFT) + 2, 0);
@@ -980,8 +1003,11 @@ static int load_tile(rc_engine *e, int ti)
             e->h_tx[t].start = st;
             ttx.push_back(e->h_tx[t]);
             gid.push_back(t);
-            const int64_t L = (int64_t)e->h_tx[t].len;
-            koff.push_back(koff.back() + (uint64_t)(L >= W16 ? L - W16 + 1 : 0));
+            if (subj[s]) {
+                itx.push_back(e->h_tx[t]);
+                const int64_t L = (int64_t)e->h_tx[t].len;
+                koff.push_back(koff.back() + (uint64_t)(L >= W16 ? L - W16 + 1 : 0));
+            }
             setbit(st);
         }
         // the sample's padding is a boundary too (DUST runs end there)
@@ -997,6 +1023,7 @@ static int load_tile(rc_engine *e, int ti)
     if (koff.back() > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "more than 2^32 seed positions in a tile");
     CHK(up(e->d_tx, e->h_tx));
     CHK(up(e->d_tile_tx, ttx));
+    CHK(up(e->d_tile_itx, itx));
     CHK(up(e->d_kpos_off, koff));
     CHK(up(e->d_pos_tx, pos_tx));
     CHK(up(e->d_sample_pos, spos));
@@ -1004,6 +1031,8 @@ static int load_tile(rc_engine *e, int ti)
     e->h_koff = koff;
     e->tile_gid = gid;
     e->tile_ntx = (uint32_t)ttx.size();
+    e->tile_nitx = (uint32_t)itx.size();
+    e->tile_share = share;
     // the packed working copy's source: d_ascii itself or a gathered copy
     if (!direct) {
         CHK(e->d_tile_ascii.ensure(total + 64));
@@ -1137,10 +1166,10 @@ static int build_index_of(rc_engine *e, const TxInfo *txl, uint32_t n_tx, uint64
     return RC_OK;
 }
 
-// The seed index of the loaded tile: every 16-mer position of its transcripts.
+// The seed index of the loaded tile: every 16-mer position of its subject samples' transcripts.
 static int build_index(rc_engine *e, const std::function<int()> &after_fill = nullptr)
 {
-    return build_index_of(e, e->d_tile_tx.p, e->tile_ntx, e->h_koff[e->tile_ntx], e->d_kpos_off.p, e->d_ent,
+    return build_index_of(e, e->d_tile_itx.p, e->tile_nitx, e->h_koff[e->tile_nitx], e->d_kpos_off.p, e->d_ent,
                           e->d_ent2, e->d_bucket, e->index_bits, e->n_index, after_fill);
 }
 
@@ -1224,17 +1253,37 @@ static void shard_pairs(rc_engine *e)
 // The directed searches of tile ti: per query sample the bit set of its
 // subject samples (spec 5b: only a -> b of a pair), and the runs of
 // consecutive query samples (one seed launch each: their genes are contiguous).
+// Subject-sample bit rows (tmw words per query sample) and the range of
+// each row's set bits ([first, one past last), empty N, 0).
+static int mask_words(int N) { return (N + 63) / 64; }
+static void mask_ranges(const std::vector<uint64_t> &mask, int N, std::vector<int32_t> &range)
+{
+    const int tw = mask_words(N);
+    range.assign((size_t)2 * N, 0);
+    for (int q = 0; q < N; q++) {
+        int lo = N, hi = 0;
+        for (int w = 0; w < tw; w++) {
+            const uint64_t m = mask[(size_t)q * tw + w];
+            if (!m) continue;
+            lo = std::min(lo, 64 * w + __builtin_ctzll(m));
+            hi = std::max(hi, 64 * w + 64 - __builtin_clzll(m));
+        }
+        range[2 * q] = lo;
+        range[2 * q + 1] = hi;
+    }
+}
+
 static void tile_plan(rc_engine *e, int ti, std::vector<uint64_t> &tmask, std::vector<std::pair<int, int>> &runs)
 {
-    const int N = (int)e->samples.size();
-    tmask.assign((size_t)4 * N, 0);
+    const int N = (int)e->samples.size(), tw = mask_words(N);
+    tmask.assign((size_t)tw * N, 0);
     std::vector<char> q(N, 0);
     for (auto &pr : e->tiles[ti].pairs) {
         const int a = pr.first, b = pr.second;
-        tmask[4 * a + (b >> 6)] |= 1ull << (b & 63);
+        tmask[(size_t)tw * a + (b >> 6)] |= 1ull << (b & 63);
         q[a] = 1;
         if (!e->o.symmetric && !e->share) {   // the pair's second directed search: query b, subject a
-            tmask[4 * b + (a >> 6)] |= 1ull << (a & 63);
+            tmask[(size_t)tw * b + (a >> 6)] |= 1ull << (a & 63);
             q[b] = 1;
         }
     }
@@ -1258,11 +1307,11 @@ static void tile_plan(rc_engine *e, int ti, std::vector<uint64_t> &tmask, std::v
 // query's gene (rs_key, rs_idx) for the forward pass to merge. n_rs = count.
 static int reverse_pass(rc_engine *e, int ti, const Db &db, const Index &ixm, uint32_t &n_rs)
 {
-    const int N = (int)e->samples.size();
-    std::vector<uint64_t> rmask((size_t)4 * N, 0);
+    const int N = (int)e->samples.size(), tw = mask_words(N);
+    std::vector<uint64_t> rmask((size_t)tw * N, 0);
     std::vector<char> q(N, 0);
     for (auto &pr : e->tiles[ti].pairs) {
-        rmask[4 * pr.second + (pr.first >> 6)] |= 1ull << (pr.first & 63);
+        rmask[(size_t)tw * pr.second + (pr.first >> 6)] |= 1ull << (pr.first & 63);
         q[pr.second] = 1;
     }
     std::vector<std::pair<int, int>> runs;
@@ -1276,8 +1325,12 @@ static int reverse_pass(rc_engine *e, int ti, const Db &db, const Index &ixm, ui
         runs.push_back({s0, t});
         s0 = t;
     }
+    std::vector<int32_t> rrange;
+    mask_ranges(rmask, N, rrange);
     CHK(e->d_rtmask.ensure(rmask.size()));
+    CHK(e->d_rtrange.ensure(rrange.size()));
     HIPCHK(hipMemcpyAsync(e->d_rtmask.p, rmask.data(), rmask.size() * 8, hipMemcpyHostToDevice, e->st));
+    HIPCHK(hipMemcpyAsync(e->d_rtrange.p, rrange.data(), rrange.size() * 4, hipMemcpyHostToDevice, e->st));
     std::vector<uint32_t> ilist, ioff(1, 0);
     for (auto &r : runs) ioff.push_back(ioff.back() + iso_genes(e, e->sample_gene_begin[r.first],
                                                                  e->sample_gene_begin[r.second], ilist));
@@ -1312,6 +1365,10 @@ static int reverse_pass(rc_engine *e, int ti, const Db &db, const Index &ixm, ui
             S.gene_begin = e->sample_gene_begin[r.first];
             S.gene_end = e->sample_gene_begin[r.second];
             S.tmask = e->d_rtmask.p;
+            S.tmw = tw;
+            S.trange = e->d_rtrange.p;
+            S.xbits = e->xbits;
+            S.max_iso = max_iso(e->xbits);
             S.status = e->d_status.p;
             S.big_out = e->d_big_out.p;   // (never used: the pass keeps no seeds of its own)
             S.big_n = e->d_rctr.p + 2;
@@ -1323,7 +1380,8 @@ static int reverse_pass(rc_engine *e, int ti, const Db &db, const Index &ixm, ui
         HIPCHK(hipMemcpyAsync(&cnt, e->d_rctr.p + 1, sizeof cnt, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipStreamSynchronize(e->st));
-        if (status & 2u) return fail(RC_E_LIMIT, "a query gene has more than " + std::to_string(MAX_ISO) + " isoforms");
+        if (status & 2u)
+            return fail(RC_E_LIMIT, "a query gene has more than " + std::to_string(max_iso(e->xbits)) + " isoforms");
         if (cnt <= e->rseed_cap) break;
         e->rseed_cap = cnt + cnt / 4 + 1024;
     }
@@ -1460,12 +1518,7 @@ static int align_tile(rc_engine *e, int ti)
     CHK(build_index(e, dust && !dust_early ? std::function<int()>(start_dust) : nullptr));
     HIPCHK(hipGetLastError());
     if (dust) HIPCHK(hipStreamWaitEvent(e->st, e->evd[1], 0));
-    {
-        // both directed searches of a pair from one candidate set (query =
-        // the lower sample); RC_SHARE=0 runs them one by one
-        const char *sv = getenv("RC_SHARE");
-        e->share = !e->o.symmetric && !(sv && atoi(sv) == 0);
-    }
+    e->share = share_mode(e);   // (load_tile built the index list for it)
     // shared searches with DUST: reverse-search runs with no usable word of
     // the forward query inside come from a reverse pass over a near-mask index
     const bool revpass = e->share && dust;
@@ -1476,8 +1529,13 @@ static int align_tile(rc_engine *e, int ti)
     std::vector<std::pair<int, int>> runs;
     tile_plan(e, ti, tmask, runs);
     const size_t R = runs.size(), RT = R;
+    const int tw = mask_words(N);
+    std::vector<int32_t> trange;
+    mask_ranges(tmask, N, trange);
     CHK(e->d_tmask.ensure(tmask.size()));
+    CHK(e->d_trange.ensure(trange.size()));
     HIPCHK(hipMemcpyAsync(e->d_tmask.p, tmask.data(), tmask.size() * 8, hipMemcpyHostToDevice, e->st));
+    HIPCHK(hipMemcpyAsync(e->d_trange.p, trange.data(), trange.size() * 4, hipMemcpyHostToDevice, e->st));
     // per run: its genes [g0, g1) and its slice of the (gene, sample) arrays
     std::vector<uint32_t> rg0(RT), rg1(RT);
     std::vector<uint32_t> ilist, ioff(1, 0);
@@ -1504,7 +1562,7 @@ static int align_tile(rc_engine *e, int ti)
         for (size_t r = 0; r < RT; r++)
             for (int q = runs[r].first; q < runs[r].second; q++) {
                 uint64_t ns = 0;
-                for (int w = 0; w < 4; w++) ns += (uint64_t)__builtin_popcountll(tmask[4 * q + w]);
+                for (int w = 0; w < tw; w++) ns += (uint64_t)__builtin_popcountll(tmask[(size_t)tw * q + w]);
                 nb += (uint64_t)(e->sample_gene_begin[q + 1] - e->sample_gene_begin[q]) * ns;
             }
         e->seed_cap = std::max<uint64_t>(e->seed_cap, nb * 16 / NSHARD + 4096);
@@ -1577,6 +1635,10 @@ static int align_tile(rc_engine *e, int ti)
             S.gc_off = e->d_gc_off.p + gcb[r];
             S.gc_cnt = e->d_gc_cnt.p + gcb[r];
             S.tmask = e->d_tmask.p;
+            S.tmw = tw;
+            S.trange = e->d_trange.p;
+            S.xbits = e->xbits;
+            S.max_iso = max_iso(e->xbits);
             S.status = e->d_status.p;
             S.big_out = e->d_big_out.p;
             S.big_n = big_n;
@@ -1590,7 +1652,8 @@ static int align_tile(rc_engine *e, int ti)
             HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
             HIPCHK(hipMemcpyAsync(&nb, big_n, sizeof nb, hipMemcpyDeviceToHost, e->st));
             HIPCHK(hipStreamSynchronize(e->st));
-            if (status & 2u) return fail(RC_E_LIMIT, "a query gene has more than " + std::to_string(MAX_ISO) + " isoforms");
+            if (status & 2u)
+                return fail(RC_E_LIMIT, "a query gene has more than " + std::to_string(max_iso(e->xbits)) + " isoforms");
             if (status & 16u)
                 return fail(RC_E_LIMIT, "a candidate's first seed of a directed search is past seed 65534");
             if (status & 8u) {   // the big-pass list itself overflowed
@@ -2525,7 +2588,7 @@ int rc_plan_pairs(const int64_t *sample_bases, int32_t n_samples, int32_t shard_
 {
     if (!pair_first || shard_count < 1 || n_samples < 0 || (n_samples && !sample_bases))
         return fail(RC_E_ARG, "bad argument");
-    if (n_samples > 256) return fail(RC_E_LIMIT, "more than 256 samples");
+    if (n_samples > MAX_SAMPLES) return fail(RC_E_LIMIT, "more than 65535 samples");
     std::vector<int32_t> pa, pb;
     std::vector<int64_t> first;
     plan::plan_pairs(sample_bases, n_samples, shard_count, pa, pb, first);

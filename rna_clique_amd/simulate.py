@@ -322,6 +322,12 @@ CONFIGS = {
     "C4": dict(taxa=64, genes=50000, seed=490, len_loc=950, len_n=100, len_p=0.5),
     # C5 uses per-node random streams: one shard's samples can be generated alone
     "C5": dict(taxa=128, genes=100000, seed=491, len_uniform=(200, 5000), node_rng=True),
+    # C5's tree is deep (its deepest pair 22.3 branch-length units apart, C4's
+    # 8.1): at minimal_config's rate 0.01 that pair differs at ~19 % of sites
+    # and no gene keeps a reciprocal best hit in all 8128 pairs, so no ideal
+    # 128-clique exists and the reference raises NoIdealComponentsError. C5s:
+    # the same samples' shape and tree at rate 0.0036 (deepest pair ~8 %, C4's)
+    "C5s": dict(taxa=128, genes=100000, seed=491, len_uniform=(200, 5000), node_rng=True, mutation_rate=0.0036),
     # C3 with the features of real transcriptomes (correctness variant of the
     # GPU tests; a bench workload too): 10 % two-isoform genes, indels, half the
     # genes on the minus strand, 2 % recent paralogs, poly-A tails on 20 %

@@ -174,8 +174,17 @@ def main():
         t_graph = time.perf_counter() - t0
         n_edges = len(allrec) // Engine.edge_record_size()
         del allrec
-        labels, mat = g.distance()
         gst = g.stats()
+        print(json.dumps({"graph_stats": gst}), flush=True)
+        from rna_clique_amd._native import NativeError
+        try:
+            labels, mat = g.distance()
+        except NativeError as ex:
+            # a pair without ideal rows: the reference's NoIdealComponentsError
+            # (filtered_distance.py:242-247); consistent only if no ideal
+            # component exists at all (an ideal clique spans every pair)
+            print(f"distance: {ex}", flush=True)
+            labels, mat = None, None
         gtm = g.timings()
         unum, uden = g.pair_sums(unfiltered=True)
         num, den = g.pair_sums()
@@ -184,15 +193,21 @@ def main():
     bad_sums = [(a, b) for (a, b), v in own_usums.items() if (int(unum[a, b]), int(uden[a, b])) != v]
     if bad_sums:
         failures.append(f"unfiltered sums differ from the owning rank's for {len(bad_sums)} pairs, e.g. {bad_sums[:3]}")
-    if not (np.array_equal(mat, mat.T) and np.all(np.diag(mat) == 0) and np.all((mat >= 0) & (mat <= 1))):
-        failures.append("matrix not symmetric / hollow / in [0, 1]")
-    if not np.all(den[~np.eye(N, dtype=bool)] > 0):
-        failures.append("a pair with no ideal rows")
-    parent, _, leaves = tree
-    truth = tree_splits(parent, leaves, {leaf: meta[i].name for i, leaf in enumerate(leaves)})
-    rf = robinson_foulds(nj_splits(mat, list(labels)), truth)
-    if rf != 0:
-        failures.append(f"NJ tree of the matrix: Robinson-Foulds {rf} vs the simulated tree")
+    off = ~np.eye(N, dtype=bool)
+    rf = None
+    if mat is None:
+        if gst["ideal_components"] != 0 or np.any(den[off] != 0):
+            failures.append("NoIdealComponentsError although ideal components exist")
+    else:
+        if not (np.array_equal(mat, mat.T) and np.all(np.diag(mat) == 0) and np.all((mat >= 0) & (mat <= 1))):
+            failures.append("matrix not symmetric / hollow / in [0, 1]")
+        if not np.all(den[off] > 0):
+            failures.append("a pair with no ideal rows")
+        parent, _, leaves = tree
+        truth = tree_splits(parent, leaves, {leaf: meta[i].name for i, leaf in enumerate(leaves)})
+        rf = robinson_foulds(nj_splits(mat, list(labels)), truth)
+        if rf != 0:
+            failures.append(f"NJ tree of the matrix: Robinson-Foulds {rf} vs the simulated tree")
     # graph engine model: edge records + per-gene union-find / ideal arrays + pair sums
     n_genes = sum(genes)
     g_model = n_edges * Engine.edge_record_size() + n_genes * 17 + len(order) * 32
@@ -212,8 +227,11 @@ def main():
         "graph": {"edges": n_edges, "import_s": round(t_graph, 3), "stats": gst,
                   "device_gb": round(g_bytes / 1e9, 2), "model_gb": round(g_model / 1e9, 2),
                   "graph_ms": round(gtm["graph_ms"], 1), "reduce_ms": round(gtm["reduce_ms"], 1)},
-        "matrix": {"labels": labels, "min_offdiag": float(mat[~np.eye(N, dtype=bool)].min()),
-                   "max": float(mat.max()), "rf_vs_simulated_tree": rf},
+        "matrix": None if mat is None else {
+            "labels": labels, "min_offdiag": float(mat[off].min()), "max": float(mat.max()),
+            "rf_vs_simulated_tree": rf},
+        "no_ideal_components": mat is None,
+        "unfiltered_pairs_with_rows": int(np.count_nonzero(uden[off]) // 2),
         "oracle_pairs": checked,
         # one GPU per rank: the job takes the slowest rank's align + finish,
         # then the exchange and the graph phase (measured here on one GPU)

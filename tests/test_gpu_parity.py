@@ -443,3 +443,65 @@ def test_degenerate_transcripts(native, dust):
         eng.distance()
     assert ei.value.code == RC_E_NO_IDEAL
     eng.close()
+
+
+def test_more_than_256_samples(native):
+    """300 samples (round 3 refused more than 256: 8-bit sample fields, a
+    256-bit subject mask, one seed pass over all subjects). The reference
+    enumerates any N (find_all_pairs.py:224). Pairs on both sides of 256 --
+    sample indices in the seed passes' second 256-sample block -- bit-exact
+    against the oracle (both directed searches, tables, unfiltered sums);
+    the matrix hollow and symmetric, every pair with ideal rows."""
+    import itertools
+    from oracle.parity import check_pairs
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(300, 12, seed=61)
+    eng = _run_sim(samples)
+    st = eng.stats()
+    assert st["sample_count"] == 300 and st["ideal_components"] > 0
+    picks = [(0, 1), (0, 299), (255, 256), (256, 257), (100, 280), (298, 299), (17, 255), (254, 299)]
+    msgs = check_pairs(eng, samples, picks)
+    assert not msgs, "\n".join(msgs[:10])
+    labels, mat = eng.distance()
+    assert np.array_equal(mat, mat.T) and np.all(np.diag(mat) == 0)
+    # every pair has a table (ideal rows on both sides)
+    num, den = eng.pair_sums()
+    assert all(den[a, b] > 0 for a, b in itertools.combinations(range(300), 2))
+    eng.close()
+
+
+def test_gene_with_4200_isoforms(native):
+    """A gene with 4200 transcripts (more than round 3's 4095: the 12-bit
+    isoform field of the seed key; the field now takes what the longest
+    transcript leaves, 65535 here) against a one-isoform ortholog, bit-exact
+    vs the oracle. The reference keeps every isoform (select_top_genes.py:
+    121-127)."""
+    from rna_clique_amd.simulate import Sample, simulate
+    samples, _ = simulate(2, 20, seed=62, len_loc=900, len_n=200, len_p=0.5)
+    s = samples[0]
+    rng = np.random.default_rng(5)
+    g0 = int(s.gene[0])
+    base = s.seq[int(s.tx_offsets[0]):int(s.tx_offsets[1])]
+    seqs, genes, isos, covs = [], [], [], []
+    for i in range(4200):
+        v = base.copy()
+        pos = rng.choice(v.size, size=max(1, v.size // 60), replace=False)
+        v[pos] = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, pos.size)]
+        seqs.append(v)
+        genes.append(g0)
+        isos.append(i + 1)
+        covs.append(float(s.cov[0]) * 0.999 ** i)
+    for t in range(1, s.n_tx):
+        seqs.append(s.seq[int(s.tx_offsets[t]):int(s.tx_offsets[t + 1])])
+        genes.append(int(s.gene[t]))
+        isos.append(int(s.iso[t]))
+        covs.append(float(s.cov[t]))
+    offs = np.zeros(len(seqs) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([x.size for x in seqs])
+    samples[0] = Sample(s.name, np.concatenate(seqs), offs, np.array(genes, np.int32), np.array(isos, np.int32),
+                        np.array(covs))
+    eng = _run_sim(samples)
+    msgs, summary = full_check(eng, samples)
+    assert not msgs, "\n".join(msgs[:10])
+    assert summary["hsps"] > 4200
+    eng.close()

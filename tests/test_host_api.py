@@ -271,7 +271,8 @@ def test_matrix_h5_reads_back_with_libhdf5(tmp_path):
 # ---------------------------------------------------------------- shard planning
 
 
-@pytest.mark.parametrize("n,shards", [(4, 1), (4, 2), (5, 8), (32, 8), (13, 3), (2, 4), (64, 8), (32, 5)])
+@pytest.mark.parametrize("n,shards", [(4, 1), (4, 2), (5, 8), (32, 8), (13, 3), (2, 4), (64, 8), (32, 5),
+                                      (300, 1), (300, 8), (1000, 8)])
 def test_plan_shards_partitions_pairs(native, n, shards):
     from rna_clique_amd.distributed import plan_pairs, plan_shards
     rng = np.random.default_rng(n * 7 + shards)
