@@ -1635,12 +1635,27 @@ struct RowLds {
     int meta[RM_N];
     int st[RS_N];
 };
+// Windowed staging (WIN): a row's four staging slots (0: query forward, 1:
+// subject forward, 2: query reverse complement, 3: subject reverse
+// complement) hold windows of sw words of the packed tile arrays; the running
+// extension walks slot a against slot b. Per row: the global base of the
+// extension's start on each side (a: offset ni = 0, b: j = ni - diagonal =
+// 0), the side's array (bit 0: 0 = F, 1 = RC) and slot (bits 1-2), the
+// window's [lo, lim] in extension offsets, and the first word of each slot.
+enum { WM_GA0, WM_GB0, WM_AARR, WM_BARR, WM_ALO, WM_ALIM, WM_BLO, WM_BLIM, WM_W0, WM_N = WM_W0 + 4 };
+struct RowWin {
+    int w[WM_N];
+};
 // LDS of a row-kernel block: staging (2 guard words + rows x arrays x sw
-// words), shard prefix, rows' bookkeeping, 8 block counters
-__host__ __device__ constexpr size_t row_lds_bytes(int rw, int na, int sw)
+// words), shard prefix, rows' bookkeeping (+ window bookkeeping), 8 block counters
+__host__ __device__ constexpr size_t row_lds_bytes(int rw, int na, int sw, bool win = false)
 {
-    return ((size_t)(EBLOCK / rw) * na * sw + 2) * 8 + (NSHARD + 1) * 8 + (size_t)(EBLOCK / rw) * sizeof(RowLds) + 32;
+    return ((size_t)(EBLOCK / rw) * na * sw + 2) * 8 + (NSHARD + 1) * 8 + (size_t)(EBLOCK / rw) * sizeof(RowLds) + 32 +
+           (win ? (size_t)(EBLOCK / rw) * sizeof(RowWin) : 0);
 }
+// windowed slot limits: a slide from offset ni with at most mw bases reads
+// bases up to ni + mw + 46 (three dwords from the position's dword)
+constexpr int WIN_MARGIN = 48;
 
 // Extension of every candidate's FIRST seed (its smallest (x, y): always
 // extended, RC-megablast spec 3) to the right and to the left. Anything
@@ -1660,7 +1675,12 @@ __host__ __device__ constexpr size_t row_lds_bytes(int rw, int na, int sw)
 // SAVE (32-lane rows): an extension that outgrows the window is saved for the
 // 64-lane pass to continue (a separate instantiation: the save code's
 // registers cost the plain kernel 7 % at C3, where nearly nothing overflows).
-template <bool AMB, int RW, int MINW, bool SAVE = false>
+// WIN: transcripts longer than the staging slot -- each slot holds a window
+// of the sequence from the extension's start, refilled from HBM when a
+// slide would read past it (or a lane's position lies before it); the
+// refill places the window at the lowest position still to be read, so the
+// extension is the same as with the whole transcripts staged.
+template <bool AMB, int RW, int MINW, bool SAVE = false, bool WIN = false>
 __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
 {
     constexpr int RROWS = EBLOCK / RW;   // rows per block
@@ -1677,6 +1697,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
     RowLds *const rows_lds = reinterpret_cast<RowLds *>(sprefix + NSHARD + 1);
     uint32_t *const rcnt = reinterpret_cast<uint32_t *>(rows_lds + RROWS);   // extensions, candidates, overflows
     uint32_t &s_ncand = rcnt[4];
+    RowWin *const rows_win = reinterpret_cast<RowWin *>(rcnt + 8);   // (WIN only)
     {
         const RowArgsK K = row_args();
         if (threadIdx.x < 4) rcnt[threadIdx.x] = 0;
@@ -1699,6 +1720,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
     const uint32_t moff = 128u * (uint32_t)sw;
     RowLds &RL = rows_lds[rs];
     int *meta = RL.meta;
+    int *const wm = rows_win[rs].w;   // (WIN only)
     const int X = row_args()->P.xdrop;
     // candidates come in chunks from a global counter (P.chunk >= 1); the
     // record of the next one is prefetched (one dword per lane) while the
@@ -1772,10 +1794,144 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
     int score = 0, bound = 0;                             // of the last step
     bool swap = false;                                    // spec 4b: query = the higher-numbered sample
     unsigned long long steps = 0;                         // row steps (wave-uniform count)
+    int wlo = 0, wlim = 0;                                // WIN: the lane's window [wlo, wlim] in extension offsets
+
+    // ---- windowed staging (WIN) ----
+    using GW = const __attribute__((address_space(1))) uint64_t *;
+    // a packed tile array: 0 = F, 1 = RC (mask: their ambiguity masks)
+    auto warr = [](int arr, bool mask) -> GW {
+        const RowArgsK K = row_args();
+        GW f = (GW)(mask ? K->db.AF : K->db.F), r = (GW)(mask ? K->db.ARC : K->db.RC);
+        asm volatile("" : "+s"(f), "+s"(r));
+        return arr ? r : f;
+    };
+    // LDS base position of a slot's word 0
+    auto slot_base = [&](int slot) -> uint32_t { return base0 + 32u * (uint32_t)sw * (uint32_t)slot; };
+    // the window of `slot`: words W .. of array arr, at most through word ew
+    // (the last one a read of the side's sequence can reach)
+    auto win_load = [&](int slot, int arr, uint32_t W, uint32_t ew) {
+        const int n = ew >= W ? (int)min((uint32_t)sw, ew - W + 1u) : 0;
+        GW src = warr(arr, false) + W;
+        uint64_t *dst = stg + (size_t)slot * sw;
+        for (int w = rl; w < n; w += RW) dst[w] = src[w];
+        if (AMB) {
+            GW msrc = warr(arr, true) + W;
+            uint64_t *mdst = stg + (size_t)(4 + slot) * sw;
+            for (int w = rl; w < n; w += RW) mdst[w] = msrc[w];
+        }
+    };
+    // global start base of each slot's extension: right (slots 0, 1: the
+    // forward arrays from the seed's end), left (2, 3: the reverse
+    // complements from the seed's start, walked forward); and its sequence end
+    auto slot_g = [&](int slot, uint32_t &g, uint32_t &e) {
+        const uint32_t total = (uint32_t)row_args()->db.total;
+        const uint32_t q0 = (uint32_t)meta[RM_REC + RC_Q0], s0 = (uint32_t)meta[RM_REC + RC_S0];
+        const uint32_t Lq = (uint32_t)meta[RM_REC + RC_LQ], Lt = (uint32_t)meta[RM_REC + RC_LT];
+        const uint32_t x = (uint32_t)meta[RM_X], y = (uint32_t)meta[RM_Y], len = (uint32_t)meta[RM_LEN];
+        if (slot == 0) { g = q0 + x + len; e = q0 + Lq; }
+        else if (slot == 1) { g = s0 + y + len; e = s0 + Lt; }
+        else if (slot == 2) { g = total - q0 - x; e = total - q0; }
+        else { g = total - s0 - y; e = total - s0; }
+    };
+    auto slot_arr = [&](int slot) -> int {
+        const int strand = (meta[RM_REC + RC_CNT_STRAND] >> 16) & 1;
+        return slot == 0 ? strand : (slot == 1 ? 0 : (slot == 2 ? 1 - strand : 1));
+    };
+    // the lane's window from the row's bookkeeping (diagonal kk = k + kof)
+    auto win_lane = [&](int kk) {
+        wlo = max(wm[WM_ALO], wm[WM_BLO] + kk);
+        wlim = min(wm[WM_ALIM], wm[WM_BLIM] + kk);
+    };
+    // an extension starts (dir 0 right, 1 left): its sides' slots, start
+    // bases and windows (as staged); pa, pbk, wlo, wlim of diagonal k
+    auto win_begin = [&](int dir) {
+        const int qsl = dir ? 2 : 0, tsl = dir ? 3 : 1;
+        const int asl = swap ? tsl : qsl, bsl = swap ? qsl : tsl;
+        uint32_t ga, gb, ea, eb;
+        slot_g(asl, ga, ea);
+        slot_g(bsl, gb, eb);
+        const uint32_t Wa = (uint32_t)wm[WM_W0 + asl], Wb = (uint32_t)wm[WM_W0 + bsl];
+        const int alo = (int)(32u * Wa - ga), blo = (int)(32u * Wb - gb);
+        __builtin_amdgcn_wave_barrier();
+        if (rl == 0) {
+            wm[WM_GA0] = (int)ga;
+            wm[WM_GB0] = (int)gb;
+            wm[WM_AARR] = slot_arr(asl) | (asl << 1);
+            wm[WM_BARR] = slot_arr(bsl) | (bsl << 1);
+            wm[WM_ALO] = alo;
+            wm[WM_ALIM] = alo + 32 * sw - WIN_MARGIN;
+            wm[WM_BLO] = blo;
+            wm[WM_BLIM] = blo + 32 * sw - WIN_MARGIN;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        pa = slot_base(asl) + (ga - 32u * Wa);
+        pb = slot_base(bsl) + (gb - 32u * Wb);
+        pbk = pb - (uint32_t)k;
+        win_lane(k);
+    };
+    // refill the row's two windows at the lowest positions still to be read
+    // (row-uniform amin on side a, bmin on side b)
+    auto win_fill = [&](int amin, int bmin) {
+        const uint32_t ga = (uint32_t)wm[WM_GA0], gb = (uint32_t)wm[WM_GB0];
+        const int aa = wm[WM_AARR], ba = wm[WM_BARR];
+        const uint32_t Wa = (ga + (uint32_t)amin) >> 5, Wb = (gb + (uint32_t)bmin) >> 5;
+        win_load(aa >> 1, aa & 1, Wa, (ga + (uint32_t)alen + 47u) >> 5);
+        win_load(ba >> 1, ba & 1, Wb, (gb + (uint32_t)blen + 47u) >> 5);
+        const int alo = (int)(32u * Wa - ga), blo = (int)(32u * Wb - gb);
+        __builtin_amdgcn_wave_barrier();
+        if (rl == 0) {
+            wm[WM_W0 + (aa >> 1)] = (int)Wa;
+            wm[WM_W0 + (ba >> 1)] = (int)Wb;
+            wm[WM_ALO] = alo;
+            wm[WM_ALIM] = alo + 32 * sw - WIN_MARGIN;
+            wm[WM_BLO] = blo;
+            wm[WM_BLIM] = blo + 32 * sw - WIN_MARGIN;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const int kk = k + meta[RM_KOF];
+        pa = slot_base(aa >> 1) + (ga - 32u * Wa);
+        pbk = slot_base(ba >> 1) + (gb - 32u * Wb) - (uint32_t)kk;
+        win_lane(kk);
+    };
+    // finish the slides whose reads left the window (pend): refill the
+    // windows of the rows concerned at their lowest pending position, go on
+    // sliding; the lowest pending lane always advances (it is inside both
+    // new windows), so this ends. Wave-uniform call.
+    auto win_resolve = [&](int ni, int &s, int m, bool pend) {
+        do {
+            const int kk = k + meta[RM_KOF];
+            const int c = ni + s;
+            const int amin = -rw_max<RW>(pend ? -c : -INT_MAX), bmin = -rw_max<RW>(pend ? -(c - kk) : -INT_MAX);
+            if (amin != INT_MAX) win_fill(amin, bmin);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (pend) {
+                const int c2 = ni + s, mr = m - s;
+                const int mw = c2 < wlo ? -1 : min(mr, wlim - c2);
+                const int s2 = slide_fwd<AMB>(pa + (uint32_t)c2, pbk + (uint32_t)c2, mw, moff);
+                pend = mw < mr && s2 >= mw;
+                s += s2;
+            }
+        } while (ballot(pend));
+    };
 
     auto ext_init = [&](int done_act) {
         int r0 = 0;
-        if (rl == RC0) r0 = slide_fwd<AMB>(pa, pb, min(alen, blen), moff);
+        if constexpr (WIN) {
+            win_begin(done_act == A_LDONE ? 1 : 0);
+            const int m0 = min(alen, blen);
+            bool pend = false;
+            if (rl == RC0) {
+                const int mw = min(m0, wlim);
+                r0 = slide_fwd<AMB>(pa, pb, mw, moff);
+                pend = mw < m0 && r0 >= mw;
+            }
+            if (ballot(pend)) win_resolve(0, r0, m0, pend);
+        } else {
+            if (rl == RC0) r0 = slide_fwd<AMB>(pa, pb, min(alen, blen), moff);
+        }
         r0 = __shfl(r0, RW * row + RC0);
         best = 2 * r0;
         bl = RC0;
@@ -1787,7 +1943,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
         R = rl == RC0 ? r0 : -1;
         goe = 0;
         d6 = 0;
-        pbk = pb - (uint32_t)k;
+        if constexpr (!WIN) pbk = pb - (uint32_t)k;   // (WIN: win_begin / win_fill set it)
         blk = blen + k;
         nkd = -k;
         if (rl == 0) {
@@ -1842,17 +1998,39 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 const int strand = (meta[RM_REC + RC_CNT_STRAND] >> 16) & 1;
                 const int nwq = (int)(((q0 & 31) + (uint64_t)Lq) >> 5) + 3;
                 const int nwt = (int)(((s0 & 31) + (uint64_t)Lt) >> 5) + 3;
+                const RowArgsK K = row_args();
+                uint32_t qb = 0, tb = 0;
+                if constexpr (WIN) {
+                    // the first seed, then each slot's window from its
+                    // extension's start (right: the seed's end; left: its start)
+                    const uint32_t e01 = (uint32_t)meta[RM_REC + RC_E01];
+                    const GSeed g0 =
+                        K->P.seeds[(uint32_t)meta[RM_REC + RC_SOFF] + (K->P.which ? e01 >> 16 : e01 & 0xFFFFu)];
+                    if (rl == 0) {
+                        meta[RM_X] = (int)g0.x;
+                        meta[RM_Y] = (int)g0.y;
+                        meta[RM_LEN] = (int)(g0.len & SEED_LEN);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    for (int sl = 0; sl < 4; sl++) {
+                        uint32_t g, e;
+                        slot_g(sl, g, e);
+                        win_load(sl, slot_arr(sl), g >> 5, (e + 47u) >> 5);
+                        if (rl == 0) wm[WM_W0 + sl] = (int)(g >> 5);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                } else {
                 if (nwq > sw || nwt > sw || (Lq >> 5) + 3 > sw || (Lt >> 5) + 3 > sw) {
                     if (rl == 0 && row_args()->P.why) atomicAdd(&row_args()->P.why[0], 1ull);
                     defer(ci, false);
                     continue;
                 }
                 // raw words of query and subject, and the first seed: one round trip
-                const RowArgsK K = row_args();
                 // both strands' pointers as scalars, selected per lane (an
                 // indexed read of the kernarg segment would be a vector load,
                 // one more round trip in front of the staging loads)
-                using GW = const __attribute__((address_space(1))) uint64_t *;
                 GW dF = (GW)K->db.F, dRC = (GW)K->db.RC;
                 asm volatile("" : "+s"(dF), "+s"(dRC));
                 const GW QA = strand ? dRC : dF;
@@ -1882,11 +2060,8 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                     for (int w = rl; w < nwq; w += RW) stg[4 * sw + w] = qm[w];
                     for (int w = rl; w < nwt; w += RW) stg[5 * sw + w] = tm[w];
                 }
-                const uint32_t qb = base0 + (uint32_t)(q0 & 31), tb = base0 + 32u * (uint32_t)sw + (uint32_t)(s0 & 31);
-                if (rl == 0) {
-                    meta[RM_QB] = (int)qb;
-                    meta[RM_TB] = (int)tb;
-                }
+                qb = base0 + (uint32_t)(q0 & 31);
+                tb = base0 + 32u * (uint32_t)sw + (uint32_t)(s0 & 31);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 stage_rev(stg + 2 * sw, qb, Lq);
@@ -1897,6 +2072,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
+                }
                 if (rl == 0) atomicAdd(&rcnt[1], 1u);
                 // right extension from the seed's end
                 const int x = meta[RM_X], y = meta[RM_Y], len = meta[RM_LEN];
@@ -1942,7 +2118,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                             wg = rec[RES_PWG];
                             wd = rec[RES_PWD];
                         }
-                        pbk = pb - (uint32_t)k;
+                        if constexpr (WIN) win_begin(phase == A_LDONE ? 1 : 0); else pbk = pb - (uint32_t)k;
                         blk = blen + k;
                         nkd = -(k + d6);
                         if (rl == 0) {
@@ -2008,6 +2184,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 pbk -= (uint32_t)s;
                 blk += s;
                 nkd -= s;
+                if constexpr (WIN) win_lane(k + kn);
                 if (rl == 0) {
                     meta[RM_KOF] = kn;
                     atomicAdd(&rcnt[3], 1u);
@@ -2122,7 +2299,26 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
             // score and bound of the lanes dead before the step keep stale
             // values (loop-carried: nothing to materialize), never read
             // unmasked (mi and mcont are ANDed with the live lanes)
-            if (ni >= 0) {
+            if constexpr (WIN) {
+                // slides stop at the window; the ones that reached it (or
+                // start outside it) are finished after a refill
+                int m = 0, s = 0;
+                bool pend = false;
+                if (ni >= 0) {
+                    m = min(alen - ni, blk - ni);
+                    const int mw = ni < wlo ? -1 : min(m, wlim - ni);
+                    s = slide_fwd<AMB>(pa + (uint32_t)ni, pbk + (uint32_t)ni, mw, moff);
+                    pend = mw < m && s >= mw;
+                }
+                if (ballot(pend)) win_resolve(ni, s, m, pend);
+                if (ni >= 0) {
+                    ni += s;
+                    if (s > 0) ng &= ~(3 << EBIT);
+                    score = 2 * ni + nkd;   // 2 ni - k - d6
+                    if (score < best - X) ni = -1;
+                    bound = score + 2 * (m - s);
+                }
+            } else if (ni >= 0) {
                 const int m = min(alen - ni, blk - ni);
                 const int s = slide_fwd<AMB>(pa + (uint32_t)ni, pbk + (uint32_t)ni, m, moff);
                 ni += s;
@@ -2530,30 +2726,70 @@ static unsigned resident_blocks(K kernel, size_t lds)
     return (unsigned)(cus * per_cu);
 }
 
+// A row-kernel launch: the windowed instantiation when the staging slot is
+// shorter than the longest transcript (P.win), one resident round of blocks.
+template <bool A, int RWV, bool SV, bool WV>
+static void launch_rows_t(const Db &db, const ExtParams &P, hipStream_t st)
+{
+    auto kern = extend_rows_kernel<A, RWV, ROW_MIN_WAVES, SV, WV>;
+    const size_t lds = row_lds_bytes(RWV, A ? 8 : 4, P.dsw, WV);
+    hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, lds)), dim3(EBLOCK), lds, st, RowArgs{db, P});
+}
+template <int RWV, bool SV = false>
+static void launch_rows(bool amb, const Db &db, const ExtParams &P, hipStream_t st)
+{
+    if (amb) {
+        if (P.win) launch_rows_t<true, RWV, SV, true>(db, P, st); else launch_rows_t<true, RWV, SV, false>(db, P, st);
+    } else {
+        if (P.win) launch_rows_t<false, RWV, SV, true>(db, P, st); else launch_rows_t<false, RWV, SV, false>(db, P, st);
+    }
+}
+
+// Staging slot (u64 words per staged array) the 32-lane row kernel can have
+// at ROW_MIN_WAVES waves per SIMD (7 blocks per CU in 160 KB of LDS); a longer
+// transcript runs on the windowed instantiation.
+int row_slot_words_max(bool amb)
+{
+    const int na = amb ? 8 : 4, rows = EBLOCK / 32;
+    const size_t per_block = (size_t)(160 * 1024) / (size_t)ROW_MIN_WAVES;
+    const size_t fixed = row_lds_bytes(32, na, 0, true);
+    return (int)((per_block - fixed) / ((size_t)rows * na * 8));
+}
+
 // Row kernel (first seeds) over all candidates, first_finish_kernel, then
 // extend_kernel over the candidates either deferred (sub-band overflow,
-// transcripts longer than the row staging slot, seeds outside the first box).
-// The deferred count stays on the device: the list launch reads it.
+// seeds outside the first box; without the windowed kernel transcripts
+// longer than the row staging slot). The deferred count stays on the device:
+// the list launch reads it.
 void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_width, hipStream_t st)
 {
     if (P.n_cand == 0) return;
+    (void)row_width;
     ExtParams W = P;
     W.list = nullptr;
     W.list_n = nullptr;
     // saved extension states: only the shared-search 32-lane passes write
     // them and only their 64-lane passes read them
     W.resume = nullptr;
-    const int rw = row_width == 16 ? 16 : 32;
-    auto lds_of = [&](int w) { return row_lds_bytes(w, amb ? 8 : 4, P.dsw); };
-#define RC_LAUNCH_ROWS_S(A, RWV, MW, SV, PRM)                                                             \
-    do {                                                                                                  \
-        auto kern = extend_rows_kernel<A, RWV, MW, SV>;                                                   \
-        const size_t lds = lds_of(RWV);                                                                   \
-        hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, lds)), dim3(EBLOCK), lds, st, RowArgs{db, PRM});\
-    } while (0)
-#define RC_LAUNCH_ROWS(A, RWV, MW, PRM) RC_LAUNCH_ROWS_S(A, RWV, MW, false, PRM)
-    const char *mwv = getenv("RC_ROW_WAVES");
-    const int mw = mwv ? atoi(mwv) : ROW_MIN_WAVES;
+    auto extend_lists = [&](const ExtParams &B) {
+        for (int dir = 0; dir < (B.share ? 2 : 1); dir++) {
+            ExtParams W3 = B;
+            W3.dir = dir;
+            if (dir) {
+                W3.defer = P.defer_r;
+                W3.defer_count = P.defer_r_count;
+            }
+            if (amb) {
+                auto kern = extend_kernel<true>;
+                hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W3);
+            } else {
+                auto kern = extend_kernel<false>;
+                hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W3);
+            }
+        }
+    };
+    uint64_t g = (P.n_cand + 255) / 256;
+    if (g > 65536) g = 65536;
     if (P.share) {
         // shared searches: first seeds e0 over every candidate, then e1 over
         // list2 (reverse searches whose first seed is another seed), then each
@@ -2573,22 +2809,14 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
             V.work = wk;
             V.wide = nullptr;
             V.wide_n = nullptr;
-            if (amb) RC_LAUNCH_ROWS(true, 64, ROW_MIN_WAVES, V); else RC_LAUNCH_ROWS(false, 64, ROW_MIN_WAVES, V);
+            launch_rows<64>(amb, db, V, st);
         };
         W.which = 0;
         W.wide = widep ? P.wide0 : nullptr;
         W.wide_n = P.wide0_n;
-        W.resume = widep && rw == 32 ? P.resume : nullptr;
-        // RC_ROW_WIDTH=16: the sliding sub-band on 16-lane rows (4 candidates per wave)
+        W.resume = widep ? P.resume : nullptr;
         auto rows_pass = [&](const ExtParams &B) {
-            if (rw == 16) {
-                if (amb) RC_LAUNCH_ROWS(true, 16, ROW_MIN_WAVES, B); else RC_LAUNCH_ROWS(false, 16, ROW_MIN_WAVES, B);
-            } else if (B.resume) {
-                if (amb) RC_LAUNCH_ROWS_S(true, 32, ROW_MIN_WAVES, true, B);
-                else RC_LAUNCH_ROWS_S(false, 32, ROW_MIN_WAVES, true, B);
-            } else {
-                if (amb) RC_LAUNCH_ROWS(true, 32, ROW_MIN_WAVES, B); else RC_LAUNCH_ROWS(false, 32, ROW_MIN_WAVES, B);
-            }
+            if (B.resume) launch_rows<32, true>(amb, db, B, st); else launch_rows<32>(amb, db, B, st);
         };
         rows_pass(W);
         if (widep) wide_pass(W, P.wide0, P.wide0_n, P.work_w0);
@@ -2603,55 +2831,20 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
         if (widep) wide_pass(W2, P.wide1, P.wide1_n, P.work_w1);
         W.list = nullptr;
         W.list_n = nullptr;
-        uint64_t g = (P.n_cand + 255) / 256;
-        if (g > 65536) g = 65536;
         hipLaunchKernelGGL(first_finish_kernel, dim3((unsigned)g), dim3(256), 0, st, W);
-        for (int dir = 0; dir < 2; dir++) {
-            ExtParams W3 = W;
-            W3.dir = dir;
-            if (dir) {
-                W3.defer = P.defer_r;
-                W3.defer_count = P.defer_r_count;
-            }
-            if (amb) {
-                auto kern = extend_kernel<true>;
-                hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W3);
-            } else {
-                auto kern = extend_kernel<false>;
-                hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W3);
-            }
-        }
+        extend_lists(W);
         return;
     }
-    // pass 1: 16- or 32-diagonal rows over every candidate
-    if (rw == 16) {
-        if (amb) RC_LAUNCH_ROWS(true, 16, ROW_MIN_WAVES, W); else RC_LAUNCH_ROWS(false, 16, ROW_MIN_WAVES, W);
-    } else if (mw == 5) {
-        if (amb) RC_LAUNCH_ROWS(true, 32, 5, W); else RC_LAUNCH_ROWS(false, 32, 5, W);
-    } else if (mw == 6) {
-        if (amb) RC_LAUNCH_ROWS(true, 32, 6, W); else RC_LAUNCH_ROWS(false, 32, 6, W);
-    } else if (mw == 8) {
-        if (amb) RC_LAUNCH_ROWS(true, 32, 8, W); else RC_LAUNCH_ROWS(false, 32, 8, W);
-    } else {
-        if (amb) RC_LAUNCH_ROWS(true, 32, ROW_MIN_WAVES, W); else RC_LAUNCH_ROWS(false, 32, ROW_MIN_WAVES, W);
-    }
+    // independent searches / spec 5b: 32-lane rows over every candidate
+    launch_rows<32>(amb, db, W, st);
     // pass 2 (RC_ROW64=1; off by default: at C3 neutral, at C3v 7 % slower,
     // because 40 % of what it finishes still has seeds outside the first box
     // and is redone whole by the one-wave kernel): the candidates whose
     // frontier left the sub-band, on 64-lane rows (the spec's whole band)
     const char *r64 = getenv("RC_ROW64");
     if (!(r64 && atoi(r64))) {
-        ExtParams W3 = W;
-        uint64_t g = (P.n_cand + 255) / 256;
-        if (g > 65536) g = 65536;
-        hipLaunchKernelGGL(first_finish_kernel, dim3((unsigned)g), dim3(256), 0, st, W3);
-        if (amb) {
-            auto kern = extend_kernel<true>;
-            hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W3);
-        } else {
-            auto kern = extend_kernel<false>;
-            hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W3);
-        }
+        hipLaunchKernelGGL(first_finish_kernel, dim3((unsigned)g), dim3(256), 0, st, W);
+        extend_lists(W);
         return;
     }
     ExtParams W2 = W;
@@ -2660,22 +2853,12 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
     W2.defer = P.defer2;
     W2.defer_count = P.defer2_count;
     W2.work = P.work2;
-    if (amb) RC_LAUNCH_ROWS(true, 64, ROW_MIN_WAVES, W2); else RC_LAUNCH_ROWS(false, 64, ROW_MIN_WAVES, W2);
-#undef RC_LAUNCH_ROWS
-#undef RC_LAUNCH_ROWS_S
-    uint64_t g = (P.n_cand + 255) / 256;
-    if (g > 65536) g = 65536;
+    launch_rows<64>(amb, db, W2, st);
     ExtParams W3 = W;
     W3.defer = P.defer2;
     W3.defer_count = P.defer2_count;
     hipLaunchKernelGGL(first_finish_kernel, dim3((unsigned)g), dim3(256), 0, st, W3);
-    if (amb) {
-        auto kern = extend_kernel<true>;
-        hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W3);
-    } else {
-        auto kern = extend_kernel<false>;
-        hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W3);
-    }
+    extend_lists(W3);
 }
 
 void launch_group(const GroupParams &P, int pass, hipStream_t st)

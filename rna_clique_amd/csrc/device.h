@@ -245,9 +245,10 @@ struct ExtParams {
     unsigned int *status;         // bit 0 overflow
     unsigned long long *counters; // [0] greedy steps, [1] extensions, [2] candidates (one atomic per wave),
                                   // [4] full-band recomputations
-    // two-candidate kernel: staging slot (u64 words per sequence) and the
-    // candidates it defers to the one-wave kernel (transcripts past the slot)
+    // row kernels: staging slot (u64 words per sequence); win: the slot is
+    // shorter than the longest transcript, the windowed instantiation runs
     int32_t dsw;
+    int32_t win;
     int32_t *cand_box;            // row kernel: status + right/left results of each candidate's first seed
     int32_t chunk;                // row kernel: candidates per work grab (0: static round robin)
     unsigned long long *work;     // row kernel: work counter
@@ -302,7 +303,6 @@ constexpr int HSP_FWD = 2, HSP_REV = 4, HSP_IDX_SHIFT = 3;
 // cand_box record: BOX_REC ints per candidate (align.hip FX_*)
 constexpr int BOX_REC = 12;
 
-constexpr int DSTAGE_MAX = 4096;   // longest transcript the two-candidate extension stages
 
 // group kernels: candidates of each (gene, sample) -> contiguous HSP groups.
 // Direct groups (gene of the query sample, higher subject sample) come in

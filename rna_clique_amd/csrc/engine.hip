@@ -60,6 +60,7 @@ uint32_t dust_scratch_words(uint32_t);
 uint64_t dust_event_words(uint32_t);
 void launch_extend(bool, const Db &, const ExtParams &, hipStream_t);
 void launch_extend_rows(bool, const Db &, const ExtParams &, int, hipStream_t);
+int row_slot_words_max(bool amb);
 void launch_group(const GroupParams &, int, hipStream_t);
 
 void launch_rbh(const RbhParams &, int, hipStream_t);
@@ -1778,7 +1779,18 @@ static int align_tile(rc_engine *e, int ti)
         X.ovf_count = e->d_count.p;
         X.status = e->d_status.p;
         X.counters = e->d_count.p + 1;
-        X.dsw = ((std::min(e->max_len, DSTAGE_MAX) + 31) >> 5) + 3;   // row staging slot (u64 words)
+        {
+            // row staging slot (u64 words): whole transcripts when the longest
+            // fits the slot the 32-lane kernel has at full occupancy, else
+            // windows of that slot (the windowed instantiation). RC_WIN_WORDS
+            // forces windows of that many words (tests: many refills).
+            const int need = ((e->max_len + 31) >> 5) + 4;
+            const int smax = row_slot_words_max(e->has_amb);
+            const char *wwv = getenv("RC_WIN_WORDS");
+            const int forced = wwv ? std::max(4, atoi(wwv)) : 0;
+            X.win = forced ? 1 : (need > smax ? 1 : 0);
+            X.dsw = forced ? std::min(forced, smax) : std::min(need, smax);
+        }
         X.defer = e->d_defer.p;
         X.defer_count = e->d_count.p + 6;
         X.work = e->d_count.p + 7;

@@ -205,6 +205,36 @@ def test_simulated_parity_long_and_gappy(native, lens, indel):
     msgs, summary = full_check(eng, samples)
     assert not msgs, "\n".join(msgs[:10])
     assert summary["hsps"] > 0
+    # transcripts past the row kernels' slot run on its windowed form: none
+    # is left to the one-wave kernel for its length
+    tm = eng.timings()
+    assert tm["defer_length"] == 0 and tm["defer_gaveup"] == 0
+
+
+@pytest.mark.parametrize("words,share,amb", [(4, 1, False), (9, 1, False), (5, 0, False), (6, 1, True)])
+def test_windowed_staging_exact(native, monkeypatch, words, share, amb):
+    """The row kernels' windowed staging (windows of `words` u64 words, 80 to
+    240 bases past the read margin: a refill every few steps) gives every HSP,
+    table and distance of the whole-transcript staging: indels (wide live
+    bands, the 64-lane pass resuming 32-lane extensions), minus strands,
+    isoforms, poly-A tails, ambiguous bases; shared and one-by-one searches."""
+    monkeypatch.setenv("RC_WIN_WORDS", str(words))
+    monkeypatch.setenv("RC_SHARE", str(share))
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(4, 100, seed=23, p_iso2=0.2, indel_rate=0.004, p_revcomp=0.5, polya=(0.3, 10, 40),
+                          len_loc=600, len_n=2000, len_p=0.5)
+    if amb:
+        rng = np.random.default_rng(7)
+        for sm in samples:
+            seq = sm.seq.copy()
+            pos = np.flatnonzero(rng.random(seq.size) < 0.003)
+            seq[pos] = ord("N")
+            sm.seq = seq
+    eng = _run_sim(samples)
+    msgs, summary = full_check(eng, samples)
+    assert not msgs, "\n".join(msgs[:10])
+    tm = eng.timings()
+    assert summary["hsps"] > 0 and tm["defer_length"] == 0 and (tm["ext_wide"] > 0 or not share)
 
 
 @pytest.mark.parametrize("top_matches,keep_all,two_pass", [(1, True, False), (1, False, False), (2, True, False),
@@ -455,7 +485,9 @@ def test_more_than_256_samples(native):
     import itertools
     from oracle.parity import check_pairs
     from rna_clique_amd.simulate import simulate
-    samples, _ = simulate(300, 12, seed=61)
+    # (rate 0.003: the 300-taxon tree's deepest pair is 16 branch-length units
+    # apart, ~5 % divergence -- every gene a 300-clique, as at C3)
+    samples, _ = simulate(300, 12, seed=61, mutation_rate=0.003)
     eng = _run_sim(samples)
     st = eng.stats()
     assert st["sample_count"] == 300 and st["ideal_components"] > 0
