@@ -14,6 +14,7 @@
 // Semantics: oracle/align_oracle.c ("RC-megablast v1"), bit for bit.
 #include "device.h"
 
+#include <algorithm>
 #include <climits>
 #include <cstdlib>
 #include <type_traits>
@@ -135,7 +136,8 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
 {
     const uint64_t big_e = BIG ? P.big_list[blockIdx.x] : 0ull;
     const uint32_t g = BIG ? P.gene_begin + (uint32_t)(big_e >> 16)
-                           : (ISOG ? P.iso_list[blockIdx.x] : P.gene_begin + blockIdx.x);
+                           : (ISOG ? P.iso_list[blockIdx.x]
+                                   : P.gene_begin + (P.gene_order ? (uint32_t)P.gene_order[blockIdx.x] : blockIdx.x));
     if (g >= P.gene_end) return;
     const int tid = threadIdx.x;
 
@@ -255,20 +257,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
     const uint32_t qpb0 = (uint32_t)db.sample_pos_begin[Q], qpb1 = (uint32_t)db.sample_pos_begin[Q + 1];
     // the reverse pass's seeds of this gene's transcripts: [sh_rs0, sh_rs1) of rs_key
     if (P.rs_n) {
-        if (tid < 2) {
-            const uint32_t key = g + (uint32_t)tid;
-            uint32_t lo = 0, n = P.rs_n;
-            while (n) {
-                const uint32_t h = n >> 1;
-                if (P.rs_key[lo + h] < key) {
-                    lo += h + 1;
-                    n -= h + 1;
-                } else {
-                    n = h;
-                }
-            }
-            (tid ? sh_rs1 : sh_rs0) = lo;
-        }
+        if (tid < 2) (tid ? sh_rs1 : sh_rs0) = P.rs_range[2 * (size_t)(g - P.gene_begin) + tid];   // (rs_range_kernel)
         __syncthreads();
     }
     while (T0 < Tr) {
@@ -864,6 +853,95 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
         for (int i = 0; i < 5; i++) atomicAdd(&P.prof[i], tph[i]);
 #endif
 #undef SEED_TICK
+}
+
+// Reverse-only seeds of each query gene of [g0, g1): the lower bounds of g
+// and g + 1 in rs_key (sorted by forward gene), one thread per gene (instead
+// of a dependent binary search at the start of every seed workgroup).
+__global__ void rs_range_kernel(const uint32_t *__restrict__ rs_key, uint32_t rs_n, uint32_t g0, uint32_t g1,
+                                uint32_t *__restrict__ out)
+{
+    const uint64_t n = (uint64_t)(g1 - g0) * 2;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t key = g0 + (uint32_t)(i >> 1) + (uint32_t)(i & 1);
+        uint32_t lo = 0, m = rs_n;
+        while (m) {
+            const uint32_t h = m >> 1;
+            if (rs_key[lo + h] < key) {
+                lo += h + 1;
+                m -= h + 1;
+            } else {
+                m = h;
+            }
+        }
+        out[i] = lo;
+    }
+}
+
+__device__ __forceinline__ uint32_t fmix32(uint32_t h)
+{
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    return h ^ (h >> 16);
+}
+// reverse complement of a 16-mer (base i at bits 2i, 2i + 1)
+__device__ __forceinline__ uint32_t rc16(uint32_t k)
+{
+    uint32_t x = ~k;
+    x = ((x >> 2) & 0x33333333u) | ((x & 0x33333333u) << 2);
+    x = ((x >> 4) & 0x0F0F0F0Fu) | ((x & 0x0F0F0F0Fu) << 4);
+    return __builtin_bswap32(x);
+}
+
+// The order the seed kernel takes a launch's query genes in: by the smallest
+// hash of the canonical 16-mers (strand-independent) of the gene's first
+// transcript. Orthologous genes of different query samples share most of
+// their 16-mers, hence usually this minimum, and so run close together: the
+// index lines, transcript records and subject windows one of them loads are
+// then still in L2 / the Infinity Cache for the others (results do not
+// depend on the order). One thread per gene; keys = minimum << 32 | index.
+__global__ void gene_key_kernel(Db db, uint32_t g0, uint32_t g1, uint64_t *__restrict__ keys)
+{
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < (uint64_t)(g1 - g0);
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t g = g0 + (uint32_t)i;
+        const TxInfo ti = db.tx[db.gene_tx[db.gene_tx_off[g]]];
+        uint32_t best = 0xFFFFFFFFu;
+        const uint64_t s0 = ti.start;
+        const int L = (int)ti.len;
+        if (L >= W16) {
+            // 32-base words of the transcript, each giving the 16-mers that start in it
+            uint64_t w = win(db.F, s0);
+            for (int p0 = 0; p0 + W16 <= L; p0 += 32) {
+                const uint64_t nx = win(db.F, s0 + (uint64_t)p0 + 32);
+                const int nk = min(32, L - W16 + 1 - p0);
+                for (int j = 0; j < nk; j++) {
+                    const uint32_t k = (uint32_t)((w >> (2 * j)) | (j ? nx << (64 - 2 * j) : 0ull));
+                    best = min(best, fmix32(min(k, rc16(k))));
+                }
+                w = nx;
+            }
+        }
+        keys[i] = ((uint64_t)best << 32) | (uint64_t)i;
+    }
+}
+
+void launch_rs_range(const uint32_t *rs_key, uint32_t rs_n, uint32_t g0, uint32_t g1, uint32_t *out, hipStream_t st)
+{
+    const uint64_t n = (uint64_t)(g1 - g0) * 2;
+    if (!n) return;
+    const uint64_t g = std::min<uint64_t>((n + 255) / 256, 65536);
+    hipLaunchKernelGGL(rs_range_kernel, dim3((unsigned)g), dim3(256), 0, st, rs_key, rs_n, g0, g1, out);
+}
+
+void launch_gene_key(const Db &db, uint32_t g0, uint32_t g1, uint64_t *keys, hipStream_t st)
+{
+    const uint64_t n = g1 - g0;
+    if (!n) return;
+    const uint64_t g = std::min<uint64_t>((n + 255) / 256, 65536);
+    hipLaunchKernelGGL(gene_key_kernel, dim3((unsigned)g), dim3(256), 0, st, db, g0, g1, keys);
 }
 
 // ------------------------------------------------------------------------
@@ -1551,13 +1629,34 @@ __device__ __forceinline__ int lane_sel_k(uint64_t m, int b)
     return r;
 }
 
-// Matching bases from (pa, pb) forward, at most maxn; positions are absolute
-// LDS base positions (lds_win2); masks (AMB) sit `moff` bases further on.
+// 32 bases of each side from the dwords at byte addresses a, b holding the
+// bases at LDS base positions pa, pb (+ a multiple of 16): three dword reads
+// and two funnel shifts per side
+__device__ __forceinline__ void lds_pair_at(uint32_t a, uint32_t b, uint32_t pa, uint32_t pb, uint64_t &wa,
+                                            uint64_t &wb)
+{
+    uint64_t a01, b01;
+    uint32_t a2, b2;
+    asm volatile("ds_read2_b32 %0, %4 offset1:1\n\t"
+                 "ds_read_b32 %1, %4 offset:8\n\t"
+                 "ds_read2_b32 %2, %5 offset1:1\n\t"
+                 "ds_read_b32 %3, %5 offset:8\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(a01), "=&v"(a2), "=&v"(b01), "=&v"(b2)
+                 : "v"(a), "v"(b));
+    wa = lds_join(a01, a2, pa);
+    wb = lds_join(b01, b2, pb);
+}
+
+// Matching bases from (pa, pb) forward, at most maxn (>= 0); positions are
+// absolute LDS base positions (lds_win2); masks (AMB) sit `moff` bases
+// further on. Reads bases up to pa + max(maxn, 1) + 47 (WIN_MARGIN).
 template <bool AMB>
 __device__ __forceinline__ int slide_fwd(uint32_t pa, uint32_t pb, int maxn, uint32_t moff)
 {
     // the first window outside any loop (a mismatch within 32 bases is the
-    // common case); lanes on a run of 32+ matches continue in the loop
+    // common case); lanes on a run of 32+ matches go on in the loop, whose
+    // dword addresses advance by 8 bytes per 32 bases (the shifts stay)
     uint64_t x = lds_diff(pa, pb);
     if (AMB) {
         uint64_t ma, mb;
@@ -1566,12 +1665,14 @@ __device__ __forceinline__ int slide_fwd(uint32_t pa, uint32_t pb, int maxn, uin
     }
     int n = x ? (int)(__builtin_ctzll(x) >> 1) : 32;
     if (n == 32 && maxn > 32) {
+        uint32_t a = ((pa + 32u) >> 2) & ~3u, b = ((pb + 32u) >> 2) & ~3u;
         for (;;) {
-            x = lds_diff(pa + (uint32_t)n, pb + (uint32_t)n);
+            uint64_t wa, wb;
+            lds_pair_at(a, b, pa, pb, wa, wb);
+            x = wa ^ wb;
             if (AMB) {
-                uint64_t ma, mb;
-                lds_win2(pa + (uint32_t)n + moff, pb + (uint32_t)n + moff, ma, mb);
-                x |= ma | mb;
+                lds_pair_at(a + moff / 4u, b + moff / 4u, pa, pb, wa, wb);
+                x |= wa | wb;
             }
             if (x) {
                 n += (int)(__builtin_ctzll(x) >> 1);
@@ -1579,11 +1680,12 @@ __device__ __forceinline__ int slide_fwd(uint32_t pa, uint32_t pb, int maxn, uin
             }
             n += 32;
             if (n >= maxn) break;
+            a += 8u;
+            b += 8u;
         }
     }
-    return min(n, max(maxn, 0));
+    return min(n, maxn);
 }
-
 
 // per-row bookkeeping in LDS: the candidate record (CAND_DWORDS dwords) and state
 enum { RM_REC = 0, RM_CLO = CAND_DWORDS, RM_CHI, RM_QB, RM_TB, RM_X, RM_Y, RM_LEN,
@@ -1654,7 +1756,8 @@ __host__ __device__ constexpr size_t row_lds_bytes(int rw, int na, int sw, bool 
            (win ? (size_t)(EBLOCK / rw) * sizeof(RowWin) : 0);
 }
 // windowed slot limits: a slide from offset ni with at most mw bases reads
-// bases up to ni + mw + 46 (three dwords from the position's dword)
+// bases up to ni + max(mw, 1) + 47 (slide_fwd: three dwords from the dword
+// holding the last window's start)
 constexpr int WIN_MARGIN = 48;
 
 // Extension of every candidate's FIRST seed (its smallest (x, y): always
@@ -1910,7 +2013,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
             if (pend) {
                 const int c2 = ni + s, mr = m - s;
                 const int mw = c2 < wlo ? -1 : min(mr, wlim - c2);
-                const int s2 = slide_fwd<AMB>(pa + (uint32_t)c2, pbk + (uint32_t)c2, mw, moff);
+                const int s2 = slide_fwd<AMB>(pa + (uint32_t)c2, pbk + (uint32_t)c2, max(mw, 0), moff);
                 pend = mw < mr && s2 >= mw;
                 s += s2;
             }
@@ -1925,7 +2028,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
             bool pend = false;
             if (rl == RC0) {
                 const int mw = min(m0, wlim);
-                r0 = slide_fwd<AMB>(pa, pb, mw, moff);
+                r0 = slide_fwd<AMB>(pa, pb, max(mw, 0), moff);
                 pend = mw < m0 && r0 >= mw;
             }
             if (ballot(pend)) win_resolve(0, r0, m0, pend);
@@ -2307,7 +2410,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 if (ni >= 0) {
                     m = min(alen - ni, blk - ni);
                     const int mw = ni < wlo ? -1 : min(m, wlim - ni);
-                    s = slide_fwd<AMB>(pa + (uint32_t)ni, pbk + (uint32_t)ni, mw, moff);
+                    s = slide_fwd<AMB>(pa + (uint32_t)ni, pbk + (uint32_t)ni, max(mw, 0), moff);
                     pend = mw < m && s >= mw;
                 }
                 if (ballot(pend)) win_resolve(ni, s, m, pend);

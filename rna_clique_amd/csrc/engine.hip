@@ -54,6 +54,8 @@ void launch_near_fill(bool, const TxInfo *, uint32_t, const uint8_t *, const uin
                       const uint64_t *, uint64_t *, uint64_t, unsigned long long *, hipStream_t);
 void launch_seed(bool, const Db &, const Index &, const SeedParams &, hipStream_t);
 void launch_seed_big(bool, const Db &, const Index &, const SeedParams &, uint32_t, hipStream_t);
+void launch_rs_range(const uint32_t *, uint32_t, uint32_t, uint32_t, uint32_t *, hipStream_t);
+void launch_gene_key(const Db &, uint32_t, uint32_t, uint64_t *, hipStream_t);
 void launch_dust(bool, uint64_t, const uint64_t *, const uint64_t *, const uint64_t *, const TxInfo *, uint32_t, int,
                  int, int, uint32_t *, uint64_t *, uint32_t, int, uint64_t *, hipStream_t);
 uint32_t dust_scratch_words(uint32_t);
@@ -347,7 +349,8 @@ struct rc_engine {
     int mindex_bits = 16;
     uint64_t n_mindex = 0, mnear_cap = 0;
     DBuf<LSeed> d_rseeds;
-    DBuf<uint32_t> d_rseed_gene, d_rs_key, d_rs_idx;
+    DBuf<uint32_t> d_rseed_gene, d_rs_key, d_rs_idx, d_rs_range;
+    DBuf<uint64_t> d_gkey, d_gkey2;   // seed launches' gene order (gene_key_kernel, sorted)
     DBuf<unsigned long long> d_rctr;   // [0] near-index entries, [1] reverse-only seeds
     DBuf<uint64_t> d_rtmask;
     DBuf<int32_t> d_trange, d_rtrange;   // [N][2] subject-sample range of each query sample (tmask / rtmask)
@@ -1301,6 +1304,27 @@ static void tile_plan(rc_engine *e, int ti, std::vector<uint64_t> &tmask, std::v
     }
 }
 
+// The order a seed launch over the genes [g0, g1) takes them in (sorted
+// minimum-hash keys, gene_key_kernel: orthologs of different query samples
+// together), or null with RC_GENE_ORDER=0.
+static int gene_order(rc_engine *e, const Db &db, uint32_t g0, uint32_t g1, const uint64_t *&order)
+{
+    static const bool off = getenv("RC_GENE_ORDER") && atoi(getenv("RC_GENE_ORDER")) == 0;
+    order = nullptr;
+    const uint32_t n = g1 - g0;
+    if (off || n < 2) return RC_OK;
+    CHK(e->d_gkey.ensure(n));
+    CHK(e->d_gkey2.ensure(n));
+    launch_gene_key(db, g0, g1, e->d_gkey.p, e->st);
+    HIPCHK(hipGetLastError());
+    size_t tmp = 0;
+    HIPCHK(rocprim::radix_sort_keys(nullptr, tmp, e->d_gkey.p, e->d_gkey2.p, (size_t)n, 0u, 64u, e->st));
+    CHK(e->d_tmp.ensure(tmp));
+    HIPCHK(rocprim::radix_sort_keys(e->d_tmp.p, tmp, e->d_gkey.p, e->d_gkey2.p, (size_t)n, 0u, 64u, e->st));
+    order = e->d_gkey2.p;
+    return RC_OK;
+}
+
 // The reverse pass of shared searches with DUST: queries = the
 // higher sample of each pair of tile ti, subjects = the near-mask index ixm.
 // It keeps only the reverse-search runs the forward pass cannot see, as SEED_R
@@ -1365,6 +1389,7 @@ static int reverse_pass(rc_engine *e, int ti, const Db &db, const Index &ixm, ui
             S.rseed_n = e->d_rctr.p + 1;
             S.gene_begin = e->sample_gene_begin[r.first];
             S.gene_end = e->sample_gene_begin[r.second];
+            CHK(gene_order(e, db, S.gene_begin, S.gene_end, S.gene_order));
             S.tmask = e->d_rtmask.p;
             S.tmw = tw;
             S.trange = e->d_rtrange.p;
@@ -1625,6 +1650,12 @@ static int align_tile(rc_engine *e, int ti)
             S.list2_n = e->d_count.p + 16;
             S.gene_begin = rg0[r];
             S.gene_end = rg1[r];
+            if (n_rs) {
+                CHK(e->d_rs_range.ensure((size_t)2 * (rg1[r] - rg0[r]) + 2));
+                launch_rs_range(e->d_rs_key.p, n_rs, rg0[r], rg1[r], e->d_rs_range.p, e->st);
+                S.rs_range = e->d_rs_range.p;
+            }
+            CHK(gene_order(e, db, rg0[r], rg1[r], S.gene_order));
             S.iso_list = e->d_iso_list.p + ioff[r];
             S.iso_n = ioff[r + 1] - ioff[r];
             S.seeds = e->d_seeds.p;
