@@ -38,7 +38,15 @@ extern "C" {
 #define RC_E_NO_IDEAL (-5)   /* a pair has no ideal-component rows:
                                 NoIdealComponentsError, filtered_distance.py:242-247 */
 #define RC_E_CAPACITY (-6)   /* caller buffer too small */
-#define RC_E_LIMIT (-7)      /* input beyond a documented engine limit */
+#define RC_E_LIMIT (-7)      /* input beyond a documented engine limit: */
+/*   samples per engine            65535
+ *   transcripts per engine        2^27
+ *   transcript length             16 Mbp
+ *   transcripts (isoforms) / gene 65535 while the longest transcript is under
+ *                                 1 Mbp; 2^(36 - b) - 1 for a longest length of
+ *                                 b bits (4095 at 16 Mbp)
+ *   bases per alignment tile      2^32 (a shard is cut into tiles below that)
+ *   seeds per (query gene, subject sample) pass 2^22 */
 #define RC_E_IO (-8)         /* file could not be written */
 
 typedef struct rc_engine rc_engine;
@@ -135,6 +143,8 @@ typedef struct rc_timing {
                                  up on their first seed (transcript length) */
     double defer_outside;     /* directed searches the one-wave kernel took because a seed lies outside
                                  their first HSP's box (more than one HSP) */
+    double index_reused;      /* alignment tiles that reused the previous tile's 16-mer index and subject
+                                 DUST masks (split tiles of one subject chunk) */
 } rc_timing;
 
 void rc_default_opts(rc_opts *opts);

@@ -136,8 +136,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
 {
     const uint64_t big_e = BIG ? P.big_list[blockIdx.x] : 0ull;
     const uint32_t g = BIG ? P.gene_begin + (uint32_t)(big_e >> 16)
-                           : (ISOG ? P.iso_list[blockIdx.x]
-                                   : P.gene_begin + (P.gene_order ? (uint32_t)P.gene_order[blockIdx.x] : blockIdx.x));
+                           : (ISOG ? P.iso_list[blockIdx.x] : P.gene_begin + blockIdx.x);
     if (g >= P.gene_end) return;
     const int tid = threadIdx.x;
 
@@ -878,70 +877,12 @@ __global__ void rs_range_kernel(const uint32_t *__restrict__ rs_key, uint32_t rs
     }
 }
 
-__device__ __forceinline__ uint32_t fmix32(uint32_t h)
-{
-    h ^= h >> 16;
-    h *= 0x85ebca6bu;
-    h ^= h >> 13;
-    h *= 0xc2b2ae35u;
-    return h ^ (h >> 16);
-}
-// reverse complement of a 16-mer (base i at bits 2i, 2i + 1)
-__device__ __forceinline__ uint32_t rc16(uint32_t k)
-{
-    uint32_t x = ~k;
-    x = ((x >> 2) & 0x33333333u) | ((x & 0x33333333u) << 2);
-    x = ((x >> 4) & 0x0F0F0F0Fu) | ((x & 0x0F0F0F0Fu) << 4);
-    return __builtin_bswap32(x);
-}
-
-// The order the seed kernel takes a launch's query genes in: by the smallest
-// hash of the canonical 16-mers (strand-independent) of the gene's first
-// transcript. Orthologous genes of different query samples share most of
-// their 16-mers, hence usually this minimum, and so run close together: the
-// index lines, transcript records and subject windows one of them loads are
-// then still in L2 / the Infinity Cache for the others (results do not
-// depend on the order). One thread per gene; keys = minimum << 32 | index.
-__global__ void gene_key_kernel(Db db, uint32_t g0, uint32_t g1, uint64_t *__restrict__ keys)
-{
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < (uint64_t)(g1 - g0);
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t g = g0 + (uint32_t)i;
-        const TxInfo ti = db.tx[db.gene_tx[db.gene_tx_off[g]]];
-        uint32_t best = 0xFFFFFFFFu;
-        const uint64_t s0 = ti.start;
-        const int L = (int)ti.len;
-        if (L >= W16) {
-            // 32-base words of the transcript, each giving the 16-mers that start in it
-            uint64_t w = win(db.F, s0);
-            for (int p0 = 0; p0 + W16 <= L; p0 += 32) {
-                const uint64_t nx = win(db.F, s0 + (uint64_t)p0 + 32);
-                const int nk = min(32, L - W16 + 1 - p0);
-                for (int j = 0; j < nk; j++) {
-                    const uint32_t k = (uint32_t)((w >> (2 * j)) | (j ? nx << (64 - 2 * j) : 0ull));
-                    best = min(best, fmix32(min(k, rc16(k))));
-                }
-                w = nx;
-            }
-        }
-        keys[i] = ((uint64_t)best << 32) | (uint64_t)i;
-    }
-}
-
 void launch_rs_range(const uint32_t *rs_key, uint32_t rs_n, uint32_t g0, uint32_t g1, uint32_t *out, hipStream_t st)
 {
     const uint64_t n = (uint64_t)(g1 - g0) * 2;
     if (!n) return;
     const uint64_t g = std::min<uint64_t>((n + 255) / 256, 65536);
     hipLaunchKernelGGL(rs_range_kernel, dim3((unsigned)g), dim3(256), 0, st, rs_key, rs_n, g0, g1, out);
-}
-
-void launch_gene_key(const Db &db, uint32_t g0, uint32_t g1, uint64_t *keys, hipStream_t st)
-{
-    const uint64_t n = g1 - g0;
-    if (!n) return;
-    const uint64_t g = std::min<uint64_t>((n + 255) / 256, 65536);
-    hipLaunchKernelGGL(gene_key_kernel, dim3((unsigned)g), dim3(256), 0, st, db, g0, g1, keys);
 }
 
 // ------------------------------------------------------------------------

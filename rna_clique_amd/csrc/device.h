@@ -199,9 +199,6 @@ struct SeedParams {
     const uint32_t *rs_key, *rs_idx;
     uint32_t rs_n;
     const uint32_t *rs_range;     // [(g - gene_begin) * 2]: gene g's reverse-only seeds [rs_key lower bounds of g, g + 1)
-    // the order the launch's workgroups take the genes of [gene_begin,
-    // gene_end) in (low 32 bits: g - gene_begin), or null (gene order)
-    const uint64_t *gene_order;
     uint32_t *list2;              // shared searches: slots of the candidates with e1 != SEED_NONE
     unsigned long long *list2_n;
     uint32_t gene_begin, gene_end;   // shard

@@ -55,7 +55,6 @@ void launch_near_fill(bool, const TxInfo *, uint32_t, const uint8_t *, const uin
 void launch_seed(bool, const Db &, const Index &, const SeedParams &, hipStream_t);
 void launch_seed_big(bool, const Db &, const Index &, const SeedParams &, uint32_t, hipStream_t);
 void launch_rs_range(const uint32_t *, uint32_t, uint32_t, uint32_t, uint32_t *, hipStream_t);
-void launch_gene_key(const Db &, uint32_t, uint32_t, uint64_t *, hipStream_t);
 void launch_dust(bool, uint64_t, const uint64_t *, const uint64_t *, const uint64_t *, const TxInfo *, uint32_t, int,
                  int, int, uint32_t *, uint64_t *, uint32_t, int, uint64_t *, hipStream_t);
 uint32_t dust_scratch_words(uint32_t);
@@ -307,6 +306,12 @@ struct rc_engine {
     struct Tile {
         std::vector<int> samples;                 // ascending
         std::vector<std::pair<int, int>> pairs;   // (a, b), a < b
+        // split tiles (a shard cut into several, every a below every b):
+        // the b chunk's samples sit at bstart, the same in every tile of that
+        // chunk, so consecutive tiles of one b chunk share its 16-mer index
+        // and its DUST masks (only the a part is redone)
+        int bchunk = -1;
+        uint64_t bstart = 0;
     };
     std::vector<Tile> tiles;
     int64_t tiles_for = -1;
@@ -317,6 +322,11 @@ struct rc_engine {
     uint32_t tile_ntx = 0;              // the tile's transcripts (DUST, near-mask index)
     uint32_t tile_nitx = 0;             // ... of its subject samples (the 16-mer index)
     bool tile_share = false;            // the search mode the loaded tile's index list was built for
+    uint32_t tile_a_ntx = 0;            // split tiles: transcripts of the a part (the first ones)
+    // the b chunk (split tiles) whose index and DUST masks the device holds
+    // from this run's previous tile (-1: none)
+    int idx_bchunk = -1;
+    uint64_t idx_bstart = 0;
     uint64_t hsp_used = 0;              // HSPs appended to d_hsp by the tiles of this run
 
     // external HSPs
@@ -350,7 +360,6 @@ struct rc_engine {
     uint64_t n_mindex = 0, mnear_cap = 0;
     DBuf<LSeed> d_rseeds;
     DBuf<uint32_t> d_rseed_gene, d_rs_key, d_rs_idx, d_rs_range;
-    DBuf<uint64_t> d_gkey, d_gkey2;   // seed launches' gene order (gene_key_kernel, sorted)
     DBuf<unsigned long long> d_rctr;   // [0] near-index entries, [1] reverse-only seeds
     DBuf<uint64_t> d_rtmask;
     DBuf<int32_t> d_trange, d_rtrange;   // [N][2] subject-sample range of each query sample (tmask / rtmask)
@@ -913,16 +922,24 @@ static void plan_tiles(rc_engine *e)
         }
         return out;
     };
-    const auto CA = ub <= cap ? std::vector<std::vector<int>>{U} : chunks(A, cap / 2);
-    const auto CB = ub <= cap ? std::vector<std::vector<int>>{U} : chunks(B, cap / 2);
+    const bool multi = ub > cap;
+    const auto CA = !multi ? std::vector<std::vector<int>>{U} : chunks(A, cap / 2);
+    const auto CB = !multi ? std::vector<std::vector<int>>{U} : chunks(B, cap / 2);
+    static const bool no_split = getenv("RC_TILE_SPLIT") && atoi(getenv("RC_TILE_SPLIT")) == 0;
+    uint64_t amax = 0;
     for (size_t j = 0; j < CB.size(); j++)
         for (size_t i = 0; i < CA.size(); i++) {
             rc_engine::Tile t;
             std::vector<char> ina(e->samples.size(), 0), inb(e->samples.size(), 0);
             for (int s : CA[i]) ina[s] = 1;
             for (int s : CB[j]) inb[s] = 1;
+            int amax_s = -1, bmin_s = INT32_MAX;
             for (auto &pr : pairs)
-                if (ina[pr.first] && inb[pr.second]) t.pairs.push_back(pr);
+                if (ina[pr.first] && inb[pr.second]) {
+                    t.pairs.push_back(pr);
+                    amax_s = std::max(amax_s, pr.first);
+                    bmin_s = std::min(bmin_s, pr.second);
+                }
             if (t.pairs.empty()) continue;
             for (auto &pr : t.pairs) {
                 t.samples.push_back(pr.first);
@@ -930,8 +947,20 @@ static void plan_tiles(rc_engine *e)
             }
             std::sort(t.samples.begin(), t.samples.end());
             t.samples.erase(std::unique(t.samples.begin(), t.samples.end()), t.samples.end());
+            if (multi && !no_split && amax_s < bmin_s) {
+                // every a below every b: the b part (all of CB[j]: each of its
+                // samples pairs with the a's) after a part padded to the
+                // largest a part of any split tile
+                t.bchunk = (int)j;
+                uint64_t ab = 0;
+                for (int s : t.samples)
+                    if (s <= amax_s) ab += bases(s);
+                amax = std::max(amax, ab);
+            }
             e->tiles.push_back(t);
         }
+    for (auto &t : e->tiles)
+        if (t.bchunk >= 0) t.bstart = amax;
 }
 
 // Device tables of tile ti: packed working copy (gathered from d_ascii unless
@@ -947,11 +976,16 @@ static int load_tile(rc_engine *e, int ti)
     std::vector<char> in(N, 0);
     for (int s : T.samples) in[s] = 1;
     // layout: tile samples in ascending order, each at a TILE_ALIGN boundary;
-    // d_ascii holds exactly that layout when the tile is every resident sample
+    // d_ascii holds exactly that layout when the tile is every resident sample.
+    // A split tile's b part starts at T.bstart (after the a part's padding)
     uint64_t pos = 0;
-    bool direct = true;
+    bool direct = T.bchunk < 0;
+    int amax_s = -1;
+    if (T.bchunk >= 0)
+        for (auto &pr : T.pairs) amax_s = std::max(amax_s, pr.first);
     for (int s = 0; s < N; s++) {
         if (!in[s]) continue;
+        if (T.bchunk >= 0 && s > amax_s && pos < T.bstart) pos = T.bstart;
         e->tile_pos[s] = pos;
         direct = direct && e->samples[s].abase == pos;
         pos += align_up(e->samples[s].nbases);
@@ -1036,6 +1070,9 @@ static int load_tile(rc_engine *e, int ti)
     e->tile_gid = gid;
     e->tile_ntx = (uint32_t)ttx.size();
     e->tile_nitx = (uint32_t)itx.size();
+    e->tile_a_ntx = 0;
+    if (T.bchunk >= 0)
+        for (const TxInfo &x : ttx) e->tile_a_ntx += x.start < T.bstart ? 1u : 0u;
     e->tile_share = share;
     // the packed working copy's source: d_ascii itself or a gathered copy
     if (!direct) {
@@ -1304,27 +1341,6 @@ static void tile_plan(rc_engine *e, int ti, std::vector<uint64_t> &tmask, std::v
     }
 }
 
-// The order a seed launch over the genes [g0, g1) takes them in (sorted
-// minimum-hash keys, gene_key_kernel: orthologs of different query samples
-// together), or null with RC_GENE_ORDER=0.
-static int gene_order(rc_engine *e, const Db &db, uint32_t g0, uint32_t g1, const uint64_t *&order)
-{
-    static const bool off = getenv("RC_GENE_ORDER") && atoi(getenv("RC_GENE_ORDER")) == 0;
-    order = nullptr;
-    const uint32_t n = g1 - g0;
-    if (off || n < 2) return RC_OK;
-    CHK(e->d_gkey.ensure(n));
-    CHK(e->d_gkey2.ensure(n));
-    launch_gene_key(db, g0, g1, e->d_gkey.p, e->st);
-    HIPCHK(hipGetLastError());
-    size_t tmp = 0;
-    HIPCHK(rocprim::radix_sort_keys(nullptr, tmp, e->d_gkey.p, e->d_gkey2.p, (size_t)n, 0u, 64u, e->st));
-    CHK(e->d_tmp.ensure(tmp));
-    HIPCHK(rocprim::radix_sort_keys(e->d_tmp.p, tmp, e->d_gkey.p, e->d_gkey2.p, (size_t)n, 0u, 64u, e->st));
-    order = e->d_gkey2.p;
-    return RC_OK;
-}
-
 // The reverse pass of shared searches with DUST: queries = the
 // higher sample of each pair of tile ti, subjects = the near-mask index ixm.
 // It keeps only the reverse-search runs the forward pass cannot see, as SEED_R
@@ -1389,7 +1405,6 @@ static int reverse_pass(rc_engine *e, int ti, const Db &db, const Index &ixm, ui
             S.rseed_n = e->d_rctr.p + 1;
             S.gene_begin = e->sample_gene_begin[r.first];
             S.gene_end = e->sample_gene_begin[r.second];
-            CHK(gene_order(e, db, S.gene_begin, S.gene_end, S.gene_order));
             S.tmask = e->d_rtmask.p;
             S.tmw = tw;
             S.trange = e->d_rtrange.p;
@@ -1510,10 +1525,16 @@ static int align_tile(rc_engine *e, int ti)
                 e->has_amb ? e->d_ARC.p + FRONT_PAD : nullptr, e->st);
     HIPCHK(hipGetLastError());
     const bool dust = e->o.dust_level > 0;
+    // a split tile of the b chunk the previous tile had: its 16-mer index
+    // (the b part's) and the b part's DUST masks are on the device already
+    const rc_engine::Tile &TT = e->tiles[ti];
+    const bool reuse = TT.bchunk >= 0 && TT.bchunk == e->idx_bchunk && TT.bstart == e->idx_bstart &&
+                       e->d_dmask.cap >= (total >> 6) + 4;
+    const uint64_t dtot = reuse ? TT.bstart : total;   // DUST's range: the a part only when reusing
     if (dust) {
         const size_t mw = (total >> 6) + 4;
         CHK(e->d_dmask.ensure(mw));
-        HIPCHK(hipMemsetAsync(e->d_dmask.p, 0, mw * 8, e->st));
+        HIPCHK(hipMemsetAsync(e->d_dmask.p, 0, (reuse ? 1 + (dtot >> 6) : mw) * 8, e->st));
     }
     HIPCHK(hipEventRecord(e->ev[1], e->st));
     // DUST masks of the tile's transcripts (the query side), bit per base, on
@@ -1530,8 +1551,9 @@ static int align_tile(rc_engine *e, int ti)
         HIPCHK(hipEventRecord(e->evd[2], e->st));
         HIPCHK(hipStreamWaitEvent(e->st2, e->evd[2], 0));
         HIPCHK(hipEventRecord(e->evd[0], e->st2));
-        launch_dust(e->has_amb, total, e->d_F.p + FRONT_PAD, e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr,
-                    e->d_txstart.p + 1, e->d_tile_tx.p, e->tile_ntx, e->o.dust_level, e->o.dust_window,
+        launch_dust(e->has_amb, dtot, e->d_F.p + FRONT_PAD, e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr,
+                    e->d_txstart.p + 1, e->d_tile_tx.p, reuse ? e->tile_a_ntx : e->tile_ntx, e->o.dust_level,
+                    e->o.dust_window,
                     e->o.dust_linker, e->d_dust_scratch.p, e->d_dust_events.p, dblocks, dwaves, e->d_dmask.p + 1,
                     e->st2);
         HIPCHK(hipGetLastError());
@@ -1541,7 +1563,14 @@ static int align_tile(rc_engine *e, int ti)
     const char *dev = getenv("RC_DUST_EARLY");
     const bool dust_early = !(dev && atoi(dev) == 0);
     if (dust && dust_early) CHK(start_dust());
-    CHK(build_index(e, dust && !dust_early ? std::function<int()>(start_dust) : nullptr));
+    if (reuse) {
+        if (dust && !dust_early) CHK(start_dust());
+        e->tm.index_reused += 1.0;
+    } else {
+        CHK(build_index(e, dust && !dust_early ? std::function<int()>(start_dust) : nullptr));
+    }
+    e->idx_bchunk = TT.bchunk;
+    e->idx_bstart = TT.bstart;
     HIPCHK(hipGetLastError());
     if (dust) HIPCHK(hipStreamWaitEvent(e->st, e->evd[1], 0));
     e->share = share_mode(e);   // (load_tile built the index list for it)
@@ -1655,7 +1684,6 @@ static int align_tile(rc_engine *e, int ti)
                 launch_rs_range(e->d_rs_key.p, n_rs, rg0[r], rg1[r], e->d_rs_range.p, e->st);
                 S.rs_range = e->d_rs_range.p;
             }
-            CHK(gene_order(e, db, rg0[r], rg1[r], S.gene_order));
             S.iso_list = e->d_iso_list.p + ioff[r];
             S.iso_n = ioff[r + 1] - ioff[r];
             S.seeds = e->d_seeds.p;
@@ -2059,6 +2087,7 @@ static int do_align(rc_engine *e)
     }
     e->hsp_used = 0;
     e->n_seeds = e->n_cands = 0;
+    e->idx_bchunk = -1;   // every run builds its indexes and masks anew
     // the tile loaded last goes first (its tables stay on the device)
     const int nt = (int)e->tiles.size();
     const int first = (e->tile_loaded >= 0 && e->tile_loaded < nt) ? e->tile_loaded : 0;

@@ -359,10 +359,15 @@ def test_tables_and_graph_reload(native, tmp_path):
     assert np.array_equal(again.get_dissimilarity_df().to_numpy(), want.to_numpy())
 
 
-def test_tiles_match_one_pass(native, monkeypatch):
+@pytest.mark.parametrize("split", [1, 0])
+def test_tiles_match_one_pass(native, monkeypatch, split):
     """A shard whose samples do not fit one alignment pass is cut into tiles
     (a- and b-chunks, positions relative to each tile, HSPs appended): forced
-    here with a small RC_TILE_BASES, the results equal one pass bit for bit."""
+    here with a small RC_TILE_BASES, the results equal one pass bit for bit.
+    split 1 (default): tiles with every a below every b place the b chunk at
+    a fixed position, and consecutive tiles of one b chunk reuse its 16-mer
+    index and DUST masks; split 0 (RC_TILE_SPLIT=0) rebuilds both per tile."""
+    monkeypatch.setenv("RC_TILE_SPLIT", str(split))
     from rna_clique_amd.engine import Engine
     from rna_clique_amd.simulate import simulate
     samples, _ = simulate(6, 150, seed=23, p_iso2=0.2, indel_rate=0.002, p_revcomp=0.3,
@@ -373,7 +378,8 @@ def test_tiles_match_one_pass(native, monkeypatch):
     monkeypatch.setenv("RC_TILE_BASES", str(3 * per))
     eng = _load(Engine(device=0), samples)
     eng.run()
-    assert eng.timings()["tiles"] > 1
+    tm = eng.timings()
+    assert tm["tiles"] > 1 and (tm["index_reused"] > 0) == bool(split)
     for q in range(6):
         for s in range(6):
             if q != s:
