@@ -925,7 +925,7 @@ static void plan_tiles(rc_engine *e)
     const bool multi = ub > cap;
     const auto CA = !multi ? std::vector<std::vector<int>>{U} : chunks(A, cap / 2);
     const auto CB = !multi ? std::vector<std::vector<int>>{U} : chunks(B, cap / 2);
-    static const bool no_split = getenv("RC_TILE_SPLIT") && atoi(getenv("RC_TILE_SPLIT")) == 0;
+    const bool no_split = getenv("RC_TILE_SPLIT") && atoi(getenv("RC_TILE_SPLIT")) == 0;   // (per plan: tests flip it)
     uint64_t amax = 0;
     for (size_t j = 0; j < CB.size(); j++)
         for (size_t i = 0; i < CA.size(); i++) {
