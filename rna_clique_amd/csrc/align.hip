@@ -1589,55 +1589,6 @@ __device__ __forceinline__ void lds_pair_at(uint32_t a, uint32_t b, uint32_t pa,
     wb = lds_join(b01, b2, pb);
 }
 
-// A slide's first window, split so that its LDS reads are in flight while
-// the step computes other things: lds_issue2 starts the reads of the 32
-// bases at pa and at pb, lds_wait2 waits for them (its operands tie the
-// registers to the wait), slide_fwd_from goes on like slide_fwd.
-#ifndef RC_SLIDE_PREFETCH
-#define RC_SLIDE_PREFETCH 0   // measured A/B build: -DRC_SLIDE_PREFETCH=1
-#endif
-constexpr bool SLIDE_PREFETCH = RC_SLIDE_PREFETCH;
-struct LdsWin2 {
-    uint64_t a01, b01;
-    uint32_t a2, b2;
-};
-__device__ __forceinline__ void lds_issue2(uint32_t pa, uint32_t pb, LdsWin2 &w)
-{
-    const uint32_t aa = (pa >> 2) & ~3u, ab = (pb >> 2) & ~3u;
-    asm volatile("ds_read2_b32 %0, %4 offset1:1\n\t"
-                 "ds_read_b32 %1, %4 offset:8\n\t"
-                 "ds_read2_b32 %2, %5 offset1:1\n\t"
-                 "ds_read_b32 %3, %5 offset:8"
-                 : "=&v"(w.a01), "=&v"(w.a2), "=&v"(w.b01), "=&v"(w.b2)
-                 : "v"(aa), "v"(ab));
-}
-__device__ __forceinline__ void lds_wait2(LdsWin2 &w)
-{
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w.a01), "+v"(w.a2), "+v"(w.b01), "+v"(w.b2));
-}
-__device__ __forceinline__ int slide_fwd_from(const LdsWin2 &w, uint32_t pa, uint32_t pb, int maxn)
-{
-    uint64_t x = lds_join(w.a01, w.a2, pa) ^ lds_join(w.b01, w.b2, pb);
-    int n = x ? (int)(__builtin_ctzll(x) >> 1) : 32;
-    if (n == 32 && maxn > 32) {
-        uint32_t a = ((pa + 32u) >> 2) & ~3u, b = ((pb + 32u) >> 2) & ~3u;
-        for (;;) {
-            uint64_t wa, wb;
-            lds_pair_at(a, b, pa, pb, wa, wb);
-            x = wa ^ wb;
-            if (x) {
-                n += (int)(__builtin_ctzll(x) >> 1);
-                break;
-            }
-            n += 32;
-            if (n >= maxn) break;
-            a += 8u;
-            b += 8u;
-        }
-    }
-    return min(n, maxn);
-}
-
 // Matching bases from (pa, pb) forward, at most maxn (>= 0); positions are
 // absolute LDS base positions (lds_win2); masks (AMB) sit `moff` bases
 // further on. Reads bases up to pa + max(maxn, 1) + 47 (WIN_MARGIN).
@@ -2383,11 +2334,6 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
             const int cil = ((uint32_t)Rl < (uint32_t)alen) ? Rl + 1 : -1;
             const int cd = (Rr >= 0 && Rr <= blk) ? Rr : -1;
             int ni = max(max(cm, cil), cd);
-            // (no ambiguity masks, whole-transcript staging) the slide's first
-            // window reads go out now, the gap-state work below hides their latency
-            LdsWin2 w1;
-            if constexpr (SLIDE_PREFETCH && !AMB && !WIN)
-                if (ni >= 0) lds_issue2(pa + (uint32_t)ni, pbk + (uint32_t)ni, w1);
             const bool fm = ni >= 0 && cm == ni, fi = !fm && cil == ni;
             // gap state of the chosen move: G | O << 13 | E << 26 (E: 1 insertion, 2 deletion)
             const int src = fm ? goe : (fi ? gl : gr);
@@ -2418,13 +2364,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 }
             } else if (ni >= 0) {
                 const int m = min(alen - ni, blk - ni);
-                int s;
-                if constexpr (SLIDE_PREFETCH && !AMB) {
-                    lds_wait2(w1);
-                    s = slide_fwd_from(w1, pa + (uint32_t)ni, pbk + (uint32_t)ni, m);
-                } else {
-                    s = slide_fwd<AMB>(pa + (uint32_t)ni, pbk + (uint32_t)ni, m, moff);
-                }
+                const int s = slide_fwd<AMB>(pa + (uint32_t)ni, pbk + (uint32_t)ni, m, moff);
                 ni += s;
                 if (s > 0) ng &= ~(3 << EBIT);
                 score = 2 * ni + nkd;   // 2 ni - k - d6

@@ -110,7 +110,8 @@ __device__ __forceinline__ void ratio_max(int &n, int &d, int m, int e)
 }
 
 template <bool AMB>
-__global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t total, uint64_t nwords, const uint64_t *__restrict__ F,
+__global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t begin, uint64_t total, uint64_t nwords,
+                                                  const uint64_t *__restrict__ F,
                                                   const uint64_t *__restrict__ AF,
                                                   const uint64_t *__restrict__ txstart, int T, int W,
                                                   uint64_t *__restrict__ evs, uint32_t *__restrict__ scratch,
@@ -127,7 +128,7 @@ __global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t total, 
     __shared__ uint32_t cnt_lds[DW * 17];
     uint8_t *const C = reinterpret_cast<uint8_t *>(cnt_lds + 17 * lane);
     uint64_t *ev = evs + (size_t)blockIdx.x * DEVCAP * 3 * DW + lane;         // [event][field][lane]
-    const uint64_t nchunk = (total + DCHUNK - 1) / DCHUNK;
+    const uint64_t nchunk = (total - begin + DCHUNK - 1) / DCHUNK;   // chunks of [begin, total)
     auto word = [&](uint64_t w) -> uint64_t { return w < nwords ? F[w] : 0ull; };
     auto aword = [&](uint64_t w) -> uint64_t { return AMB && w < nwords ? AF[w] : 0ull; };
     // wave-uniform chunk rounds (the whole wave meets in phase B); a lane past
@@ -135,7 +136,7 @@ __global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t total, 
     for (uint64_t chb = (uint64_t)blockIdx.x * DW; chb < nchunk; chb += (uint64_t)gridDim.x * DW) {
         const uint64_t ch = chb + (uint64_t)lane;
         const bool have = ch < nchunk;
-        const uint64_t c0 = have ? ch * DCHUNK : total, c1 = have ? min(c0 + DCHUNK, total) : total;
+        const uint64_t c0 = have ? begin + ch * DCHUNK : total, c1 = have ? min(c0 + DCHUNK, total) : total;
         const uint64_t lim = have ? min(c1 + (uint64_t)W, total) : total;   // the scan's reach
         // ---------------- B: the events, in order per lane (state kept across runs of B) ----------------
         uint64_t set = 0, prs = ~0ull;   // slots holding a perfect interval; their run's start
@@ -459,12 +460,14 @@ __global__ void dust_linker_kernel(const TxInfo *__restrict__ tx, uint32_t n_tx,
     }
 }
 
-void launch_dust(bool amb, uint64_t total, const uint64_t *F, const uint64_t *AF, const uint64_t *txstart,
+// the masks of the transcripts in [begin, total) (begin: a multiple of DCHUNK
+// where a transcript starts; the packed arrays are read from position 0)
+void launch_dust(bool amb, uint64_t begin, uint64_t total, const uint64_t *F, const uint64_t *AF, const uint64_t *txstart,
                  const TxInfo *tx, uint32_t n_tx, int level, int window, int linker, uint32_t *scratch,
                  uint64_t *events, uint32_t scratch_blocks, int max_waves, uint64_t *mask, hipStream_t st)
 {
-    if (total == 0) return;
-    const uint64_t nchunk = (total + DCHUNK - 1) / DCHUNK;
+    if (total <= begin) return;
+    const uint64_t nchunk = (total - begin + DCHUNK - 1) / DCHUNK;
     // every block resident at once (the chunks then split evenly: a second
     // round of blocks would double the kernel's time for a few waves)
     int dev = 0, ncu = 0, per_cu = 0;
@@ -478,11 +481,11 @@ void launch_dust(bool amb, uint64_t total, const uint64_t *F, const uint64_t *AF
     const uint64_t g = std::min<uint64_t>(std::min<uint64_t>((nchunk + DW - 1) / DW, scratch_blocks), resident);
     const uint64_t nwords = (total + 31) / 32 + 2;   // readable packed words (the arrays carry padding)
     if (amb)
-        hipLaunchKernelGGL(dust_kernel<true>, dim3((unsigned)g), dim3(DW), 0, st, total, nwords, F, AF, txstart, level,
+        hipLaunchKernelGGL(dust_kernel<true>, dim3((unsigned)g), dim3(DW), 0, st, begin, total, nwords, F, AF, txstart, level,
                            window, events, scratch, mask);
     else
-        hipLaunchKernelGGL(dust_kernel<false>, dim3((unsigned)g), dim3(DW), 0, st, total, nwords, F, AF, txstart,
-                           level, window, events, scratch, mask);
+        hipLaunchKernelGGL(dust_kernel<false>, dim3((unsigned)g), dim3(DW), 0, st, begin, total, nwords, F, AF,
+                           txstart, level, window, events, scratch, mask);
     if (linker > 1 && n_tx)
         hipLaunchKernelGGL(dust_linker_kernel, dim3((n_tx + 255) / 256 < 65536 ? (n_tx + 255) / 256 : 65536), dim3(256),
                            0, st, tx, n_tx, linker, mask);

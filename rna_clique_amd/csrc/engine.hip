@@ -55,7 +55,7 @@ void launch_near_fill(bool, const TxInfo *, uint32_t, const uint8_t *, const uin
 void launch_seed(bool, const Db &, const Index &, const SeedParams &, hipStream_t);
 void launch_seed_big(bool, const Db &, const Index &, const SeedParams &, uint32_t, hipStream_t);
 void launch_rs_range(const uint32_t *, uint32_t, uint32_t, uint32_t, uint32_t *, hipStream_t);
-void launch_dust(bool, uint64_t, const uint64_t *, const uint64_t *, const uint64_t *, const TxInfo *, uint32_t, int,
+void launch_dust(bool, uint64_t, uint64_t, const uint64_t *, const uint64_t *, const uint64_t *, const TxInfo *, uint32_t, int,
                  int, int, uint32_t *, uint64_t *, uint32_t, int, uint64_t *, hipStream_t);
 uint32_t dust_scratch_words(uint32_t);
 uint64_t dust_event_words(uint32_t);
@@ -322,7 +322,8 @@ struct rc_engine {
     uint32_t tile_ntx = 0;              // the tile's transcripts (DUST, near-mask index)
     uint32_t tile_nitx = 0;             // ... of its subject samples (the 16-mer index)
     bool tile_share = false;            // the search mode the loaded tile's index list was built for
-    uint32_t tile_a_ntx = 0;            // split tiles: transcripts of the a part (the first ones)
+    uint32_t tile_a_ntx = 0;
+    uint64_t tile_a_end = 0;            // split tiles: end of the a part (its padding runs to bstart)            // split tiles: transcripts of the a part (the first ones)
     // the b chunk (split tiles) whose index and DUST masks the device holds
     // from this run's previous tile (-1: none)
     int idx_bchunk = -1;
@@ -994,6 +995,13 @@ static int load_tile(rc_engine *e, int ti)
         if (e->samples[s].resident && e->samples[s].nbases && !in[s]) direct = false;
     const uint64_t total = pos;
     if (total >= (1ull << 32)) return fail(RC_E_LIMIT, "a tile of more than 2^32 bases");
+    // a split tile's a part ends here (DUST skips the padding up to T.bstart)
+    e->tile_a_end = total;
+    if (T.bchunk >= 0) {
+        e->tile_a_end = 0;
+        for (int s = 0; s <= amax_s; s++)
+            if (in[s]) e->tile_a_end = e->tile_pos[s] + align_up(e->samples[s].nbases);
+    }
     // sample ranges, monotone over all N + 1 (a sample outside the tile is empty)
     std::vector<uint64_t> spos(N + 1);
     {
@@ -1530,7 +1538,7 @@ static int align_tile(rc_engine *e, int ti)
     const rc_engine::Tile &TT = e->tiles[ti];
     const bool reuse = TT.bchunk >= 0 && TT.bchunk == e->idx_bchunk && TT.bstart == e->idx_bstart &&
                        e->d_dmask.cap >= (total >> 6) + 4;
-    const uint64_t dtot = reuse ? TT.bstart : total;   // DUST's range: the a part only when reusing
+    const uint64_t dtot = reuse ? TT.bstart : total;   // masks cleared: the a part only when reusing
     if (dust) {
         const size_t mw = (total >> 6) + 4;
         CHK(e->d_dmask.ensure(mw));
@@ -1551,11 +1559,20 @@ static int align_tile(rc_engine *e, int ti)
         HIPCHK(hipEventRecord(e->evd[2], e->st));
         HIPCHK(hipStreamWaitEvent(e->st2, e->evd[2], 0));
         HIPCHK(hipEventRecord(e->evd[0], e->st2));
-        launch_dust(e->has_amb, dtot, e->d_F.p + FRONT_PAD, e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr,
-                    e->d_txstart.p + 1, e->d_tile_tx.p, reuse ? e->tile_a_ntx : e->tile_ntx, e->o.dust_level,
-                    e->o.dust_window,
-                    e->o.dust_linker, e->d_dust_scratch.p, e->d_dust_events.p, dblocks, dwaves, e->d_dmask.p + 1,
-                    e->st2);
+        // the transcripts' ranges only: a split tile's a part, then (unless
+        // its masks are kept) the b part -- not the padding between them
+        auto dust_range = [&](uint64_t b, uint64_t t, uint32_t tx0, uint32_t ntx) {
+            launch_dust(e->has_amb, b, t, e->d_F.p + FRONT_PAD, e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr,
+                        e->d_txstart.p + 1, e->d_tile_tx.p + tx0, ntx, e->o.dust_level, e->o.dust_window,
+                        e->o.dust_linker, e->d_dust_scratch.p, e->d_dust_events.p, dblocks, dwaves,
+                        e->d_dmask.p + 1, e->st2);
+        };
+        if (TT.bchunk >= 0) {
+            dust_range(0, e->tile_a_end, 0, e->tile_a_ntx);
+            if (!reuse) dust_range(TT.bstart, total, e->tile_a_ntx, e->tile_ntx - e->tile_a_ntx);
+        } else {
+            dust_range(0, total, 0, e->tile_ntx);
+        }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e->evd[1], e->st2));
         return RC_OK;

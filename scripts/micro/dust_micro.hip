@@ -5,7 +5,7 @@
 #include <cstdlib>
 #include <vector>
 namespace rcg {
-void launch_dust(bool, uint64_t, const uint64_t *, const uint64_t *, const uint64_t *, const TxInfo *, uint32_t, int,
+void launch_dust(bool, uint64_t, uint64_t, const uint64_t *, const uint64_t *, const uint64_t *, const TxInfo *, uint32_t, int,
                  int, int, uint32_t *, uint64_t *, uint32_t, int, uint64_t *, hipStream_t);
 uint32_t dust_scratch_words(uint32_t);
 uint64_t dust_event_words(uint32_t);
@@ -39,7 +39,7 @@ int main(int argc, char **argv)
     for (int it = 0; it < 3; it++) {
         hipMemset(M, 0, tb.size() * 8);
         hipEventRecord(a, 0);
-        launch_dust(false, total, F, nullptr, TB + 1, nullptr, 0, 20, 64, 1, S, E, blocks, 0, M + 1, 0);
+        launch_dust(false, 0, total, F, nullptr, TB + 1, nullptr, 0, 20, 64, 1, S, E, blocks, 0, M + 1, 0);
         hipEventRecord(b, 0);
         hipEventSynchronize(b);
         float ms; hipEventElapsedTime(&ms, a, b);
