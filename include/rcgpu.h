@@ -262,6 +262,23 @@ int rc_timings(rc_engine *eng, rc_timing *t);
  * its concatenated transcripts (1 = masked query base, spec 1b of the oracle);
  * all zero when DUST is off. buf == NULL queries the size. */
 int rc_dust_mask(rc_engine *eng, int32_t s, uint8_t *buf, uint64_t cap, uint64_t *n);
+/* DUST masks shared across shards (each sample masked once, on one rank that
+ * holds it; the rest of the query-side DUST of TabularBlastnSearch's blastn
+ * -dust default, find_homologs.py:124, is then a copy). Layout: the listed
+ * samples in order, ceil(bases / 64) uint64 words each; bit b of word w =
+ * base 64 w + b of the sample's concatenated transcripts (1 = masked); bits
+ * past its last base 0.
+ * rc_dust_masks: the masks of resident samples, computed in a pass of their
+ * own (results of an earlier rc_align are dropped: call it before rc_align);
+ * out == NULL queries n_words. `on_device`: out is a device pointer.
+ * rc_set_dust_masks: masks for these samples (replacing any given before;
+ * n = 0 clears them): rc_align copies them into its tiles instead of running
+ * DUST on those samples. They must come from engines with the same DUST
+ * options. */
+int rc_dust_masks(rc_engine *eng, const int32_t *samples, int32_t n, uint64_t *out, uint64_t cap_words,
+                  uint64_t *n_words, int on_device);
+int rc_set_dust_masks(rc_engine *eng, const int32_t *samples, int32_t n, const uint64_t *bits, uint64_t n_words,
+                      int on_device);
 
 /* ---- outputs next to matrix.h5 (od2 tables, graph.pkl) -------------------
  * rc_write_outputs: the gene matches table files of pairs (s1[i], s2[i]) at

@@ -131,6 +131,8 @@ SIGNATURES = {
     "rc_distance_subset": (ctypes.c_int, [VP, VP, ctypes.c_int32, VP]),
     "rc_timings": (ctypes.c_int, [VP, P(RcTiming)]),
     "rc_dust_mask": (ctypes.c_int, [VP, ctypes.c_int32, VP, ctypes.c_uint64, P(ctypes.c_uint64)]),
+    "rc_dust_masks": (ctypes.c_int, [VP, VP, ctypes.c_int32, VP, ctypes.c_uint64, P(ctypes.c_uint64), ctypes.c_int]),
+    "rc_set_dust_masks": (ctypes.c_int, [VP, VP, ctypes.c_int32, VP, ctypes.c_uint64, ctypes.c_int]),
     "rc_fasta_open": (ctypes.c_int, [ctypes.c_char_p, P(VP)]),
     "rc_fasta_close": (ctypes.c_int, [VP]),
     "rc_fasta_info": (ctypes.c_int, [VP, P(ctypes.c_uint64), P(ctypes.c_uint64), P(ctypes.c_uint64)]),

@@ -322,8 +322,10 @@ struct rc_engine {
     uint32_t tile_ntx = 0;              // the tile's transcripts (DUST, near-mask index)
     uint32_t tile_nitx = 0;             // ... of its subject samples (the 16-mer index)
     bool tile_share = false;            // the search mode the loaded tile's index list was built for
-    uint32_t tile_a_ntx = 0;
-    uint64_t tile_a_end = 0;            // split tiles: end of the a part (its padding runs to bstart)            // split tiles: transcripts of the a part (the first ones)
+    std::vector<uint32_t> tile_tx_first;   // first transcript (in d_tile_tx) of each sample of the tile
+    // DUST masks given by rc_set_dust_masks (computed once per sample across
+    // shards): word offset of each sample's mask in d_dust_imp, ~0 = not given
+    std::vector<uint64_t> dust_imp_off;
     // the b chunk (split tiles) whose index and DUST masks the device holds
     // from this run's previous tile (-1: none)
     int idx_bchunk = -1;
@@ -376,7 +378,7 @@ struct rc_engine {
     DBuf<uint64_t> d_sort_status;
     uint32_t sort_epoch = 0;
     DBuf<uint32_t> d_bucket, d_pos_tx;
-    DBuf<uint64_t> d_sample_pos, d_txstart, d_kpos_rel, d_dmask;
+    DBuf<uint64_t> d_sample_pos, d_txstart, d_kpos_rel, d_dmask, d_dust_imp;
     DBuf<uint32_t> d_dust_scratch;
     DBuf<uint64_t> d_dust_events;
     DBuf<unsigned long long> d_prof;
@@ -995,13 +997,6 @@ static int load_tile(rc_engine *e, int ti)
         if (e->samples[s].resident && e->samples[s].nbases && !in[s]) direct = false;
     const uint64_t total = pos;
     if (total >= (1ull << 32)) return fail(RC_E_LIMIT, "a tile of more than 2^32 bases");
-    // a split tile's a part ends here (DUST skips the padding up to T.bstart)
-    e->tile_a_end = total;
-    if (T.bchunk >= 0) {
-        e->tile_a_end = 0;
-        for (int s = 0; s <= amax_s; s++)
-            if (in[s]) e->tile_a_end = e->tile_pos[s] + align_up(e->samples[s].nbases);
-    }
     // sample ranges, monotone over all N + 1 (a sample outside the tile is empty)
     std::vector<uint64_t> spos(N + 1);
     {
@@ -1040,7 +1035,9 @@ static int load_tile(rc_engine *e, int ti)
         const uint64_t q = p + 64;
         txb[q >> 6] |= 1ull << (q & 63);
     };
+    e->tile_tx_first.assign(N + 1, 0);
     for (int s = 0; s < N; s++) {
+        e->tile_tx_first[s] = (uint32_t)ttx.size();
         if (!in[s]) continue;
         const SampleRec &S = e->samples[s];
         const uint64_t p0 = e->tile_pos[s];
@@ -1066,6 +1063,7 @@ static int load_tile(rc_engine *e, int ti)
             pos_tx[b] = t;
         }
     }
+    e->tile_tx_first[N] = (uint32_t)ttx.size();
     if (koff.back() > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "more than 2^32 seed positions in a tile");
     CHK(up(e->d_tx, e->h_tx));
     CHK(up(e->d_tile_tx, ttx));
@@ -1078,9 +1076,6 @@ static int load_tile(rc_engine *e, int ti)
     e->tile_gid = gid;
     e->tile_ntx = (uint32_t)ttx.size();
     e->tile_nitx = (uint32_t)itx.size();
-    e->tile_a_ntx = 0;
-    if (T.bchunk >= 0)
-        for (const TxInfo &x : ttx) e->tile_a_ntx += x.start < T.bstart ? 1u : 0u;
     e->tile_share = share;
     // the packed working copy's source: d_ascii itself or a gathered copy
     if (!direct) {
@@ -1506,15 +1501,12 @@ static int grow_hsp(rc_engine *e, uint64_t n)
 // One alignment pass over tile ti: pack, DUST, index, seeds (one launch per
 // run of query samples), extension, and the (query gene, subject sample) HSP
 // groups appended to the shard's store.
-static int align_tile(rc_engine *e, int ti)
+// The loaded tile's packed working copy (FRONT_PAD zero words in front, zero
+// words behind); ev[0] marks the start of the packing.
+static int pack_tile(rc_engine *e)
 {
-    CHK(load_tile(e, ti));
-    const int N = (int)e->samples.size();
     const uint64_t total = e->tile_total;
     const uint64_t nwords = (total + 31) / 32 + 2;
-    const uint32_t n_genes = (uint32_t)e->gene_sample.size();
-    const size_t ngrp = (size_t)n_genes * N;
-    // packed working copy (FRONT_PAD zero words in front, zero words behind)
     CHK(e->d_F.ensure(nwords + 4 + FRONT_PAD));
     CHK(e->d_RC.ensure(nwords + 4 + FRONT_PAD));
     HIPCHK(hipMemsetAsync(e->d_F.p, 0, FRONT_PAD * 8, e->st));
@@ -1532,6 +1524,49 @@ static int align_tile(rc_engine *e, int ti)
                 e->d_RC.p + FRONT_PAD, e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr,
                 e->has_amb ? e->d_ARC.p + FRONT_PAD : nullptr, e->st);
     HIPCHK(hipGetLastError());
+    return RC_OK;
+}
+
+// DUST masks of the given tile samples (ascending) into d_dmask, on stream st:
+// one launch per run of consecutive samples (the transcripts' ranges only,
+// not the padding between a split tile's parts)
+static int dust_samples(rc_engine *e, const std::vector<int> &ss, hipStream_t st)
+{
+    const uint32_t dblocks = 256 * 28;   // at least the resident waves of the chunk kernel (<= 7 per SIMD): their scratch
+    CHK(e->d_dust_scratch.ensure(dust_scratch_words(dblocks)));
+    CHK(e->d_dust_events.ensure(dust_event_words(dblocks)));
+    const char *dwv = getenv("RC_DUST_WAVES");
+    const int dwaves = dwv ? atoi(dwv) : 0;   // 0: every resident wave (measured best; 1-3 starve DUST)
+    int f = -1, l = -1;
+    auto flush = [&]() {
+        if (f >= 0) {
+            const uint32_t tx0 = e->tile_tx_first[f];
+            launch_dust(e->has_amb, e->tile_pos[f], e->tile_pos[l] + align_up(e->samples[l].nbases),
+                        e->d_F.p + FRONT_PAD, e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr, e->d_txstart.p + 1,
+                        e->d_tile_tx.p + tx0, e->tile_tx_first[l + 1] - tx0, e->o.dust_level, e->o.dust_window,
+                        e->o.dust_linker, e->d_dust_scratch.p, e->d_dust_events.p, dblocks, dwaves,
+                        e->d_dmask.p + 1, st);
+        }
+        f = l = -1;
+    };
+    for (int s : ss) {
+        if (f >= 0 && e->tile_pos[s] != e->tile_pos[l] + align_up(e->samples[l].nbases)) flush();
+        if (f < 0) f = s;
+        l = s;
+    }
+    flush();
+    HIPCHK(hipGetLastError());
+    return RC_OK;
+}
+
+static int align_tile(rc_engine *e, int ti)
+{
+    CHK(load_tile(e, ti));
+    const int N = (int)e->samples.size();
+    const uint64_t total = e->tile_total;
+    const uint32_t n_genes = (uint32_t)e->gene_sample.size();
+    const size_t ngrp = (size_t)n_genes * N;
+    CHK(pack_tile(e));
     const bool dust = e->o.dust_level > 0;
     // a split tile of the b chunk the previous tile had: its 16-mer index
     // (the b part's) and the b part's DUST masks are on the device already
@@ -1539,10 +1574,25 @@ static int align_tile(rc_engine *e, int ti)
     const bool reuse = TT.bchunk >= 0 && TT.bchunk == e->idx_bchunk && TT.bstart == e->idx_bstart &&
                        e->d_dmask.cap >= (total >> 6) + 4;
     const uint64_t dtot = reuse ? TT.bstart : total;   // masks cleared: the a part only when reusing
+    // the samples whose masks DUST computes here, in tile order: a split
+    // tile's a part and (unless its masks are kept) its b part, all samples
+    // of any other tile -- except those given by rc_set_dust_masks, whose
+    // masks are copied in (samples start at 256-base boundaries: whole words)
+    std::vector<int> dust_here;
     if (dust) {
         const size_t mw = (total >> 6) + 4;
         CHK(e->d_dmask.ensure(mw));
         HIPCHK(hipMemsetAsync(e->d_dmask.p, 0, (reuse ? 1 + (dtot >> 6) : mw) * 8, e->st));
+        for (int s : TT.samples) {
+            if (reuse && e->tile_pos[s] >= TT.bstart) continue;
+            const uint64_t io = s < (int)e->dust_imp_off.size() ? e->dust_imp_off[s] : ~0ull;
+            if (io == ~0ull) {
+                dust_here.push_back(s);
+            } else if (e->samples[s].nbases) {
+                HIPCHK(hipMemcpyAsync(e->d_dmask.p + 1 + (e->tile_pos[s] >> 6), e->d_dust_imp.p + io,
+                                      ((e->samples[s].nbases + 63) >> 6) * 8, hipMemcpyDeviceToDevice, e->st));
+            }
+        }
     }
     HIPCHK(hipEventRecord(e->ev[1], e->st));
     // DUST masks of the tile's transcripts (the query side), bit per base, on
@@ -1551,29 +1601,10 @@ static int align_tile(rc_engine *e, int ti)
     // phase 55.7 vs 58.1 ms at C3 when started after the sort's table kernels;
     // RC_DUST_EARLY=0 starts it there).
     auto start_dust = [&]() -> int {
-        const uint32_t dblocks = 256 * 28;   // at least the resident waves of the chunk kernel (<= 7 per SIMD): their scratch
-        CHK(e->d_dust_scratch.ensure(dust_scratch_words(dblocks)));
-        CHK(e->d_dust_events.ensure(dust_event_words(dblocks)));
-        const char *dwv = getenv("RC_DUST_WAVES");
-        const int dwaves = dwv ? atoi(dwv) : 0;   // 0: every resident wave (measured best; 1-3 starve DUST)
         HIPCHK(hipEventRecord(e->evd[2], e->st));
         HIPCHK(hipStreamWaitEvent(e->st2, e->evd[2], 0));
         HIPCHK(hipEventRecord(e->evd[0], e->st2));
-        // the transcripts' ranges only: a split tile's a part, then (unless
-        // its masks are kept) the b part -- not the padding between them
-        auto dust_range = [&](uint64_t b, uint64_t t, uint32_t tx0, uint32_t ntx) {
-            launch_dust(e->has_amb, b, t, e->d_F.p + FRONT_PAD, e->has_amb ? e->d_AF.p + FRONT_PAD : nullptr,
-                        e->d_txstart.p + 1, e->d_tile_tx.p + tx0, ntx, e->o.dust_level, e->o.dust_window,
-                        e->o.dust_linker, e->d_dust_scratch.p, e->d_dust_events.p, dblocks, dwaves,
-                        e->d_dmask.p + 1, e->st2);
-        };
-        if (TT.bchunk >= 0) {
-            dust_range(0, e->tile_a_end, 0, e->tile_a_ntx);
-            if (!reuse) dust_range(TT.bstart, total, e->tile_a_ntx, e->tile_ntx - e->tile_a_ntx);
-        } else {
-            dust_range(0, total, 0, e->tile_ntx);
-        }
-        HIPCHK(hipGetLastError());
+        CHK(dust_samples(e, dust_here, e->st2));
         HIPCHK(hipEventRecord(e->evd[1], e->st2));
         return RC_OK;
     };
@@ -2602,6 +2633,121 @@ int rc_dust_mask(rc_engine *e, int32_t s, uint8_t *buf, uint64_t cap, uint64_t *
     for (uint64_t i = 0; i < S.nbases; i++) {
         const uint64_t p = b0 + i;
         buf[i] = (uint8_t)((words[(p >> 6) - w0] >> (p & 63)) & 1);
+    }
+    return RC_OK;
+}
+
+// DUST masks computed once per sample across shards: each
+// sample's mask is made on one rank that holds it (rc_dust_masks), the masks
+// are exchanged, and every rank hands them to its engine (rc_set_dust_masks),
+// whose alignment then copies them into its tiles instead of running DUST.
+// Layout: the listed samples in order, ceil(bases / 64) words each, bit b of
+// word w = base 64 w + b of the sample (1: masked); bits past the last base 0.
+static uint64_t mask_words(const rc_engine *e, const int32_t *samples, int32_t n)
+{
+    uint64_t w = 0;
+    for (int32_t i = 0; i < n; i++) w += (e->samples[samples[i]].nbases + 63) >> 6;
+    return w;
+}
+
+int rc_dust_masks(rc_engine *e, const int32_t *samples, int32_t n, uint64_t *out, uint64_t cap_words,
+                  uint64_t *n_words, int on_device)
+{
+    if (!e || !n_words || n < 0 || (n && !samples)) return fail(RC_E_ARG, "null argument");
+    CHK(upload(e));
+    const int N = (int)e->samples.size();
+    for (int32_t i = 0; i < n; i++) {
+        if (samples[i] < 0 || samples[i] >= N) return fail(RC_E_ARG, "bad sample");
+        if (!e->samples[samples[i]].resident)
+            return fail(RC_E_STATE, "sample " + e->samples[samples[i]].label + " was added without its sequence");
+    }
+    const uint64_t words = mask_words(e, samples, n);
+    *n_words = words;
+    if (!out) return RC_OK;
+    if (cap_words < words) return fail(RC_E_CAPACITY, "buffer too small");
+    CHK(set_device(e));
+    // a pass of its own: the tile tables of a previous run are replaced, so
+    // its results are dropped (as by a new rc_align)
+    e->aligned = e->finished = e->rbh_done = false;
+    std::vector<int> ss(samples, samples + n);
+    std::sort(ss.begin(), ss.end());
+    ss.erase(std::unique(ss.begin(), ss.end()), ss.end());
+    // a tile of these samples alone: packed, their DUST masks, copied out
+    rc_engine::Tile T;
+    T.samples = ss;
+    e->tiles.push_back(T);
+    e->tile_loaded = -1;
+    const int ti = (int)e->tiles.size() - 1;
+    int rc = load_tile(e, ti);
+    if (rc == RC_OK) rc = pack_tile(e);
+    const bool dust = e->o.dust_level > 0 && !e->external;
+    if (rc == RC_OK && dust) {
+        const size_t mw = (e->tile_total >> 6) + 4;
+        rc = e->d_dmask.ensure(mw);
+        if (rc == RC_OK && hipMemsetAsync(e->d_dmask.p, 0, mw * 8, e->st) != hipSuccess)
+            rc = fail(RC_E_HIP, "hipMemsetAsync");
+        if (rc == RC_OK) rc = dust_samples(e, ss, e->st);
+    }
+    std::vector<uint64_t> tail;   // last word of each listed sample, bits past its end cleared
+    uint64_t o = 0;
+    for (int32_t i = 0; rc == RC_OK && i < n; i++) {
+        const int s = samples[i];
+        const uint64_t nb = e->samples[s].nbases, nw = (nb + 63) >> 6;
+        if (!nw) continue;
+        hipError_t h = hipSuccess;
+        if (dust) {
+            h = hipMemcpyAsync(out + o, e->d_dmask.p + 1 + (e->tile_pos[s] >> 6), nw * 8,
+                               on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, e->st);
+        } else if (on_device) {
+            h = hipMemsetAsync(out + o, 0, nw * 8, e->st);
+        } else {
+            std::memset(out + o, 0, nw * 8);
+        }
+        if (h != hipSuccess) rc = fail(RC_E_HIP, "mask copy");
+        o += nw;
+    }
+    if (rc == RC_OK && hipStreamSynchronize(e->st) != hipSuccess) rc = fail(RC_E_HIP, "hipStreamSynchronize");
+    o = 0;
+    for (int32_t i = 0; rc == RC_OK && dust && i < n; i++) {
+        const uint64_t nb = e->samples[samples[i]].nbases, nw = (nb + 63) >> 6;
+        o += nw;
+        if (!nw || !(nb & 63)) continue;
+        const uint64_t keep = (1ull << (nb & 63)) - 1ull;
+        if (on_device) {
+            uint64_t w = 0;
+            if (hipMemcpy(&w, out + o - 1, 8, hipMemcpyDeviceToHost) != hipSuccess ||
+                (w &= keep, hipMemcpy(out + o - 1, &w, 8, hipMemcpyHostToDevice)) != hipSuccess)
+                rc = fail(RC_E_HIP, "mask tail");
+        } else {
+            out[o - 1] &= keep;
+        }
+    }
+    e->tiles.pop_back();
+    e->tile_loaded = -1;
+    e->idx_bchunk = -1;
+    return rc;
+}
+
+int rc_set_dust_masks(rc_engine *e, const int32_t *samples, int32_t n, const uint64_t *bits, uint64_t n_words,
+                      int on_device)
+{
+    if (!e || n < 0 || (n && !samples)) return fail(RC_E_ARG, "null argument");
+    CHK(upload(e));
+    const int N = (int)e->samples.size();
+    for (int32_t i = 0; i < n; i++)
+        if (samples[i] < 0 || samples[i] >= N) return fail(RC_E_ARG, "bad sample");
+    const uint64_t words = mask_words(e, samples, n);
+    if (n_words != words) return fail(RC_E_ARG, "mask words do not match the samples' lengths");
+    if (words && !bits) return fail(RC_E_ARG, "null argument");
+    CHK(set_device(e));
+    e->dust_imp_off.assign(N, ~0ull);
+    CHK(e->d_dust_imp.ensure(std::max<uint64_t>(words, 1)));
+    if (words)
+        HIPCHK(hipMemcpy(e->d_dust_imp.p, bits, words * 8, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+    uint64_t o = 0;
+    for (int32_t i = 0; i < n; i++) {
+        e->dust_imp_off[samples[i]] = o;
+        o += (e->samples[samples[i]].nbases + 63) >> 6;
     }
     return RC_OK;
 }

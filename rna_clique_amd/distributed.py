@@ -12,8 +12,11 @@ of the gene matches tables and graph edges. The ideal-clique filter needs the
 whole graph, so the edge records (20 B each: two node ids, the pair, and the
 edge's nident and length - gaps sums) are all-gathered once -- over RCCL on
 GPUs, gloo on CPU -- and every rank runs connected components, the ideal
-filter and the pair sums over all of them. That is the only collective on the
-data path.
+filter and the pair sums over all of them. Before the alignment the ranks
+exchange DUST masks (each sample masked once, by one rank that holds it:
+dust_owners / exchange_dust), so the query-side masking does not repeat on
+every rank that holds a sample. These two all-gathers are the only
+collectives on the data path.
 """
 from __future__ import annotations
 
@@ -157,8 +160,59 @@ def exchange_edges(eng, process_group=None):
         eng.import_edges(allt.numpy())
 
 
+def dust_owners(sample_bases, shard_count):
+    """The rank that makes each sample's DUST mask (-1: no rank holds it):
+    one of the ranks holding the sample, the one with the fewest bases
+    assigned so far, largest samples first -- so every mask is computed once
+    and the work is spread over the ranks."""
+    order, first = plan_pairs(sample_bases, shard_count)
+    n = len(sample_bases)
+    holders = [set() for _ in range(n)]
+    for r in range(shard_count):
+        for a, b in order[int(first[r]):int(first[r + 1])]:
+            holders[a].add(r)
+            holders[b].add(r)
+    load = [0] * shard_count
+    owner = [-1] * n
+    for s in sorted(range(n), key=lambda s: (-int(sample_bases[s]), s)):
+        if holders[s]:
+            r = min(holders[s], key=lambda r: (load[r], r))
+            owner[s] = r
+            load[r] += int(sample_bases[s])
+    return owner
+
+
+def exchange_dust(eng, process_group=None):
+    """Every sample's DUST mask made once: this rank masks the samples
+    dust_owners gives it, the masks are all-gathered (1 bit per base; 200 MB
+    at C3) and each engine takes them (rc_set_dust_masks) instead of masking
+    its resident samples itself. A no-op without DUST or with one rank."""
+    import torch
+    import torch.distributed as dist
+    W, R = world(process_group)
+    if W == 1 or getattr(eng, "dust", None) is None:
+        return
+    owner = dust_owners(eng.bases, W)
+    mine = [s for s in range(len(owner)) if owner[s] == R]
+    everyone = [s for r in range(W) for s in range(len(owner)) if owner[s] == r]
+    on_gpu = dist.get_backend(process_group) != "gloo" and torch.cuda.is_available()
+    if on_gpu:
+        nw = sum((eng.bases[s] + 63) // 64 for s in mine)
+        local = torch.empty(max(nw, 1), dtype=torch.int64, device="cuda")[:nw]
+        eng.dust_masks(mine, local)
+        allt, total = all_gather_records(local.view(torch.uint8), 8, process_group)
+        torch.cuda.current_stream().synchronize()
+        eng.set_dust_masks(everyone, allt.contiguous().view(torch.int64)[:total])
+    else:
+        local = torch.from_numpy(eng.dust_masks(mine).view(np.uint8))
+        allt, total = all_gather_records(local, 8, process_group)
+        eng.set_dust_masks(everyone, allt.numpy().view(np.uint64))
+
+
 def sharded_run(eng, process_group=None):
-    """rc_run for a sharded engine: align + RBH locally, exchange, graph."""
+    """rc_run for a sharded engine: DUST masks made once across the ranks,
+    align + RBH locally, exchange, graph."""
+    exchange_dust(eng, process_group)
     eng.align()
     eng.finish()
     exchange_edges(eng, process_group)

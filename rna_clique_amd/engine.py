@@ -44,6 +44,8 @@ class Engine:
         self._h = h
         self.labels = []
         self.n_tx = []
+        self.bases = []      # each sample's sequence length (resident or not)
+        self.resident = []
         self.shard_count = int(shard_count)
 
     def close(self):
@@ -83,6 +85,8 @@ class Engine:
             iso.ctypes.data_as(P(ctypes.c_int32)), n_tx, ctypes.byref(sid)))
         self.labels.append(str(label))
         self.n_tx.append(n_tx)
+        self.bases.append(int(offs[-1]) if n_tx else 0)
+        self.resident.append(seq is not None)
         return sid.value
 
     def add_hsps(self, q, s, hsps):
@@ -235,6 +239,39 @@ class Engine:
     def dust_mask(self, s):
         """DUST mask of sample s (uint8 per base, 1 = masked query base)."""
         return self._sized(nat.lib().rc_dust_mask, np.uint8, int(s))
+
+    def dust_masks(self, samples, out=None):
+        """The DUST masks of resident samples, computed in a pass of their own
+        (before align): uint64 words, ceil(bases / 64) per sample in the given
+        order (rc_dust_masks). Into `out` (a CUDA uint64/int64 tensor, device
+        to device) or a new host array."""
+        L = nat.lib()
+        ss = np.ascontiguousarray(list(samples), dtype=np.int32)
+        sp = ss.ctypes.data_as(ctypes.c_void_p)
+        n = ctypes.c_uint64()
+        nat.check(L.rc_dust_masks(self._h, sp, len(ss), None, 0, ctypes.byref(n), 0))
+        if out is not None:
+            if out.numel() < n.value:
+                raise ValueError("mask buffer too small")
+            nat.check(L.rc_dust_masks(self._h, sp, len(ss), ctypes.c_void_p(out.data_ptr()), n.value,
+                                      ctypes.byref(n), 1))
+            return n.value
+        buf = np.zeros(n.value, dtype=np.uint64)
+        nat.check(L.rc_dust_masks(self._h, sp, len(ss), buf.ctypes.data_as(ctypes.c_void_p), n.value,
+                                  ctypes.byref(n), 0))
+        return buf
+
+    def set_dust_masks(self, samples, bits):
+        """Masks for these samples (layout of dust_masks; a host uint64 array
+        or a CUDA tensor): align copies them instead of running DUST on them."""
+        L = nat.lib()
+        ss = np.ascontiguousarray(list(samples), dtype=np.int32)
+        sp = ss.ctypes.data_as(ctypes.c_void_p)
+        if isinstance(bits, np.ndarray):
+            b = np.ascontiguousarray(bits, dtype=np.uint64)
+            nat.check(L.rc_set_dust_masks(self._h, sp, len(ss), b.ctypes.data_as(ctypes.c_void_p), len(b), 0))
+        else:
+            nat.check(L.rc_set_dust_masks(self._h, sp, len(ss), ctypes.c_void_p(bits.data_ptr()), bits.numel(), 1))
 
     def timings(self):
         t = nat.RcTiming()

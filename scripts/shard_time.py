@@ -3,7 +3,13 @@ index, seed, extension, groups, RBH) on one GPU, shard by shard -- the
 strong-scaling projection of bench.py --gpus K without the edge exchange and
 the (replicated) graph phase.
 
-    python scripts/shard_time.py --config C3 --shards 8
+    python scripts/shard_time.py --config C3 --shards 8 [--share-dust]
+
+--share-dust: the DUST masks are made once per sample across the ranks
+(distributed.exchange_dust): a rank's timed work is its own samples' masks
+(rc_dust_masks) plus its alignment with every mask given (rc_set_dust_masks);
+the other ranks' masks are made untimed beforehand, and the all-gather is
+modelled (`exchange_model_ms`: the gathered bytes at 100 GB/s).
 """
 import argparse
 import json
@@ -20,21 +26,38 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--shards", type=int, default=8)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--share-dust", action="store_true")
     args = ap.parse_args()
+    import numpy as np
     import torch
+    from rna_clique_amd import distributed
     from rna_clique_amd.engine import Engine
     from rna_clique_amd.simulate import simulate, CONFIGS
     samples, _ = simulate(**CONFIGS[args.config])
-    out = {"config": args.config, "shards": args.shards, "ms": [], "phases": []}
+    out = {"config": args.config, "shards": args.shards, "share_dust": args.share_dust, "ms": [], "phases": []}
+    bases = [len(s.seq) for s in samples]
+    owner = distributed.dust_owners(bases, args.shards)
+    if args.share_dust:
+        out["exchange_model_ms"] = round(sum(bases) / 8 / 100e9 * 1e3, 2)
+        out["dust_owned_gbp"] = [round(sum(b for b, o in zip(bases, owner) if o == r) / 1e9, 3)
+                                 for r in range(args.shards)]
     for r in range(args.shards):
         eng = Engine(device=0, shard_rank=r, shard_count=args.shards)
         for s in samples:
             eng.add_sample(s.name, s.seq, s.tx_offsets, s.gene, s.iso)
         eng.upload()
+        if args.share_dust:
+            need = sorted(distributed.needed_samples(bases, args.shards, r))
+            mine = [s for s in need if owner[s] == r]
+            others = [s for s in need if owner[s] != r]
+            other_w = eng.dust_masks(others)   # the other ranks' share (untimed)
         best = None
         for _ in range(args.reps):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
+            if args.share_dust:
+                own_w = eng.dust_masks(mine)
+                eng.set_dust_masks(mine + others, np.concatenate([own_w, other_w]))
             eng.align()
             eng.finish()
             torch.cuda.synchronize()

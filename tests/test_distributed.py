@@ -64,6 +64,76 @@ def _worker(rank, world, port, sizes, q):
         dist.destroy_process_group()
 
 
+class FakeDustEngine(FakeShardEngine):
+    """The part of Engine the DUST-mask exchange touches: a sample's mask is
+    ceil(bases / 64) words, word i of sample s = s << 32 | i."""
+
+    dust = (20, 64, 1)
+
+    def __init__(self, rank, bases):
+        super().__init__(rank, 1)
+        self.bases = list(bases)
+        self.made = None
+        self.given = None
+
+    def words(self, s):
+        n = (self.bases[s] + 63) // 64
+        return (np.uint64(s) << np.uint64(32)) | np.arange(n, dtype=np.uint64)
+
+    def dust_masks(self, samples, out=None):
+        assert out is None
+        self.made = list(samples)
+        return np.concatenate([self.words(s) for s in samples] + [np.zeros(0, np.uint64)])
+
+    def set_dust_masks(self, samples, bits):
+        self.given = (list(samples), np.asarray(bits).copy())
+
+
+def _dust_worker(rank, world, port, bases, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rna_clique_amd import distributed
+        eng = FakeDustEngine(rank, bases)
+        distributed.exchange_dust(eng)
+        q.put((rank, eng.made, eng.given[0], eng.given[1].tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bases", [(130, 64, 1, 0, 500, 7), (64, 64)])
+def test_gloo_dust_exchange_world2(bases):
+    """Every sample's DUST mask is made by exactly one rank that holds it, and
+    after the all-gather every rank holds every mask, bit for bit."""
+    from rna_clique_amd import distributed
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dust_worker, args=(r, 2, port, bases, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in procs:
+        r, made, samples, blob = q.get(timeout=120)
+        got[r] = (made, samples, blob)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    owner = distributed.dust_owners(list(bases), 2)
+    order, first = distributed.plan_pairs(list(bases), 2)
+    for r in range(2):
+        held = {s for p in order[int(first[r]):int(first[r + 1])] for s in p}
+        assert got[r][0] == [s for s in range(len(bases)) if owner[s] == r]
+        assert set(got[r][0]) <= held
+    made_all = got[0][0] + got[1][0]
+    assert sorted(made_all) == sorted(s for s in range(len(bases)) if owner[s] >= 0)
+    eng = FakeDustEngine(0, bases)
+    want = np.concatenate([eng.words(s) for s in made_all] + [np.zeros(0, np.uint64)]).tobytes()
+    for r in range(2):
+        assert got[r][1] == made_all and got[r][2] == want
+
+
 @pytest.mark.parametrize("sizes", [(3, 5), (0, 4), (0, 0)])
 def test_gloo_edge_exchange_world2(sizes):
     ctx = mp.get_context("spawn")

@@ -63,6 +63,52 @@ def test_sharded_engines_match_unsharded(native, shards):
         assert all(list(g.adj[n]) == list(g_ref.adj[n]) for n in g_ref.nodes)
 
 
+@pytest.mark.parametrize("shards", [3])
+def test_dust_masks_once_per_sample(native, shards):
+    """rc_dust_masks / rc_set_dust_masks: the masks a pass of their own makes
+    are the run's masks bit for bit (poly-A tails: DUST masks something), and
+    sharded engines that take each other's masks (every sample masked by one
+    shard, distributed.dust_owners) give the unsharded run's results."""
+    from rna_clique_amd import distributed
+    from rna_clique_amd.engine import Engine
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(5, 120, seed=9, p_iso2=0.2, polya=(0.5, 12, 40))
+    ref = _load(Engine(device=0), samples)
+    ref.run()
+    eng = _load(Engine(device=0), samples)
+    words = eng.dust_masks([4, 0, 2])
+    o = 0
+    for s in (4, 0, 2):
+        nb = len(samples[s].seq)
+        nw = (nb + 63) // 64
+        bits = np.unpackbits(words[o:o + nw].view(np.uint8), bitorder="little")
+        assert np.array_equal(bits[:nb], ref.dust_mask(s)), s
+        assert not bits[nb:].any()
+        o += nw
+    assert o == len(words) and ref.dust_mask(4).any()
+    # every sample masked once, by its owner shard; each shard takes them all
+    bases = [len(s.seq) for s in samples]
+    owner = distributed.dust_owners(bases, shards)
+    engines = [_load(Engine(device=0, shard_rank=r, shard_count=shards), samples) for r in range(shards)]
+    made = [e.dust_masks([s for s in range(len(samples)) if owner[s] == r]) for r, e in enumerate(engines)]
+    everyone = [s for r in range(shards) for s in range(len(samples)) if owner[s] == r]
+    allw = np.concatenate(made)
+    for e in engines:
+        e.set_dust_masks(everyone, allw)
+        e.align()
+        e.finish()
+    allb = np.concatenate([e.export_edges() for e in engines])
+    pairs = engines[0].pair_order()
+    for e in engines:
+        e.import_edges(allb)
+        assert np.array_equal(e.distance()[1], ref.distance()[1])
+        for p in range(*e.shard_pairs()):
+            a, b = pairs[p]
+            assert e.pair_rows(a, b).tobytes() == ref.pair_rows(a, b).tobytes()
+            assert e.hsps(a, b).tobytes() == ref.hsps(a, b).tobytes()
+            assert e.hsps(b, a).tobytes() == ref.hsps(b, a).tobytes()
+
+
 def _top_select(sample, top):
     """Top-gene rule restated: max coverage per gene, heapq.nlargest((cov, gene))."""
     best = defaultdict(float)
