@@ -183,46 +183,6 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
     // table and the host's word-item prefix); a block-uniform branch
     const bool isog = BIG ? niso > (uint32_t)ISO_LDS : ISOG;
     if (!BIG && !ISOG && niso > (uint32_t)ISO_LDS) return;   // the ISOG launch takes this gene
-    if (!isog) {
-        for (uint32_t i = tid; i < niso; i += SBLOCK) {
-            const uint32_t gtx = db.gene_tx[t0 + i];
-            const TxInfo ti = db.tx[gtx];
-            iso_gtx[i] = gtx;
-            iso_start[i] = ti.start;
-            iso_len[i] = ti.len;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t pre = 0;
-            for (uint32_t i = 0; i < niso; i++) {
-                iso_pre[i] = pre;
-                const int L = (int)iso_len[i];
-                pre += (L >= W16) ? 2u * (uint32_t)((L - W16) / stride + 1) : 0u;
-            }
-            iso_pre[niso] = pre;
-        }
-        __syncthreads();
-    }
-    const uint32_t *const gpre = P.iso_pre_g + t0 + g;
-    auto I_gtx = [&](uint32_t i) -> uint32_t { return isog ? db.gene_tx[t0 + i] : iso_gtx[i]; };
-    auto I_start = [&](uint32_t i) -> uint64_t { return isog ? db.tx[db.gene_tx[t0 + i]].start : iso_start[i]; };
-    auto I_len = [&](uint32_t i) -> int { return isog ? (int)db.tx[db.gene_tx[t0 + i]].len : (int)iso_len[i]; };
-    auto I_pre = [&](uint32_t i) -> uint32_t { return isog ? gpre[i] : iso_pre[i]; };
-    const uint32_t n_items = I_pre(niso);
-#ifdef RC_ROW_TIMING
-    unsigned long long tph[6] = {0, 0, 0, 0, 0, 0};
-    unsigned long long tc = __builtin_readcyclecounter();
-    auto tick = [&](int i) {
-        const unsigned long long t = __builtin_readcyclecounter();
-        tph[i] += t - tc;
-        tc = t;
-    };
-#define SEED_TICK(i) tick(i)
-#else
-#define SEED_TICK(i) ((void)0)
-#endif
-    const uint32_t gl = g - P.gene_begin;
-
     // subject samples of this query sample in this shard (spec 5b: the
     // higher-numbered ones only, the pair's other direction is the mirror
     // image): its row of tmask; tm holds the bits of the current pass's
@@ -254,11 +214,49 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
     int T1 = min(Tr, T0 + PASS_SAMPLES);
     pass_mask(T0);
     const uint32_t qpb0 = (uint32_t)db.sample_pos_begin[Q], qpb1 = (uint32_t)db.sample_pos_begin[Q + 1];
-    // the reverse pass's seeds of this gene's transcripts: [sh_rs0, sh_rs1) of rs_key
-    if (P.rs_n) {
-        if (tid < 2) (tid ? sh_rs1 : sh_rs0) = P.rs_range[2 * (size_t)(g - P.gene_begin) + tid];   // (rs_range_kernel)
+    // the reverse pass's seeds of this gene's transcripts: [sh_rs0, sh_rs1) of
+    // rs_key (rs_range_kernel), loaded beside the isoform tables
+    if (P.rs_n && tid < 2) (tid ? sh_rs1 : sh_rs0) = P.rs_range[2 * (size_t)(g - P.gene_begin) + tid];
+    if (!isog) {
+        for (uint32_t i = tid; i < niso; i += SBLOCK) {
+            const IsoRec r = db.giso[t0 + i];
+            iso_gtx[i] = r.gtx;
+            iso_start[i] = r.start;
+            iso_len[i] = r.len;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t pre = 0;
+            for (uint32_t i = 0; i < niso; i++) {
+                iso_pre[i] = pre;
+                const int L = (int)iso_len[i];
+                pre += (L >= W16) ? 2u * (uint32_t)((L - W16) / stride + 1) : 0u;
+            }
+            iso_pre[niso] = pre;
+        }
         __syncthreads();
     }
+    const uint32_t *const gpre = P.iso_pre_g + t0 + g;
+    auto I_gtx = [&](uint32_t i) -> uint32_t { return isog ? db.giso[t0 + i].gtx : iso_gtx[i]; };
+    auto I_start = [&](uint32_t i) -> uint64_t { return isog ? (uint64_t)db.giso[t0 + i].start : iso_start[i]; };
+    auto I_len = [&](uint32_t i) -> int { return isog ? (int)db.giso[t0 + i].len : (int)iso_len[i]; };
+    auto I_pre = [&](uint32_t i) -> uint32_t { return isog ? gpre[i] : iso_pre[i]; };
+    const uint32_t n_items = I_pre(niso);
+#ifdef RC_ROW_TIMING
+    unsigned long long tph[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long tc = __builtin_readcyclecounter();
+    auto tick = [&](int i) {
+        const unsigned long long t = __builtin_readcyclecounter();
+        tph[i] += t - tc;
+        tc = t;
+    };
+#define SEED_TICK(i) tick(i)
+#else
+#define SEED_TICK(i) ((void)0)
+#endif
+    const uint32_t gl = g - P.gene_begin;
+
+    if (P.rs_n) __syncthreads();   // sh_rs0 / sh_rs1
     while (T0 < Tr) {
         if (tid == 0) {
             sh_nseed = 0;
@@ -293,6 +291,9 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
             bool ok = false;
             int p = 0, strand = 0;
             uint32_t ii = 0;
+            // the word's k-mer, the 32 query bases before it (canonical
+            // pre-test) and its bucket are loaded together with its DUST
+            // usability, in flight across the D(p) barriers below
             if (it < n_items) {
                 if (!isog) {
                     while (ii + 1 < niso && iso_pre[ii + 1] <= it) ii++;
@@ -310,7 +311,20 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                 strand = rem >= ns ? 1 : 0;
                 p = (int)(rem - (strand ? ns : 0)) * stride;
                 info = (uint32_t)p | ((uint32_t)strand << 24);
-                ok = word_usable<AMB>(db, I_start(ii), I_len(ii), strand, p, total);
+                const QGeo qg = {I_start(ii), I_len(ii)};
+                const uint64_t qp = qfwd_pos(qg, strand, total, p);
+                const uint64_t *QA = strand ? db.RC : db.F;
+                key = (uint32_t)win(QA, qp);
+                if (fast && p >= stride) {
+                    qlw = win_s(QA, (int64_t)qp - 32);
+                    if (AMB) qlm = win_s(strand ? db.ARC : db.AF, (int64_t)qp - 32);
+                }
+                ok = word_usable<AMB>(db, qg.qs, qg.Lq, strand, p, total);
+                if (ok) {
+                    const uint32_t b = key >> (32 - ix.bits);
+                    lo = ix.bucket[b];
+                    cnt = ix.bucket[b + 1];
+                }
             }
             // D(p): the previous usable word of the same isoform and strand is
             // item it - k (p - k s), in this batch's LDS or looked up again
@@ -331,16 +345,9 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
             __syncthreads();
             it_d[tid] = D;
             if (it < n_items) {
-                QGeo qg = {I_start(ii), I_len(ii)};
-                const uint64_t qp = qfwd_pos(qg, strand, total, p);
-                const uint64_t *QA = strand ? db.RC : db.F;
                 if (ok) {
-                    key = (uint32_t)win(QA, qp);
-                    // the whole bucket of the key's top bits (one round trip, no
-                    // search): the hit loop filters by key and subject range
-                    const uint32_t b = key >> (32 - ix.bits);
-                    lo = ix.bucket[b];
-                    cnt = ix.bucket[b + 1] - lo;
+                    // the bucket of the key's top bits
+                    cnt -= lo;
                     // entries are ascending (k-mer, position) and the subject
                     // samples a contiguous position range: two lower bounds in
                     // the bucket (searched together) leave exactly the key's
@@ -359,11 +366,9 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     }
                     lo = b0;
                     cnt = b1 - b0;
-                    // the 32 query bases before p (canonical pre-test)
-                    if (fast && p >= stride) {
-                        qlw = win_s(QA, (int64_t)qp - 32);
-                        if (AMB) qlm = win_s(strand ? db.ARC : db.AF, (int64_t)qp - 32);
-                    }
+                } else {
+                    key = 0;
+                    qlw = qlm = 0;
                 }
             }
             it_lo[tid] = lo;
@@ -606,6 +611,11 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
         }
         SEED_TICK(2);
         const uint32_t nseed = sh_nseed;
+        // the pass's seed and candidate slots are claimed as soon as their
+        // counts are known; the atomics' round trips run under the sort and
+        // the segment scan (the results are only read by thread 0, later)
+        unsigned long long sb_claim = 0, cb_claim = 0;
+        if (tid == 0 && nseed) sb_claim = atomicAdd(&P.seed_count[shard], (unsigned long long)nseed);
         // sort by (k1, y). Chunks of SBLOCK seeds: one per thread, bitonic in
         // registers -- partners within the wave by lane exchange, the few
         // stages across waves through the chunk's LDS. Then (LDS pass) merge
@@ -723,13 +733,25 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
             if (f) seg_begin[pos] = (SegIdx)i;
             nseg += tot;
         }
-        if (tid == 0) seg_begin[nseg] = (SegIdx)nseed;
+        if (tid == 0) {
+            seg_begin[nseg] = (SegIdx)nseed;
+            if (nseg) cb_claim = atomicAdd(&P.cand_count[shard], (unsigned long long)nseg);
+        }
         const int NT = T1 - T0;   // <= PASS_SAMPLES: counts by T - T0
         for (int T = tid; T < NT; T += SBLOCK) tcnt[T] = 0;
         __syncthreads();
+        // the subject transcript of segment tid is kept for the candidate
+        // write in the word-item arrays (free after the hits; tile positions
+        // are < 2^32)
         for (uint32_t sg = tid; sg < nseg; sg += SBLOCK) {
             const uint32_t gtx = key_gtx(seeds[seg_begin[sg]].k1, xb);
-            const int T = db.tx[gtx].sample - T0;
+            const TxInfo st = db.tx[gtx];
+            if (sg == (uint32_t)tid) {
+                it_lo[tid] = (uint32_t)st.start;
+                it_cnt[tid] = st.len;
+                it_info[tid] = (uint32_t)st.sample;
+            }
+            const int T = st.sample - T0;
             seg_T[sg] = (uint8_t)T;
             atomicAdd(&tcnt[T], 1u);
         }
@@ -741,9 +763,9 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
             if (tid < NT) tpre[tid] = pre;
         }
         if (tid == 0) {
-            sh_sbase = nseed ? atomicAdd(&P.seed_count[shard], (unsigned long long)nseed) : 0ull;
-            sh_cbase = nseg ? atomicAdd(&P.cand_count[shard], (unsigned long long)nseg) : 0ull;
-            if (sh_sbase + nseed > P.seed_cap || sh_cbase + nseg > P.cand_cap) atomicOr(P.status, 1u);
+            sh_sbase = sb_claim;
+            sh_cbase = cb_claim;
+            if (sb_claim + nseed > P.seed_cap || cb_claim + nseg > P.cand_cap) atomicOr(P.status, 1u);
         }
         __syncthreads();
         const bool room = sh_sbase + nseed <= P.seed_cap && sh_cbase + nseg <= P.cand_cap;
@@ -813,7 +835,14 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     const uint64_t qstart = I_start(qi);
                     const int qlen = I_len(qi);
                     c.q0 = (uint32_t)(c.strand ? total - qstart - (uint64_t)qlen : qstart);
-                    const TxInfo st = db.tx[gtx];
+                    TxInfo st;
+                    if (c0 == 0) {
+                        st.start = it_lo[tid];
+                        st.len = it_cnt[tid];
+                        st.sample = (int)it_info[tid];
+                    } else {
+                        st = db.tx[gtx];
+                    }
                     c.s0 = (uint32_t)st.start;
                     c.Lq = (int32_t)qlen;
                     c.Lt = (int32_t)st.len;

@@ -61,6 +61,11 @@ struct DRow {
 };
 
 // Everything the kernels need to see, passed by value.
+// a gene's transcripts in gene_tx order, with their tile records (the seed
+// kernel's isoform tables in one load)
+struct IsoRec {
+    uint32_t start, len, gtx, pad;
+};
 struct Db {
     const uint64_t *F, *RC;     // 2-bit packed forward / reverse-complement
     const uint64_t *AF, *ARC;   // ambiguity masks (2 bits per base) or null
@@ -68,6 +73,7 @@ struct Db {
     const TxInfo *tx;
     const uint32_t *tx_gene;    // global gene of each transcript
     const uint32_t *gene_tx_off, *gene_tx;   // CSR: transcripts of each gene
+    const IsoRec *giso;                      // per gene_tx entry: its transcript's tile record
     const int32_t *gene_sample;
     const uint32_t *sample_gene_begin;       // n_samples + 1
     const uint32_t *sample_tx_begin;         // n_samples + 1
@@ -80,19 +86,33 @@ struct Db {
 // 16-mer index: one u64 per indexed position, (k-mer << 32) | global base
 // position, sorted by k-mer (stable, so positions ascend inside a k-mer run);
 // bucket[b] = first entry whose k-mer has top `bits` bits >= b.
+// block of 2^POS_TX_SHIFT positions -> the transcript holding its first base
+// (the last one starting at or before it), with that transcript's record, so
+// a position inside it resolves in one load
+struct PosTx {
+    uint32_t t, start, len;
+    int32_t sample;
+};
 struct Index {
     const uint64_t *ent;
     const uint32_t *bucket;     // 2^bits + 1 offsets
-    const uint32_t *pos_tx;     // transcript holding base (p >> POS_TX_SHIFT) << POS_TX_SHIFT
+    const PosTx *pos_tx;        // per block of POS_TX_SHIFT bases
     int32_t bits;
 };
 constexpr int POS_TX_SHIFT = 8;
 
-// transcript of a global base position: the block table, then forward
+// transcript of a tile position: the block's record, else forward from it
 __device__ __forceinline__ uint32_t tx_of_pos(const Db &db, const Index &ix, uint32_t pos, TxInfo &ti)
 {
-    uint32_t t = ix.pos_tx[pos >> POS_TX_SHIFT];
-    ti = db.tx[t];
+    const PosTx r = ix.pos_tx[pos >> POS_TX_SHIFT];
+    uint32_t t = r.t;
+    if (pos - r.start < r.len) {
+        ti.start = r.start;
+        ti.len = r.len;
+        ti.sample = r.sample;
+        return t;
+    }
+    ti = db.tx[++t];
     while ((uint64_t)pos >= ti.start + ti.len) ti = db.tx[++t];
     return t;
 }

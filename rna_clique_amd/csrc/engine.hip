@@ -350,6 +350,7 @@ struct rc_engine {
     DBuf<TxInfo> d_tile_tx, d_tile_itx;
     DBuf<uint64_t> d_F, d_RC, d_AF, d_ARC;
     DBuf<TxInfo> d_tx;
+    DBuf<IsoRec> d_giso;
     DBuf<uint32_t> d_tx_gene, d_gene_tx_off, d_gene_tx, d_sample_gene_begin, d_sample_tx_begin;
     DBuf<int32_t> d_gene_sample;
     DBuf<uint64_t> d_kpos_off, d_kcnt;
@@ -377,7 +378,8 @@ struct rc_engine {
     DBuf<uint32_t> d_sort_scratch, d_gen_tile;
     DBuf<uint64_t> d_sort_status;
     uint32_t sort_epoch = 0;
-    DBuf<uint32_t> d_bucket, d_pos_tx;
+    DBuf<uint32_t> d_bucket;
+    DBuf<PosTx> d_pos_tx;
     DBuf<uint64_t> d_sample_pos, d_txstart, d_kpos_rel, d_dmask, d_dust_imp;
     DBuf<uint32_t> d_dust_scratch;
     DBuf<uint64_t> d_dust_events;
@@ -806,6 +808,14 @@ static int upload(rc_engine *e)
         e->h_tx[t].sample = e->tx_sample[t];
     }
     CHK(up(e->d_tx, e->h_tx));
+    {
+        std::vector<IsoRec> giso(e->gene_tx.size());
+        for (size_t k = 0; k < giso.size(); k++) {
+            const TxInfo &x = e->h_tx[e->gene_tx[k]];
+            giso[k] = IsoRec{(uint32_t)x.start, x.len, e->gene_tx[k], 0u};
+        }
+        CHK(up(e->d_giso, giso));
+    }
     CHK(up(e->d_tx_gene, e->tx_gene));
     std::vector<uint32_t> tx_pos(n_tx, 0);
     for (uint32_t g = 0; g < n_genes; g++)
@@ -1029,7 +1039,7 @@ static int load_tile(rc_engine *e, int ti)
     std::vector<TxInfo> ttx, itx;
     std::vector<uint32_t> gid;
     std::vector<uint64_t> koff(1, 0);
-    std::vector<uint32_t> pos_tx((total >> POS_TX_SHIFT) + 2, 0);
+    std::vector<PosTx> pos_tx((total >> POS_TX_SHIFT) + 2, PosTx{0, 0, 0, 0});
     std::vector<uint64_t> txb((total >> 6) + 4, 0);
     auto setbit = [&](uint64_t p) {
         const uint64_t q = p + 64;
@@ -1060,12 +1070,20 @@ static int load_tile(rc_engine *e, int ti)
         for (uint64_t b = p0 >> POS_TX_SHIFT; b < (p0 + align_up(S.nbases)) >> POS_TX_SHIFT; b++) {
             const uint64_t p = b << POS_TX_SHIFT;
             while (t + 1 < S.tx_begin + S.n_tx && p0 + (e->tx_start[t + 1] - S.base) <= p) t++;
-            pos_tx[b] = t;
+            pos_tx[b] = PosTx{t, (uint32_t)e->h_tx[t].start, e->h_tx[t].len, e->h_tx[t].sample};
         }
     }
     e->tile_tx_first[N] = (uint32_t)ttx.size();
     if (koff.back() > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "more than 2^32 seed positions in a tile");
     CHK(up(e->d_tx, e->h_tx));
+    {
+        std::vector<IsoRec> giso(e->gene_tx.size());
+        for (size_t k = 0; k < giso.size(); k++) {
+            const TxInfo &x = e->h_tx[e->gene_tx[k]];
+            giso[k] = IsoRec{(uint32_t)x.start, x.len, e->gene_tx[k], 0u};
+        }
+        CHK(up(e->d_giso, giso));
+    }
     CHK(up(e->d_tile_tx, ttx));
     CHK(up(e->d_tile_itx, itx));
     CHK(up(e->d_kpos_off, koff));
@@ -1276,6 +1294,7 @@ static Db make_db(rc_engine *e)
     db.tx_gene = e->d_tx_gene.p;
     db.gene_tx_off = e->d_gene_tx_off.p;
     db.gene_tx = e->d_gene_tx.p;
+    db.giso = e->d_giso.p;
     db.gene_sample = e->d_gene_sample.p;
     db.sample_gene_begin = e->d_sample_gene_begin.p;
     db.sample_tx_begin = e->d_sample_tx_begin.p;
@@ -2672,12 +2691,25 @@ int rc_dust_masks(rc_engine *e, const int32_t *samples, int32_t n, uint64_t *out
     std::vector<int> ss(samples, samples + n);
     std::sort(ss.begin(), ss.end());
     ss.erase(std::unique(ss.begin(), ss.end()), ss.end());
-    // a tile of these samples alone: packed, their DUST masks, copied out
-    rc_engine::Tile T;
-    T.samples = ss;
-    e->tiles.push_back(T);
-    e->tile_loaded = -1;
-    const int ti = (int)e->tiles.size() - 1;
+    // the pass: the shard's own alignment tile when it is a single tile
+    // holding these samples (its tables stay loaded for rc_align), else a
+    // tile of these samples alone; packed, their DUST masks, copied out
+    if (e->tiles_for != (int64_t)e->pair0 || e->tiles.empty()) {
+        plan_tiles(e);
+        e->tiles_for = (int64_t)e->pair0;
+        e->tile_loaded = -1;
+    }
+    bool own = e->tiles.size() == 1;
+    for (int s : ss)
+        own = own && std::binary_search(e->tiles[0].samples.begin(), e->tiles[0].samples.end(), s);
+    int ti = 0;
+    if (!own) {
+        rc_engine::Tile T;
+        T.samples = ss;
+        e->tiles.push_back(T);
+        e->tile_loaded = -1;
+        ti = (int)e->tiles.size() - 1;
+    }
     int rc = load_tile(e, ti);
     if (rc == RC_OK) rc = pack_tile(e);
     const bool dust = e->o.dust_level > 0 && !e->external;
@@ -2722,8 +2754,10 @@ int rc_dust_masks(rc_engine *e, const int32_t *samples, int32_t n, uint64_t *out
             out[o - 1] &= keep;
         }
     }
-    e->tiles.pop_back();
-    e->tile_loaded = -1;
+    if (!own) {
+        e->tiles.pop_back();
+        e->tile_loaded = -1;
+    }
     e->idx_bchunk = -1;
     return rc;
 }

@@ -7,9 +7,10 @@ the (replicated) graph phase.
 
 --share-dust: the DUST masks are made once per sample across the ranks
 (distributed.exchange_dust): a rank's timed work is its own samples' masks
-(rc_dust_masks) plus its alignment with every mask given (rc_set_dust_masks);
-the other ranks' masks are made untimed beforehand, and the all-gather is
-modelled (`exchange_model_ms`: the gathered bytes at 100 GB/s).
+(rc_dust_masks, into a device buffer) plus its alignment with every mask
+given (rc_set_dust_masks, device to device); the other ranks' masks are made
+untimed beforehand, and the all-gather is modelled (`exchange_model_ms`: the
+gathered bytes at 100 GB/s).
 """
 import argparse
 import json
@@ -50,14 +51,18 @@ def main():
             need = sorted(distributed.needed_samples(bases, args.shards, r))
             mine = [s for s in need if owner[s] == r]
             others = [s for s in need if owner[s] != r]
-            other_w = eng.dust_masks(others)   # the other ranks' share (untimed)
+            # the other ranks' share, made untimed (on the device, as after the all-gather)
+            other_w = torch.from_numpy(eng.dust_masks(others).view(np.int64)).cuda()
+            n_own = sum((bases[s] + 63) // 64 for s in mine)
+            allw = torch.empty(n_own + other_w.numel(), dtype=torch.int64, device="cuda")
+            allw[n_own:] = other_w
         best = None
         for _ in range(args.reps):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             if args.share_dust:
-                own_w = eng.dust_masks(mine)
-                eng.set_dust_masks(mine + others, np.concatenate([own_w, other_w]))
+                eng.dust_masks(mine, allw[:n_own])    # this rank's masks, device to device
+                eng.set_dust_masks(mine + others, allw)
             eng.align()
             eng.finish()
             torch.cuda.synchronize()
