@@ -243,7 +243,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
     auto I_pre = [&](uint32_t i) -> uint32_t { return isog ? gpre[i] : iso_pre[i]; };
     const uint32_t n_items = I_pre(niso);
 #ifdef RC_ROW_TIMING
-    unsigned long long tph[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long tph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tc = __builtin_readcyclecounter();
     auto tick = [&](int i) {
         const unsigned long long t = __builtin_readcyclecounter();
@@ -257,6 +257,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
     const uint32_t gl = g - P.gene_begin;
 
     if (P.rs_n) __syncthreads();   // sh_rs0 / sh_rs1
+    SEED_TICK(8);
     while (T0 < Tr) {
         if (tid == 0) {
             sh_nseed = 0;
@@ -343,6 +344,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                 }
             }
             __syncthreads();
+            SEED_TICK(9);
             it_d[tid] = D;
             if (it < n_items) {
                 if (ok) {
@@ -423,6 +425,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                         if (live[j]) chk[(uint32_t)j * SBLOCK + (uint32_t)tid] = (uint32_t)hev[j];
                     __syncthreads();
                 }
+                SEED_TICK(5);
 #pragma unroll
                 for (int j = 0; j < HBATCH; j++) {
                     const uint32_t pos = (uint32_t)hev[j];
@@ -476,6 +479,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
+                SEED_TICK(6);
                 // pass B: the full canonical test and the seed of each queued hit
                 for (uint32_t q = (uint32_t)lane; q < qn; q += 64) {
                     const uint32_t pos = wqp[q];
@@ -585,6 +589,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
+                SEED_TICK(7);
             }
             __syncthreads();
         }
@@ -878,7 +883,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
     }
 #ifdef RC_ROW_TIMING
     if (tid == 0 && P.prof)
-        for (int i = 0; i < 5; i++) atomicAdd(&P.prof[i], tph[i]);
+        for (int i = 0; i < 10; i++) atomicAdd(&P.prof[i], tph[i]);
 #endif
 #undef SEED_TICK
 }

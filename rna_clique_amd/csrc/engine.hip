@@ -1721,8 +1721,8 @@ static int align_tile(rc_engine *e, int ti)
         HIPCHK(hipMemsetAsync(e->d_shard_cnt.p, 0, 2 * NSHARD * sizeof(unsigned long long), e->st));
         HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
         if (gcb[RT]) HIPCHK(hipMemsetAsync(e->d_gc_cnt.p, 0, gcb[RT] * 4, e->st));
-        CHK(e->d_prof.ensure(8));
-        HIPCHK(hipMemsetAsync(e->d_prof.p, 0, 8 * sizeof(unsigned long long), e->st));
+        CHK(e->d_prof.ensure(10));
+        HIPCHK(hipMemsetAsync(e->d_prof.p, 0, 10 * sizeof(unsigned long long), e->st));
         bool again = false;
         n_big = 0;
         for (size_t r = 0; r < RT && !again; r++) {
@@ -1983,10 +1983,12 @@ static int align_tile(rc_engine *e, int ti)
         HIPCHK(hipStreamSynchronize(e->st));
         if (ctr[8] || ctr[9]) {   // built with RC_ROW_TIMING: wave cycles in transitions / steps
             fprintf(stderr, "row kernel wave-cycles: transitions %.4g steps %.4g\n", (double)ctr[8], (double)ctr[9]);
-            unsigned long long pr[8];
+            unsigned long long pr[10];
             HIPCHK(hipMemcpy(pr, e->d_prof.p, sizeof pr, hipMemcpyDeviceToHost));
-            fprintf(stderr, "seed kernel block-cycles: words %.4g scan %.4g hits %.4g sort %.4g write %.4g\n",
-                    (double)pr[0], (double)pr[1], (double)pr[2], (double)pr[3], (double)pr[4]);
+            fprintf(stderr, "seed kernel block-cycles: prologue %.4g words: usable %.4g lookup %.4g scan %.4g "
+                            "hits %.4g (loads %.4g pretest %.4g full test %.4g) sort %.4g write %.4g\n",
+                    (double)pr[8], (double)pr[9], (double)pr[0], (double)pr[1], (double)(pr[2] + pr[5] + pr[6] + pr[7]),
+                    (double)pr[5], (double)pr[6], (double)pr[7], (double)pr[3], (double)pr[4]);
         }
         if (!(status & 1u)) {
             e->tm.ext_steps += (double)ctr[0];
