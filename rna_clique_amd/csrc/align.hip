@@ -30,7 +30,10 @@ constexpr int SBLOCK = 256;
 #endif
 constexpr int SEED_CAP = RC_SEED_CAP;   // seeds of one pass in LDS (a power of two: the bitonic sort pads to one)
 static_assert((SEED_CAP & (SEED_CAP - 1)) == 0, "RC_SEED_CAP must be a power of two");
-constexpr int HBATCH = 4;                          // hits per lane per batch of the seed kernel
+#ifndef RC_HBATCH
+#define RC_HBATCH 4
+#endif
+constexpr int HBATCH = RC_HBATCH;                  // hits per lane per batch of the seed kernel
 constexpr int PASS_SAMPLES = 256;                  // subject samples of one seed pass (per-sample counts in LDS)
 
 constexpr int EBLOCK = 256;
