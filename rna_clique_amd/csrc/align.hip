@@ -500,13 +500,15 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     // loads go out together, the bounds are applied afterwards
                     TxInfo st;
                     const uint32_t stx = tx_of_pos(db, ix, pos, st);
-                    uint64_t xl = 0, xr = 0;
+                    uint64_t xl = 0, xr = 0, xr2 = 0;   // xr2: the next 32 bases right (exact runs are long)
                     if (fast) {
                         xl = win_s(QA, (int64_t)qp - 32) ^ win_s(db.F, (int64_t)pos - 32);
                         xr = win(QA, qp + W16) ^ win(db.F, (uint64_t)pos + W16);
+                        xr2 = win(QA, qp + W16 + 32) ^ win(db.F, (uint64_t)pos + W16 + 32);
                         if (AMB) {
                             xl |= win_s(QAM, (int64_t)qp - 32) | win_s(db.AF, (int64_t)pos - 32);
                             xr |= win(QAM, qp + W16) | win(db.AF, (uint64_t)pos + W16);
+                            xr2 |= win(QAM, qp + W16 + 32) | win(db.AF, (uint64_t)pos + W16 + 32);
                         }
                     }
                     // (pos in [pb0, pb1): st.sample is in [T0, T1))
@@ -530,10 +532,12 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     int r;
                     if (fast && xr) {
                         r = min((int)(__builtin_ctzll(xr) >> 1), max(maxr, 0));
+                    } else if (fast && xr2) {
+                        r = min(32 + (int)(__builtin_ctzll(xr2) >> 1), max(maxr, 0));
                     } else {
-                        const int r0 = fast ? min(32, max(maxr, 0)) : 0;
-                        r = r0 + lcp<AMB>(QA, QAM, qp + (uint64_t)(W16 + r0), db.F, db.AF,
-                                          st.start + (uint64_t)(off + W16 + r0), maxr - r0);
+                        const int r0 = fast ? min(64, max(maxr, 0)) : 0;
+                        r = r0 + lcp64<AMB>(QA, QAM, qp + (uint64_t)(W16 + r0), db.F, db.AF,
+                                            st.start + (uint64_t)(off + W16 + r0), maxr - r0);
                     }
                     const int len = l + W16 + r;
                     if (len < P.word) continue;

@@ -421,6 +421,34 @@ __device__ __forceinline__ int lcp(const uint64_t *__restrict__ A, const uint64_
     return maxn > 0 ? maxn : 0;
 }
 
+// lcp, 64 bases per round trip (three words of each array in flight
+// together): the seed kernel's right extensions of long exact runs
+template <bool AMB, typename PT>
+__device__ __forceinline__ int lcp64(const uint64_t *__restrict__ A, const uint64_t *__restrict__ AA, PT pa,
+                                     const uint64_t *__restrict__ B, const uint64_t *__restrict__ BA, PT pb,
+                                     int maxn)
+{
+    auto w2 = [](uint64_t lo, uint64_t hi, unsigned sh) { return (lo >> sh) | ((hi << 1) << (63u - sh)); };
+    int n = 0;
+    while (n < maxn) {
+        const PT a = pa + (PT)n, b = pb + (PT)n;
+        const uint64_t *pA = A + (a >> 5), *pB = B + (b >> 5);
+        const unsigned sa = (unsigned)(a & 31) * 2u, sb = (unsigned)(b & 31) * 2u;
+        const uint64_t a0 = pA[0], a1 = pA[1], a2 = pA[2], b0 = pB[0], b1 = pB[1], b2 = pB[2];
+        uint64_t x0 = w2(a0, a1, sa) ^ w2(b0, b1, sb), x1 = w2(a1, a2, sa) ^ w2(b1, b2, sb);
+        if (AMB) {
+            const uint64_t *qA = AA + (a >> 5), *qB = BA + (b >> 5);
+            const uint64_t m0 = qA[0], m1 = qA[1], m2 = qA[2], n0 = qB[0], n1 = qB[1], n2 = qB[2];
+            x0 |= w2(m0, m1, sa) | w2(n0, n1, sb);
+            x1 |= w2(m1, m2, sa) | w2(n1, n2, sb);
+        }
+        const int k = x0 ? (int)(__builtin_ctzll(x0) >> 1) : (x1 ? 32 + (int)(__builtin_ctzll(x1) >> 1) : 64);
+        n += k;
+        if (k < 64) return n < maxn ? n : maxn;
+    }
+    return maxn > 0 ? maxn : 0;
+}
+
 // 32 bases at a signed base position (arrays carry two zero words in front,
 // so p >= -64 stays in bounds)
 __device__ __forceinline__ uint64_t win_s(const uint64_t *__restrict__ a, int64_t p)

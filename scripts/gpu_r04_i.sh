@@ -1,4 +1,5 @@
-# Round 4 (i): seed-kernel occupancy A/B at C3 and C3v: the default build
+# Round 4 (i): parity of the seed kernel with 64-base right extensions, its
+# block-cycle split, and an occupancy A/B at C3 and C3v: the default build
 # (1024-seed LDS passes, 4 waves/SIMD) against 512-seed passes at 5 waves
 # (s5) and 6 waves with 2 hits per lane (s6), 256-seed passes at 7 waves
 # (s7) and 8 waves with 1 hit per lane (s8).
@@ -7,6 +8,10 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 D=gpurun_out/r04_i
 mkdir -p $D
+timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_api.py -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > $D/gpu_tests.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 $D/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+RC_LIB=rna_clique_amd/librcgpu_timing.so timeout -k 10 200 python bench.py --config C3 --steps 1 --warmup 1 --no-cpu-baseline --no-e2e > $D/C3_timing.json 2> $D/C3_timing.err
+rc=$?; echo "C3 timing rc=$rc"; grep -a "block-cycles" $D/C3_timing.err; [ $rc -eq 0 ] || exit $rc
 for cfg in C3 C3v; do
   reps=2; [ $cfg = C3v ] && reps=1
   for i in $(seq 1 $reps); do
