@@ -22,11 +22,16 @@
 namespace rcg {
 
 constexpr int SBLOCK = 256;
+// Seed kernel occupancy (r04, profiles/r04_i, C3 seed kernel per step):
+// 1024-seed LDS passes at 4 workgroups per CU 79.5 ms; 512-seed passes at 5
+// (96 VGPRs, 28 KB LDS) 70.7; 6 (2 hits per lane) 74.7; 256-seed passes at
+// 7 or 8: 92 / 98 (more passes halve their subject range). C3v: 103-104 ms
+// at 4 and 5 alike.
 #ifndef RC_SEED_CAP
-#define RC_SEED_CAP 1024
+#define RC_SEED_CAP 512
 #endif
 #ifndef RC_SEED_WAVES
-#define RC_SEED_WAVES 1   // measured: a 4-wave bound (<= 128 VGPRs, more SGPR spills) is 7 % slower
+#define RC_SEED_WAVES 5
 #endif
 constexpr int SEED_CAP = RC_SEED_CAP;   // seeds of one pass in LDS (a power of two: the bitonic sort pads to one)
 static_assert((SEED_CAP & (SEED_CAP - 1)) == 0, "RC_SEED_CAP must be a power of two");
