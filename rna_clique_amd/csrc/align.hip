@@ -1638,6 +1638,9 @@ __device__ __forceinline__ void lds_pair_at(uint32_t a, uint32_t b, uint32_t pa,
 // Matching bases from (pa, pb) forward, at most maxn (>= 0); positions are
 // absolute LDS base positions (lds_win2); masks (AMB) sit `moff` bases
 // further on. Reads bases up to pa + max(maxn, 1) + 47 (WIN_MARGIN).
+#ifndef RC_SLIDE_UNIFORM
+#define RC_SLIDE_UNIFORM 1
+#endif
 template <bool AMB>
 __device__ __forceinline__ int slide_fwd(uint32_t pa, uint32_t pb, int maxn, uint32_t moff)
 {
@@ -1651,6 +1654,28 @@ __device__ __forceinline__ int slide_fwd(uint32_t pa, uint32_t pb, int maxn, uin
         x |= ma | mb;
     }
     int n = x ? (int)(__builtin_ctzll(x) >> 1) : 32;
+#if RC_SLIDE_UNIFORM
+    // the loop is wave-uniform (a ballot per round): lanes whose run ended
+    // keep their count and stop advancing; no exec-mask bookkeeping per round
+    // (the dword addresses follow n: a stopped lane re-reads its last window)
+    bool go = n == 32 && maxn > 32;
+    if (__builtin_amdgcn_ballot_w64(go)) {
+        const uint32_t a0 = ((pa + 32u) >> 2) & ~3u, b0 = ((pb + 32u) >> 2) & ~3u;
+        do {
+            const uint32_t o = ((uint32_t)(n - 32) >> 2) & ~7u;
+            uint64_t wa, wb;
+            lds_pair_at(a0 + o, b0 + o, pa, pb, wa, wb);
+            x = wa ^ wb;
+            if (AMB) {
+                lds_pair_at(a0 + o + moff / 4u, b0 + o + moff / 4u, pa, pb, wa, wb);
+                x |= wa | wb;
+            }
+            const int k = x ? (int)(__builtin_ctzll(x) >> 1) : 32;
+            n = go ? n + k : n;
+            go = go && k == 32 && n < maxn;
+        } while (__builtin_amdgcn_ballot_w64(go));
+    }
+#else
     if (n == 32 && maxn > 32) {
         uint32_t a = ((pa + 32u) >> 2) & ~3u, b = ((pb + 32u) >> 2) & ~3u;
         for (;;) {
@@ -1671,6 +1696,7 @@ __device__ __forceinline__ int slide_fwd(uint32_t pa, uint32_t pb, int maxn, uin
             b += 8u;
         }
     }
+#endif
     return min(n, maxn);
 }
 
@@ -1790,7 +1816,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
     RowWin *const rows_win = reinterpret_cast<RowWin *>(rcnt + 8);   // (WIN only)
     {
         const RowArgsK K = row_args();
-        if (threadIdx.x < 4) rcnt[threadIdx.x] = 0;
+        if (threadIdx.x < 4 || threadIdx.x == 5) rcnt[threadIdx.x] = 0;   // [5]: 6 x row steps
         for (int i = threadIdx.x; i <= NSHARD; i += EBLOCK) sprefix[i] = K->P.shard_prefix[i];
         // list mode: the candidates are P.list[0, *P.list_n) (a previous row
         // kernel's deferrals), else the linear index space over the shards
@@ -1883,7 +1909,6 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
     int blk = 0, nkd = 0;
     int score = 0, bound = 0;                             // of the last step
     bool swap = false;                                    // spec 4b: query = the higher-numbered sample
-    unsigned long long steps = 0;                         // row steps (wave-uniform count)
     int wlo = 0, wlim = 0;                                // WIN: the lane's window [wlo, wlim] in extension offsets
 
     // ---- windowed staging (WIN) ----
@@ -2032,6 +2057,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
         }
         R = rl == RC0 ? r0 : -1;
         goe = 0;
+        if (rl == 0 && d6) atomicAdd(&rcnt[5], (uint32_t)d6);   // the previous extension's steps
         d6 = 0;
         if constexpr (!WIN) pbk = pb - (uint32_t)k;   // (WIN: win_begin / win_fill set it)
         blk = blen + k;
@@ -2195,6 +2221,9 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                                 const int u = alen; alen = blen; blen = u;
                             }
                         }
+                        // the previous extension's steps; the resumed one's steps
+                        // before the resume were counted by its first pass
+                        if (rl == 0) atomicAdd(&rcnt[5], (uint32_t)(d6 - rec[RES_D6]));
                         d6 = rec[RES_D6];
                         best = rec[RES_BEST];
                         const int kb = rec[RES_PK];
@@ -2365,7 +2394,6 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
         const bool ext = act >= A_STEP_R;
         const uint64_t mext = m_ge(act, A_STEP_R);
         if (!mext) break;
-        steps += (unsigned long long)(__builtin_popcountll(rw_spread<RW>(mext)) / RW);   // scalar
         // ---------------- one greedy step of every extending row ----------------
         if (ext) {
             d6 += 6;
@@ -2468,9 +2496,10 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
     }
 #endif
     unsigned long long *const ctr = row_args()->P.counters;
-    if (lane == 0 && ctr) atomicAdd(&ctr[0], steps);
+    if (rl == 0 && d6) atomicAdd(&rcnt[5], (uint32_t)d6);   // the last extension's steps
     __syncthreads();
     if (threadIdx.x < 4 && ctr) atomicAdd(&ctr[1 + threadIdx.x], (unsigned long long)rcnt[threadIdx.x]);   // [4]: slides
+    if (threadIdx.x == 5 && ctr) atomicAdd(&ctr[0], (unsigned long long)(rcnt[5] / 6u));
 }
 
 // The candidates' first-seed extensions -> box; the other seeds of the
