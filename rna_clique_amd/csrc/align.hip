@@ -1907,6 +1907,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
     // pb - k (b position of diagonal k at a offset 0), blen + k, -(k + d6)
     uint32_t pbk = 0;
     int blk = 0, nkd = 0;
+    int mnk = 0;   // min(alen, blk): a step's room along its diagonal is mnk - ni
     int score = 0, bound = 0;                             // of the last step
     bool swap = false;                                    // spec 4b: query = the higher-numbered sample
     int wlo = 0, wlim = 0;                                // WIN: the lane's window [wlo, wlim] in extension offsets
@@ -2061,6 +2062,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
         d6 = 0;
         if constexpr (!WIN) pbk = pb - (uint32_t)k;   // (WIN: win_begin / win_fill set it)
         blk = blen + k;
+        mnk = max(min(alen, blk), 0);
         nkd = -k;
         if (rl == 0) {
             atomicAdd(&rcnt[0], 1u);
@@ -2239,6 +2241,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                         }
                         if constexpr (WIN) win_begin(phase == A_LDONE ? 1 : 0); else pbk = pb - (uint32_t)k;
                         blk = blen + k;
+                        mnk = max(min(alen, blk), 0);
                         nkd = -(k + d6);
                         if (rl == 0) {
                             atomicAdd(&rcnt[0], 1u);
@@ -2302,6 +2305,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 // into the per-lane constants (pb and blen are not kept)
                 pbk -= (uint32_t)s;
                 blk += s;
+                mnk = max(min(alen, blk), 0);
                 nkd -= s;
                 if constexpr (WIN) win_lane(k + kn);
                 if (rl == 0) {
@@ -2404,7 +2408,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
             // frontier value R >= 0 has j = R - k >= 0, so unsigned compares
             // carry the lower bounds)
             // (j = R - k < blen  <=>  R < blk;  j + 1 = Rr - k < blen + 1  <=>  Rr <= blk)
-            const int cm = ((uint32_t)R < (uint32_t)alen && R < blk) ? R + 1 : -1;
+            const int cm = ((uint32_t)R < (uint32_t)mnk) ? R + 1 : -1;
             const int cil = ((uint32_t)Rl < (uint32_t)alen) ? Rl + 1 : -1;
             const int cd = (Rr >= 0 && Rr <= blk) ? Rr : -1;
             int ni = max(max(cm, cil), cd);
@@ -2413,7 +2417,9 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
             const int src = fm ? goe : (fi ? gl : gr);
             const int e = fm ? 0 : (fi ? 1 : 2);
             const int pe = (src >> EBIT) & 3;
-            int ng = (src & ~(3 << EBIT)) + (fm ? 0 : 1 + (pe == e ? 0 : (1 << OBIT)) + (e << EBIT));
+            // (E goes in after the slide: matches after the move clear it)
+            const int ngb = (src & ~(3 << EBIT)) + (fm ? 0 : 1 + (pe == e ? 0 : (1 << OBIT)));
+            int ee = e;
             // score and bound of the lanes dead before the step keep stale
             // values (loop-carried: nothing to materialize), never read
             // unmasked (mi and mcont are ANDed with the live lanes)
@@ -2423,7 +2429,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 int m = 0, s = 0;
                 bool pend = false;
                 if (ni >= 0) {
-                    m = min(alen - ni, blk - ni);
+                    m = mnk - ni;
                     const int mw = ni < wlo ? -1 : min(m, wlim - ni);
                     s = slide_fwd<AMB>(pa + (uint32_t)ni, pbk + (uint32_t)ni, max(mw, 0), moff);
                     pend = mw < m && s >= mw;
@@ -2431,20 +2437,21 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 if (ballot(pend)) win_resolve(ni, s, m, pend);
                 if (ni >= 0) {
                     ni += s;
-                    if (s > 0) ng &= ~(3 << EBIT);
+                    if (s > 0) ee = 0;
                     score = 2 * ni + nkd;   // 2 ni - k - d6
                     if (score < best - X) ni = -1;
                     bound = score + 2 * (m - s);
                 }
             } else if (ni >= 0) {
-                const int m = min(alen - ni, blk - ni);
+                const int m = mnk - ni;
                 const int s = slide_fwd<AMB>(pa + (uint32_t)ni, pbk + (uint32_t)ni, m, moff);
                 ni += s;
-                if (s > 0) ng &= ~(3 << EBIT);
+                if (s > 0) ee = 0;
                 score = 2 * ni + nkd;   // 2 ni - k - d6
                 if (score < best - X) ni = -1;
                 bound = score + 2 * (m - s);
             }
+            const int ng = ngb + (ee << EBIT);
             R = ni;
             goe = ng;
             const bool live = ni >= 0;

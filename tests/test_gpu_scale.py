@@ -7,7 +7,7 @@
   unsharded run's distances, sums, edges and ideal nodes bit for bit, and
   every shard's tables equal the unsharded tables of the same pairs
   (find_all_pairs.py:224-228 runs the pairs independently).
-* C5 (128 x 100 000, 200 bp - 5 kb, BASELINE configs[4]): rank 2 of 8 -- the
+* C5 (128 x 100 000, 200 bp - 5 kb, BASELINE configs[4]): the rank of 8 with the largest modelled footprint -- the
   largest modelled HBM footprint -- alone on the GPU with only its 65 of 128
   samples generated and resident, cut into alignment tiles: whole-shard
   properties, determinism, two owned pairs bit-exact vs the oracle, and the
@@ -224,15 +224,17 @@ def test_C5_one_rank_shard(native):
     from bench import shard_samples
     from rna_clique_amd import distributed
     from rna_clique_amd.engine import Engine
+    from rna_clique_amd.simulate import CONFIGS, simulate
     S = 8
-    # the rank with the largest modelled footprint (rank 2 at C5)
-    with _heartbeat("C5: generate rank 2's samples"):
-        samples, need, (order, first) = shard_samples("C5", S, 2)
-    bases = [int(s.tx_offsets[-1]) for s in samples]
-    genes = [len(np.unique(s.gene)) for s in samples]
+    # the rank with the largest modelled footprint (from the metadata alone)
+    meta, _ = simulate(only=[], **CONFIGS["C5"])
+    bases = [int(s.tx_offsets[-1]) for s in meta]
+    genes = [len(np.unique(s.gene)) for s in meta]
+    del meta
     model = distributed.hbm_footprint(bases, genes, S)
     R = int(np.argmax(model))
-    assert R == 2
+    with _heartbeat(f"C5: generate rank {R}'s samples"):
+        samples, need, (order, first) = shard_samples("C5", S, R)
     assert len(need) < len(samples) and all((samples[i].seq is None) == (i not in need) for i in range(128))
     free0, _ = torch.cuda.mem_get_info(0)
     eng = Engine(device=0, shard_rank=R, shard_count=S)
@@ -242,7 +244,7 @@ def test_C5_one_rank_shard(native):
         eng.align()
         eng.finish()
     tm = eng.timings()
-    print(f"  C5 rank 2: {tm['tiles']:.0f} tiles, {tm['total_ms']:.0f} ms", flush=True)
+    print(f"  C5 rank {R}: {tm['tiles']:.0f} tiles, {tm['total_ms']:.0f} ms", flush=True)
     assert tm["tiles"] > 1
     free1, _ = torch.cuda.mem_get_info(0)
     own = eng.owned_pairs()
