@@ -39,7 +39,10 @@ static_assert((SEED_CAP & (SEED_CAP - 1)) == 0, "RC_SEED_CAP must be a power of 
 #define RC_HBATCH 4
 #endif
 constexpr int HBATCH = RC_HBATCH;                  // hits per lane per batch of the seed kernel
-constexpr int PASS_SAMPLES = 256;                  // subject samples of one seed pass (per-sample counts in LDS)
+#ifndef RC_PASS_SAMPLES
+#define RC_PASS_SAMPLES 256
+#endif
+constexpr int PASS_SAMPLES = RC_PASS_SAMPLES;                // subject samples of one seed pass (per-sample counts in LDS)
 
 constexpr int EBLOCK = 256;
 constexpr int EWAVES = EBLOCK / 64;

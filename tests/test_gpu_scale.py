@@ -7,8 +7,8 @@
   unsharded run's distances, sums, edges and ideal nodes bit for bit, and
   every shard's tables equal the unsharded tables of the same pairs
   (find_all_pairs.py:224-228 runs the pairs independently).
-* C5 (128 x 100 000, 200 bp - 5 kb, BASELINE configs[4]): the rank of 8 with the largest modelled footprint -- the
-  largest modelled HBM footprint -- alone on the GPU with only its 65 of 128
+* C5 (128 x 100 000, 200 bp - 5 kb, BASELINE configs[4]): the rank of 8 with
+  the largest modelled HBM footprint alone on the GPU with only its ~60 of 128
   samples generated and resident, cut into alignment tiles: whole-shard
   properties, determinism, two owned pairs bit-exact vs the oracle, and the
   measured HBM use against distributed.hbm_footprint's model.
