@@ -1911,7 +1911,6 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
     uint32_t pbk = 0;
     int blk = 0, nkd = 0;
     int mnk = 0;   // min(alen, blk): a step's room along its diagonal is mnk - ni
-    int score = 0, bound = 0;                             // of the last step
     bool swap = false;                                    // spec 4b: query = the higher-numbered sample
     int wlo = 0, wlim = 0;                                // WIN: the lane's window [wlo, wlim] in extension offsets
 
@@ -2074,15 +2073,6 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
         }
         act = (min(alen, blen) - r0 <= 0) ? done_act : done_act + (A_STEP_R - A_RDONE);
     };
-    // reversed copy of a staged array: word w holds bases L - 1 - 32 w down to
-    // L - 32 (w + 1) of the array whose base 0 sits at LDS base position fb
-    auto stage_rev = [&](uint64_t *dst, uint32_t fb, int L) {
-        const int nw = (L >> 5) + 3;
-        for (int w = rl; w < nw; w += RW) {
-            const int fp = L - 32 * (w + 1);
-            dst[w] = fp > -32 ? rev2(lds_win1((uint32_t)((int)fb + fp))) : 0ull;
-        }
-    };
 
 #ifdef RC_ROW_TIMING
     unsigned long long t_tr = 0, t_st = 0;
@@ -2143,7 +2133,14 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                 } else {
-                if (nwq > sw || nwt > sw || (Lq >> 5) + 3 > sw || (Lt >> 5) + 3 > sw) {
+                // the left extensions walk reversed copies: the other
+                // orientation's array from the mirrored start (complements on
+                // both sides: the same matches), staged like the forward ones
+                const uint64_t total = K->db.total;
+                const uint64_t rq0 = total - q0 - (uint64_t)Lq, rs0 = total - s0 - (uint64_t)Lt;
+                const int nwqr = (int)(((rq0 & 31) + (uint64_t)Lq) >> 5) + 3;
+                const int nwtr = (int)(((rs0 & 31) + (uint64_t)Lt) >> 5) + 3;
+                if (nwq > sw || nwt > sw || nwqr > sw || nwtr > sw) {
                     if (rl == 0 && row_args()->P.why) atomicAdd(&row_args()->P.why[0], 1ull);
                     defer(ci, false);
                     continue;
@@ -2154,8 +2151,9 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 // one more round trip in front of the staging loads)
                 GW dF = (GW)K->db.F, dRC = (GW)K->db.RC;
                 asm volatile("" : "+s"(dF), "+s"(dRC));
-                const GW QA = strand ? dRC : dF;
+                const GW QA = strand ? dRC : dF, QR = strand ? dF : dRC;
                 const GW qw = QA + (q0 >> 5), tw = dF + (s0 >> 5);
+                const GW qrw = QR + (rq0 >> 5), trw = dRC + (rs0 >> 5);
                 {
                     const uint32_t e01 = (uint32_t)meta[RM_REC + RC_E01];
                     const GSeed g0 =
@@ -2174,22 +2172,23 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 }
                 for (int w = rl + 2 * RW; w < nwq; w += RW) stg[w] = qw[w];
                 for (int w = rl + 2 * RW; w < nwt; w += RW) stg[sw + w] = tw[w];
+                for (int w = rl; w < nwqr; w += RW) stg[2 * sw + w] = qrw[w];
+                for (int w = rl; w < nwtr; w += RW) stg[3 * sw + w] = trw[w];
                 if (AMB) {
                     GW dAF = (GW)K->db.AF, dARC = (GW)K->db.ARC;
                     asm volatile("" : "+s"(dAF), "+s"(dARC));
                     const GW qm = (strand ? dARC : dAF) + (q0 >> 5), tm = dAF + (s0 >> 5);
+                    const GW qrm = (strand ? dAF : dARC) + (rq0 >> 5), trm = dARC + (rs0 >> 5);
                     for (int w = rl; w < nwq; w += RW) stg[4 * sw + w] = qm[w];
                     for (int w = rl; w < nwt; w += RW) stg[5 * sw + w] = tm[w];
+                    for (int w = rl; w < nwqr; w += RW) stg[6 * sw + w] = qrm[w];
+                    for (int w = rl; w < nwtr; w += RW) stg[7 * sw + w] = trm[w];
                 }
                 qb = base0 + (uint32_t)(q0 & 31);
                 tb = base0 + 32u * (uint32_t)sw + (uint32_t)(s0 & 31);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                stage_rev(stg + 2 * sw, qb, Lq);
-                stage_rev(stg + 3 * sw, tb, Lt);
-                if (AMB) {
-                    stage_rev(stg + 6 * sw, qb + moff, Lq);
-                    stage_rev(stg + 7 * sw, tb + moff, Lt);
+                if (rl == 0) {
+                    meta[RM_QB] = (int)(bqr + (uint32_t)(rq0 & 31));
+                    meta[RM_TB] = (int)(btr + (uint32_t)(rs0 & 31));
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
@@ -2217,9 +2216,9 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                         if (phase == A_LDONE) {
                             if (rl < 5) meta[RM_RSC + rl] = rec[RES_RSC + rl];
                             // left extension: forward from reversed position L - x
-                            pa = bqr + (uint32_t)(Lq - x);
+                            pa = (uint32_t)meta[RM_QB] + (uint32_t)(Lq - x);
                             alen = x;
-                            pb = btr + (uint32_t)(Lt - y);
+                            pb = (uint32_t)meta[RM_TB] + (uint32_t)(Lt - y);
                             blen = y;
                             if (swap) {
                                 const uint32_t t = pa; pa = pb; pb = t;
@@ -2348,9 +2347,9 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                     // (= base x - 1) of the reversed copies
                     const int x = meta[RM_X], y = meta[RM_Y];
                     const int Lq = meta[RM_REC + RC_LQ], Lt = meta[RM_REC + RC_LT];
-                    pa = bqr + (uint32_t)(Lq - x);
+                    pa = (uint32_t)meta[RM_QB] + (uint32_t)(Lq - x);
                     alen = x;
-                    pb = btr + (uint32_t)(Lt - y);
+                    pb = (uint32_t)meta[RM_TB] + (uint32_t)(Lt - y);
                     blen = y;
                     if (swap) {
                         const uint32_t t = pa; pa = pb; pb = t;
@@ -2423,9 +2422,11 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
             // (E goes in after the slide: matches after the move clear it)
             const int ngb = (src & ~(3 << EBIT)) + (fm ? 0 : 1 + (pe == e ? 0 : (1 << OBIT)));
             int ee = e;
-            // score and bound of the lanes dead before the step keep stale
-            // values (loop-carried: nothing to materialize), never read
-            // unmasked (mi and mcont are ANDed with the live lanes)
+            // the score of a lane live after the step; its bound (the score
+            // if every remaining base matched): 2 (ni + s) - k - d6 + 2 (m - s)
+            // = 2 min(alen, blk) + nkd, on every lane (only live lanes' are read)
+            int score = 0;
+            const int bound = 2 * mnk + nkd;
             if constexpr (WIN) {
                 // slides stop at the window; the ones that reached it (or
                 // start outside it) are finished after a refill
@@ -2443,7 +2444,6 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                     if (s > 0) ee = 0;
                     score = 2 * ni + nkd;   // 2 ni - k - d6
                     if (score < best - X) ni = -1;
-                    bound = score + 2 * (m - s);
                 }
             } else if (ni >= 0) {
                 const int m = mnk - ni;
@@ -2452,7 +2452,6 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 if (s > 0) ee = 0;
                 score = 2 * ni + nkd;   // 2 ni - k - d6
                 if (score < best - X) ni = -1;
-                bound = score + 2 * (m - s);
             }
             const int ng = ngb + (ee << EBIT);
             R = ni;
