@@ -154,7 +154,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
     using SegIdx = typename std::conditional<BIG, uint32_t, uint16_t>::type;
     __shared__ LSeed seeds_lds[BIG ? 1 : SEED_CAP];
     __shared__ SegIdx seg_lds[BIG ? 1 : SEED_CAP + 1];
-    __shared__ uint8_t segT_lds[BIG ? 1 : SEED_CAP];
+    __shared__ __attribute__((aligned(16))) uint8_t segT_lds[BIG ? 4 : SEED_CAP];
     const uint32_t cap = BIG ? P.big_cap : (uint32_t)SEED_CAP;
     LSeed *const seeds = BIG ? P.big_seeds + (size_t)blockIdx.x * cap : seeds_lds;
     SegIdx *const seg_begin = BIG ? reinterpret_cast<SegIdx *>(P.big_seg + (size_t)blockIdx.x * (cap + 1)) : seg_lds;
@@ -228,26 +228,21 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
     // the reverse pass's seeds of this gene's transcripts: [sh_rs0, sh_rs1) of
     // rs_key (rs_range_kernel), loaded beside the isoform tables
     if (P.rs_n && tid < 2) (tid ? sh_rs1 : sh_rs0) = P.rs_range[2 * (size_t)(g - P.gene_begin) + tid];
+    // (the word-item prefix of the gene's isoforms comes from the host's
+    // table, P.iso_pre_g: gene g's niso + 1 entries start at t0 + g)
+    const uint32_t *const gpre = P.iso_pre_g + t0 + g;
     if (!isog) {
-        for (uint32_t i = tid; i < niso; i += SBLOCK) {
-            const IsoRec r = db.giso[t0 + i];
-            iso_gtx[i] = r.gtx;
-            iso_start[i] = r.start;
-            iso_len[i] = r.len;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t pre = 0;
-            for (uint32_t i = 0; i < niso; i++) {
-                iso_pre[i] = pre;
-                const int L = (int)iso_len[i];
-                pre += (L >= W16) ? 2u * (uint32_t)((L - W16) / stride + 1) : 0u;
+        for (uint32_t i = tid; i <= niso; i += SBLOCK) {
+            if (i < niso) {
+                const IsoRec r = db.giso[t0 + i];
+                iso_gtx[i] = r.gtx;
+                iso_start[i] = r.start;
+                iso_len[i] = r.len;
             }
-            iso_pre[niso] = pre;
+            iso_pre[i] = gpre[i];
         }
         __syncthreads();
     }
-    const uint32_t *const gpre = P.iso_pre_g + t0 + g;
     auto I_gtx = [&](uint32_t i) -> uint32_t { return isog ? db.giso[t0 + i].gtx : iso_gtx[i]; };
     auto I_start = [&](uint32_t i) -> uint64_t { return isog ? (uint64_t)db.giso[t0 + i].start : iso_start[i]; };
     auto I_len = [&](uint32_t i) -> int { return isog ? (int)db.giso[t0 + i].len : (int)iso_len[i]; };
@@ -810,10 +805,20 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     const uint32_t gtx = key_gtx(k1, xb);
                     const int T = seg_T[sg];   // - T0
                     uint32_t rk = 0;   // rank among earlier candidates of the same sample
-                    if (T1 - T0 == 1)
+                    if (T1 - T0 == 1) {
                         rk = sg;
-                    else
-                        for (uint32_t s2 = 0; s2 < sg; s2++) rk += seg_T[s2] == T;
+                    } else {
+                        // four samples per dword: bytes equal to T are the zero
+                        // bytes of w ^ T x 0x01010101
+                        const uint32_t pat = 0x01010101u * (uint32_t)T;
+                        const uint32_t *const w4 = reinterpret_cast<const uint32_t *>(seg_T);
+                        auto zb = [](uint32_t x) {
+                            return (uint32_t)__builtin_popcount(~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u);
+                        };
+                        const uint32_t nf = sg >> 2;
+                        for (uint32_t q = 0; q < nf; q++) rk += zb(w4[q] ^ pat);
+                        if (sg & 3u) rk += zb((w4[nf] ^ pat) | (0xFFFFFFFFu << (8u * (sg & 3u))));
+                    }
                     Cand c;
                     c.seed_off = (uint32_t)(sbase + b0);
                     c.q_gtx = I_gtx(key_iso(k1, xb));
@@ -892,8 +897,10 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
         }
         T0 = T1;
         T1 = min(Tr, T0 + PASS_SAMPLES);
-        pass_mask(T0);
-        __syncthreads();
+        if (T0 < Tr) {   // (no next pass: no mask to load, nothing to wait for)
+            pass_mask(T0);
+            __syncthreads();
+        }
         SEED_TICK(4);
     }
 #ifdef RC_ROW_TIMING
