@@ -616,11 +616,11 @@ static void shard_pairs(rc_engine *e);
 // shard, so the shard's samples -- the ones it holds, indexes and scans --
 // are [a0, a1) u [b0, b1):
 //   pair work    2 x (L_a + L_b) per pair (seed hits, extension, RBH)
-//   queries     21 x L_s per query sample (the seed kernel's per-gene work)
-//   subjects    21 x L_s per subject sample (16-mer index + reverse pass)
-// (r04: least squares over the eight C3 rank shards, scripts/shard_time.py:
-// seed kernel 1.6 ms per query sample and 0.7 per subject sample, index 0.9
-// per subject sample, extension 0.26 ms per pair, DUST shared). Pairs are
+//   queries      9 x L_s per query sample (the seed kernel's per-gene work)
+//   subjects    15 x L_s per subject sample (16-mer index + reverse pass)
+// (r04: least squares over the eight C3 rank shards with shared DUST masks,
+// scripts/shard_time.py, profiles/r04_n: 0.94 ms per query sample, 1.5 per
+// subject sample, 0.41 per pair). Pairs are
 // numbered shard by shard, subject-major inside a shard; one shard gives the
 // plain subject-major order (0,1), (0,2), (1,2), (0,3), ...
 namespace plan {
@@ -649,7 +649,7 @@ struct Planner {
             if (ae > r.a0) pw += S(r.a0, ae) + (double)(ae - r.a0) * (SL[b + 1] - SL[b]);
         }
         // a sample that is both a query and a subject of the rank pays both
-        return 2.0 * pw + 21.0 * (S(r.a0, r.a1) + S(r.b0, r.b1));
+        return 2.0 * pw + 9.0 * S(r.a0, r.a1) + 15.0 * S(r.b0, r.b1);
     }
     std::pair<double, std::vector<Rect>> best(Rect r, int k)
     {

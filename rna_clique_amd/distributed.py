@@ -182,15 +182,17 @@ def dust_owners(sample_bases, shard_count):
     return owner
 
 
-def exchange_dust(eng, process_group=None):
+def exchange_dust(eng, process_group=None, force=False):
     """Every sample's DUST mask made once: this rank masks the samples
     dust_owners gives it, the masks are all-gathered (1 bit per base; 200 MB
     at C3) and each engine takes them (rc_set_dust_masks) instead of masking
-    its resident samples itself. A no-op without DUST or with one rank."""
+    its resident samples itself. A no-op without DUST or with one rank
+    (`force`: run the exchange on a one-rank group too -- the tests' way to
+    drive the device path on a one-GPU box)."""
     import torch
     import torch.distributed as dist
     W, R = world(process_group)
-    if W == 1 or getattr(eng, "dust", None) is None:
+    if (W == 1 and not force) or getattr(eng, "dust", None) is None:
         return
     owner = dust_owners(eng.bases, W)
     mine = [s for s in range(len(owner)) if owner[s] == R]

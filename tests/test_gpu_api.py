@@ -537,24 +537,28 @@ def _rccl_worker(port, q):
         from rna_clique_amd import distributed
         from rna_clique_amd.engine import Engine
         from rna_clique_amd.simulate import simulate
-        samples, _ = simulate(4, 100, seed=41)
+        samples, _ = simulate(4, 100, seed=41, polya=(0.5, 12, 40))
         eng = _load(Engine(device=0, shard_rank=0, shard_count=1), samples)
+        # the DUST masks over RCCL too (one rank owns them all): device
+        # buffers, all-gather, rc_set_dust_masks from the device
+        distributed.exchange_dust(eng, force=True)
         distributed.sharded_run(eng)        # RCCL branch: device export, all-gather, device import
-        q.put(eng.distance()[1].tobytes())
+        q.put((eng.distance()[1].tobytes(), eng.hsps(0, 1).tobytes(), eng.hsps(1, 0).tobytes()))
     finally:
         dist.destroy_process_group()
 
 
 def test_rccl_exchange_world1(native):
-    """exchange_edges over an RCCL process group (world 1 on the one GPU of
-    the test box: the device-to-device branch end to end)."""
+    """exchange_dust and exchange_edges over an RCCL process group (world 1 on
+    the one GPU of the test box: the device-to-device branches end to end)."""
     import socket
     import torch.multiprocessing as mp
     from rna_clique_amd.engine import Engine
     from rna_clique_amd.simulate import simulate
-    samples, _ = simulate(4, 100, seed=41)
+    samples, _ = simulate(4, 100, seed=41, polya=(0.5, 12, 40))
     ref = _load(Engine(device=0), samples)
     ref.run()
+    assert ref.dust_mask(0).any()
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -566,4 +570,4 @@ def test_rccl_exchange_world1(native):
     got = q.get(timeout=300)
     p.join(timeout=120)
     assert p.exitcode == 0
-    assert got == ref.distance()[1].tobytes()
+    assert got == (ref.distance()[1].tobytes(), ref.hsps(0, 1).tobytes(), ref.hsps(1, 0).tobytes())
