@@ -458,7 +458,12 @@ def main():
             "traffic_source": prof["file"] if prof else "no PMC profile of these sources (src_hash "
                                                        f"{src_hash()})",
             "kernel": "seed_kernel + extension kernels", "kernel_ms": round(avg_k, 3),
-            "bytes_per_launch": int(bytes_launch)}
+            "bytes_per_launch": int(bytes_launch),
+            # what achieved/frac are, and what actually binds these kernels
+            # (DESIGN.md §4): neither is at an HBM wall
+            "achieved_is": "SURVEY.md 8d algorithmic bytes (a model) / live kernel time",
+            "binding": {"seed_kernel": "latency: waves parked on memory and barriers (PMC SQ_WAIT_ANY)",
+                        "extend_rows_kernel": "VALU issue (see issue_extension)"}}
     if prof and prof.get("issue"):
         roof["issue_extension"] = issue_roofline(prof["issue"], tm["align_kernel_ms"])
     if cpu:
