@@ -2,7 +2,7 @@
 # each under its own time limit.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-D=gpurun_out/r04_final
+D=gpurun_out/${R04_TAG:-r04_final}
 mkdir -p $D
 rocm-smi --showproductname > $D/smi.txt 2>&1 || true
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1

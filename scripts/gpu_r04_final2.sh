@@ -5,7 +5,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-D=gpurun_out/r04_final
+D=gpurun_out/${R04_TAG:-r04_final}
 mkdir -p $D
 nproc > $D/nproc.txt; lscpu > $D/lscpu.txt 2>&1 || true
 timeout -k 10 600 python bench.py --config C3 --steps 10 --warmup 1 > $D/C3_bench.json 2> $D/C3_bench.err
