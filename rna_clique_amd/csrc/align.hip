@@ -1598,18 +1598,6 @@ __device__ __forceinline__ void lds_win2(uint32_t pa, uint32_t pb, uint64_t &wa,
     wa = lds_join(a01, a2, pa);
     wb = lds_join(b01, b2, pb);
 }
-__device__ __forceinline__ uint64_t lds_win1(uint32_t p)
-{
-    const uint32_t a = (p >> 2) & ~3u;
-    uint64_t w01;
-    uint32_t w2;
-    asm volatile("ds_read2_b32 %0, %2 offset1:1\n\t"
-                 "ds_read_b32 %1, %2 offset:8\n\t"
-                 "s_waitcnt lgkmcnt(0)"
-                 : "=&v"(w01), "=&v"(w2)
-                 : "v"(a));
-    return lds_join(w01, w2, p);
-}
 __device__ __forceinline__ uint64_t lds_diff(uint32_t pa, uint32_t pb)
 {
     uint64_t a, b;
@@ -1837,7 +1825,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
     const int lane = threadIdx.x & 63, rl = lane & (RW - 1), row = lane / RW;
     const int rs = threadIdx.x / RW;                      // row slot in the block
     const int k = rl - RC0;                               // this lane's diagonal
-    // two guard words in front: reversed staging reads up to 31 bases before an array
+    // two guard words in front (windows read from a word boundary before a position)
     uint64_t *stg = rstg + 2 + (size_t)rs * NA * sw;      // Q, T, Qr, Tr, [QM, TM, QMr, TMr]
     // absolute LDS base position of the row's Q array (the staging's LDS
     // offset: the low half of its generic address)
