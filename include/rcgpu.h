@@ -145,6 +145,8 @@ typedef struct rc_timing {
                                  their first HSP's box (more than one HSP) */
     double index_reused;      /* alignment tiles that reused the previous tile's 16-mer index and subject
                                  DUST masks (split tiles of one subject chunk) */
+    double ext_retries;       /* extend_kernel reruns after the HSP overflow buffer overflowed (the buffer
+                                 grows to fit; the row kernels' results are kept) */
 } rc_timing;
 
 void rc_default_opts(rc_opts *opts);

@@ -87,7 +87,8 @@ class RcTiming(ctypes.Structure):
         "reduce_ms", "total_ms", "seed_kernel_ms", "align_kernel_ms", "ext_steps",
         "ext_calls", "ext_fullband", "ext_deferred", "big_passes", "tiles", "dust_ms",
         "band_bound", "maxhsp_bound", "ext_second", "near_index", "reverse_seeds", "ext_slides", "ext_wide", "dev_bytes",
-        "dev_peak_bytes", "defer_length", "defer_gaveup", "defer_outside", "index_reused")]
+        "dev_peak_bytes", "defer_length", "defer_gaveup", "defer_outside", "index_reused",
+        "ext_retries")]
 
 
 assert HSP_DTYPE.itemsize == ctypes.sizeof(RcHsp)

@@ -2884,7 +2884,49 @@ int row_slot_words_max(bool amb)
 // seeds outside the first box; without the windowed kernel transcripts
 // longer than the row staging slot). The deferred count stays on the device:
 // the list launch reads it.
-void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_width, hipStream_t st)
+// extend_kernel over the searches the row kernels left (B.defer, and for
+// shared searches the reverse ones, B.defer_r)
+static void extend_lists(bool amb, const Db &db, const ExtParams &B, hipStream_t st)
+{
+    for (int dir = 0; dir < (B.share ? 2 : 1); dir++) {
+        ExtParams W3 = B;
+        W3.dir = dir;
+        if (dir) {
+            W3.defer = B.defer_r;
+            W3.defer_count = B.defer_r_count;
+        }
+        if (amb) {
+            auto kern = extend_kernel<true>;
+            hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W3);
+        } else {
+            auto kern = extend_kernel<false>;
+            hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W3);
+        }
+    }
+}
+
+// The extend_kernel launches of launch_extend_rows alone: after it ran with
+// lists = false, or again after the HSP overflow buffer overflowed (only
+// extend_kernel writes it; the row kernels' results, first_finish_kernel's
+// and the defer lists stand)
+void launch_extend_retry(bool amb, const Db &db, const ExtParams &P, hipStream_t st)
+{
+    if (P.n_cand == 0) return;
+    ExtParams W = P;
+    W.list = nullptr;
+    W.list_n = nullptr;
+    W.resume = nullptr;
+    const char *r64 = getenv("RC_ROW64");
+    if (!P.share && r64 && atoi(r64)) {
+        W.defer = P.defer2;
+        W.defer_count = P.defer2_count;
+    }
+    extend_lists(amb, db, W, st);
+}
+
+// lists = false: up to first_finish_kernel only (the caller sizes the HSP
+// overflow buffer from the defer counts, then launch_extend_retry)
+void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_width, hipStream_t st, bool lists)
 {
     if (P.n_cand == 0) return;
     (void)row_width;
@@ -2895,21 +2937,7 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
     // them and only their 64-lane passes read them
     W.resume = nullptr;
     auto extend_lists = [&](const ExtParams &B) {
-        for (int dir = 0; dir < (B.share ? 2 : 1); dir++) {
-            ExtParams W3 = B;
-            W3.dir = dir;
-            if (dir) {
-                W3.defer = P.defer_r;
-                W3.defer_count = P.defer_r_count;
-            }
-            if (amb) {
-                auto kern = extend_kernel<true>;
-                hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W3);
-            } else {
-                auto kern = extend_kernel<false>;
-                hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, 0)), dim3(EBLOCK), 0, st, db, W3);
-            }
-        }
+        if (lists) rcg::extend_lists(amb, db, B, st);
     };
     uint64_t g = (P.n_cand + 255) / 256;
     if (g > 65536) g = 65536;

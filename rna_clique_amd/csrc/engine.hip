@@ -60,7 +60,8 @@ void launch_dust(bool, uint64_t, uint64_t, const uint64_t *, const uint64_t *, c
 uint32_t dust_scratch_words(uint32_t);
 uint64_t dust_event_words(uint32_t);
 void launch_extend(bool, const Db &, const ExtParams &, hipStream_t);
-void launch_extend_rows(bool, const Db &, const ExtParams &, int, hipStream_t);
+void launch_extend_rows(bool, const Db &, const ExtParams &, int, hipStream_t, bool);
+void launch_extend_retry(bool, const Db &, const ExtParams &, hipStream_t);
 int row_slot_words_max(bool amb);
 void launch_group(const GroupParams &, int, hipStream_t);
 
@@ -1691,7 +1692,9 @@ static int align_tile(rc_engine *e, int ti)
             }
         e->seed_cap = std::max<uint64_t>(e->seed_cap, nb * 16 / NSHARD + 4096);
         e->cand_cap = std::max<uint64_t>(e->cand_cap, nb * 2 / NSHARD + 1024);
-        e->ovf_cap = std::max<uint64_t>(e->ovf_cap, nb / 4 + 1024);
+        // (RC_OVF_CAP0: a smaller first guess, for tests of the overflow retry)
+        const char *oc = getenv("RC_OVF_CAP0");
+        e->ovf_cap = std::max<uint64_t>(e->ovf_cap, oc ? (uint64_t)std::max(1, atoi(oc)) : nb / 4 + 1024);
     }
     Db db = make_db(e);
     Index ix;
@@ -1883,10 +1886,16 @@ static int align_tile(rc_engine *e, int ti)
     for (int attempt = 0;; attempt++) {
         if (attempt == 4) return fail(RC_E_NOMEM, "HSP overflow buffer kept overflowing");
         CHK(e->d_ovf.ensure(e->ovf_cap));
-        HIPCHK(hipMemsetAsync(e->d_count.p, 0, 12 * sizeof(unsigned long long), e->st));
-        HIPCHK(hipMemsetAsync(e->d_count.p + 14, 0, 2 * sizeof(unsigned long long), e->st));
-        HIPCHK(hipMemsetAsync(e->d_count.p + 17, 0, 2 * sizeof(unsigned long long), e->st));
-        HIPCHK(hipMemsetAsync(e->d_count.p + 20, 0, 7 * sizeof(unsigned long long), e->st));
+        if (attempt == 0) {
+            HIPCHK(hipMemsetAsync(e->d_count.p, 0, 12 * sizeof(unsigned long long), e->st));
+            HIPCHK(hipMemsetAsync(e->d_count.p + 14, 0, 2 * sizeof(unsigned long long), e->st));
+            HIPCHK(hipMemsetAsync(e->d_count.p + 17, 0, 2 * sizeof(unsigned long long), e->st));
+            HIPCHK(hipMemsetAsync(e->d_count.p + 20, 0, 7 * sizeof(unsigned long long), e->st));
+        } else {
+            // a retry redoes extend_kernel only: its overflow count restarts,
+            // every other counter and list stands
+            HIPCHK(hipMemsetAsync(e->d_count.p, 0, sizeof(unsigned long long), e->st));
+        }
         HIPCHK(hipMemsetAsync(e->d_status.p, 0, 4 * sizeof(unsigned int), e->st));
         ExtParams X{};
         X.xdrop = e->o.xdrop_half;
@@ -1960,12 +1969,36 @@ static int align_tile(rc_engine *e, int ti)
             const char *rv = getenv("RC_REUSE");   // 0: extend_kernel redoes every search's first seed
             X.reuse_first = rv ? atoi(rv) : 1;
         }
-        HIPCHK(hipEventRecord(e->ev[10], e->st));
-        {
+        if (attempt == 0) {
+            HIPCHK(hipEventRecord(e->ev[10], e->st));
             // sub-band row width of the extension (16 or 32 diagonals); RC_ROW_WIDTH overrides
             const char *rwv = getenv("RC_ROW_WIDTH");
             const int rw = rwv ? atoi(rwv) : 32;
-            launch_extend_rows(e->has_amb, db, X, rw, e->st);
+            launch_extend_rows(e->has_amb, db, X, rw, e->st, false);
+            HIPCHK(hipGetLastError());
+            // only the searches the row kernels left (defer lists) can have
+            // more than one HSP, at most MAX_HSP - 1 more each: the overflow
+            // buffer at twice their count (about 1.1 more each at C3v), so a
+            // first run rarely redoes extend_kernel
+            unsigned long long dn[3] = {0, 0, 0};
+            HIPCHK(hipMemcpyAsync(&dn[0], X.defer_count, sizeof dn[0], hipMemcpyDeviceToHost, e->st));
+            HIPCHK(hipMemcpyAsync(&dn[1], e->d_count.p + 17, sizeof dn[1], hipMemcpyDeviceToHost, e->st));
+            if (X.defer2_count)
+                HIPCHK(hipMemcpyAsync(&dn[2], X.defer2_count, sizeof dn[2], hipMemcpyDeviceToHost, e->st));
+            HIPCHK(hipStreamSynchronize(e->st));
+            const uint64_t want = std::min<uint64_t>(2 * (dn[0] + dn[1] + dn[2]), (uint64_t)(MAX_HSP - 1) *
+                                                     (dn[0] + dn[1] + dn[2])) + 1024;
+            if (want > e->ovf_cap && !getenv("RC_OVF_CAP0")) {
+                e->ovf_cap = want;
+                CHK(e->d_ovf.ensure(e->ovf_cap));
+                X.ovf = e->d_ovf.p;
+                X.ovf_cap = e->ovf_cap;
+            }
+            launch_extend_retry(e->has_amb, db, X, e->st);
+        } else {
+            X.counters = nullptr;   // (the first attempt counted this work)
+            launch_extend_retry(e->has_amb, db, X, e->st);
+            e->tm.ext_retries += 1.0;
         }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e->ev[11], e->st));

@@ -160,6 +160,27 @@ def test_simulated_parity_variants(native):
     assert st["components"] > st["ideal_components"] > 0
 
 
+@pytest.mark.parametrize("share", ["1", "0"])
+def test_hsp_overflow_retry(native, monkeypatch, share):
+    """A first HSP overflow buffer far too small (RC_OVF_CAP0): the engine
+    redoes only extend_kernel with a larger one (the row kernels' results and
+    the defer lists stand) -- same HSPs as the oracle, same statistics as a
+    run without the retry."""
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(4, 150, seed=23, p_iso2=0.2, indel_rate=0.004, p_revcomp=0.5, p_paralog=0.1)
+    monkeypatch.setenv("RC_SHARE", share)
+    ref = _run_sim(samples)
+    want = ref.stats()
+    ref.close()
+    monkeypatch.setenv("RC_OVF_CAP0", "8")
+    eng = _run_sim(samples)
+    assert eng.timings()["ext_retries"] >= 1
+    assert eng.stats() == want
+    msgs, summary = full_check(eng, samples)
+    assert not msgs, "\n".join(msgs[:10])
+    assert summary["hsps"] > 0
+
+
 def test_simulated_parity_large_index(native):
     """More than 2^20 indexed positions: the onesweep-sorted index (smaller
     ones take rocPRIM's merge-sort path, sorted on all 64 bits)."""
