@@ -193,3 +193,146 @@ def test_c5_fits_hbm_per_rank():
     # sharding divides the resident bases and the HSP store
     one = distributed.hbm_footprint(bases, [genes] * n, 1)[0]
     assert max(fp) < 0.65 * one
+
+
+class OracleShardEngine:
+    """The engine's sharded surface computed on the CPU oracles, so that the
+    N > 1 host path runs on real alignments: its pairs from plan_pairs, DUST
+    masks made by their owners and exchanged (each rank checks what it
+    receives against its own), both directed searches and the gene matches
+    table of each owned pair, the edges all-gathered, then the graph phase
+    (components, ideal nodes) on every rank's edges and this rank's pair sums.
+    Edge records are this stand-in's own 20-byte layout (the exchange moves
+    opaque records)."""
+
+    def __init__(self, samples, rank, world, dust=(20, 64, 1)):
+        from oracle.align import OracleDB
+        from rna_clique_amd import distributed
+        self.samples = samples
+        self.names = [s.name for s in samples]
+        self.db = OracleDB(samples)
+        self.bases = [int(s.seq.size) for s in samples]
+        self.dust = dust
+        order, first = distributed.plan_pairs(self.bases, world)
+        self.pairs = [tuple(int(x) for x in p) for p in order[int(first[rank]):int(first[rank + 1])]]
+        self.made, self.received_ok = [], None
+        self.edges, self.sums = [], {}
+
+    @staticmethod
+    def edge_record_size():
+        return 20
+
+    def _mask_words(self, s):
+        m = self.db.dust_mask(s, *self.dust).astype(np.uint8)
+        m = np.concatenate([m, np.zeros(-m.size % 64, np.uint8)])
+        return np.packbits(m, bitorder="little").view(np.uint64)
+
+    def dust_masks(self, samples, out=None):
+        assert out is None
+        self.made = list(samples)
+        return np.concatenate([self._mask_words(s) for s in samples] + [np.zeros(0, np.uint64)])
+
+    def set_dust_masks(self, samples, bits):
+        want = np.concatenate([self._mask_words(s) for s in samples] + [np.zeros(0, np.uint64)])
+        self.received_ok = np.array_equal(np.asarray(bits, dtype=np.uint64), want)
+
+    def align(self):
+        from oracle import post_oracle
+        from oracle.parity import hits_for_post
+        for a, b in self.pairs:
+            ora = {(q, s): self.db.align(q, s, 28, 108, 1e-99, False, self.dust) for q, s in ((a, b), (b, a))}
+            hits = hits_for_post(self.samples, self.db, ora, self.names)
+            t1, t2 = self.names[a], self.names[b]
+            rows = post_oracle.match_table(post_oracle.parse_hits(hits[(t2, t1)], post_oracle.default_parse_id),
+                                           post_oracle.parse_hits(hits[(t1, t2)], post_oracle.default_parse_id))
+            self.sums[(a, b)] = rows
+            for r in rows:
+                self.edges.append((a, r["sgene"], b, r["qgene"]))
+
+    def finish(self):
+        pass
+
+    def local_edge_count(self):
+        return len(self.edges)
+
+    def export_edges(self, out=None):
+        assert out is None
+        rec = np.array([e + (0,) for e in self.edges], dtype=np.int32).reshape(-1, 5)
+        return rec.view(np.uint8).reshape(-1)
+
+    def import_edges(self, buf, n=None):
+        from oracle import post_oracle
+        rec = np.asarray(buf, dtype=np.uint8).view(np.int32).reshape(-1, 5)
+        nodes, edges = set(), set()
+        for sa, ga, sb, gb, _ in rec.tolist():
+            u, v = (self.names[sa], ga), (self.names[sb], gb)
+            nodes |= {u, v}
+            edges.add(tuple(sorted((u, v))))
+        valid = post_oracle.ideal_nodes(nodes, edges)
+        self.sums = {(a, b): post_oracle.pair_sums(self.names[a], self.names[b], rows, valid)
+                     for (a, b), rows in self.sums.items()}
+
+
+def _oracle_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rna_clique_amd import distributed
+        from rna_clique_amd.simulate import simulate
+        samples, _ = simulate(4, 40, seed=77, p_iso2=0.2, indel_rate=0.003, polya=(0.3, 10, 40))
+        eng = OracleShardEngine(samples, rank, world)
+        distributed.sharded_run(eng)
+        # every rank's pair sums to every rank (32-byte records)
+        local = np.array([[a, b, n_, d_] for (a, b), (n_, d_) in sorted(eng.sums.items())],
+                         dtype=np.int64).reshape(-1, 4)
+        allt, total = distributed.all_gather_records(torch.from_numpy(local.view(np.uint8).reshape(-1)), 32)
+        sums = allt.numpy()[:total * 32].view(np.int64).reshape(-1, 4).tolist()
+        q.put((rank, eng.pairs, eng.made, eng.received_ok, sums))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_oracle_shards_match_one_process():
+    """Two gloo ranks, each computing its planned pairs on the CPU oracle:
+    after the DUST-mask exchange, the edge all-gather and the graph phase on
+    every rank's edges, the ranks' pair sums give the one-process oracle's
+    distance matrix exactly (the real-data counterpart of the FakeShardEngine
+    tests; the GPU engine's own 2-rank path is test_gpu_api.py's RCCL test)."""
+    from oracle import post_oracle
+    from oracle.align import OracleDB
+    from oracle.parity import hits_for_post, oracle_all_hsps
+    from rna_clique_amd import distributed
+    from rna_clique_amd.simulate import simulate
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_oracle_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in procs:
+        r, pairs, made, ok, sums = q.get(timeout=300)
+        got[r] = (pairs, made, ok, sums)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    samples, _ = simulate(4, 40, seed=77, p_iso2=0.2, indel_rate=0.003, polya=(0.3, 10, 40))
+    names = [s.name for s in samples]
+    bases = [int(s.seq.size) for s in samples]
+    # the plan: every pair on exactly one rank; every mask made once, received intact
+    assert sorted(got[0][0] + got[1][0]) == [(a, b) for a in range(4) for b in range(a + 1, 4)]
+    owner = distributed.dust_owners(bases, 2)
+    assert sorted(got[0][1] + got[1][1]) == sorted(s for s in range(4) if owner[s] >= 0)
+    assert got[0][2] and got[1][2]
+    assert got[0][3] == got[1][3] and len(got[0][3]) == 6
+    # against the one-process oracle path
+    db = OracleDB(samples)
+    hits = hits_for_post(samples, db, oracle_all_hsps(db, 4, dust=(20, 64, 1), threads=4), names)
+    res = post_oracle.run_pipeline(names, hits, post_oracle.default_parse_id)
+    sums = {(names[a], names[b]): (n_, d_) for a, b, n_, d_ in got[0][3]}
+    assert sums == res["sums"]
+    lab_s, mat_s = post_oracle.distance_matrix(names, sums)
+    lab_o, mat_o = post_oracle.distance_matrix(names, res["sums"])
+    assert lab_s == lab_o and mat_s == mat_o
+    assert len(res["valid"]) > 0
