@@ -34,3 +34,34 @@ def native():
     build_native()
     from rna_clique_amd import _native
     return _native.lib()
+
+
+@pytest.fixture(autouse=True)
+def _gpu_heartbeat(request):
+    """GPU tests: a line appended to gpurun_out/heartbeat.log every 30 s while
+    the test runs. A GPU run is taken to be hung after 3 minutes with nothing
+    new on stdout, stderr or under gpurun_out/, and pytest prints nothing
+    during a test (-q) -- the full-size config tests (simulation, engine,
+    oracle pairs) run longer than that."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    import threading
+    import time
+    stop = threading.Event()
+    name = request.node.nodeid
+
+    def beat():
+        t0 = time.time()
+        os.makedirs("gpurun_out", exist_ok=True)
+        while not stop.wait(30):
+            with open(os.path.join("gpurun_out", "heartbeat.log"), "a") as f:
+                f.write(f"{time.strftime('%H:%M:%S')} {name}: {time.time() - t0:.0f} s\n")
+
+    t = threading.Thread(target=beat, daemon=True)
+    t.start()
+    try:
+        yield
+    finally:
+        stop.set()
+        t.join(timeout=5)
