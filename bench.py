@@ -139,6 +139,20 @@ def issue_roofline(iss, align_kernel_ms):
             "kernel_ms_source": iss.get("kernel_ms_source") if own else "live extension kernels (HIP events)"}
 
 
+def binding(prof, issue):
+    """What the PMC profile of these very sources says binds the two hot
+    kernels: the seed kernel's share of wave cycles spent waiting, the row
+    kernel's VALU issue fraction. Only written when such a profile exists."""
+    out = {}
+    sk = prof.get("kernels", {}).get("seed_kernel", {})
+    if sk.get("SQ_WAVE_CYCLES"):
+        w = sk["SQ_WAIT_ANY"] / sk["SQ_WAVE_CYCLES"]
+        out["seed_kernel"] = f"waves wait {100 * w:.0f}% of their cycles (SQ_WAIT_ANY / SQ_WAVE_CYCLES, {prof['file']})"
+    if issue:
+        out["extend_rows_kernel"] = f"VALU issue at {100 * issue['frac']:.0f}% of peak (issue_extension)"
+    return out
+
+
 _CPU_SAMPLES = None
 
 
@@ -317,9 +331,16 @@ def shard_emulation(args):
         eng.add_sample(s.name, s.seq if i in need else None, s.tx_offsets, s.gene, s.iso)
     del samples
     eng.upload()
+    cold = []   # the warmup calls: the first one allocates every device buffer
     for _ in range(args.warmup):
+        t0 = time.perf_counter()
         eng.align()
         eng.finish()
+        cold.append(round(time.perf_counter() - t0, 3))
+        tmc = eng.timings()
+        cold_phases = {k: round(tmc[k], 1) for k in ("load_ms", "align_wall_ms", "host_wait_ms", "index_ms",
+                                                      "seed_kernel_ms", "align_kernel_ms", "dust_ms")}
+        print(json.dumps({"warmup_s": cold[-1], "phases_ms": cold_phases}), flush=True)
     times = []
     for _ in range(args.steps):
         t0 = time.perf_counter()
@@ -338,6 +359,7 @@ def shard_emulation(args):
             "total_pairs": len(order), "resident_samples": len(need),
             "resident_bases": int(sum(bases[i] for i in need)),
             "value": round(my_pairs / dt, 3), "unit": "sample-pairs/s", "s_per_step": round(dt, 3),
+            "cold_s": cold, "warm_s": [round(x, 3) for x in times],
             "steps": args.steps, "warmup": args.warmup,
             "projected_job_pairs_per_s_if_balanced": round(len(order) / dt, 1),
             "hbm_used_gb": round((free0 - free1) / 1e9, 2), "hbm_total_gb": round(total / 1e9, 1),
@@ -461,11 +483,11 @@ def main():
             "bytes_per_launch": int(bytes_launch),
             # what achieved/frac are, and what actually binds these kernels
             # (DESIGN.md §4): neither is at an HBM wall
-            "achieved_is": "SURVEY.md 8d algorithmic bytes (a model) / live kernel time",
-            "binding": {"seed_kernel": "latency: waves parked on memory and barriers (PMC SQ_WAIT_ANY)",
-                        "extend_rows_kernel": "VALU issue (see issue_extension)"}}
+            "achieved_is": "SURVEY.md 8d algorithmic bytes (a model) / live kernel time"}
     if prof and prof.get("issue"):
         roof["issue_extension"] = issue_roofline(prof["issue"], tm["align_kernel_ms"])
+    if prof:
+        roof["binding"] = binding(prof, roof.get("issue_extension"))
     if cpu:
         cpu["gpu_speedup"] = round(value / cpu["value"], 1)
     line = {

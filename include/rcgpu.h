@@ -147,6 +147,9 @@ typedef struct rc_timing {
                                  DUST masks (split tiles of one subject chunk) */
     double ext_retries;       /* extend_kernel reruns after the HSP overflow buffer overflowed (the buffer
                                  grows to fit; the row kernels' results are kept) */
+    double load_ms;           /* host wall time loading alignment tiles (tile tables, working copy) */
+    double align_wall_ms;     /* host wall time of rc_align (every tile, kernels and host work) */
+    double host_wait_ms;      /* host wall time blocked on the engine's stream inside rc_align */
 } rc_timing;
 
 void rc_default_opts(rc_opts *opts);
@@ -205,6 +208,16 @@ int rc_finish(rc_engine *eng);
 uint64_t rc_edge_record_size(void);
 int rc_export_edges(rc_engine *eng, void *buf, uint64_t cap, uint64_t *n, int on_device);
 int rc_import_edges(rc_engine *eng, const void *buf, uint64_t n, int on_device);
+/* The same import from `parts` blocks: block r starts at record r * stride of
+ * buf and holds counts[r] records (an all-gather's padded receive buffer, taken
+ * as it is). Device records are range-checked on the device (RC_E_ARG). */
+int rc_import_edge_parts(rc_engine *eng, const void *buf, const uint64_t *counts, int32_t parts, uint64_t stride,
+                         int on_device);
+/* Free the alignment working set of a finished run (tile copies, 16-mer
+ * indexes, seeds, candidates, extension scratch) before the edge exchange;
+ * rows, HSPs, edges and inputs stay, and the next rc_align allocates the rest
+ * again. rc_dust_mask needs a new rc_align afterwards. */
+int rc_trim(rc_engine *eng);
 /* Graph-only mode (SampleSimilarity(graph, comparison_dfs), filtered_distance.py:
  * 162-169, and its from_filenames resume path :291-317): on a fresh engine
  * whose samples carry one zero-length transcript per gene (seq may be NULL),
@@ -271,8 +284,10 @@ int rc_dust_mask(rc_engine *eng, int32_t s, uint8_t *buf, uint64_t cap, uint64_t
  * base 64 w + b of the sample's concatenated transcripts (1 = masked); bits
  * past its last base 0.
  * rc_dust_masks: the masks of resident samples, computed in a pass of their
- * own (results of an earlier rc_align are dropped: call it before rc_align);
- * out == NULL queries n_words. `on_device`: out is a device pointer.
+ * own; out == NULL queries n_words. `on_device`: out is a device pointer.
+ * Results of an earlier rc_align / rc_finish stay valid (they do not depend
+ * on the loaded tile's tables); rc_dust_mask then reads this pass's tile and
+ * fails with RC_E_STATE when the pass used a tile of its own.
  * rc_set_dust_masks: masks for these samples (replacing any given before;
  * n = 0 clears them): rc_align copies them into its tiles instead of running
  * DUST on those samples. They must come from engines with the same DUST

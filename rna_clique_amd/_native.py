@@ -88,7 +88,7 @@ class RcTiming(ctypes.Structure):
         "ext_calls", "ext_fullband", "ext_deferred", "big_passes", "tiles", "dust_ms",
         "band_bound", "maxhsp_bound", "ext_second", "near_index", "reverse_seeds", "ext_slides", "ext_wide", "dev_bytes",
         "dev_peak_bytes", "defer_length", "defer_gaveup", "defer_outside", "index_reused",
-        "ext_retries")]
+        "ext_retries", "load_ms", "align_wall_ms", "host_wait_ms")]
 
 
 assert HSP_DTYPE.itemsize == ctypes.sizeof(RcHsp)
@@ -114,6 +114,8 @@ SIGNATURES = {
     "rc_edge_record_size": (ctypes.c_uint64, []),
     "rc_export_edges": (ctypes.c_int, [VP, VP, ctypes.c_uint64, P(ctypes.c_uint64), ctypes.c_int]),
     "rc_import_edges": (ctypes.c_int, [VP, VP, ctypes.c_uint64, ctypes.c_int]),
+    "rc_import_edge_parts": (ctypes.c_int, [VP, VP, VP, ctypes.c_int32, ctypes.c_uint64, ctypes.c_int]),
+    "rc_trim": (ctypes.c_int, [VP]),
     "rc_set_sample_count": (ctypes.c_int, [VP, ctypes.c_int32]),
     "rc_shard_pairs": (ctypes.c_int, [VP, P(ctypes.c_int64), P(ctypes.c_int64)]),
     "rc_plan_shards": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.c_int32, VP]),

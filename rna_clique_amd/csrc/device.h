@@ -66,6 +66,16 @@ struct DRow {
 struct IsoRec {
     uint32_t start, len, gtx, pad;
 };
+// One sample of an alignment tile (load_tile -> launch_tile_tables): its
+// transcripts [tx0, tx0 + ntx) (global ids) sit at tile position pos; their
+// slots in the tile's transcript list (ttx0) and, for an indexed (subject)
+// sample, in the index list (itx0, else ~0u) with its first k-mer slot kbase.
+// pad_bit: the tile position where its bases end when padding follows (a
+// transcript-start bit there stops DUST runs), else ~0.
+struct TileSeg {
+    uint64_t pos, kbase, pad_bit;
+    uint32_t tx0, ntx, ttx0, itx0;
+};
 struct Db {
     const uint64_t *F, *RC;     // 2-bit packed forward / reverse-complement
     const uint64_t *AF, *ARC;   // ambiguity masks (2 bits per base) or null

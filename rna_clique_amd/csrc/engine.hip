@@ -50,6 +50,10 @@ uint64_t os_gen_tile_words(uint64_t n);
 void os_fill_hist(const TxInfo *tx, uint32_t n_tx, const uint64_t *F, const uint64_t *koff, uint64_t *ent,
                   uint64_t n, uint32_t *scratch, hipStream_t st);
 void launch_tx_masked(const TxInfo *, uint32_t, const uint64_t *, uint8_t *, hipStream_t);
+void launch_edge_check(const DEdge *, uint64_t, uint32_t, uint64_t, unsigned int *, hipStream_t);
+void launch_tile_tables(const TileSeg *, uint32_t, uint32_t, const uint64_t *, const uint64_t *, TxInfo *, TxInfo *,
+                        uint32_t *, TxInfo *, uint64_t *, uint32_t, uint64_t, uint64_t *, IsoRec *, uint64_t,
+                        const uint64_t *, PosTx *, uint64_t, hipStream_t);
 void launch_near_fill(bool, const TxInfo *, uint32_t, const uint8_t *, const uint64_t *, const uint64_t *,
                       const uint64_t *, uint64_t *, uint64_t, unsigned long long *, hipStream_t);
 void launch_seed(bool, const Db &, const Index &, const SeedParams &, hipStream_t);
@@ -300,8 +304,11 @@ struct rc_engine {
     uint64_t n_items = 0;
     int index_bits = 16;
     uint64_t n_index = 0;               // entries of the loaded tile's index
-    std::vector<uint64_t> h_koff;       // closed-form k-mer slot prefix per indexed tile transcript
-    std::vector<TxInfo> h_tx;           // every transcript; start = position in the loaded tile
+    uint64_t tile_npos = 0;             // 16-mer positions of the loaded tile's indexed transcripts
+    std::vector<TxInfo> h_tx;           // every transcript (start 0: the device table holds tile starts)
+    std::vector<uint64_t> sample_kmers; // 16-mer positions of each sample's transcripts
+    std::vector<TileSeg> h_segs;        // the loaded tile's samples (load_tile)
+    std::vector<uint64_t> h_spos, h_send;
 
     // tiles of this shard (plan_tiles) and the one whose tables are loaded
     struct Tile {
@@ -349,6 +356,10 @@ struct rc_engine {
     // device buffers
     DBuf<uint8_t> d_ascii, d_tile_ascii;
     DBuf<TxInfo> d_tile_tx, d_tile_itx;
+    DBuf<uint32_t> d_tile_gid;          // global id of each tile transcript
+    DBuf<TileSeg> d_tile_segs;
+    DBuf<uint64_t> d_tile_send, d_tx_rel, d_kpre;   // tile sample ends; per transcript: start in its sample,
+                                                    // 16-mer slots of its sample's transcripts before it
     DBuf<uint64_t> d_F, d_RC, d_AF, d_ARC;
     DBuf<TxInfo> d_tx;
     DBuf<IsoRec> d_giso;
@@ -360,7 +371,6 @@ struct rc_engine {
     DBuf<uint8_t> d_tile_masked;
     DBuf<uint64_t> d_ment, d_ment2;
     DBuf<uint32_t> d_mbucket;
-    std::vector<uint32_t> tile_gid;
     int mindex_bits = 16;
     uint64_t n_mindex = 0, mnear_cap = 0;
     DBuf<LSeed> d_rseeds;
@@ -449,6 +459,20 @@ struct rc_engine {
 };
 
 static int set_device(rc_engine *e) { HIPCHK(hipSetDevice(e->o.device)); return RC_OK; }
+
+static double wall_ms()
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// the alignment's blocking waits on the engine's stream (rc_timing.host_wait_ms)
+static int wait_st(rc_engine *e)
+{
+    const double t0 = wall_ms();
+    HIPCHK(hipStreamSynchronize(e->st));
+    e->tm.host_wait_ms += wall_ms() - t0;
+    return RC_OK;
+}
 
 // Both directed searches of a pair from one candidate set (query = the lower
 // sample), unless spec 5b or RC_SHARE=0 (one after the other)
@@ -812,6 +836,26 @@ static int upload(rc_engine *e)
     }
     CHK(up(e->d_tx, e->h_tx));
     {
+        // per transcript: its start within its sample and the 16-mer slots of
+        // the sample's transcripts before it (the tile tables' inputs)
+        std::vector<uint64_t> rel(n_tx), kpre(n_tx);
+        e->sample_kmers.assign(N, 0);
+        for (int si = 0; si < N; si++) {
+            const SampleRec &S = e->samples[si];
+            uint64_t k = 0;
+            for (uint32_t t = S.tx_begin; t < S.tx_begin + S.n_tx; t++) {
+                rel[t] = e->tx_start[t] - S.base;
+                kpre[t] = k;
+                const int64_t L = (int64_t)e->h_tx[t].len;
+                k += (uint64_t)(L >= W16 ? L - W16 + 1 : 0);
+            }
+            e->sample_kmers[si] = k;
+        }
+        CHK(up(e->d_tx_rel, rel));
+        CHK(up(e->d_kpre, kpre));
+        HIPCHK(hipStreamSynchronize(e->st));   // (rel, kpre are about to go)
+    }
+    {
         std::vector<IsoRec> giso(e->gene_tx.size());
         for (size_t k = 0; k < giso.size(); k++) {
             const TxInfo &x = e->h_tx[e->gene_tx[k]];
@@ -987,7 +1031,6 @@ static int load_tile(rc_engine *e, int ti)
 {
     const rc_engine::Tile &T = e->tiles[ti];
     const int N = (int)e->samples.size();
-    const uint32_t n_tx = (uint32_t)e->tx_sample.size();
     e->tile_pos.assign(N + 1, 0);
     std::vector<char> in(N, 0);
     for (int s : T.samples) in[s] = 1;
@@ -1010,15 +1053,6 @@ static int load_tile(rc_engine *e, int ti)
         if (e->samples[s].resident && e->samples[s].nbases && !in[s]) direct = false;
     const uint64_t total = pos;
     if (total >= (1ull << 32)) return fail(RC_E_LIMIT, "a tile of more than 2^32 bases");
-    // sample ranges, monotone over all N + 1 (a sample outside the tile is empty)
-    std::vector<uint64_t> spos(N + 1);
-    {
-        uint64_t next = total;
-        for (int s = N; s >= 0; s--) {
-            if (s < N && in[s]) next = e->tile_pos[s];
-            spos[s] = next;
-        }
-    }
     e->tile_total = total;
     e->tile_direct = direct;
     // the 16-mer index holds the tile's subject samples only: the b of each
@@ -1030,73 +1064,73 @@ static int load_tile(rc_engine *e, int ti)
         subj[pr.second] = 1;
         if (!share && !e->o.symmetric) subj[pr.first] = 1;
     }
-    auto up = [&](auto &buf, const auto &vec) -> int {
-        using Tv = typename std::remove_reference<decltype(vec)>::type::value_type;
-        CHK(buf.ensure(vec.size()));
-        if (!vec.empty())
-            HIPCHK(hipMemcpyAsync(buf.p, vec.data(), vec.size() * sizeof(Tv), hipMemcpyHostToDevice, e->st));
-        return RC_OK;
-    };
-    // transcript starts in the tile; the tile's transcripts (index) with their
-    // closed-form k-mer slots; blocks of positions -> transcript
-    std::vector<TxInfo> ttx, itx;
-    std::vector<uint32_t> gid;
-    std::vector<uint64_t> koff(1, 0);
-    std::vector<PosTx> pos_tx((total >> POS_TX_SHIFT) + 2, PosTx{0, 0, 0, 0});
-    std::vector<uint64_t> txb((total >> 6) + 4, 0);
-    auto setbit = [&](uint64_t p) {
-        const uint64_t q = p + 64;
-        txb[q >> 6] |= 1ull << (q & 63);
-    };
+    // Per tile sample one TileSeg; the device builds every per-transcript and
+    // per-base table from them (launch_tile_tables): transcript starts in the
+    // tile, the tile's transcripts and the index's with their closed-form
+    // k-mer slots, the transcript-start bits and the position -> transcript
+    // blocks. The host keeps O(samples) bookkeeping only.
+    auto &segs = e->h_segs;
+    auto &spos = e->h_spos;   // sample ranges, monotone over all N + 1 (a sample outside the tile is empty)
+    auto &send = e->h_send;   // one past each tile sample's padded range (0: not in the tile)
+    segs.clear();
+    spos.assign(N + 1, total);
+    send.assign(N, 0);
+    {
+        uint64_t next = total;
+        for (int s = N; s >= 0; s--) {
+            if (s < N && in[s]) next = e->tile_pos[s];
+            spos[s] = next;
+        }
+    }
+    uint32_t n_ttx = 0, n_itx = 0;
+    uint64_t npos = 0;
     e->tile_tx_first.assign(N + 1, 0);
     for (int s = 0; s < N; s++) {
-        e->tile_tx_first[s] = (uint32_t)ttx.size();
+        e->tile_tx_first[s] = n_ttx;
         if (!in[s]) continue;
         const SampleRec &S = e->samples[s];
-        const uint64_t p0 = e->tile_pos[s];
-        for (uint32_t t = S.tx_begin; t < S.tx_begin + S.n_tx; t++) {
-            const uint64_t st = p0 + (e->tx_start[t] - S.base);
-            e->h_tx[t].start = st;
-            ttx.push_back(e->h_tx[t]);
-            gid.push_back(t);
-            if (subj[s]) {
-                itx.push_back(e->h_tx[t]);
-                const int64_t L = (int64_t)e->h_tx[t].len;
-                koff.push_back(koff.back() + (uint64_t)(L >= W16 ? L - W16 + 1 : 0));
-            }
-            setbit(st);
-        }
-        // the sample's padding is a boundary too (DUST runs end there)
-        if (S.nbases < align_up(S.nbases)) setbit(p0 + S.nbases);
-        // position blocks of this sample -> its transcripts
-        uint32_t t = S.tx_begin;
-        for (uint64_t b = p0 >> POS_TX_SHIFT; b < (p0 + align_up(S.nbases)) >> POS_TX_SHIFT; b++) {
-            const uint64_t p = b << POS_TX_SHIFT;
-            while (t + 1 < S.tx_begin + S.n_tx && p0 + (e->tx_start[t + 1] - S.base) <= p) t++;
-            pos_tx[b] = PosTx{t, (uint32_t)e->h_tx[t].start, e->h_tx[t].len, e->h_tx[t].sample};
+        send[s] = e->tile_pos[s] + align_up(S.nbases);
+        if (!S.n_tx) continue;
+        TileSeg g;
+        g.pos = e->tile_pos[s];
+        g.kbase = npos;
+        g.pad_bit = S.nbases < align_up(S.nbases) ? e->tile_pos[s] + S.nbases : ~0ull;
+        g.tx0 = S.tx_begin;
+        g.ntx = S.n_tx;
+        g.ttx0 = n_ttx;
+        g.itx0 = subj[s] ? n_itx : ~0u;
+        segs.push_back(g);
+        n_ttx += S.n_tx;
+        if (subj[s]) {
+            n_itx += S.n_tx;
+            npos += e->sample_kmers[s];
         }
     }
-    e->tile_tx_first[N] = (uint32_t)ttx.size();
-    if (koff.back() > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "more than 2^32 seed positions in a tile");
-    CHK(up(e->d_tx, e->h_tx));
-    {
-        std::vector<IsoRec> giso(e->gene_tx.size());
-        for (size_t k = 0; k < giso.size(); k++) {
-            const TxInfo &x = e->h_tx[e->gene_tx[k]];
-            giso[k] = IsoRec{(uint32_t)x.start, x.len, e->gene_tx[k], 0u};
-        }
-        CHK(up(e->d_giso, giso));
-    }
-    CHK(up(e->d_tile_tx, ttx));
-    CHK(up(e->d_tile_itx, itx));
-    CHK(up(e->d_kpos_off, koff));
-    CHK(up(e->d_pos_tx, pos_tx));
-    CHK(up(e->d_sample_pos, spos));
-    CHK(up(e->d_txstart, txb));
-    e->h_koff = koff;
-    e->tile_gid = gid;
-    e->tile_ntx = (uint32_t)ttx.size();
-    e->tile_nitx = (uint32_t)itx.size();
+    e->tile_tx_first[N] = n_ttx;
+    if (npos > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "more than 2^32 seed positions in a tile");
+    const uint64_t nblocks = (total >> POS_TX_SHIFT) + 2, nwb = (total >> 6) + 4;
+    CHK(e->d_tile_segs.ensure(std::max<size_t>(segs.size(), 1)));
+    CHK(e->d_tile_tx.ensure(std::max<uint32_t>(n_ttx, 1)));
+    CHK(e->d_tile_gid.ensure(std::max<uint32_t>(n_ttx, 1)));
+    CHK(e->d_tile_itx.ensure(std::max<uint32_t>(n_itx, 1)));
+    CHK(e->d_kpos_off.ensure((size_t)n_itx + 1));
+    CHK(e->d_pos_tx.ensure(nblocks));
+    CHK(e->d_sample_pos.ensure(spos.size()));
+    CHK(e->d_tile_send.ensure(send.size()));
+    CHK(e->d_txstart.ensure(nwb));
+    if (!segs.empty())
+        HIPCHK(hipMemcpyAsync(e->d_tile_segs.p, segs.data(), segs.size() * sizeof(TileSeg), hipMemcpyHostToDevice, e->st));
+    HIPCHK(hipMemcpyAsync(e->d_sample_pos.p, spos.data(), spos.size() * 8, hipMemcpyHostToDevice, e->st));
+    HIPCHK(hipMemcpyAsync(e->d_tile_send.p, send.data(), send.size() * 8, hipMemcpyHostToDevice, e->st));
+    HIPCHK(hipMemsetAsync(e->d_txstart.p, 0, nwb * 8, e->st));
+    launch_tile_tables(e->d_tile_segs.p, (uint32_t)segs.size(), n_ttx, e->d_tx_rel.p, e->d_kpre.p, e->d_tx.p,
+                       e->d_tile_tx.p, e->d_tile_gid.p, e->d_tile_itx.p, e->d_kpos_off.p, n_itx, npos,
+                       e->d_txstart.p, e->d_giso.p, e->gene_tx.size(), e->d_tile_send.p, e->d_pos_tx.p, nblocks,
+                       e->st);
+    HIPCHK(hipGetLastError());
+    e->tile_npos = npos;
+    e->tile_ntx = n_ttx;
+    e->tile_nitx = n_itx;
     e->tile_share = share;
     // the packed working copy's source: d_ascii itself or a gathered copy
     if (!direct) {
@@ -1107,9 +1141,9 @@ static int load_tile(rc_engine *e, int ti)
                 HIPCHK(hipMemcpyAsync(e->d_tile_ascii.p + e->tile_pos[s], e->d_ascii.p + e->samples[s].abase,
                                       e->samples[s].nbases, hipMemcpyDeviceToDevice, e->st));
     }
-    HIPCHK(hipStreamSynchronize(e->st));   // host vectors outlive the copies
+    // (no wait: the host tables above are engine members, kept until the
+    // next load, which comes after this tile's last wait)
     e->tile_loaded = ti;
-    (void)n_tx;
     return RC_OK;
 }
 
@@ -1199,7 +1233,7 @@ static int build_index_of(rc_engine *e, const TxInfo *txl, uint32_t n_tx, uint64
         HIPCHK(rocprim::exclusive_scan(e->d_tmp.p, tmp, e->d_kcnt.p, e->d_kpos_rel.p, (uint64_t)0,
                                        (size_t)n_tx + 1, rocprim::plus<uint64_t>(), e->st));
         HIPCHK(hipMemcpyAsync(&npos, e->d_kpos_rel.p + n_tx, sizeof(uint64_t), hipMemcpyDeviceToHost, e->st));
-        HIPCHK(hipStreamSynchronize(e->st));
+        CHK(wait_st(e));
         offs = e->d_kpos_rel.p;
     }
     CHK(ent.ensure(std::max<uint64_t>(npos, 1)));
@@ -1234,7 +1268,7 @@ static int build_index_of(rc_engine *e, const TxInfo *txl, uint32_t n_tx, uint64
 // The seed index of the loaded tile: every 16-mer position of its subject samples' transcripts.
 static int build_index(rc_engine *e, const std::function<int()> &after_fill = nullptr)
 {
-    return build_index_of(e, e->d_tile_itx.p, e->tile_nitx, e->h_koff[e->tile_nitx], e->d_kpos_off.p, e->d_ent,
+    return build_index_of(e, e->d_tile_itx.p, e->tile_nitx, e->tile_npos, e->d_kpos_off.p, e->d_ent,
                           e->d_ent2, e->d_bucket, e->index_bits, e->n_index, after_fill);
 }
 
@@ -1262,7 +1296,7 @@ static int build_masked_index(rc_engine *e)
                          e->d_rctr.p, e->st);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(&cnt, e->d_rctr.p, sizeof cnt, hipMemcpyDeviceToHost, e->st));
-        HIPCHK(hipStreamSynchronize(e->st));
+        CHK(wait_st(e));
         if (cnt <= e->mnear_cap) break;
         e->mnear_cap = cnt + cnt / 4 + (1u << 20);
     }
@@ -1445,7 +1479,7 @@ static int reverse_pass(rc_engine *e, int ti, const Db &db, const Index &ixm, ui
         unsigned int status = 0;
         HIPCHK(hipMemcpyAsync(&cnt, e->d_rctr.p + 1, sizeof cnt, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
-        HIPCHK(hipStreamSynchronize(e->st));
+        CHK(wait_st(e));
         if (status & 2u)
             return fail(RC_E_LIMIT, "a query gene has more than " + std::to_string(max_iso(e->xbits)) + " isoforms");
         if (cnt <= e->rseed_cap) break;
@@ -1515,7 +1549,7 @@ static int grow_hsp(rc_engine *e, uint64_t n)
         return fail(RC_E_NOMEM, "hipMalloc of " + std::to_string(cap * sizeof(DHsp)) + " bytes failed");
     }
     if (e->hsp_used) HIPCHK(hipMemcpyAsync(np, e->d_hsp.p, e->hsp_used * sizeof(DHsp), hipMemcpyDeviceToDevice, e->st));
-    HIPCHK(hipStreamSynchronize(e->st));
+    CHK(wait_st(e));
     e->d_hsp.adopt(np, cap);
     return RC_OK;
 }
@@ -1583,7 +1617,11 @@ static int dust_samples(rc_engine *e, const std::vector<int> &ss, hipStream_t st
 
 static int align_tile(rc_engine *e, int ti)
 {
-    CHK(load_tile(e, ti));
+    {
+        const double t0 = wall_ms();
+        CHK(load_tile(e, ti));
+        e->tm.load_ms += wall_ms() - t0;
+    }
     const int N = (int)e->samples.size();
     const uint64_t total = e->tile_total;
     const uint32_t n_genes = (uint32_t)e->gene_sample.size();
@@ -1593,7 +1631,11 @@ static int align_tile(rc_engine *e, int ti)
     // a split tile of the b chunk the previous tile had: its 16-mer index
     // (the b part's) and the b part's DUST masks are on the device already
     const rc_engine::Tile &TT = e->tiles[ti];
-    const bool reuse = TT.bchunk >= 0 && TT.bchunk == e->idx_bchunk && TT.bstart == e->idx_bstart &&
+    // (only while the index holds the b part alone: with one directed search
+    // at a time -- RC_SHARE=0, not spec 5b -- it holds the a part's samples
+    // too, and they differ from tile to tile)
+    const bool b_only_index = share_mode(e) || e->o.symmetric;
+    const bool reuse = b_only_index && TT.bchunk >= 0 && TT.bchunk == e->idx_bchunk && TT.bstart == e->idx_bstart &&
                        e->d_dmask.cap >= (total >> 6) + 4;
     const uint64_t dtot = reuse ? TT.bstart : total;   // masks cleared: the a part only when reusing
     // the samples whose masks DUST computes here, in tile order: a split
@@ -1783,7 +1825,7 @@ static int align_tile(rc_engine *e, int ti)
             unsigned long long nb = 0;   // (big_n: d_count[12], next to the extension's counters [0, 11))
             HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
             HIPCHK(hipMemcpyAsync(&nb, big_n, sizeof nb, hipMemcpyDeviceToHost, e->st));
-            HIPCHK(hipStreamSynchronize(e->st));
+            CHK(wait_st(e));
             if (status & 2u)
                 return fail(RC_E_LIMIT, "a query gene has more than " + std::to_string(max_iso(e->xbits)) + " isoforms");
             if (status & 16u)
@@ -1827,7 +1869,7 @@ static int align_tile(rc_engine *e, int ti)
                 unsigned long long nr = 0;
                 HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
                 HIPCHK(hipMemcpyAsync(&nr, big_retry_n, sizeof nr, hipMemcpyDeviceToHost, e->st));
-                HIPCHK(hipStreamSynchronize(e->st));
+                CHK(wait_st(e));
                 if (status & 16u)
                     return fail(RC_E_LIMIT, "a candidate's first seed of a directed search is past seed 65534");
                 again = (status & 1u) != 0;
@@ -1841,7 +1883,7 @@ static int align_tile(rc_engine *e, int ti)
         }
         HIPCHK(hipEventRecord(e->ev[9], e->st));
         HIPCHK(hipMemcpyAsync(shard_cnt.data(), e->d_shard_cnt.p, 2 * NSHARD * 8, hipMemcpyDeviceToHost, e->st));
-        HIPCHK(hipStreamSynchronize(e->st));
+        CHK(wait_st(e));
         if (!again) break;
         uint64_t ms = 0, mc = 0;
         for (int i = 0; i < NSHARD; i++) {
@@ -1985,7 +2027,7 @@ static int align_tile(rc_engine *e, int ti)
             HIPCHK(hipMemcpyAsync(&dn[1], e->d_count.p + 17, sizeof dn[1], hipMemcpyDeviceToHost, e->st));
             if (X.defer2_count)
                 HIPCHK(hipMemcpyAsync(&dn[2], X.defer2_count, sizeof dn[2], hipMemcpyDeviceToHost, e->st));
-            HIPCHK(hipStreamSynchronize(e->st));
+            CHK(wait_st(e));
             const uint64_t want = std::min<uint64_t>(2 * (dn[0] + dn[1] + dn[2]), (uint64_t)(MAX_HSP - 1) *
                                                      (dn[0] + dn[1] + dn[2])) + 1024;
             if (want > e->ovf_cap && !getenv("RC_OVF_CAP0")) {
@@ -2015,7 +2057,7 @@ static int align_tile(rc_engine *e, int ti)
         HIPCHK(hipMemcpyAsync(&ovn, e->d_count.p, sizeof ovn, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipMemcpyAsync(ctr, e->d_count.p + 1, sizeof ctr, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
-        HIPCHK(hipStreamSynchronize(e->st));
+        CHK(wait_st(e));
         if (ctr[8] || ctr[9]) {   // built with RC_ROW_TIMING: wave cycles in transitions / steps
             fprintf(stderr, "row kernel wave-cycles: transitions %.4g steps %.4g\n", (double)ctr[8], (double)ctr[9]);
             unsigned long long pr[10];
@@ -2110,7 +2152,7 @@ static int align_tile(rc_engine *e, int ti)
         CHK(exscan(e->d_mcnt.p, e->d_mscan.p, ngrp + 1));
         HIPCHK(hipMemcpyAsync(&nm, e->d_mscan.p + ngrp, 8, hipMemcpyDeviceToHost, e->st));
     }
-    HIPCHK(hipStreamSynchronize(e->st));
+    CHK(wait_st(e));
     uint64_t ndt = 0;
     for (uint64_t v : nd) ndt += v;
     const uint64_t nh = e->hsp_used + ndt + nm;
@@ -2142,7 +2184,7 @@ static int align_tile(rc_engine *e, int ti)
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e->ev[4], e->st));
-    HIPCHK(hipEventSynchronize(e->ev[4]));
+    CHK(wait_st(e));
     e->hsp_used = nh;
     e->tm.pack_ms += ev_ms(e, 0, 1);
     e->tm.index_ms += ev_ms(e, 1, 2);
@@ -2156,12 +2198,22 @@ static int align_tile(rc_engine *e, int ti)
     return RC_OK;
 }
 
+static int do_align_tiles(rc_engine *e);
+
 static int do_align(rc_engine *e)
 {
     CHK(upload(e));
     CHK(set_device(e));
     e->aligned = e->finished = e->rbh_done = false;
     e->tm = rc_timing{};
+    const double t0 = wall_ms();
+    const int rc = do_align_tiles(e);
+    e->tm.align_wall_ms = wall_ms() - t0;
+    return rc;
+}
+
+static int do_align_tiles(rc_engine *e)
+{
     if (e->external) {
         HIPCHK(hipEventRecord(e->ev[0], e->st));
         CHK(load_external(e));
@@ -2722,9 +2774,9 @@ int rc_dust_masks(rc_engine *e, const int32_t *samples, int32_t n, uint64_t *out
     if (!out) return RC_OK;
     if (cap_words < words) return fail(RC_E_CAPACITY, "buffer too small");
     CHK(set_device(e));
-    // a pass of its own: the tile tables of a previous run are replaced, so
-    // its results are dropped (as by a new rc_align)
-    e->aligned = e->finished = e->rbh_done = false;
+    // a pass of its own: the tile tables of a previous run are replaced. Its
+    // results stay valid: HSP groups, RBH rows and edges read only the
+    // transcripts' lengths and samples, never a tile's positions or masks
     std::vector<int> ss(samples, samples + n);
     std::sort(ss.begin(), ss.end());
     ss.erase(std::unique(ss.begin(), ss.end()), ss.end());
@@ -2850,7 +2902,22 @@ int rc_export_edges(rc_engine *e, void *buf, uint64_t cap, uint64_t *n, int on_d
 
 int rc_import_edges(rc_engine *e, const void *buf, uint64_t n, int on_device)
 {
-    if (!e || (n && !buf)) return fail(RC_E_ARG, "null argument");
+    return rc_import_edge_parts(e, buf, &n, 1, n, on_device);
+}
+
+// parts blocks of records, block r at record r * stride of buf with counts[r]
+// valid records: the concatenation is imported (an all-gather's padded
+// receive buffer goes in as it is, no compacted copy outside the engine)
+int rc_import_edge_parts(rc_engine *e, const void *buf, const uint64_t *counts, int32_t parts, uint64_t stride,
+                         int on_device)
+{
+    if (!e || parts < 0 || (parts && !counts)) return fail(RC_E_ARG, "null argument");
+    uint64_t n = 0;
+    for (int32_t r = 0; r < parts; r++) {
+        if (counts[r] > stride) return fail(RC_E_ARG, "a part holds more records than the stride");
+        n += counts[r];
+    }
+    if (n && !buf) return fail(RC_E_ARG, "null argument");
     if (!e->rbh_done) {
         // a fresh engine (samples added, nothing aligned): graph-only mode,
         // the records describe an imported graph and its tables
@@ -2861,21 +2928,84 @@ int rc_import_edges(rc_engine *e, const void *buf, uint64_t n, int on_device)
     CHK(set_device(e));
     const uint32_t ng = (uint32_t)e->gene_sample.size();
     const uint64_t np = e->pair_a.size();
-    if (!on_device && n) {
-        const DEdge *ed = static_cast<const DEdge *>(buf);
-        for (uint64_t i = 0; i < n; i++) {
-            const bool node = ed[i].pair == NODE_REC;
-            if (ed[i].a >= ng || ed[i].b >= ng || (!node && (ed[i].pair & ~EDGE_SUM_ONLY) >= np) ||
-                (node && ed[i].a != ed[i].b))
-                return fail(RC_E_ARG, "edge record out of range");
+    const DEdge *src = static_cast<const DEdge *>(buf);
+    if (!on_device) {
+        for (int32_t r = 0; r < parts; r++) {
+            const DEdge *ed = src + (uint64_t)r * stride;
+            for (uint64_t i = 0; i < counts[r]; i++) {
+                const bool node = ed[i].pair == NODE_REC;
+                if (ed[i].a >= ng || ed[i].b >= ng || (!node && (ed[i].pair & ~EDGE_SUM_ONLY) >= np) ||
+                    (node && ed[i].a != ed[i].b))
+                    return fail(RC_E_ARG, "edge record out of range");
+            }
         }
     }
+    // the local edges are replaced: their buffer goes before the new one is
+    // allocated (a sharded rank's peak holds the gathered records once)
+    if (e->d_edges.cap < n) e->d_edges.release();
     CHK(e->d_edges.ensure(n));
-    if (n)
-        HIPCHK(hipMemcpy(e->d_edges.p, buf, n * sizeof(DEdge), on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+    const hipMemcpyKind kind = on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    uint64_t o = 0;
+    for (int32_t r = 0; r < parts; r++) {
+        if (counts[r])
+            HIPCHK(hipMemcpyAsync(e->d_edges.p + o, src + (uint64_t)r * stride, counts[r] * sizeof(DEdge), kind, e->st));
+        o += counts[r];
+    }
     e->n_edges = n;
     e->n_local_edges = 0;   // the local edges are gone
+    if (on_device) {
+        // the same range check on the device: a malformed all-gather must not
+        // reach the union-find kernels
+        unsigned int bad = 0;
+        HIPCHK(hipMemsetAsync(e->d_status.p + 2, 0, sizeof(unsigned int), e->st));
+        launch_edge_check(e->d_edges.p, n, ng, np, e->d_status.p + 2, e->st);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(&bad, e->d_status.p + 2, sizeof bad, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipStreamSynchronize(e->st));
+        if (bad) {
+            e->n_edges = 0;
+            return fail(RC_E_ARG, "edge record out of range");
+        }
+    } else {
+        HIPCHK(hipStreamSynchronize(e->st));   // (the caller's host buffer is not retained)
+    }
     return do_graph(e);
+}
+
+// Free the alignment working set of a finished run: tile copies, indexes,
+// seeds, candidates, extension and grouping scratch. What the results need
+// stays (inputs, HSP store and groups, table rows, edges, graph arrays); the
+// next rc_align allocates the rest again.
+int rc_trim(rc_engine *e)
+{
+    if (!e) return fail(RC_E_ARG, "null engine");
+    CHK(set_device(e));
+    HIPCHK(hipStreamSynchronize(e->st));
+    HIPCHK(hipStreamSynchronize(e->st2));
+    e->d_tile_ascii.release(); e->d_tile_tx.release(); e->d_tile_itx.release(); e->d_tile_gid.release();
+    e->d_tile_segs.release(); e->d_tile_send.release();
+    e->d_F.release(); e->d_RC.release(); e->d_AF.release(); e->d_ARC.release();
+    e->d_kpos_off.release(); e->d_kcnt.release(); e->d_kpos_rel.release();
+    e->d_tile_masked.release(); e->d_ment.release(); e->d_ment2.release(); e->d_mbucket.release();
+    e->d_rseeds.release(); e->d_rseed_gene.release(); e->d_rs_key.release(); e->d_rs_idx.release();
+    e->d_rs_range.release(); e->d_rctr.release(); e->d_rtmask.release(); e->d_trange.release(); e->d_rtrange.release();
+    e->d_ent.release(); e->d_ent2.release(); e->d_sort_scratch.release(); e->d_gen_tile.release();
+    e->d_sort_status.release(); e->d_bucket.release(); e->d_pos_tx.release(); e->d_sample_pos.release();
+    e->d_txstart.release(); e->d_dmask.release(); e->d_dust_scratch.release(); e->d_dust_events.release();
+    e->d_prof.release(); e->d_tmp.release(); e->d_seeds.release(); e->d_cands.release();
+    e->d_cand_hsp.release(); e->d_ovf.release(); e->d_cand_nh.release(); e->d_cand_box.release();
+    e->d_cand_box2.release(); e->d_cand_hsp_r.release(); e->d_cand_nh_r.release(); e->d_cand_ovf_r.release();
+    e->d_defer_r.release(); e->d_list2.release(); e->d_wide0.release(); e->d_wide1.release(); e->d_resume.release();
+    e->d_rows_tmp.release(); e->d_edges_tmp.release(); e->d_cand_ovf.release(); e->d_gc_off.release();
+    e->d_gc_cnt.release(); e->d_gcount.release(); e->d_defer.release(); e->d_defer2.release(); e->d_gscan.release();
+    e->d_mscan.release(); e->d_mkey.release(); e->d_tmask.release(); e->d_mbig.release(); e->d_mcnt.release();
+    e->d_mcur.release(); e->d_big_out.release(); e->d_big_list.release(); e->d_big_retry.release();
+    e->d_big_seeds.release(); e->d_big_seg.release(); e->d_big_segT.release(); e->d_cnt4.release();
+    e->tile_loaded = -1;   // (rc_dust_mask reads a loaded tile: none now)
+    e->idx_bchunk = -1;
+    e->mnear_cap = 0;
+    e->res_cap = 0;
+    return RC_OK;
 }
 
 // The sample pairs in the engine's subject-major order ((0,1), (0,2), (1,2),

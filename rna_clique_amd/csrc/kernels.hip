@@ -741,6 +741,101 @@ void launch_bucket_fill(const uint64_t *ent, uint64_t n, int bits, uint32_t *buc
     hipLaunchKernelGGL(bucket_fill_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, ent, n, bits, bucket);
 }
 
+// ------------------------------------------------------------------------
+// tile tables (load_tile): built on the device from one TileSeg per tile
+// sample, so a tile load moves O(samples) bytes over PCIe instead of
+// per-transcript and per-base tables
+// ------------------------------------------------------------------------
+
+// last segment whose ttx0 <= i (segments ascend by ttx0, none empty)
+__device__ inline uint32_t seg_of(const TileSeg *segs, uint32_t nseg, uint32_t i)
+{
+    uint32_t lo = 0, hi = nseg;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (segs[mid].ttx0 <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// One thread per tile transcript: its start in the tile into the global
+// transcript table, the tile list (and its global id), the index list with
+// its k-mer slot (subject samples), and its start bit (bit start + 64 of
+// txb: the seed kernel reads it one word in). Threads < nseg also set the
+// bit at the end of their sample's bases when padding follows.
+__global__ void tile_tx_kernel(const TileSeg *__restrict__ segs, uint32_t nseg, uint32_t n_ttx,
+                               const uint64_t *__restrict__ tx_rel, const uint64_t *__restrict__ kpre,
+                               TxInfo *__restrict__ tx, TxInfo *__restrict__ ttx, uint32_t *__restrict__ gid,
+                               TxInfo *__restrict__ itx, uint64_t *__restrict__ koff, uint32_t n_itx, uint64_t npos,
+                               unsigned long long *__restrict__ txb)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nseg && segs[i].pad_bit != ~0ull) {
+        const uint64_t q = segs[i].pad_bit + 64;
+        atomicOr(&txb[q >> 6], 1ull << (q & 63));
+    }
+    if (i == 0) koff[n_itx] = npos;
+    if (i >= n_ttx) return;
+    const TileSeg S = segs[seg_of(segs, nseg, i)];
+    const uint32_t k = i - S.ttx0, t = S.tx0 + k;
+    TxInfo x = tx[t];
+    x.start = S.pos + tx_rel[t];
+    tx[t] = x;
+    ttx[i] = x;
+    gid[i] = t;
+    if (S.itx0 != ~0u) {
+        itx[S.itx0 + k] = x;
+        koff[S.itx0 + k] = S.kbase + kpre[t];
+    }
+    const uint64_t q = x.start + 64;
+    atomicOr(&txb[q >> 6], 1ull << (q & 63));
+}
+
+// The isoform records of every gene follow their transcripts' tile starts.
+__global__ void tile_giso_kernel(const TxInfo *__restrict__ tx, IsoRec *__restrict__ giso, uint64_t n)
+{
+    for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x)
+        giso[k].start = (uint32_t)tx[giso[k].gtx].start;
+}
+
+// Position -> transcript blocks: block b (bases [b << POS_TX_SHIFT, ...)) of
+// a sample's padded range holds the sample's last transcript starting at or
+// before the block's first base; blocks outside every sample are zero.
+__global__ void tile_pos_tx_kernel(const TxInfo *__restrict__ ttx, const uint32_t *__restrict__ gid, uint32_t n_ttx,
+                                   const uint64_t *__restrict__ send, PosTx *__restrict__ pos_tx, uint64_t nblocks)
+{
+    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nblocks;
+         b += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t p = b << POS_TX_SHIFT;
+        uint32_t lo = 0, hi = n_ttx;   // first transcript starting after p
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (ttx[mid].start <= p) lo = mid + 1; else hi = mid;
+        }
+        PosTx r{0, 0, 0, 0};
+        if (lo) {
+            const TxInfo x = ttx[lo - 1];
+            if (p < send[x.sample]) r = PosTx{gid[lo - 1], (uint32_t)x.start, x.len, x.sample};
+        }
+        pos_tx[b] = r;
+    }
+}
+
+void launch_tile_tables(const TileSeg *segs, uint32_t nseg, uint32_t n_ttx, const uint64_t *tx_rel,
+                        const uint64_t *kpre, TxInfo *tx, TxInfo *ttx, uint32_t *gid, TxInfo *itx, uint64_t *koff,
+                        uint32_t n_itx, uint64_t npos, uint64_t *txb, IsoRec *giso, uint64_t n_giso,
+                        const uint64_t *send, PosTx *pos_tx, uint64_t nblocks, hipStream_t st)
+{
+    const uint32_t n = std::max<uint32_t>(std::max(n_ttx, nseg), 1u);
+    hipLaunchKernelGGL(tile_tx_kernel, dim3((n + 255) / 256), dim3(256), 0, st, segs, nseg, n_ttx, tx_rel, kpre, tx,
+                       ttx, gid, itx, koff, n_itx, npos, (unsigned long long *)txb);
+    if (n_giso)
+        hipLaunchKernelGGL(tile_giso_kernel, dim3(grid_for(n_giso, 256)), dim3(256), 0, st, tx, giso, n_giso);
+    if (nblocks)
+        hipLaunchKernelGGL(tile_pos_tx_kernel, dim3(grid_for(nblocks, 256)), dim3(256), 0, st, ttx, gid, n_ttx, send,
+                           pos_tx, nblocks);
+}
+
 // 1 iff transcript i of the list holds a DUST-masked base (one thread each)
 __global__ void tx_masked_kernel(const TxInfo *txl, uint32_t n, const uint64_t *dmask, uint8_t *out)
 {
@@ -906,6 +1001,26 @@ void launch_distance(const unsigned long long *num, const unsigned long long *de
     if (!n) return;
     hipLaunchKernelGGL(distance_kernel, dim3((n + 255) / 256), dim3(256), 0, st, num, den, pair_index, order, N,
                        M, out, status);
+}
+
+// Imported edge records in range (rc_import_edges from the device): node ids
+// below n_genes, a pair index (with the sums-only flag) below n_pairs, or a
+// node-only record a == b. Any other record sets *bad.
+__global__ void edge_check_kernel(const DEdge *edges, uint64_t n, uint32_t ng, uint64_t np, unsigned int *bad)
+{
+    bool b = false;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const DEdge d = edges[i];
+        const bool node = d.pair == NODE_REC;
+        b |= d.a >= ng || d.b >= ng || (!node && (uint64_t)(d.pair & ~EDGE_SUM_ONLY) >= np) || (node && d.a != d.b);
+    }
+    if (__any(b) && (threadIdx.x & 63) == 0) atomicOr(bad, 1u);
+}
+
+void launch_edge_check(const DEdge *edges, uint64_t n, uint32_t ng, uint64_t np, unsigned int *bad, hipStream_t st)
+{
+    if (!n) return;
+    hipLaunchKernelGGL(edge_check_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, edges, n, ng, np, bad);
 }
 
 void launch_gather_rows(const DHsp *hsp, const DRow *rows, uint64_t n, DHsp *out, hipStream_t st)

@@ -140,24 +140,48 @@ def all_gather_records(local, record_size, process_group=None, device=None):
     return out, sum(counts)
 
 
-def exchange_edges(eng, process_group=None):
+def exchange_edges(eng, process_group=None, trim=None):
     """All-gather the shards' graph edges and run the graph phase on them.
-    The engine must have run align() and finish()."""
+    The engine must have run align() and finish().
+
+    RCCL path: the counts go first; each rank's records are exported straight
+    into its own slot of one padded receive buffer (W x the largest count),
+    gathered in place, and the engine imports that buffer as it is
+    (rc_import_edge_parts: no compacting copy). `trim`: free the engine's
+    alignment working set first (rc_trim) -- None = only when the receive
+    buffer and the imported records would not fit in free device memory
+    (C5: 17 GB + 16 GB beside a ~146 GB alignment working set)."""
     import torch
     import torch.distributed as dist
     rs = eng.edge_record_size()
     on_gpu = dist.get_backend(process_group) != "gloo" and torch.cuda.is_available()
-    if on_gpu:
-        n = eng.local_edge_count()
-        local = torch.empty(max(n * rs, 1), dtype=torch.uint8, device="cuda")[:n * rs]
-        eng.export_edges(local)            # device-to-device, engine stream synced
-        allt, total = all_gather_records(local, rs, process_group)
-        torch.cuda.current_stream().synchronize()   # engine runs on its own stream
-        eng.import_edges(allt.contiguous(), total)
-    else:
+    if not on_gpu:
         local = torch.from_numpy(eng.export_edges())
         allt, total = all_gather_records(local, rs, process_group)
         eng.import_edges(allt.numpy())
+        return
+    W, R = world(process_group)
+    n = eng.local_edge_count()
+    c = torch.tensor([n], dtype=torch.int64, device="cuda")
+    cs = [torch.zeros_like(c) for _ in range(W)]
+    dist.all_gather(cs, c, group=process_group)
+    counts = [int(x.item()) for x in cs]
+    mx = max(counts)
+    if trim is None:
+        free, _ = torch.cuda.mem_get_info()
+        trim = (W * mx + sum(counts)) * rs > 0.9 * free
+    if trim:
+        eng.trim()
+    recv = torch.empty(max(W * mx * rs, 1), dtype=torch.uint8, device="cuda")
+    if mx:
+        mine = recv[R * mx * rs:(R + 1) * mx * rs]
+        eng.export_edges(mine)             # device-to-device, engine stream synced
+        dist.all_gather_into_tensor(recv[:W * mx * rs], mine, group=process_group)
+        torch.cuda.current_stream().synchronize()   # the engine runs on its own stream
+    eng.import_edge_parts(recv, counts, mx)
+    del recv
+    if mx * W * rs >= (1 << 30):
+        torch.cuda.empty_cache()   # the engine allocates outside torch's pool
 
 
 def dust_owners(sample_bases, shard_count):

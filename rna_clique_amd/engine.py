@@ -176,6 +176,24 @@ class Engine:
             n = buf.numel() // rs if n is None else int(n)
             nat.check(L.rc_import_edges(self._h, ctypes.c_void_p(buf.data_ptr()), n, 1))
 
+    def import_edge_parts(self, buf, counts, stride):
+        """import_edges from blocks: block r starts at record r * stride of
+        `buf` (a CUDA uint8 tensor or host uint8 array) and holds counts[r]
+        records -- e.g. an all-gather's padded receive buffer as it is."""
+        L = nat.lib()
+        c = np.ascontiguousarray(counts, dtype=np.uint64)
+        if isinstance(buf, np.ndarray):
+            buf = np.ascontiguousarray(buf, dtype=np.uint8)
+            ptr, dev = buf.ctypes.data_as(ctypes.c_void_p), 0
+        else:
+            ptr, dev = ctypes.c_void_p(buf.data_ptr()), 1
+        nat.check(L.rc_import_edge_parts(self._h, ptr, c.ctypes.data_as(ctypes.c_void_p), len(c), int(stride), dev))
+
+    def trim(self):
+        """Free the alignment working set of a finished run (rc_trim): rows,
+        HSPs and edges stay; the next align() allocates it again."""
+        nat.check(nat.lib().rc_trim(self._h))
+
     # ------------------------------------------------------------- results
     def _sized(self, fn, dtype, *args):
         n = ctypes.c_uint64()

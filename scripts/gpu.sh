@@ -1,0 +1,62 @@
+# One parameterised GPU-box script (run through gpurun): every step writes
+# under gpurun_out/$TAG/ and appends the exact command it ran to
+# gpurun_out/$TAG/commands.txt, so each profiles/<tag>/ says what produced it.
+#
+#   bash scripts/gpu.sh TAG STEP [STEP ...]
+#
+# Steps (each under its own time limit; the script stops at the first failure):
+#   smoke            __graft_entry__.smoke()
+#   tests            every -m gpu test, one process
+#   tests:EXPR       -m gpu tests matching -k EXPR
+#   bench[:CFG]      bench.py --config CFG (default C3), 3 steps, no CPU baseline, no e2e
+#   benchfull        bench.py with its defaults (CPU baseline + wall-clock leg)
+#   e2e[:CFG]        bench.py with the wall-clock leg, no CPU baseline
+#   stats[:CFG]      rocprofv3 --kernel-trace --stats of bench.py --config CFG
+#   pmc[:CFG]        the PMC passes of scripts/gpu_pmc.sh (same-source counters)
+#   shard:CFG:R/S    bench.py --shard R/S --config CFG (1 step, 1 warmup)
+#   shardprof:CFG:R/S  the same under rocprofv3 --kernel-trace --hip-trace --stats
+#   c5full[:CFG]     scripts/c5_full.py (default C5s)
+#   py:SCRIPT[:ARGS] python SCRIPT ARGS (ARGS: commas become spaces)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+TAG=$1; shift
+D=gpurun_out/$TAG
+mkdir -p "$D"
+log() { echo "$*" >> "$D/commands.txt"; }
+run() {   # run LIMIT OUTFILE CMD...: one GPU step under its own time limit
+  local lim=$1 out=$2; shift 2
+  log "timeout -k 10 $lim $* > $out 2>&1"
+  timeout -k 10 "$lim" "$@" > "$out" 2>&1
+  local rc=$?
+  echo "[$TAG] $* -> rc=$rc"; tail -3 "$out"
+  return $rc
+}
+for step in "$@"; do
+  IFS=: read -r kind a b <<< "$step"
+  case $kind in
+    smoke) run 300 "$D/smoke.log" python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+    tests) if [ -n "$a" ]; then
+             run 1100 "$D/gpu_tests_$a.log" python -u -m pytest tests -m gpu -k "$a" -x -v --timeout 700 --timeout-method thread -p no:cacheprovider || exit $?
+           else
+             run 1100 "$D/gpu_tests.log" python -u -m pytest tests -m gpu -x -v --timeout 700 --timeout-method thread -p no:cacheprovider || exit $?
+           fi ;;
+    bench) c=${a:-C3}; run 600 "$D/${c}_bench.json" python bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e || exit $? ;;
+    benchfull) run 900 "$D/bench_default.json" python bench.py || exit $? ;;
+    e2e) c=${a:-C3}; run 600 "$D/${c}_e2e.json" python bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
+    stats) c=${a:-C3}
+           run 600 "$D/${c}_stats.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$D/${c}_stats" -o run -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e || exit $? ;;
+    pmc) c=${a:-C3}; log "bash scripts/gpu_pmc.sh $c  (-> gpurun_out/pmc_$c)"; bash scripts/gpu_pmc.sh "$c" || exit $? ;;
+    shard) run 900 "$D/${a}_shard${b//\//of}.json" python -u bench.py --shard "$b" --config "$a" --steps 1 --warmup 1 || exit $? ;;
+    shardprof) P="$D/${a}_shardprof${b//\//of}"
+           run 900 "$P.log" rocprofv3 --kernel-trace --hip-trace --stats --output-format csv -d "$P" -o run -- python3 -u bench.py --shard "$b" --config "$a" --steps 1 --warmup 1 || exit $?
+           T=$(python3 -c "import json,sys; print(int([json.loads(l) for l in open('$P.log') if l.startswith('{\"metric')][-1]['phases_ms']['tiles']))")
+           log "python3 scripts/trace_gaps.py $P $T $P.gaps.json"
+           python3 scripts/trace_gaps.py "$P" "$T" "$P.gaps.json" > /dev/null; rc=$?
+           find "$P" \( -name '*_trace.csv' -o -name '*.db' \) -delete   # (hundreds of MB; the summaries stay)
+           [ $rc -eq 0 ] || exit $rc ;;
+    c5full) c=${a:-C5s}; run 1100 "$D/${c}_full.log" python -u scripts/c5_full.py --config "$c" --out "$D/${c}_full.json" || exit $? ;;
+    py) run 900 "$D/$(basename "$a" .py).log" python -u "$a" ${b//,/ } || exit $? ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done

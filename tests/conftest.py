@@ -10,6 +10,8 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through librcgpu.so)")
+    config.addinivalue_line("markers", "heartbeat(seconds): how long the GPU heartbeat may keep a silent "
+                                       "test alive (default HEARTBEAT_S)")
 
 
 def gpu_available():
@@ -36,16 +38,23 @@ def native():
     return _native.lib()
 
 
+HEARTBEAT_S = 120
+
+
 @pytest.fixture(autouse=True)
 def _gpu_heartbeat(request):
     """GPU tests: a line appended to gpurun_out/heartbeat.log every 30 s while
     the test runs. A GPU run is taken to be hung after 3 minutes with nothing
     new on stdout, stderr or under gpurun_out/, and pytest prints nothing
     during a test (-q) -- the full-size config tests (simulation, engine,
-    oracle pairs) run longer than that."""
+    oracle pairs) run longer than that. The beat stops after the test's
+    `heartbeat` marker (about 2-3x its expected run time; HEARTBEAT_S when
+    unmarked), so a test that hangs still goes silent and is caught."""
     if request.node.get_closest_marker("gpu") is None:
         yield
         return
+    hb = request.node.get_closest_marker("heartbeat")
+    limit = float(hb.args[0]) if hb else HEARTBEAT_S
     import threading
     import time
     stop = threading.Event()
@@ -54,7 +63,7 @@ def _gpu_heartbeat(request):
     def beat():
         t0 = time.time()
         os.makedirs("gpurun_out", exist_ok=True)
-        while not stop.wait(30):
+        while not stop.wait(30) and time.time() - t0 < limit:
             with open(os.path.join("gpurun_out", "heartbeat.log"), "a") as f:
                 f.write(f"{time.strftime('%H:%M:%S')} {name}: {time.time() - t0:.0f} s\n")
 

@@ -86,6 +86,12 @@ def test_dust_masks_once_per_sample(native, shards):
         assert not bits[nb:].any()
         o += nw
     assert o == len(words) and ref.dust_mask(4).any()
+    # a mask pass after a run leaves that run's results readable and unchanged
+    rows01, hs10, dist = ref.pair_rows(0, 1).tobytes(), ref.hsps(1, 0).tobytes(), ref.distance()[1]
+    again = ref.dust_masks([1, 3])
+    assert ref.pair_rows(0, 1).tobytes() == rows01 and ref.hsps(1, 0).tobytes() == hs10
+    assert np.array_equal(ref.distance()[1], dist)
+    assert again.tobytes() == eng.dust_masks([1, 3]).tobytes()
     # every sample masked once, by its owner shard; each shard takes them all
     bases = [len(s.seq) for s in samples]
     owner = distributed.dust_owners(bases, shards)
@@ -405,15 +411,18 @@ def test_tables_and_graph_reload(native, tmp_path):
     assert np.array_equal(again.get_dissimilarity_df().to_numpy(), want.to_numpy())
 
 
-@pytest.mark.parametrize("split", [1, 0])
-def test_tiles_match_one_pass(native, monkeypatch, split):
+@pytest.mark.parametrize("split,share", [(1, 1), (0, 1), (1, 0)])
+def test_tiles_match_one_pass(native, monkeypatch, split, share):
     """A shard whose samples do not fit one alignment pass is cut into tiles
     (a- and b-chunks, positions relative to each tile, HSPs appended): forced
     here with a small RC_TILE_BASES, the results equal one pass bit for bit.
     split 1 (default): tiles with every a below every b place the b chunk at
     a fixed position, and consecutive tiles of one b chunk reuse its 16-mer
-    index and DUST masks; split 0 (RC_TILE_SPLIT=0) rebuilds both per tile."""
+    index and DUST masks; split 0 (RC_TILE_SPLIT=0) rebuilds both per tile.
+    share 0 (RC_SHARE=0: the two directed searches one after the other) puts
+    the a part into the index too, so split tiles must not reuse it."""
     monkeypatch.setenv("RC_TILE_SPLIT", str(split))
+    monkeypatch.setenv("RC_SHARE", str(share))
     from rna_clique_amd.engine import Engine
     from rna_clique_amd.simulate import simulate
     samples, _ = simulate(6, 150, seed=23, p_iso2=0.2, indel_rate=0.002, p_revcomp=0.3,
@@ -425,7 +434,7 @@ def test_tiles_match_one_pass(native, monkeypatch, split):
     eng = _load(Engine(device=0), samples)
     eng.run()
     tm = eng.timings()
-    assert tm["tiles"] > 1 and (tm["index_reused"] > 0) == bool(split)
+    assert tm["tiles"] > 1 and (tm["index_reused"] > 0) == bool(split and share)
     for q in range(6):
         for s in range(6):
             if q != s:

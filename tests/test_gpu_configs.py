@@ -77,6 +77,7 @@ def test_config_end_to_end_with_tree(native, tmp_path, cfg):
     assert _rf_to_truth(tree, samples, names, df.to_numpy()) == 0
 
 
+@pytest.mark.heartbeat(180)
 def test_config_C2_full_oracle(native):
     """C2: 8 samples x 10 000 genes, every HSP of the 56 directed searches and
     every row, edge, ideal node and distance bit-exact against the oracles."""
@@ -142,6 +143,7 @@ def covering_pairs(n, fixed, k=8, seed=2024):
 C3_PAIRS = covering_pairs(32, [(0, 1), (5, 17), (12, 31), (30, 31)])
 
 
+@pytest.mark.heartbeat(300)
 def test_config_C3_full_size(native):
     """C3 at full size (32 x 50 000, ~1.6 Gbp): 12 sampled pairs bit-exact vs
     the oracle, whole-run properties, NJ tree."""
@@ -154,6 +156,7 @@ def test_config_C3_full_size(native):
     eng.close()
 
 
+@pytest.mark.heartbeat(400)
 def test_config_C3_correctness_variant(native):
     """C3 with 10 % two-isoform genes, indels, half the genes on the minus
     strand per sample, 2 % recently duplicated genes and poly-A tails: RBH ties
@@ -166,6 +169,7 @@ def test_config_C3_correctness_variant(native):
     eng.close()
 
 
+@pytest.mark.heartbeat(400)
 def test_config_C4_full_size(native):
     """C4 (64 x 50 000, ~3.3 Gbp, 2016 pairs on one GPU): 12 sampled pairs
     bit-exact vs the oracle, whole-run properties and the NJ tree of all 64

@@ -48,7 +48,8 @@ def _records(arr, rs):
 
 class _heartbeat:
     """Prints a line every 30 s while a long step runs (GPU runs are killed
-    after 3 minutes without output; pytest -s shows these)."""
+    after 3 minutes without output; pytest -s shows these), for at most
+    10 minutes: a step that hangs still goes silent."""
 
     def __init__(self, what):
         import threading
@@ -58,7 +59,7 @@ class _heartbeat:
     def _run(self):
         import time
         t0 = time.time()
-        while not self.stop.wait(30):
+        while not self.stop.wait(30) and time.time() - t0 < 600:
             print(f"  ... {self.what}: {time.time() - t0:.0f} s", flush=True)
 
     def __enter__(self):
@@ -77,6 +78,7 @@ def _record(name, obj):
         json.dump(obj, f, indent=1)
 
 
+@pytest.mark.heartbeat(400)
 def test_C4_eight_shards_match_unsharded(native):
     from rna_clique_amd import distributed
     from rna_clique_amd.engine import Engine
@@ -134,6 +136,7 @@ def test_C4_eight_shards_match_unsharded(native):
     g.close()
 
 
+@pytest.mark.heartbeat(300)
 def test_graph_phase_at_C5_size(native):
     """The graph phase alone at C5's size (build_graph.py:40-68,
     filtered_distance.py:30-39): 128 samples x 100 000 genes (12.8 M nodes)
@@ -219,6 +222,7 @@ def test_graph_phase_at_C5_size(native):
         g.close()
 
 
+@pytest.mark.heartbeat(600)
 def test_C5_one_rank_shard(native):
     import torch
     from bench import shard_samples
