@@ -2497,8 +2497,51 @@ int rc_hsps(rc_engine *e, int32_t q, int32_t s, rc_hsp *buf, uint64_t cap, uint6
 // from the device (the engine's stream; one caller at a time).
 struct PairRaw {
     int32_t s1 = 0, s2 = 0;
-    std::vector<DRow> rows;
-    std::vector<DHsp> hs;
+    uint64_t n = 0;
+    const DRow *rows = nullptr;   // n rows and their HSPs: in the vectors, or in a pinned slab
+    const DHsp *hs = nullptr;
+    std::vector<DRow> vrows;
+    std::vector<DHsp> vhs;
+    std::shared_ptr<char> slab;   // (returned to its pool when the last holder lets go)
+};
+
+// Pinned host slabs the rows of many pairs come to by DMA (rc_write_outputs):
+// at most `cap` of them, allocated as needed, each holding `bytes`; a slab
+// goes back to the pool when its pair's last consumer drops it. Pageable
+// copies faulted fresh pages for every pair (3.6 GB at C3).
+struct SlabPool {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<char *> all, free;
+    size_t bytes = 0, cap = 0;
+    ~SlabPool()
+    {
+        for (char *p : all) (void)hipHostFree(p);
+    }
+    // a slab (blocks while all `cap` are in use); nullptr if pinning fails
+    std::shared_ptr<char> get()
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        if (free.empty() && all.size() < cap) {
+            char *p = nullptr;
+            if (hipHostMalloc((void **)&p, bytes, hipHostMallocDefault) != hipSuccess) {
+                (void)hipGetLastError();
+                return nullptr;
+            }
+            all.push_back(p);
+            free.push_back(p);
+        }
+        cv.wait(lk, [&] { return !free.empty(); });
+        char *p = free.back();
+        free.pop_back();
+        return std::shared_ptr<char>(p, [this](char *q) {
+            {
+                std::lock_guard<std::mutex> g(mu);
+                free.push_back(q);
+            }
+            cv.notify_all();
+        });
+    }
 };
 
 static int pair_row_range(rc_engine *e, int32_t s1, int32_t s2, uint64_t &r0, uint64_t &r1)
@@ -2515,22 +2558,43 @@ static int pair_row_range(rc_engine *e, int32_t s1, int32_t s2, uint64_t &r0, ui
     return RC_OK;
 }
 
-static int fetch_pair(rc_engine *e, int32_t s1, int32_t s2, PairRaw &out)
+// a pair's rows and their HSPs to the host: into `pool`'s pinned slabs when
+// given and big enough, else into the PairRaw's own vectors
+static int fetch_pair(rc_engine *e, int32_t s1, int32_t s2, PairRaw &out, SlabPool *pool = nullptr,
+                      const uint64_t *range = nullptr)
 {
     uint64_t r0 = 0, r1 = 0;
-    CHK(pair_row_range(e, s1, s2, r0, r1));
+    if (range) {
+        r0 = range[0];
+        r1 = range[1];
+    } else {
+        CHK(pair_row_range(e, s1, s2, r0, r1));
+    }
     const uint64_t nr = r1 - r0;
     out.s1 = s1;
     out.s2 = s2;
-    out.rows.resize(nr);
-    out.hs.resize(nr);
+    out.n = nr;
     if (!nr) return RC_OK;
     CHK(e->d_gather.ensure(nr));
     launch_gather_rows(e->d_hsp.p, e->d_rows.p + r0, nr, e->d_gather.p, e->st);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(out.rows.data(), e->d_rows.p + r0, nr * sizeof(DRow), hipMemcpyDeviceToHost, e->st));
-    HIPCHK(hipMemcpyAsync(out.hs.data(), e->d_gather.p, nr * sizeof(DHsp), hipMemcpyDeviceToHost, e->st));
+    DRow *rows = nullptr;
+    DHsp *hs = nullptr;
+    if (pool && nr * (sizeof(DRow) + sizeof(DHsp)) <= pool->bytes) out.slab = pool->get();
+    if (out.slab) {
+        hs = reinterpret_cast<DHsp *>(out.slab.get());
+        rows = reinterpret_cast<DRow *>(out.slab.get() + nr * sizeof(DHsp));
+    } else {
+        out.vrows.resize(nr);
+        out.vhs.resize(nr);
+        rows = out.vrows.data();
+        hs = out.vhs.data();
+    }
+    HIPCHK(hipMemcpyAsync(rows, e->d_rows.p + r0, nr * sizeof(DRow), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipMemcpyAsync(hs, e->d_gather.p, nr * sizeof(DHsp), hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
+    out.rows = rows;
+    out.hs = hs;
     return RC_OK;
 }
 
@@ -2539,9 +2603,9 @@ static int fetch_pair(rc_engine *e, int32_t s1, int32_t s2, PairRaw &out)
 static void convert_rows(const rc_engine *e, const PairRaw &raw, rc_row *buf)
 {
     const int32_t s1 = raw.s1, s2 = raw.s2;
-    const uint64_t nr = raw.rows.size();
-    const std::vector<DRow> &rows = raw.rows;
-    const std::vector<DHsp> &hs = raw.hs;
+    const uint64_t nr = raw.n;
+    const DRow *rows = raw.rows;
+    const DHsp *hs = raw.hs;
     for (uint64_t i = 0; i < nr; i++) {
         const DHsp &d = hs[i];
         rc_row &r = buf[i];
@@ -2774,61 +2838,93 @@ int rc_dust_masks(rc_engine *e, const int32_t *samples, int32_t n, uint64_t *out
     if (!out) return RC_OK;
     if (cap_words < words) return fail(RC_E_CAPACITY, "buffer too small");
     CHK(set_device(e));
-    // a pass of its own: the tile tables of a previous run are replaced. Its
+    // passes of their own: the tile tables of a previous run are replaced. Its
     // results stay valid: HSP groups, RBH rows and edges read only the
     // transcripts' lengths and samples, never a tile's positions or masks
     std::vector<int> ss(samples, samples + n);
     std::sort(ss.begin(), ss.end());
     ss.erase(std::unique(ss.begin(), ss.end()), ss.end());
-    // the pass: the shard's own alignment tile when it is a single tile
-    // holding these samples (its tables stay loaded for rc_align), else a
-    // tile of these samples alone; packed, their DUST masks, copied out
+    std::vector<std::vector<uint64_t>> oof(N);   // word offsets of each listed sample in `out` (any repeats)
+    {
+        uint64_t o = 0;
+        for (int32_t i = 0; i < n; i++) {
+            oof[samples[i]].push_back(o);
+            o += (e->samples[samples[i]].nbases + 63) >> 6;
+        }
+    }
     if (e->tiles_for != (int64_t)e->pair0 || e->tiles.empty()) {
         plan_tiles(e);
         e->tiles_for = (int64_t)e->pair0;
         e->tile_loaded = -1;
     }
+    // the shard's own alignment tile when it is a single tile holding these
+    // samples (its tables stay loaded for rc_align), else tiles of these
+    // samples alone, as many as the 2^32-base tile limit takes (a C5 rank
+    // masks ~4 Gbp); each packed, its DUST masks copied out
     bool own = e->tiles.size() == 1;
     for (int s : ss)
         own = own && std::binary_search(e->tiles[0].samples.begin(), e->tiles[0].samples.end(), s);
-    int ti = 0;
-    if (!own) {
-        rc_engine::Tile T;
-        T.samples = ss;
-        e->tiles.push_back(T);
-        e->tile_loaded = -1;
-        ti = (int)e->tiles.size() - 1;
-    }
-    int rc = load_tile(e, ti);
-    if (rc == RC_OK) rc = pack_tile(e);
-    const bool dust = e->o.dust_level > 0 && !e->external;
-    if (rc == RC_OK && dust) {
-        const size_t mw = (e->tile_total >> 6) + 4;
-        rc = e->d_dmask.ensure(mw);
-        if (rc == RC_OK && hipMemsetAsync(e->d_dmask.p, 0, mw * 8, e->st) != hipSuccess)
-            rc = fail(RC_E_HIP, "hipMemsetAsync");
-        if (rc == RC_OK) rc = dust_samples(e, ss, e->st);
-    }
-    std::vector<uint64_t> tail;   // last word of each listed sample, bits past its end cleared
-    uint64_t o = 0;
-    for (int32_t i = 0; rc == RC_OK && i < n; i++) {
-        const int s = samples[i];
-        const uint64_t nb = e->samples[s].nbases, nw = (nb + 63) >> 6;
-        if (!nw) continue;
-        hipError_t h = hipSuccess;
-        if (dust) {
-            h = hipMemcpyAsync(out + o, e->d_dmask.p + 1 + (e->tile_pos[s] >> 6), nw * 8,
-                               on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, e->st);
-        } else if (on_device) {
-            h = hipMemsetAsync(out + o, 0, nw * 8, e->st);
-        } else {
-            std::memset(out + o, 0, nw * 8);
+    std::vector<std::vector<int>> chunks;
+    if (own) {
+        chunks.push_back(ss);
+    } else {
+        const uint64_t cap = tile_cap();
+        uint64_t acc = 0;
+        for (int s : ss) {
+            const uint64_t b = align_up(e->samples[s].nbases);
+            if (chunks.empty() || (acc + b > cap && !chunks.back().empty())) {
+                chunks.push_back({});
+                acc = 0;
+            }
+            chunks.back().push_back(s);
+            acc += b;
         }
-        if (h != hipSuccess) rc = fail(RC_E_HIP, "mask copy");
-        o += nw;
     }
-    if (rc == RC_OK && hipStreamSynchronize(e->st) != hipSuccess) rc = fail(RC_E_HIP, "hipStreamSynchronize");
-    o = 0;
+    const bool dust = e->o.dust_level > 0 && !e->external;
+    int rc = RC_OK;
+    for (size_t c = 0; c < chunks.size() && rc == RC_OK; c++) {
+        int ti = 0;
+        if (!own) {
+            rc_engine::Tile T;
+            T.samples = chunks[c];
+            e->tiles.push_back(T);
+            e->tile_loaded = -1;
+            ti = (int)e->tiles.size() - 1;
+        }
+        rc = load_tile(e, ti);
+        if (rc == RC_OK) rc = pack_tile(e);
+        if (rc == RC_OK && dust) {
+            const size_t mw = (e->tile_total >> 6) + 4;
+            rc = e->d_dmask.ensure(mw);
+            if (rc == RC_OK && hipMemsetAsync(e->d_dmask.p, 0, mw * 8, e->st) != hipSuccess)
+                rc = fail(RC_E_HIP, "hipMemsetAsync");
+            if (rc == RC_OK) rc = dust_samples(e, chunks[c], e->st);
+        }
+        for (size_t k = 0; rc == RC_OK && k < chunks[c].size(); k++) {
+            const int s = chunks[c][k];
+            const uint64_t nb = e->samples[s].nbases, nw = (nb + 63) >> 6;
+            if (!nw) continue;
+            for (uint64_t w0 : oof[s]) {
+                hipError_t h = hipSuccess;
+                if (dust) {
+                    h = hipMemcpyAsync(out + w0, e->d_dmask.p + 1 + (e->tile_pos[s] >> 6), nw * 8,
+                                       on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, e->st);
+                } else if (on_device) {
+                    h = hipMemsetAsync(out + w0, 0, nw * 8, e->st);
+                } else {
+                    std::memset(out + w0, 0, nw * 8);
+                }
+                if (h != hipSuccess) rc = fail(RC_E_HIP, "mask copy");
+            }
+        }
+        if (rc == RC_OK && hipStreamSynchronize(e->st) != hipSuccess) rc = fail(RC_E_HIP, "hipStreamSynchronize");
+        if (!own) {
+            e->tiles.pop_back();
+            e->tile_loaded = -1;
+        }
+    }
+    // bits past each sample's last base cleared (its last word)
+    uint64_t o = 0;
     for (int32_t i = 0; rc == RC_OK && dust && i < n; i++) {
         const uint64_t nb = e->samples[samples[i]].nbases, nw = (nb + 63) >> 6;
         o += nw;
@@ -2842,10 +2938,6 @@ int rc_dust_masks(rc_engine *e, const int32_t *samples, int32_t n, uint64_t *out
         } else {
             out[o - 1] &= keep;
         }
-    }
-    if (!own) {
-        e->tiles.pop_back();
-        e->tile_loaded = -1;
     }
     e->idx_bchunk = -1;
     return rc;
@@ -3105,11 +3197,13 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
                 tq.pop_front();
             }
             const PairRaw &raw = *job.second;
+            const int32_t js1 = raw.s1, js2 = raw.s2;
             const long long c0 = now_ns();
-            buf.resize(raw.rows.size());
+            buf.resize(raw.n);
             convert_rows(e, raw, buf.data());
+            job.second.reset();   // (its slab goes back once the grapher is done too)
             const long long c1 = now_ns();
-            const int rc = od2_write_table(buf.data(), buf.size(), e->samples[raw.s1].label, e->samples[raw.s2].label,
+            const int rc = od2_write_table(buf.data(), buf.size(), e->samples[js1].label, e->samples[js2].label,
                                            table_paths[job.first]);
             t_conv += c1 - c0;
             t_write += now_ns() - c1;
@@ -3142,7 +3236,7 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
             }
             const PairRaw &raw = *job.second;
             const long long a0 = now_ns();
-            const size_t n = raw.rows.size();
+            const size_t n = raw.n;
             sg.resize(n);
             qg.resize(n);
             for (size_t i = 0; i < n; i++) {
@@ -3171,6 +3265,16 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
         }
         rc_graph_pickle_free(g);
     };
+    // every pair's row range first: the pinned slabs are sized to the largest
+    std::vector<uint64_t> ranges(2 * (size_t)n_pairs);
+    uint64_t max_rows = 0;
+    for (int i = 0; i < n_pairs; i++) {
+        CHK(pair_row_range(e, s1[i], s2[i], ranges[2 * i], ranges[2 * i + 1]));
+        max_rows = std::max<uint64_t>(max_rows, ranges[2 * i + 1] - ranges[2 * i]);
+    }
+    SlabPool slabs;
+    slabs.bytes = std::max<uint64_t>(max_rows, 1) * (sizeof(DRow) + sizeof(DHsp));
+    slabs.cap = (size_t)(2 * nt + 8);
     std::vector<std::thread> pool;
     if (table_paths)
         for (int i = 0; i < nt; i++) pool.emplace_back(worker);
@@ -3186,7 +3290,7 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
         }
         auto raw = std::make_shared<PairRaw>();
         const long long f0 = now_ns();
-        rc = fetch_pair(e, s1[i], s2[i], *raw);
+        rc = fetch_pair(e, s1[i], s2[i], *raw, &slabs, &ranges[2 * (size_t)i]);
         t_fetch += now_ns() - f0;
         if (rc != RC_OK) break;
         {

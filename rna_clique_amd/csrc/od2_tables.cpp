@@ -590,7 +590,11 @@ struct Block {
 struct Table {
     const rc_row *rows;
     uint64_t n;
-    std::vector<double> pident, evalue;
+    std::vector<double> pident, evalue, bits;
+    // the frame's columns, gathered once from the rows (fill_records writes
+    // them column by column into cache-sized runs of records)
+    std::vector<int32_t> ic[NCOL], label;
+    std::vector<uint8_t> rev, minus;
     DType coldt[NCOL];
     std::vector<Block> blocks;
     std::vector<uint32_t> boff;   // record offset of each block
@@ -606,45 +610,60 @@ static double printed(const char *fmt, double v)
     return std::strtod(b, nullptr);
 }
 
+// one column of a run of records: v[i] into rec i at byte offset `off`, as
+// the low `size` bytes of its little-endian value
+template <class T, class S>
+static void put_col(char *out, size_t rec, size_t off, const S *v, uint64_t i0, uint64_t i1)
+{
+    for (uint64_t i = i0; i < i1; i++) {
+        const T x = (T)v[i];
+        std::memcpy(out + i * rec + off, &x, sizeof(T));
+    }
+}
+
 static void fill_records(std::string &buf, const void *arg)
 {
     const Table &t = *static_cast<const Table *>(arg);
-    const size_t base = buf.size();
-    buf.resize(base + (size_t)t.rec * t.n);
+    const size_t base = buf.size(), rec = t.rec;
+    buf.resize(base + rec * t.n);
     char *out = &buf[base];
-    for (uint64_t i = 0; i < t.n; i++) {
-        const rc_row &r = t.rows[i];
-        char *p = out + (size_t)i * t.rec;
-        const int64_t label = r.label;
-        std::memcpy(p, &label, 8);
+    // runs of 256 records (about 20 KB: they stay in L1 while every column
+    // of the run is written)
+    for (uint64_t i0 = 0; i0 < t.n; i0 += 256) {
+        const uint64_t i1 = std::min<uint64_t>(t.n, i0 + 256);
+        put_col<int64_t>(out, rec, 0, t.label.data(), i0, i1);
         for (size_t k = 0; k < t.blocks.size(); k++) {
             const Block &b = t.blocks[k];
-            char *q = p + t.boff[k];
+            size_t off = t.boff[k];
             for (Col c : b.cols) {
+                const int sz = b.dt.size;
                 switch (b.dt.kind) {
                 case 'f': {
-                    const double v = c == PIDENT ? t.pident[i] : c == EVALUE ? t.evalue[i] : r.hsp.bits10 / 10.0;
-                    std::memcpy(q, &v, 8);
+                    const double *v = c == PIDENT ? t.pident.data() : c == EVALUE ? t.evalue.data() : t.bits.data();
+                    put_col<double>(out, rec, off, v, i0, i1);
                     break;
                 }
-                case 'b': *q = r.reverse ? 1 : 0; break;
-                case 'S': {
-                    const char *s = r.hsp.strand ? "minus" : "plus";
-                    const size_t L = std::strlen(s);
-                    std::memset(q, 0, (size_t)b.dt.size);
-                    std::memcpy(q, s, std::min<size_t>(L, (size_t)b.dt.size));
-                    break;
-                }
-                default: {
-                    if (b.categorical) {
-                        *q = 0;   // the one category's code
-                        break;
+                case 'b': put_col<uint8_t>(out, rec, off, t.rev.data(), i0, i1); break;
+                case 'S':
+                    for (uint64_t i = i0; i < i1; i++) {
+                        char *q = out + i * rec + off;
+                        const char *sv = t.minus[i] ? "minus" : "plus";
+                        std::memset(q, 0, (size_t)sz);
+                        std::memcpy(q, sv, std::min<size_t>(std::strlen(sv), (size_t)sz));
                     }
-                    const int64_t v = int_value(r, c);
-                    std::memcpy(q, &v, (size_t)b.dt.size);   // little endian: the low bytes
+                    break;
+                default:
+                    if (b.categorical) {   // the one category's code
+                        for (uint64_t i = i0; i < i1; i++) out[i * rec + off] = 0;
+                    } else {
+                        const int32_t *v = t.ic[c].data();
+                        if (sz == 1) put_col<uint8_t>(out, rec, off, v, i0, i1);
+                        else if (sz == 2) put_col<uint16_t>(out, rec, off, v, i0, i1);
+                        else if (sz == 4) put_col<uint32_t>(out, rec, off, v, i0, i1);
+                        else put_col<int64_t>(out, rec, off, v, i0, i1);
+                    }
                 }
-                }
-                q += b.dt.size;
+                off += (size_t)sz;
             }
         }
     }
@@ -656,18 +675,15 @@ static std::string build_table_file(Table &t, const std::string &ssample, const 
     // column dtypes
     t.coldt[PIDENT] = t.coldt[EVALUE] = t.coldt[BITSCORE] = DType{'f', 8};
     t.coldt[REVERSE] = DType{'b', 1};
-    bool minus = false;
-    for (uint64_t i = 0; i < n; i++) minus = minus || t.rows[i].hsp.strand != 0;
-    bool plus = false;
-    for (uint64_t i = 0; i < n; i++) plus = plus || t.rows[i].hsp.strand == 0;
-    t.coldt[SSTRAND] = DType{'S', minus ? 5 : (plus ? 4 : 1)};
+    uint64_t nminus = 0;
+    for (uint64_t i = 0; i < n; i++) nminus += t.minus[i];
+    t.coldt[SSTRAND] = DType{'S', nminus ? 5 : (n ? 4 : 1)};
     for (Col c : INT_COLS) {
-        int64_t mn = 0, mx = 0;
-        if (n) mn = mx = int_value(t.rows[0], c);
+        const int32_t *v = t.ic[c].data();
+        int32_t mn = n ? v[0] : 0, mx = mn;
         for (uint64_t i = 1; i < n; i++) {
-            const int64_t v = int_value(t.rows[i], c);
-            mn = v < mn ? v : mn;
-            mx = v > mx ? v : mx;
+            mn = v[i] < mn ? v[i] : mn;
+            mx = v[i] > mx ? v[i] : mx;
         }
         t.coldt[c] = downcast(mn, mx, n == 0);
     }
@@ -754,6 +770,27 @@ int od2_write_table(const rc_row *rows, uint64_t n, const std::string &ssample, 
     t.n = n;
     t.pident.resize(n);
     t.evalue.resize(n);
+    t.bits.resize(n);
+    t.label.resize(n);
+    t.rev.resize(n);
+    t.minus.resize(n);
+    for (od2::Col c : od2::INT_COLS) t.ic[c].resize(n);
+    using namespace od2;
+    int32_t *cl = t.ic[LENGTH].data(), *cm = t.ic[MISMATCH].data(), *cg = t.ic[GAPOPEN].data(),
+            *cqs = t.ic[QSTART].data(), *cqe = t.ic[QEND].data(), *css = t.ic[SSTART].data(),
+            *cse = t.ic[SEND].data(), *cgp = t.ic[GAPS].data(), *cni = t.ic[NIDENT].data(),
+            *cqg = t.ic[QGENE].data(), *cqi = t.ic[QISO].data(), *csg = t.ic[SGENE].data(), *csi = t.ic[SISO].data();
+    for (uint64_t i = 0; i < n; i++) {
+        const rc_row &r = rows[i];
+        cl[i] = r.hsp.length; cm[i] = r.hsp.mismatch; cg[i] = r.hsp.gapopen;
+        cqs[i] = r.hsp.qstart; cqe[i] = r.hsp.qend; css[i] = r.hsp.sstart; cse[i] = r.hsp.send;
+        cgp[i] = r.hsp.gaps; cni[i] = r.hsp.nident;
+        cqg[i] = r.qgene; cqi[i] = r.qiso; csg[i] = r.sgene; csi[i] = r.siso;
+        t.bits[i] = r.hsp.bits10 / 10.0;
+        t.label[i] = r.label;
+        t.rev[i] = r.reverse ? 1 : 0;
+        t.minus[i] = r.hsp.strand ? 1 : 0;
+    }
     // a table holds few distinct (nident, length) pairs and e-values: print
     // and parse each once (as tables.py does with np.unique)
     std::unordered_map<uint64_t, double> pmemo, ememo;

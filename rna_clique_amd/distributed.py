@@ -235,10 +235,10 @@ def exchange_dust(eng, process_group=None, force=False):
         eng.set_dust_masks(everyone, allt.numpy().view(np.uint64))
 
 
-def sharded_run(eng, process_group=None):
+def sharded_run(eng, process_group=None, trim=None):
     """rc_run for a sharded engine: DUST masks made once across the ranks,
-    align + RBH locally, exchange, graph."""
+    align + RBH locally, exchange (`trim`: see exchange_edges), graph."""
     exchange_dust(eng, process_group)
     eng.align()
     eng.finish()
-    exchange_edges(eng, process_group)
+    exchange_edges(eng, process_group, trim=trim)

@@ -34,32 +34,46 @@ from .similarity import NoIdealComponentsError, SampleSimilarity  # noqa: F401
 from .transcripts import TranscriptID, TranscriptIDParseError, default_gene_re  # noqa: F401
 
 
-def select_all(dirs, out_dir_1, transcripts, top_genes, id_parser, jobs=1):
+def select_iter(dirs, out_dir_1, transcripts, top_genes, id_parser, jobs=1):
     """select_top_and_save over every input directory (filtering_step.py:
-    129-143), in input order."""
+    129-143) on `jobs` threads, yielded in input order as each completes."""
     dirs = [Path(d) for d in dirs]
     Path(out_dir_1).mkdir(parents=True, exist_ok=True)
     work = lambda d: select_top_sample(out_dir_1, transcripts, d, top_genes, id_parser)  # noqa: E731
     if jobs <= 1 or len(dirs) <= 1:
-        return [work(d) for d in dirs]
+        yield from (work(d) for d in dirs)
+        return
     with ThreadPoolExecutor(max_workers=min(jobs, len(dirs))) as ex:
-        return list(ex.map(work, dirs))
+        yield from ex.map(work, dirs)
+
+
+def select_all(dirs, out_dir_1, transcripts, top_genes, id_parser, jobs=1):
+    """select_iter as a list."""
+    return list(select_iter(dirs, out_dir_1, transcripts, top_genes, id_parser, jobs))
 
 
 def run_engine(samples, top_matches=1, evalue=1e-99, keep_all=True, device=0,
-               process_group=None, **engine_kwargs) -> Engine:
+               process_group=None, loaded=None, **engine_kwargs) -> Engine:
     """Load the samples (labels = top-genes FASTA paths) and run the whole
     path. With an initialised torch.distributed group of size > 1 the sample
-    pairs are sharded across ranks (see distributed.py)."""
+    pairs are sharded across ranks (see distributed.py). `samples` may be an
+    iterator (one GPU: each sample goes to the device as it arrives, beside
+    the selection of the next ones); `loaded(list)` is called with all of them
+    before the run."""
     from . import distributed
     world, rank = distributed.world(process_group)
     eng = Engine(top_matches=top_matches, keep_all=keep_all, evalue=evalue,
                  device=device, shard_rank=rank, shard_count=world, **engine_kwargs)
-    # a shard holds the sequences of its own pairs' samples only
-    need = distributed.needed_samples([int(s.tx_offsets[-1]) for s in samples], world, rank) \
-        if world > 1 else range(len(samples))
+    if world > 1:
+        # a shard holds the sequences of its own pairs' samples only
+        samples = list(samples)
+        need = distributed.needed_samples([int(s.tx_offsets[-1]) for s in samples], world, rank)
+    got = []
     for i, s in enumerate(samples):
-        eng.add_sample(str(s.path), s.seq if i in need else None, s.tx_offsets, s.gene, s.iso)
+        eng.add_sample(str(s.path), s.seq if world == 1 or i in need else None, s.tx_offsets, s.gene, s.iso)
+        got.append(s)
+    if loaded is not None:
+        loaded(got)
     if world == 1:
         eng.run()
     else:
@@ -93,10 +107,16 @@ def rna_clique(
     Returns (SampleSimilarity, {top-genes FASTA path: sample name})."""
     import time
     t0 = time.perf_counter()
-    samples = select_all(dirs, out_dir_1, transcripts, top_genes, id_parser, max(1, jobs))
-    t1 = time.perf_counter()
+    # the selection of later samples runs beside the upload of earlier ones
+    got, t1 = [], [0.0]
+
+    def loaded(ss):
+        got.extend(ss)
+        t1[0] = time.perf_counter()
+    eng = run_engine(select_iter(dirs, out_dir_1, transcripts, top_genes, id_parser, max(1, jobs)),
+                     top_matches, evalue, keep_all, device, process_group, loaded=loaded)
+    samples, t1 = got, t1[0]
     pts = {s.path: s.name for s in samples}
-    eng = run_engine(samples, top_matches, evalue, keep_all, device, process_group)
     t2 = time.perf_counter()
     sim = SampleSimilarity.from_engine(eng, store_dfs=store_dfs)
     from . import distributed
@@ -125,5 +145,6 @@ def rna_clique(
 
 
 # wall-clock phases of the last rna_clique() call in this process (seconds):
-# top-gene selection, engine (load + GPU path), od2 tables, graph.pkl, matrix.h5
+# top-gene selection with the inputs' upload beside it, engine (GPU path),
+# od2 tables, graph.pkl, matrix.h5
 last_timings: dict = {}

@@ -24,10 +24,18 @@ Checks (any failure: exit 1):
 * HBM: each rank's engine peak against distributed.hbm_footprint's model,
   the graph engine's device bytes against its own model.
 
+Outputs (--outputs DIR): each rank writes the od2 gene matches tables of the
+pairs it owns (find_all_pairs.write_pair_tables: pandas table-format HDF5,
+find_all_pairs.py:87,90-117) and the graph engine -- every rank after the
+exchange, rank 0 writing -- graph.pkl (build_graph over all pairs' edges,
+filtering_step.py:157-159), timed, with their bytes; each rank's files are
+deleted once measured (C5's tables are ~2 x 10^8 rows per rank).
+
 Writes one JSON (per-rank time table, projection of 8-GPU pairs/s from the
 slowest rank, checks) to --out; prints progress lines meanwhile.
 
-    python scripts/c5_full.py [--config C5] [--shards 8] [--oracle-pairs 2] [--out gpurun_out/c5_full.json]
+    python scripts/c5_full.py [--config C5] [--shards 8] [--oracle-pairs 2] [--outputs DIR]
+                              [--out gpurun_out/c5_full.json]
 """
 from __future__ import annotations
 
@@ -72,6 +80,8 @@ def main():
     ap.add_argument("--shards", type=int, default=8)
     ap.add_argument("--oracle-pairs", type=int, default=2, help="pairs per rank checked against the oracle")
     ap.add_argument("--out", default="gpurun_out/c5_full.json")
+    ap.add_argument("--outputs", default=None, help="scratch directory: write (and time) every rank's od2 "
+                                                     "tables and graph.pkl there")
     args = ap.parse_args()
     # torch's HIP runtime first, then librcgpu.so (bench.shard_emulation)
     import torch
@@ -124,6 +134,20 @@ def main():
             t2 = time.perf_counter()
         tm = eng.timings()
         own = eng.owned_pairs()
+        outw = None
+        if args.outputs:
+            # this rank's od2 tables (the pairs it owns), then deleted
+            import shutil
+            from rna_clique_amd.find_all_pairs import write_pair_tables
+            d = os.path.join(args.outputs, f"od2_r{r}")
+            with Heartbeat(f"rank {r}/{S}: od2 tables"):
+                t0w = time.perf_counter()
+                paths = write_pair_tables(eng, [s.name for s in samples], d, lambda x: x, "h5", 16)
+                tw = time.perf_counter() - t0w
+            nbytes = sum(os.path.getsize(pth) for pth in paths.values())
+            outw = {"tables": len(paths), "tables_s": round(tw, 2), "tables_gb": round(nbytes / 1e9, 2),
+                    "rows": int(eng.stats()["table_rows"])}
+            shutil.rmtree(d, ignore_errors=True)
         if own != order[int(first[r]):int(first[r + 1])]:
             failures.append(f"rank {r}: owned pairs differ from the plan")
         edges = eng.export_edges()
@@ -149,7 +173,7 @@ def main():
                "ext_deferred": tm["ext_deferred"], "candidates": st["candidates"], "hsps": st["hsps"],
                "edges": int(len(edges) // Engine.edge_record_size()),
                "engine_peak_gb": round(tm["dev_peak_bytes"] / 1e9, 2), "hbm_model_gb": round(model[r] / 1e9, 2),
-               "picks": picks}
+               "picks": picks, "outputs": outw}
         ranks.append(row)
         print(json.dumps(row), flush=True)
         eng.close()
@@ -186,6 +210,17 @@ def main():
             print(f"distance: {ex}", flush=True)
             labels, mat = None, None
         gtm = g.timings()
+        graph_out = None
+        if args.outputs:
+            # graph.pkl from the exchanged edges (rank 0 writes it), then deleted
+            from rna_clique_amd.similarity import SampleSimilarity
+            gp = os.path.join(args.outputs, "graph.pkl")
+            t0w = time.perf_counter()
+            SampleSimilarity.from_engine(g).write_graph(gp)
+            graph_out = {"graph_pkl_s": round(time.perf_counter() - t0w, 2),
+                         "graph_pkl_gb": round(os.path.getsize(gp) / 1e9, 2)}
+            os.remove(gp)
+            print(json.dumps({"graph_pkl": graph_out}), flush=True)
         unum, uden = g.pair_sums(unfiltered=True)
         num, den = g.pair_sums()
         g_bytes = gtm["dev_bytes"]
@@ -224,7 +259,7 @@ def main():
     out = {
         "config": args.config, "samples": N, "pairs": len(order), "shards": S,
         "ranks": ranks,
-        "graph": {"edges": n_edges, "import_s": round(t_graph, 3), "stats": gst,
+        "graph": {"edges": n_edges, "import_s": round(t_graph, 3), "stats": gst, "outputs": graph_out,
                   "device_gb": round(g_bytes / 1e9, 2), "model_gb": round(g_model / 1e9, 2),
                   "graph_ms": round(gtm["graph_ms"], 1), "reduce_ms": round(gtm["reduce_ms"], 1)},
         "matrix": None if mat is None else {

@@ -115,6 +115,26 @@ def test_dust_masks_once_per_sample(native, shards):
             assert e.hsps(b, a).tobytes() == ref.hsps(b, a).tobytes()
 
 
+def test_dust_masks_in_several_passes(native, monkeypatch):
+    """rc_dust_masks over more bases than one alignment tile holds (a C5
+    rank masks ~4 Gbp): the samples go through as many mask passes as the
+    tile limit needs (forced small here), repeats included, with the same
+    words as one pass."""
+    from rna_clique_amd.engine import Engine
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(5, 120, seed=19, p_iso2=0.2, polya=(0.5, 12, 40))
+    order = [3, 0, 4, 1, 3]
+    one = _load(Engine(device=0), samples).dust_masks(order)
+    per = max(len(s.seq) for s in samples)
+    monkeypatch.setenv("RC_TILE_BASES", str(2 * per))
+    eng = _load(Engine(device=0, shard_rank=1, shard_count=3), samples)
+    need = sorted({s for p in eng.owned_pairs() for s in p})
+    many = eng.dust_masks([s for s in order if s in need])
+    ref = np.concatenate([one[sum((len(samples[t].seq) + 63) // 64 for t in order[:i]):][:(len(samples[s].seq) + 63) // 64]
+                          for i, s in enumerate(order) if s in need])
+    assert many.tobytes() == ref.tobytes() and many.any()
+
+
 def _top_select(sample, top):
     """Top-gene rule restated: max coverage per gene, heapq.nlargest((cov, gene))."""
     best = defaultdict(float)
@@ -552,7 +572,14 @@ def _rccl_worker(port, q):
         # buffers, all-gather, rc_set_dust_masks from the device
         distributed.exchange_dust(eng, force=True)
         distributed.sharded_run(eng)        # RCCL branch: device export, all-gather, device import
-        q.put((eng.distance()[1].tobytes(), eng.hsps(0, 1).tobytes(), eng.hsps(1, 0).tobytes()))
+        got = (eng.distance()[1].tobytes(), eng.hsps(0, 1).tobytes(), eng.hsps(1, 0).tobytes())
+        # again with the alignment working set freed before the exchange
+        # (rc_trim), then a third run that allocates it anew
+        distributed.sharded_run(eng, trim=True)
+        again = (eng.distance()[1].tobytes(), eng.hsps(0, 1).tobytes(), eng.hsps(1, 0).tobytes())
+        distributed.sharded_run(eng)
+        third = (eng.distance()[1].tobytes(), eng.hsps(0, 1).tobytes(), eng.hsps(1, 0).tobytes())
+        q.put(got if got == again == third else None)
     finally:
         dist.destroy_process_group()
 
@@ -580,3 +607,55 @@ def test_rccl_exchange_world1(native):
     p.join(timeout=120)
     assert p.exitcode == 0
     assert got == (ref.distance()[1].tobytes(), ref.hsps(0, 1).tobytes(), ref.hsps(1, 0).tobytes())
+
+
+def test_trim_and_edge_parts(native):
+    """rc_trim frees the alignment working set of a finished run (device
+    bytes drop; rows, HSPs and distances stay readable and unchanged; the
+    next run allocates it again and gives the same results), and
+    rc_import_edge_parts takes padded blocks -- from the host or the device,
+    device records range-checked on the device."""
+    import torch
+    from rna_clique_amd._native import NativeError
+    from rna_clique_amd.engine import Engine
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(4, 120, seed=43, p_iso2=0.2, polya=(0.3, 12, 40))
+    eng = _load(Engine(device=0), samples)
+    eng.run()
+    pairs = list(itertools.combinations(range(4), 2))
+    rows = {p: eng.pair_rows(*p).tobytes() for p in pairs}
+    hs = eng.hsps(3, 1).tobytes()
+    dist0 = eng.distance()[1]
+    edges = eng.export_edges()
+    before = eng.timings()["dev_bytes"]
+    eng.trim()
+    after = eng.timings()["dev_bytes"]
+    assert after < before - (64 << 20), (before, after)
+    assert {p: eng.pair_rows(*p).tobytes() for p in pairs} == rows and eng.hsps(3, 1).tobytes() == hs
+    assert np.array_equal(eng.distance()[1], dist0)
+    with pytest.raises(NativeError):
+        eng.dust_mask(0)   # no tile loaded after a trim
+    rs = Engine.edge_record_size()
+    recs = edges.reshape(-1, rs)
+    n = len(recs)
+    counts = [n // 3, n // 3, n - 2 * (n // 3)]
+    stride = max(counts) + 7
+    buf = np.full((3 * stride, rs), 0xAB, dtype=np.uint8)   # padding is garbage, never read
+    o = 0
+    for r, c in enumerate(counts):
+        buf[r * stride:r * stride + c] = recs[o:o + c]
+        o += c
+    eng.import_edge_parts(buf.ravel(), counts, stride)
+    assert np.array_equal(eng.distance()[1], dist0)
+    dev = torch.from_numpy(buf.ravel().copy()).cuda()
+    eng.import_edge_parts(dev, counts, stride)
+    assert np.array_equal(eng.distance()[1], dist0)
+    bad = buf.copy()
+    bad[stride + 1, 0:4] = 0xFF   # node id a out of range in block 1
+    with pytest.raises(NativeError, match="out of range"):
+        eng.import_edge_parts(torch.from_numpy(bad.ravel()).cuda(), counts, stride)
+    with pytest.raises(NativeError, match="out of range"):
+        eng.import_edge_parts(bad.ravel(), counts, stride)
+    eng.run()   # the working set allocated again
+    assert {p: eng.pair_rows(*p).tobytes() for p in pairs} == rows and eng.hsps(3, 1).tobytes() == hs
+    assert np.array_equal(eng.distance()[1], dist0)
