@@ -1,4 +1,4 @@
-"""One summary line of a bench JSON (scripts/gpu_ab_env.sh)."""
+"""One summary line of a bench JSON (A/B runs through scripts/gpu.sh)."""
 import json
 import sys
 

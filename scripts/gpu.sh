@@ -13,6 +13,9 @@
 #   e2e[:CFG]        bench.py with the wall-clock leg, no CPU baseline
 #   stats[:CFG]      rocprofv3 --kernel-trace --stats of bench.py --config CFG
 #   pmc[:CFG]        the PMC passes of scripts/gpu_pmc.sh (same-source counters)
+#   pmcx:CFG:G1;G2   PMC passes with the given counter groups (';' between passes,
+#                    ',' between counters), one rocprofv3 run each
+#   counters         rocprofv3 -L (the counters this box's agent has)
 #   shard:CFG:R/S    bench.py --shard R/S --config CFG (1 step, 1 warmup)
 #   shardprof:CFG:R/S  the same under rocprofv3 --kernel-trace --hip-trace --stats
 #   c5full[:CFG]     scripts/c5_full.py (default C5s)
@@ -47,6 +50,12 @@ for step in "$@"; do
     stats) c=${a:-C3}
            run 600 "$D/${c}_stats.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$D/${c}_stats" -o run -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e || exit $? ;;
     pmc) c=${a:-C3}; log "bash scripts/gpu_pmc.sh $c  (-> gpurun_out/pmc_$c)"; bash scripts/gpu_pmc.sh "$c" || exit $? ;;
+    pmcx) IFS=';' read -ra groups <<< "$b"; i=0
+          for grp in "${groups[@]}"; do
+            i=$((i+1))
+            run 300 "$D/pmcx_${a}_p$i.log" rocprofv3 --kernel-trace --pmc ${grp//,/ } --output-format csv -d "$D/pmcx_$a/p$i" -o run -- python3 bench.py --config "$a" --steps 1 --warmup 0 --no-cpu-baseline --no-e2e || exit $?
+          done ;;
+    counters) run 120 "$D/counters.txt" rocprofv3 -L || exit $? ;;
     shard) run 900 "$D/${a}_shard${b//\//of}.json" python -u bench.py --shard "$b" --config "$a" --steps 1 --warmup 1 || exit $? ;;
     shardprof) P="$D/${a}_shardprof${b//\//of}"
            run 900 "$P.log" rocprofv3 --kernel-trace --hip-trace --stats --output-format csv -d "$P" -o run -- python3 -u bench.py --shard "$b" --config "$a" --steps 1 --warmup 1 || exit $?
