@@ -33,6 +33,9 @@
 // od2_tables.cpp: one pair's gene matches table file
 int od2_write_table(const rc_row *rows, uint64_t n, const std::string &ssample, const std::string &qsample,
                     const std::string &path);
+// graph_pickle.cpp: a table of the pickle whose gene arrays the caller fills
+extern "C" int graph_pickle_table(rc_gpickle *g, int32_t ssample, int32_t qsample, uint64_t n, int64_t **sgene,
+                                  int64_t **qgene);
 
 namespace rcg {
 void launch_pack(const uint8_t *, uint64_t, uint64_t, uint64_t *, uint64_t *, uint64_t *, uint64_t *, hipStream_t);
@@ -3224,7 +3227,6 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
             g = nullptr;
             ok = false;
         }
-        std::vector<int64_t> sg, qg;
         for (;;) {
             std::pair<int, std::shared_ptr<PairRaw>> job;
             {
@@ -3237,18 +3239,20 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
             const PairRaw &raw = *job.second;
             const long long a0 = now_ns();
             const size_t n = raw.n;
-            sg.resize(n);
-            qg.resize(n);
-            for (size_t i = 0; i < n; i++) {
-                const DHsp &d = raw.hs[i];
-                const bool rev = raw.rows[i].reverse != 0;
-                qg[i] = e->tx_gene_id[rev ? d.s_tx : d.q_tx];   // qgene: the transcript of s2
-                sg[i] = e->tx_gene_id[rev ? d.q_tx : d.s_tx];
-            }
-            if (ok && rc_graph_pickle_add(g, raw.s1, raw.s2, sg.data(), qg.data(), n) != RC_OK) {
+            // the table's gene arrays, written in place (node numbering and
+            // edges happen in parallel when the pickle is written)
+            int64_t *sg = nullptr, *qg = nullptr;
+            if (ok && graph_pickle_table(g, raw.s1, raw.s2, n, &sg, &qg) != RC_OK) {
                 set_err(RC_E_LIMIT);
                 ok = false;
             }
+            if (ok)
+                for (size_t i = 0; i < n; i++) {
+                    const DHsp &d = raw.hs[i];
+                    const bool rev = raw.rows[i].reverse != 0;
+                    qg[i] = e->tx_gene_id[rev ? d.s_tx : d.q_tx];   // qgene: the transcript of s2
+                    sg[i] = e->tx_gene_id[rev ? d.q_tx : d.s_tx];
+                }
             t_gadd += now_ns() - a0;
             {
                 std::lock_guard<std::mutex> lk(mu);

@@ -144,16 +144,19 @@ struct Raw {
 };
 
 struct rc_gpickle {
-    NodeMap nodes;                                 // genes outside [0, DENSE)
-    std::vector<std::vector<uint32_t>> dense;      // per sample: gene -> node id + 1
+    NodeMap nodes;                                 // genes outside [0, DENSE) (sequential numbering)
+    std::vector<std::vector<uint32_t>> dense;      // per sample: gene -> node id + 1 (sequential numbering)
     static constexpr int64_t DENSE = 1 << 26;
     std::vector<NodeKey> node;                     // insertion order
-    // every row's (s-node, q-node), tables in call order; the edges (first
-    // occurrences) are picked at write time, in parallel: an edge joins two
-    // samples' genes, so only tables of the same sample pair can repeat it
+    // the tables as given (their gene arrays), in call order; node ids
+    // (first occurrences in build_graph's order) and edges (first occurrences
+    // of each node pair) are found at write time, in parallel: an edge joins
+    // two samples' genes, so only tables of the same sample pair can repeat it
     struct Tab {
+        int32_t ss, qs;   // s- and q-sample
         int32_t lo, hi;   // the sample pair (unordered)
         uint64_t off, n;  // its rows (a running row count over the tables)
+        Raw<int64_t> sg, qg;
         Raw<uint32_t> su, qu;
     };
     uint64_t rows = 0;
@@ -247,48 +250,171 @@ int rc_graph_pickle_begin(rc_gpickle **g)
 
 void rc_graph_pickle_free(rc_gpickle *g) { delete g; }
 
-int rc_graph_pickle_add(rc_gpickle *g, int32_t ssample, int32_t qsample, const int64_t *sgene, const int64_t *qgene,
-                        uint64_t n)
+// a table's gene arrays, to be filled by the caller (rc_write_outputs'
+// graph thread writes them in place); see rc_graph_pickle_add
+int graph_pickle_table(rc_gpickle *g, int32_t ssample, int32_t qsample, uint64_t n, int64_t **sgene, int64_t **qgene)
 {
-    if (!g || (n && (!sgene || !qgene))) return rcg_fail(RC_E_ARG, "null argument");
-    auto node_id = [&](int32_t s, int64_t gene) {
-        bool added = false;
-        const NodeKey k{gene, s};
-        if (s >= 0 && gene >= 0 && gene < rc_gpickle::DENSE) {
-            if ((size_t)s >= g->dense.size()) g->dense.resize((size_t)s + 1);
-            std::vector<uint32_t> &d = g->dense[s];
-            if ((size_t)gene >= d.size()) d.resize(std::max<size_t>((size_t)gene + 1, d.size() * 2), 0);
-            if (!d[gene]) {
-                d[gene] = (uint32_t)g->node.size() + 1;
-                g->node.push_back(k);
-            }
-            return d[gene] - 1;
-        }
-        const uint32_t id = g->nodes.get_or_add(k, (uint32_t)g->node.size(), added);
-        if (added) g->node.push_back(k);
-        return id;
-    };
-    // build_graph's insertion order: the table's s-nodes, then its q-nodes
     rc_gpickle::Tab T;
+    T.ss = ssample;
+    T.qs = qsample;
     T.lo = std::min(ssample, qsample);
     T.hi = std::max(ssample, qsample);
     T.off = g->rows;
     T.n = n;
-    T.su = Raw<uint32_t>(n);
-    T.qu = Raw<uint32_t>(n);
-    for (uint64_t i = 0; i < n; i++) T.su[i] = node_id(ssample, sgene[i]);
-    for (uint64_t i = 0; i < n; i++) T.qu[i] = node_id(qsample, qgene[i]);
+    T.sg = Raw<int64_t>(n);
+    T.qg = Raw<int64_t>(n);
+    *sgene = T.sg.data();
+    *qgene = T.qg.data();
     g->tabs.push_back(std::move(T));
     g->rows += n;
-    if (g->node.size() >= 0x7FFFFFFFull || g->rows >= 0xFFFFFFFFull)
+    if (g->tabs.size() >= 0x7FFFFFFFull || g->rows >= 0xFFFFFFFFull)
         return rcg_fail(RC_E_LIMIT, "graph too large for the pickle writer");
     return RC_OK;
+}
+
+int rc_graph_pickle_add(rc_gpickle *g, int32_t ssample, int32_t qsample, const int64_t *sgene, const int64_t *qgene,
+                        uint64_t n)
+{
+    if (!g || (n && (!sgene || !qgene))) return rcg_fail(RC_E_ARG, "null argument");
+    int64_t *sg = nullptr, *qg = nullptr;
+    const int rc = graph_pickle_table(g, ssample, qsample, n, &sg, &qg);
+    if (n) {
+        std::memcpy(sg, sgene, n * 8);
+        std::memcpy(qg, qgene, n * 8);
+    }
+    return rc;
+}
+
+// Node ids in build_graph's insertion order (per table its s-nodes, then its
+// q-nodes, tables in call order): a node's id is the rank of its first
+// occurrence. Dense genes (every gene in [0, DENSE) and the per-sample gene
+// ranges not much larger than the rows): the first occurrence of each
+// (sample, gene) slot by an atomic min over all rows in parallel, the slots
+// ordered by it. Otherwise the sequential walk with a hash map.
+static void number_nodes(rc_gpickle *g)
+{
+    const size_t nt = g->tabs.size();
+    int32_t ns = 0;
+    bool dense = true;
+    for (auto &T : g->tabs) {
+        dense = dense && T.ss >= 0 && T.qs >= 0;
+        ns = std::max(ns, std::max(T.ss, T.qs) + 1);
+    }
+    std::vector<int64_t> gmax((size_t)ns, -1);
+    if (dense) {
+        std::vector<int64_t> tmin(nt, 0), tsmax(nt, -1), tqmax(nt, -1);
+        parallel_for(nt, [&](size_t t) {
+            const rc_gpickle::Tab &T = g->tabs[t];
+            int64_t mn = 0, sx = -1, qx = -1;
+            for (uint64_t i = 0; i < T.n; i++) {
+                mn = std::min(mn, std::min(T.sg[i], T.qg[i]));
+                sx = std::max(sx, T.sg[i]);
+                qx = std::max(qx, T.qg[i]);
+            }
+            tmin[t] = mn;
+            tsmax[t] = sx;
+            tqmax[t] = qx;
+        });
+        for (size_t t = 0; t < nt; t++) {
+            dense = dense && tmin[t] >= 0;
+            gmax[g->tabs[t].ss] = std::max(gmax[g->tabs[t].ss], tsmax[t]);
+            gmax[g->tabs[t].qs] = std::max(gmax[g->tabs[t].qs], tqmax[t]);
+        }
+    }
+    std::vector<uint64_t> base((size_t)ns + 1, 0);
+    for (int32_t k = 0; k < ns; k++) {
+        dense = dense && gmax[k] < rc_gpickle::DENSE;
+        base[k + 1] = base[k] + (uint64_t)(gmax[k] + 1);
+    }
+    dense = dense && base[ns] <= 4 * g->rows + (1u << 24);
+    if (!dense) {
+        for (auto &T : g->tabs) {
+            auto node_id = [&](int32_t s, int64_t gene) {
+                bool added = false;
+                const NodeKey k{gene, s};
+                if (s >= 0 && gene >= 0 && gene < rc_gpickle::DENSE) {
+                    if ((size_t)s >= g->dense.size()) g->dense.resize((size_t)s + 1);
+                    std::vector<uint32_t> &d = g->dense[s];
+                    if ((size_t)gene >= d.size()) d.resize(std::max<size_t>((size_t)gene + 1, d.size() * 2), 0);
+                    if (!d[gene]) {
+                        d[gene] = (uint32_t)g->node.size() + 1;
+                        g->node.push_back(k);
+                    }
+                    return d[gene] - 1;
+                }
+                const uint32_t id = g->nodes.get_or_add(k, (uint32_t)g->node.size(), added);
+                if (added) g->node.push_back(k);
+                return id;
+            };
+            T.su = Raw<uint32_t>(T.n);
+            T.qu = Raw<uint32_t>(T.n);
+            for (uint64_t i = 0; i < T.n; i++) T.su[i] = node_id(T.ss, T.sg[i]);
+            for (uint64_t i = 0; i < T.n; i++) T.qu[i] = node_id(T.qs, T.qg[i]);
+        }
+        return;
+    }
+    const uint64_t nslot = base[ns];
+    Raw<std::atomic<uint64_t>> first(nslot);
+    parallel_for((nslot + 65535) / 65536, [&](size_t c) {
+        for (uint64_t k = c * 65536; k < std::min<uint64_t>(nslot, (c + 1) * 65536); k++)
+            first[k].store(~0ull, std::memory_order_relaxed);
+    });
+    // occurrence rank (table, side, row)
+    parallel_for(nt, [&](size_t t) {
+        const rc_gpickle::Tab &T = g->tabs[t];
+        auto seen = [&](uint64_t slot, uint64_t r) {
+            uint64_t cur = first[slot].load(std::memory_order_relaxed);
+            while (r < cur && !first[slot].compare_exchange_weak(cur, r, std::memory_order_relaxed)) {
+            }
+        };
+        for (uint64_t i = 0; i < T.n; i++) seen(base[T.ss] + (uint64_t)T.sg[i], ((uint64_t)t << 33) | i);
+        for (uint64_t i = 0; i < T.n; i++) seen(base[T.qs] + (uint64_t)T.qg[i], ((uint64_t)t << 33) | (1ull << 32) | i);
+    });
+    // the occurring slots, ordered by first occurrence
+    const size_t NC = (nslot + 65535) / 65536;
+    std::vector<uint64_t> ccount(NC + 1, 0);
+    parallel_for(NC, [&](size_t c) {
+        uint64_t k0 = 0;
+        for (uint64_t k = c * 65536; k < std::min<uint64_t>(nslot, (c + 1) * 65536); k++)
+            k0 += first[k].load(std::memory_order_relaxed) != ~0ull;
+        ccount[c + 1] = k0;
+    });
+    for (size_t c = 0; c < NC; c++) ccount[c + 1] += ccount[c];
+    const uint64_t nn = ccount[NC];
+    std::vector<std::pair<uint64_t, uint32_t>> occ(nn);   // (first rank, slot)
+    parallel_for(NC, [&](size_t c) {
+        uint64_t w = ccount[c];
+        for (uint64_t k = c * 65536; k < std::min<uint64_t>(nslot, (c + 1) * 65536); k++) {
+            const uint64_t f = first[k].load(std::memory_order_relaxed);
+            if (f != ~0ull) occ[w++] = {f, (uint32_t)k};
+        }
+    });
+    first = Raw<std::atomic<uint64_t>>();
+    std::sort(occ.begin(), occ.end());
+    Raw<uint32_t> id(nslot);
+    g->node.resize(nn);
+    parallel_for((nn + 65535) / 65536, [&](size_t c) {
+        for (uint64_t k = c * 65536; k < std::min<uint64_t>(nn, (c + 1) * 65536); k++) {
+            const uint32_t slot = occ[k].second;
+            id[slot] = (uint32_t)k;
+            const int32_t smp = (int32_t)(std::upper_bound(base.begin(), base.end(), (uint64_t)slot) - base.begin()) - 1;
+            g->node[k] = NodeKey{(int64_t)(slot - base[smp]), smp};
+        }
+    });
+    parallel_for(nt, [&](size_t t) {
+        rc_gpickle::Tab &T = g->tabs[t];
+        T.su = Raw<uint32_t>(T.n);
+        T.qu = Raw<uint32_t>(T.n);
+        for (uint64_t i = 0; i < T.n; i++) T.su[i] = id[base[T.ss] + (uint64_t)T.sg[i]];
+        for (uint64_t i = 0; i < T.n; i++) T.qu[i] = id[base[T.qs] + (uint64_t)T.qg[i]];
+        T.sg = Raw<int64_t>();
+        T.qg = Raw<int64_t>();
+    });
 }
 
 int rc_graph_pickle_write(rc_gpickle *g, const char *path, int32_t n_names, const char *const *names)
 {
     if (!g || !path || (n_names && !names)) return rcg_fail(RC_E_ARG, "null argument");
-    const size_t nn = g->node.size(), nt = g->tabs.size();
     const bool tmg = getenv("RC_OUT_TIMING") && atoi(getenv("RC_OUT_TIMING"));
     auto clk = std::chrono::steady_clock::now();
     auto lap = [&](const char *what) {
@@ -297,6 +423,10 @@ int rc_graph_pickle_write(rc_gpickle *g, const char *path, int32_t n_names, cons
         fprintf(stderr, "graph.pkl %s %.3f s\n", what, std::chrono::duration<double>(t - clk).count());
         clk = t;
     };
+    number_nodes(g);
+    lap("nodes");
+    if (g->node.size() >= 0x7FFFFFFFull) return rcg_fail(RC_E_LIMIT, "graph too large for the pickle writer");
+    const size_t nn = g->node.size(), nt = g->tabs.size();
     for (const NodeKey &k : g->node)
         if (k.sample < 0 || k.sample >= n_names) return rcg_fail(RC_E_ARG, "sample index out of range");
     // 1. the edges: first occurrence of each (s-node, q-node) pair, per

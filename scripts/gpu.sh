@@ -64,7 +64,7 @@ for step in "$@"; do
            python3 scripts/trace_gaps.py "$P" "$T" "$P.gaps.json" > /dev/null; rc=$?
            find "$P" \( -name '*_trace.csv' -o -name '*.db' \) -delete   # (hundreds of MB; the summaries stay)
            [ $rc -eq 0 ] || exit $rc ;;
-    c5full) c=${a:-C5s}; run 1100 "$D/${c}_full.log" python -u scripts/c5_full.py --config "$c" --out "$D/${c}_full.json" || exit $? ;;
+    c5full) c=${a:-C5s}; run 1100 "$D/${c}_full.log" python -u scripts/c5_full.py --config "$c" --outputs /tmp/rc_c5_outputs --out "$D/${c}_full.json" || exit $? ;;
     py) run 900 "$D/$(basename "$a" .py).log" python -u "$a" ${b//,/ } || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
