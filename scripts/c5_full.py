@@ -134,22 +134,6 @@ def main():
             t2 = time.perf_counter()
         tm = eng.timings()
         own = eng.owned_pairs()
-        outw = None
-        if args.outputs:
-            # this rank's od2 tables (the pairs it owns), then deleted
-            import shutil
-            from rna_clique_amd.find_all_pairs import write_pair_tables
-            d = os.path.join(args.outputs, f"od2_r{r}")
-            with Heartbeat(f"rank {r}/{S}: od2 tables"):
-                t0w = time.perf_counter()
-                paths = write_pair_tables(eng, [s.name for s in samples], d, lambda x: x, "h5", 16)
-                tw = time.perf_counter() - t0w
-            nbytes = sum(os.path.getsize(pth) for pth in paths.values())
-            outw = {"tables": len(paths), "tables_s": round(tw, 2), "tables_gb": round(nbytes / 1e9, 2),
-                    "rows": int(eng.stats()["table_rows"])}
-            shutil.rmtree(d, ignore_errors=True)
-        if own != order[int(first[r]):int(first[r + 1])]:
-            failures.append(f"rank {r}: owned pairs differ from the plan")
         edges = eng.export_edges()
         parts.append(edges)
         # the graph phase over the rank's own edges: its unfiltered sums (and
@@ -162,6 +146,21 @@ def main():
             own_usums[(a, b)] = (int(unum[a, b]), int(uden[a, b]))
         picks = sorted({own[0], own[len(own) // 2]})[:args.oracle_pairs] if own else []
         cap = capture_pairs(eng, picks)
+        outw = None
+        if args.outputs:
+            # this rank's od2 tables (the pairs it owns), then deleted
+            import shutil
+            from rna_clique_amd.find_all_pairs import write_pair_tables
+            d = os.path.join(args.outputs, f"od2_r{r}")
+            with Heartbeat(f"rank {r}/{S}: od2 tables"):
+                t0w = time.perf_counter()
+                paths = write_pair_tables(eng, [s.name for s in samples], d, lambda x: x, "h5", 16)
+                tw = time.perf_counter() - t0w
+            nbytes = sum(os.path.getsize(pth) for pth in paths.values())
+            outw = {"tables": len(paths), "tables_s": round(tw, 2), "tables_gb": round(nbytes / 1e9, 2)}
+            shutil.rmtree(d, ignore_errors=True)
+        if own != order[int(first[r]):int(first[r + 1])]:
+            failures.append(f"rank {r}: owned pairs differ from the plan")
         st = eng.stats()
         row = {"rank": r, "pairs": len(own), "resident_samples": len(need),
                "resident_gbp": round(sum(bases[i] for i in need) / 1e9, 3),
@@ -173,7 +172,7 @@ def main():
                "ext_deferred": tm["ext_deferred"], "candidates": st["candidates"], "hsps": st["hsps"],
                "edges": int(len(edges) // Engine.edge_record_size()),
                "engine_peak_gb": round(tm["dev_peak_bytes"] / 1e9, 2), "hbm_model_gb": round(model[r] / 1e9, 2),
-               "picks": picks, "outputs": outw}
+               "picks": picks, "outputs": dict(outw, rows=int(st["table_rows"])) if outw else None}
         ranks.append(row)
         print(json.dumps(row), flush=True)
         eng.close()
