@@ -308,6 +308,13 @@ int rc_set_dust_masks(rc_engine *eng, const int32_t *samples, int32_t n, const u
 int rc_write_outputs(rc_engine *eng, int32_t n_pairs, const int32_t *s1, const int32_t *s2,
                      const char *const *table_paths, const char *graph_path, int32_t threads);
 int rc_table_write_rows(const rc_row *rows, uint64_t n, const char *ssample, const char *qsample, const char *path);
+/* graph.pkl from the engine's graph edges (every pair, in combinations
+ * order: build_graph.py:40-68 over the tables of find_all_pairs' pairs; node
+ * and neighbour order included) -- a single-shard engine after rc_run, a
+ * sharded one after rc_import_edges. The records are sorted on the device;
+ * `threads` host threads build the pickle. RC_E_STATE for an imported graph
+ * with isolated nodes or rows outside the graph. */
+int rc_write_graph(rc_engine *eng, const char *path, int32_t threads);
 
 /* ---- FASTA input (host only; fasta.cpp) ----------------------------------
  * Replaces the Bio.SeqIO passes of TopGeneSelector (select_top_genes.py:108-127)

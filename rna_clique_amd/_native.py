@@ -144,6 +144,7 @@ SIGNATURES = {
     "rc_fasta_select": (ctypes.c_int, [VP, VP, VP, VP]),
     "rc_fasta_write": (ctypes.c_int, [VP, VP, ctypes.c_char_p, ctypes.c_int32]),
     "rc_write_outputs": (ctypes.c_int, [VP, ctypes.c_int32, VP, VP, VP, ctypes.c_char_p, ctypes.c_int32]),
+    "rc_write_graph": (ctypes.c_int, [VP, ctypes.c_char_p, ctypes.c_int32]),
     "rc_table_write_rows": (ctypes.c_int, [VP, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]),
     "rc_graph_pickle_begin": (ctypes.c_int, [P(VP)]),
     "rc_graph_pickle_add": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.c_int32, VP, VP, ctypes.c_uint64]),

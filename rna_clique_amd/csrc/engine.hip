@@ -54,6 +54,8 @@ void os_fill_hist(const TxInfo *tx, uint32_t n_tx, const uint64_t *F, const uint
                   uint64_t n, uint32_t *scratch, hipStream_t st);
 void launch_tx_masked(const TxInfo *, uint32_t, const uint64_t *, uint8_t *, hipStream_t);
 void launch_edge_check(const DEdge *, uint64_t, uint32_t, uint64_t, unsigned int *, hipStream_t);
+void launch_edge_key(const DEdge *, uint64_t, const uint32_t *, uint32_t *, uint32_t *, hipStream_t);
+void launch_edge_gather(const DEdge *, const uint32_t *, uint64_t, DEdge *, hipStream_t);
 void launch_tile_tables(const TileSeg *, uint32_t, uint32_t, const uint64_t *, const uint64_t *, TxInfo *, TxInfo *,
                         uint32_t *, TxInfo *, uint64_t *, uint32_t, uint64_t, uint64_t *, IsoRec *, uint64_t,
                         const uint64_t *, PosTx *, uint64_t, hipStream_t);
@@ -3147,6 +3149,103 @@ int rc_shard_pairs(rc_engine *e, int64_t *first, int64_t *last)
     return RC_OK;
 }
 
+// graph.pkl from the engine's graph edges: build_graph over every pair's
+// table in combinations order (find_all_pairs.py:224-228 as the one-process
+// order; build_graph.py:40-68) needs, per pair, its distinct (s-gene, q-gene)
+// edges in the order of their first table rows -- the order of the edge
+// records of that pair. The records (all pairs: a single-shard run's own, a
+// sharded run's after rc_import_edges) are stably sorted on the device by
+// their pair's combinations rank and copied to the host; tbeg[k] is the first
+// record of the k-th non-empty pair.
+static int sorted_edge_tables(rc_engine *e, std::vector<DEdge> &rec, std::vector<uint64_t> &tbeg)
+{
+    if (!e->finished) return fail(RC_E_STATE, "no results yet");
+    CHK(set_device(e));
+    const uint64_t n = e->n_edges;
+    const int N = (int)e->samples.size();
+    if (n > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "more than 2^32 graph edges");
+    std::vector<uint32_t> comb(e->pair_a.size());
+    for (size_t p = 0; p < comb.size(); p++) {
+        const uint64_t a = (uint64_t)e->pair_a[p], b = (uint64_t)e->pair_b[p];
+        comb[p] = (uint32_t)(a * (2 * (uint64_t)N - a - 1) / 2 + (b - a - 1));
+    }
+    rec.resize(n);
+    tbeg.clear();
+    if (n) {
+        DBuf<uint32_t> dcomb, k0, k1, v0, v1;
+        DBuf<DEdge> out;
+        CHK(dcomb.ensure(comb.size()));
+        CHK(k0.ensure(n));
+        CHK(k1.ensure(n));
+        CHK(v0.ensure(n));
+        CHK(v1.ensure(n));
+        HIPCHK(hipMemcpyAsync(dcomb.p, comb.data(), comb.size() * 4, hipMemcpyHostToDevice, e->st));
+        launch_edge_key(e->d_edges.p, n, dcomb.p, k0.p, v0.p, e->st);
+        HIPCHK(hipGetLastError());
+        size_t tmp = 0;
+        HIPCHK(rocprim::radix_sort_pairs(nullptr, tmp, k0.p, k1.p, v0.p, v1.p, (size_t)n, 0u, 32u, e->st));
+        CHK(e->d_tmp.ensure(tmp));
+        HIPCHK(rocprim::radix_sort_pairs(e->d_tmp.p, tmp, k0.p, k1.p, v0.p, v1.p, (size_t)n, 0u, 32u, e->st));
+        uint32_t last = 0;
+        HIPCHK(hipMemcpyAsync(&last, k1.p + n - 1, 4, hipMemcpyDeviceToHost, e->st));
+        k0.release();
+        v0.release();
+        CHK(out.ensure(n));
+        launch_edge_gather(e->d_edges.p, v1.p, n, out.p, e->st);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(rec.data(), out.p, n * sizeof(DEdge), hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipStreamSynchronize(e->st));
+        if (last == ~0u)
+            return fail(RC_E_STATE, "an imported graph with isolated nodes or rows outside it: no graph.pkl from edges");
+    }
+    for (uint64_t i = 0; i < n; i++)
+        if (i == 0 || rec[i].pair != rec[i - 1].pair) tbeg.push_back(i);
+    tbeg.push_back(n);
+    return RC_OK;
+}
+
+// the pickle of sorted_edge_tables' output (gene arrays filled on `threads`
+// host threads); RC_OK or a code (message set)
+static int write_graph_from_edges(const rc_engine *e, const std::vector<DEdge> &rec, const std::vector<uint64_t> &tbeg,
+                                  const char *path, int threads)
+{
+    rc_gpickle *g = nullptr;
+    if (rc_graph_pickle_begin(&g) != RC_OK) return fail(RC_E_NOMEM, "graph pickle");
+    std::unique_ptr<rc_gpickle, void (*)(rc_gpickle *)> hold(g, rc_graph_pickle_free);
+    const size_t nt = tbeg.empty() ? 0 : tbeg.size() - 1;
+    std::vector<int64_t *> sgp(nt), qgp(nt);
+    for (size_t t = 0; t < nt; t++) {
+        const DEdge &r0 = rec[tbeg[t]];
+        if (graph_pickle_table(g, e->gene_sample[r0.a], e->gene_sample[r0.b], tbeg[t + 1] - tbeg[t], &sgp[t], &qgp[t]) !=
+            RC_OK)
+            return RC_E_LIMIT;
+    }
+    std::atomic<size_t> next{0};
+    auto fill = [&]() {
+        for (size_t t; (t = next.fetch_add(1)) < nt;)
+            for (uint64_t i = tbeg[t]; i < tbeg[t + 1]; i++) {
+                sgp[t][i - tbeg[t]] = e->gene_id[rec[i].a];
+                qgp[t][i - tbeg[t]] = e->gene_id[rec[i].b];
+            }
+    };
+    std::vector<std::thread> th;
+    for (int k = 1; k < std::max(1, threads); k++) th.emplace_back(fill);
+    fill();
+    for (auto &x : th) x.join();
+    std::vector<const char *> names;
+    for (const SampleRec &s : e->samples) names.push_back(s.label.c_str());
+    return rc_graph_pickle_write(g, path, (int32_t)names.size(), names.data());
+}
+
+extern "C" int rc_write_graph(rc_engine *e, const char *path, int32_t threads)
+{
+    if (!e || !path) return fail(RC_E_ARG, "null argument");
+    std::vector<DEdge> rec;
+    std::vector<uint64_t> tbeg;
+    CHK(sorted_edge_tables(e, rec, tbeg));
+    return write_graph_from_edges(e, rec, tbeg, path, std::max(1, std::min(64, (int)threads)));
+}
+
 // The outputs a run writes next to matrix.h5: the od2 gene matches tables of
 // the given pairs (paths[i] for pair (s1[i], s2[i]), table_paths may be NULL)
 // and graph.pkl (graph_path, may be NULL; build_graph's graph over the pairs
@@ -3188,6 +3287,19 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
         }
         cv.notify_all();   // the fetch loop may be waiting for room
     };
+    // graph.pkl over every pair in combinations order comes from the edge
+    // records (sorted on the device first), written on its own thread beside
+    // the tables; other pair lists (and imported graphs) take the rows
+    std::vector<DEdge> grec;
+    std::vector<uint64_t> gbeg;
+    bool edge_graph = false;
+    if (graph_path) {
+        const int N = (int)e->samples.size();
+        bool all = (int64_t)n_pairs == (int64_t)N * (N - 1) / 2;
+        for (int a = 0, k = 0; all && a < N; a++)
+            for (int b = a + 1; all && b < N; b++, k++) all = s1[k] == a && s2[k] == b;
+        edge_graph = all && sorted_edge_tables(e, grec, gbeg) == RC_OK;
+    }
     auto worker = [&]() {
         std::vector<rc_row> buf;
         for (;;) {
@@ -3272,21 +3384,28 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
     // every pair's row range first: the pinned slabs are sized to the largest
     std::vector<uint64_t> ranges(2 * (size_t)n_pairs);
     uint64_t max_rows = 0;
-    for (int i = 0; i < n_pairs; i++) {
+    for (int i = 0; i < n_pairs && (table_paths || !edge_graph); i++) {
         CHK(pair_row_range(e, s1[i], s2[i], ranges[2 * i], ranges[2 * i + 1]));
         max_rows = std::max<uint64_t>(max_rows, ranges[2 * i + 1] - ranges[2 * i]);
     }
     SlabPool slabs;
     slabs.bytes = std::max<uint64_t>(max_rows, 1) * (sizeof(DRow) + sizeof(DHsp));
     slabs.cap = (size_t)(2 * nt + 8);
+    auto edge_grapher = [&]() {
+        const long long w0 = now_ns();
+        const int rc = write_graph_from_edges(e, grec, gbeg, graph_path, 8);
+        if (rc != RC_OK) set_err(rc);
+        t_gwrite += now_ns() - w0;
+    };
     std::vector<std::thread> pool;
     if (table_paths)
         for (int i = 0; i < nt; i++) pool.emplace_back(worker);
-    if (graph_path) pool.emplace_back(grapher);
-    const int per_job = (table_paths ? 1 : 0) + (graph_path ? 1 : 0);
+    if (graph_path) pool.emplace_back(edge_graph ? std::function<void()>(edge_grapher) : std::function<void()>(grapher));
+    const bool row_graph = graph_path && !edge_graph;
+    const int per_job = (table_paths ? 1 : 0) + (row_graph ? 1 : 0);
     const int max_flight = 4 * nt + 4;
     int rc = RC_OK;
-    for (int i = 0; i < n_pairs && rc == RC_OK; i++) {
+    for (int i = 0; i < n_pairs && rc == RC_OK && per_job; i++) {
         {
             std::unique_lock<std::mutex> lk(mu);
             cv.wait(lk, [&] { return in_flight < max_flight * per_job || err != RC_OK; });
@@ -3300,7 +3419,7 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
         {
             std::lock_guard<std::mutex> lk(mu);
             if (table_paths) tq.push_back({i, raw});
-            if (graph_path) gq.push_back({i, raw});
+            if (row_graph) gq.push_back({i, raw});
             in_flight += per_job;
         }
         cv.notify_all();

@@ -1023,6 +1023,34 @@ void launch_edge_check(const DEdge *edges, uint64_t n, uint32_t ng, uint64_t np,
     hipLaunchKernelGGL(edge_check_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, edges, n, ng, np, bad);
 }
 
+// graph.pkl from the edge records: each record's sort key (its pair's rank
+// in combinations order; flagged records -- sums-only rows, isolated nodes of
+// an imported graph -- are marked by ~0u) and its index
+__global__ void edge_key_kernel(const DEdge *edges, uint64_t n, const uint32_t *comb_of_pair, uint32_t *key,
+                                uint32_t *idx)
+{
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t p = edges[i].pair;
+        key[i] = (p & EDGE_SUM_ONLY) || p == NODE_REC ? ~0u : comb_of_pair[p];
+        idx[i] = (uint32_t)i;
+    }
+}
+__global__ void edge_gather_kernel(const DEdge *edges, const uint32_t *idx, uint64_t n, DEdge *out)
+{
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = edges[idx[i]];
+}
+
+void launch_edge_key(const DEdge *edges, uint64_t n, const uint32_t *comb_of_pair, uint32_t *key, uint32_t *idx,
+                     hipStream_t st)
+{
+    if (n) hipLaunchKernelGGL(edge_key_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, edges, n, comb_of_pair, key, idx);
+}
+void launch_edge_gather(const DEdge *edges, const uint32_t *idx, uint64_t n, DEdge *out, hipStream_t st)
+{
+    if (n) hipLaunchKernelGGL(edge_gather_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, edges, idx, n, out);
+}
+
 void launch_gather_rows(const DHsp *hsp, const DRow *rows, uint64_t n, DHsp *out, hipStream_t st)
 {
     if (!n) return;

@@ -207,6 +207,16 @@ class SampleSimilarity:
         engine run whose graph was never built in Python, the native writer
         streams the pairs' rows (tables.write_graph_pickle: the same Graph on
         pickle.load, without per-edge Python inserts)."""
+        if self._graph is None and self.engine is not None:
+            # the engine's edge records, sorted on the device into every
+            # pair's table in combinations order (rc_write_graph)
+            from . import _native
+            try:
+                _native.check(_native.lib().rc_write_graph(self.engine._h, str(path).encode(), 16))
+                return
+            except _native.NativeError as ex:
+                if ex.code != _native.RC_E_STATE:
+                    raise
         if self._graph is None and getattr(self.engine, "shard_count", 1) == 1:
             from .tables import write_engine_outputs
             write_engine_outputs(self.engine, list(self._pairs()), None, path)
