@@ -187,6 +187,13 @@ def test_rna_clique_end_to_end(native, tmp_path):
     with open(tmp_path / "graph.pkl", "rb") as f:
         g = pickle.load(f)
     assert g.number_of_edges() == summary["stats"]["edges"]
+    # ... node, neighbour and edge order included (the file comes from the
+    # edge records sorted on the device; sim.graph is build_graph over the
+    # pairs' rows in combinations order)
+    g_ref = sim.graph
+    assert list(g.nodes) == list(g_ref.nodes)
+    assert all(list(g.adj[n]) == list(g_ref.adj[n]) for n in g_ref.nodes)
+    assert list(g.edges) == list(g_ref.edges)
     assert sim.sample_count == len(samples)
     assert (tmp_path / "matrix.h5").stat().st_size > 0
     # restricted tables sum to the same fractions
