@@ -448,6 +448,7 @@ struct rc_engine {
     // host results
     std::vector<unsigned long long> h_num, h_den, h_num_all, h_den_all, h_stats;
     std::vector<double> h_ss;   // search space of a query of length L against sample T: [T][L]
+    std::vector<double> h_exp;  // exp(-lambda * S / 2) per raw score in half units S (stats::evalue's factor)
     rc_timing tm{};
     hipEvent_t ev[16] = {};
     hipEvent_t evd[3] = {};   // DUST start / end on st2, its start condition on st
@@ -910,6 +911,8 @@ static int upload(rc_engine *e)
             e->h_ss[k] = stats::search_space(L, e->db_len[T], e->db_n[T]);
             thr[k] = L ? stats::threshold(e->h_ss[k], e->o.evalue) : (1 << 26);
         }
+    e->h_exp.resize((size_t)2 * e->max_len + 2);
+    for (size_t sc = 0; sc < e->h_exp.size(); sc++) e->h_exp[sc] = std::exp(-stats::LAMBDA * ((int32_t)sc / 2.0));
     std::vector<int32_t> b10((size_t)2 * e->max_len + 2);
     for (size_t sc = 0; sc < b10.size(); sc++) b10[sc] = stats::bits10((int32_t)sc);
     CHK(up(e->d_thr, thr));
@@ -2419,7 +2422,10 @@ static rc_hsp to_rc_hsp(const rc_engine *e, const DHsp &d, int qs_, int ss_)
     const int64_t qlen = (int64_t)(e->tx_start[d.q_tx + 1] - e->tx_start[d.q_tx]);
     const double ss = qlen <= e->max_len ? e->h_ss[(size_t)ss_ * (e->max_len + 1) + (size_t)qlen]
                                          : stats::search_space(qlen, e->db_len[ss_], e->db_n[ss_]);
-    h.evalue = stats::evalue(ss, d.score_half);
+    // stats::evalue, its exp() taken from the table (the same product, in
+    // the same order: bit-identical)
+    h.evalue = d.score_half >= 0 && (size_t)d.score_half < e->h_exp.size() ? ss * stats::K * e->h_exp[d.score_half]
+                                                                            : stats::evalue(ss, d.score_half);
     return h;
 }
 

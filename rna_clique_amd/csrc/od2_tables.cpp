@@ -23,6 +23,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
+#include <algorithm>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -791,26 +793,40 @@ int od2_write_table(const rc_row *rows, uint64_t n, const std::string &ssample, 
         t.rev[i] = r.reverse ? 1 : 0;
         t.minus[i] = r.hsp.strand ? 1 : 0;
     }
-    // a table holds few distinct (nident, length) pairs and e-values: print
-    // and parse each once (as tables.py does with np.unique)
-    std::unordered_map<uint64_t, double> pmemo, ememo;
+    // few distinct (nident, length) pairs and e-values recur over a run's
+    // tables: each is printed and parsed once per thread, through a
+    // direct-mapped cache kept across the thread's tables (as tables.py does
+    // with np.unique per table; the values are pure functions of the key)
+    struct Memo {
+        uint64_t key[1 << 16];
+        double val[1 << 16];
+        Memo() { std::fill(key, key + (1 << 16), ~0ull); }
+    };
+    static thread_local std::unique_ptr<Memo> pm, em;
+    if (!pm) pm.reset(new Memo());
+    if (!em) em.reset(new Memo());
+    auto slot = [](uint64_t k) { return (size_t)((k * 0x9E3779B97F4A7C15ull) >> 48); };
     for (uint64_t i = 0; i < n; i++) {
         const rc_hsp &h = rows[i].hsp;
         const uint64_t pk = ((uint64_t)(uint32_t)h.nident << 32) | (uint32_t)h.length;
-        auto pi = pmemo.find(pk);
-        if (pi == pmemo.end()) {
+        const size_t ps = slot(pk);
+        if (pm->key[ps] != pk) {
             const double L = (double)(h.length > 1 ? h.length : 1);
-            pi = pmemo.emplace(pk, od2::printed("%.3f", 100.0 * (double)h.nident / L)).first;
+            pm->val[ps] = od2::printed("%.3f", 100.0 * (double)h.nident / L);
+            pm->key[ps] = pk;
         }
-        t.pident[i] = pi->second;
+        t.pident[i] = pm->val[ps];
         if (h.evalue < 1.0e-180) {
             t.evalue[i] = 0.0;
         } else {
             uint64_t ek;
             std::memcpy(&ek, &h.evalue, 8);
-            auto ei = ememo.find(ek);
-            if (ei == ememo.end()) ei = ememo.emplace(ek, od2::printed("%.2e", h.evalue)).first;
-            t.evalue[i] = ei->second;
+            const size_t es = slot(ek);
+            if (em->key[es] != ek) {
+                em->val[es] = od2::printed("%.2e", h.evalue);
+                em->key[es] = ek;
+            }
+            t.evalue[i] = em->val[es];
         }
     }
     const std::string file = od2::build_table_file(t, ssample, qsample);
