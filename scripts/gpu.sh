@@ -20,6 +20,7 @@
 #   shardprof:CFG:R/S  the same under rocprofv3 --kernel-trace --hip-trace --stats
 #   c5full[:CFG]     scripts/c5_full.py (default C5s)
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS (ARGS: commas become spaces)
+#   bin:NAME[:ARGS]  benchbin/NAME ARGS (a micro-benchmark built here, in-tree)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -65,6 +66,7 @@ for step in "$@"; do
            find "$P" \( -name '*_trace.csv' -o -name '*.db' \) -delete   # (hundreds of MB; the summaries stay)
            [ $rc -eq 0 ] || exit $rc ;;
     c5full) c=${a:-C5s}; run 1100 "$D/${c}_full.log" python -u scripts/c5_full.py --config "$c" --outputs /tmp/rc_c5_outputs --out "$D/${c}_full.json" || exit $? ;;
+    bin) run 300 "$D/${a}_${b//,/_}.log" "benchbin/$a" ${b//,/ } || exit $? ;;
     py) run 900 "$D/$(basename "$a" .py).log" python -u "$a" ${b//,/ } || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
