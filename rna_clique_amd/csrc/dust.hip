@@ -391,18 +391,12 @@ __global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t begin, 
                     const int32_t j = nb - 1;        // run offset of u
                     const int32_t pt = j - 2;        // start of the new triplet
                     const int32_t wstart = max(j + 1 - W, 0);
-                    // the leaving triplet (start j - W; its partners are its
-                    // other copies) and the entering one: both counts read in
-                    // one LDS round trip, the entering one's taken after the
-                    // decrement when they are the same triplet
-                    const bool leave = j >= W;
-                    const int ct2 = (int)C[tri2], ct = (int)C[tri];
-                    const int c2 = ct2 - 1;
-                    const int cw = (leave && tri == tri2) ? c2 : ct;   // the new triplet's copies in the window
-                    if (leave) {
+                    if (j >= W) {   // the leaving triplet (start j - W): its partners are its other copies
+                        const int c2 = (int)C[tri2] - 1;
                         C[tri2] = (uint8_t)c2;
                         rw -= c2;
                     }
+                    const int cw = (int)C[tri];   // the new triplet's copies in the window
                     C[tri] = (uint8_t)(cw + 1);
                     rw += cw;
                     Lst = max(Lst, wstart);
