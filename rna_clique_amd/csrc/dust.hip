@@ -23,11 +23,12 @@
 //     bit position). Where some suffix longer than the L-suffix may pass the
 //     level (rw * 10 > L * level: 0.7 % of the bases of random sequence),
 //     the step only appends an event (position, rw, L) to the lane's list.
-//  B. the lane's events in order: the suffixes past the L-suffix, shortest
-//     first, against the perfect intervals found so far (per start, in global
-//     scratch), from bit planes rebuilt out of the packed sequence. Deferring
-//     this rare pass keeps the scan free of the long divergent loop that one
-//     lane in three wave steps would otherwise impose on the whole wave.
+//  B. the events, owner lane by owner lane, each by the whole wave (one lane
+//     per suffix, prefix sums and a max-scan over the lanes in DPP) against
+//     the perfect intervals found so far (per start: the owner's slots, in
+//     global scratch between rounds of B, in the lanes while they run).
+//     Deferring this rare pass keeps the scan free of the long divergent
+//     loop one lane in three wave steps would otherwise impose on the wave.
 #include "device.h"
 
 #include <algorithm>
@@ -78,9 +79,6 @@ __device__ __forceinline__ uint64_t even_bits(uint64_t x)
 #ifndef RC_DUST_MINW
 #define RC_DUST_MINW 5   // waves per SIMD the registers must allow (r03: 22.7 ms at 5, 24.7 at 6, 25.5 at 7 on 1.6 Gbp random)
 #endif
-#ifndef RC_DUST_HEAVY
-#define RC_DUST_HEAVY 12   // an event whose suffix loop runs more starts than this goes to the whole wave
-#endif
 
 // wave-uniform 64-bit lane read
 __device__ __forceinline__ uint64_t rl64(uint64_t v, int l)
@@ -100,13 +98,40 @@ __device__ __forceinline__ int dust_later(uint64_t Q0, uint64_t Q1, int a)
     return a ? __builtin_popcountll(eq & bit_range(0, a - 1)) : 0;
 }
 
-// (n, d) <- the larger ratio of (n, d) and (m, e) (ties keep (n, d))
-__device__ __forceinline__ void ratio_max(int &n, int &d, int m, int e)
+// DPP scans over the wave (lane order): row_shr 1, 2, 4, 8 inside the rows of
+// 16, then row_bcast 15 and 31 across them
+__device__ __forceinline__ int dpp_add_scan(int v)
 {
-    if (m * d > n * e) {
-        n = m;
-        d = e;
-    }
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);   // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);   // row_bcast:31
+    return v;
+}
+// a ratio n / d packed as n | d << 16; RID = 0 / 1 (below every perfect one)
+constexpr uint32_t RID = 1u << 16;
+// a, unless b's ratio is larger (ties keep a)
+__device__ __forceinline__ uint32_t rmax(uint32_t a, uint32_t b)
+{
+    return (b & 0xFFFFu) * (a >> 16) > (a & 0xFFFFu) * (b >> 16) ? b : a;
+}
+__device__ __forceinline__ uint32_t dpp_max_scan(uint32_t v)
+{
+    const int RI = (int)RID;
+    v = rmax(v, (uint32_t)__builtin_amdgcn_update_dpp(RI, (int)v, 0x111, 0xF, 0xF, false));
+    v = rmax(v, (uint32_t)__builtin_amdgcn_update_dpp(RI, (int)v, 0x112, 0xF, 0xF, false));
+    v = rmax(v, (uint32_t)__builtin_amdgcn_update_dpp(RI, (int)v, 0x114, 0xF, 0xF, false));
+    v = rmax(v, (uint32_t)__builtin_amdgcn_update_dpp(RI, (int)v, 0x118, 0xF, 0xF, false));
+    v = rmax(v, (uint32_t)__builtin_amdgcn_update_dpp(RI, (int)v, 0x142, 0xA, 0xF, false));
+    v = rmax(v, (uint32_t)__builtin_amdgcn_update_dpp(RI, (int)v, 0x143, 0xC, 0xF, false));
+    return v;
+}
+// the value of the lane below (lane 0: RID): an inclusive scan made exclusive
+__device__ __forceinline__ uint32_t dpp_shr1(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)RID, (int)v, 0x138, 0xF, 0xF, false);   // wave_shr:1
 }
 
 template <bool AMB>
@@ -153,178 +178,92 @@ __global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t begin, 
                 set &= ~(1ull << k);
             }
         };
-        // an event: x = j | rw << 15 | L << 9 | rel (fields below), the bit
-        // planes Q0/Q1 of its window (bit a = the base a positions before j).
-        // The suffixes longer than the L-suffix, shortest first, against the
-        // best ratio of the perfect intervals they contain (align_oracle.c
-        // dust_run). One lane on its own event:
-        auto light_event = [&](uint64_t x, uint64_t Q0, uint64_t Q1) {
-            const int rel = (int)(x & 0x1FF), Lq = (int)((x >> 9) & 63), rwe = (int)((x >> 15) & 0x7FF);
-            const int32_t j = (int32_t)(x >> 26), pt = j - 2, wstart = max(j + 1 - W, 0), Lst = pt + 1 - Lq;
-            const uint64_t r0 = c0 + (uint64_t)rel - (uint64_t)j;   // the run's start
-            if (r0 != prs) {
-                finalize(~0ull);
-                prs = r0;
-            } else {
-                finalize((uint64_t)wstart);
-            }
-            pw = wstart;
-            int r = 0;
-            for (int32_t st = Lst; st <= pt; st++) r += dust_later(Q0, Q1, pt - st);   // the L-suffix's score
-            int mr = 0, ml = 0;
-            {   // best ratio of the perfect intervals inside the L-suffix
-                uint64_t m = set;
-                while (m) {
-                    const int k = __builtin_ctzll(m);
-                    m &= m - 1;
-                    if (wstart + ((k - wstart) & 63) < Lst) continue;
-                    const uint32_t s = slot[k];
-                    const int sr = (int)(s & 0xFFF), sl = (int)((s >> 12) & 0xFF);
-                    if (mr == 0 || sr * ml > mr * sl) { mr = sr; ml = sl; }
-                }
-            }
-            for (int32_t st = Lst - 1; st >= wstart; st--) {
-                const int l = pt - st;
-                if (T * l >= 10 * rwe) break;   // no longer suffix can pass the level
-                r += dust_later(Q0, Q1, l);
-                const int k = st & 63;
-                const bool has = (set >> k) & 1ull;
-                const uint32_t s = has ? slot[k] : 0u;
-                const int sr = (int)(s & 0xFFF), sl = (int)((s >> 12) & 0xFF);
-                if (has && (mr == 0 || sr * ml > mr * sl)) { mr = sr; ml = sl; }
-                if (r * 10 > T * l && (mr == 0 || r * ml >= mr * l)) {
-                    const int end = j + 1 - st;   // end - start
-                    int nr = r, nl = l;
-                    if (has && !(r * sl > sr * l)) { nr = sr; nl = sl; }
-                    const int ne = has ? max(end, (int)((s >> 20) & 0x1FF)) : end;
-                    slot[k] = ((uint32_t)ne << 20) | ((uint32_t)nl << 12) | (uint32_t)nr;
-                    set |= 1ull << k;
-                    mr = r;
-                    ml = l;
-                }
-            }
-        };
-        // The whole wave on lane o's event (wave-uniform x, Q0, Q1): lane k
-        // holds the owner's slot k; lane i tries the suffix starting at
-        // Lst - 1 - i. Its score is a prefix sum over the lanes; the best ratio
-        // it is compared with -- the L-suffix's perfect intervals, then every
-        // shorter suffix's slot and every shorter suffix that passes the
-        // level (a passing one that does not beat the running best leaves it
-        // unchanged) -- is an exclusive max-scan: the sequential loop's
-        // result, without its walk over up to 62 starts.
-        auto coop_event = [&](int o, uint64_t x, uint64_t Q0, uint64_t Q1) {
-            const int rel = (int)(x & 0x1FF), Lq = (int)((x >> 9) & 63), rwe = (int)((x >> 15) & 0x7FF);
-            const int32_t j = (int32_t)(x >> 26), pt = j - 2, wstart = max(j + 1 - W, 0), Lst = pt + 1 - Lq;
-            const uint64_t oc0 = rl64(c0, o), oc1 = rl64(c1, o);
-            uint64_t oset = rl64(set, o), oprs = rl64(prs, o);
-            const int opw = __builtin_amdgcn_readlane(pw, o);
-            uint32_t *const os = slot0 + o * DWIN_MAX;
-            const uint64_t r0 = oc0 + (uint64_t)rel - (uint64_t)j;
-            bool mine = (oset >> lane) & 1ull;
-            uint32_t sv = mine ? os[lane] : 0u;
-            // finalize: the owner's intervals that start before the window (all
-            // of them on a new run)
-            if (mine) {
-                const uint64_t a = (uint64_t)opw + (uint64_t)((lane - opw) & 63);
-                if (r0 != oprs || a < (uint64_t)wstart) {
-                    if (oprs + a < oc1) dust_mark(mask, oprs + a, oprs + a + ((sv >> 20) & 0x1FFu));
-                    mine = false;
-                }
-            }
-            oset = __ballot(mine);
-            oprs = r0;
-            // the L-suffix's score: triplets ending a = 0 .. Lq - 1 back
-            int v = lane < Lq ? dust_later(Q0, Q1, lane) : 0;
-#pragma unroll
-            for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d);
-            const int rL = v;
-            // the best ratio inside the L-suffix (slots starting at or after Lst)
-            int mn = 0, md = 1;
-            {
-                const int startk = wstart + ((lane - wstart) & 63);
-                int n = 0, dd = 1;
-                if (mine && startk >= Lst) {
-                    n = (int)(sv & 0xFFF);
-                    dd = (int)((sv >> 12) & 0xFF);
-                }
-#pragma unroll
-                for (int d = 32; d; d >>= 1) {
-                    const int n2 = __shfl_xor(n, d), d2 = __shfl_xor(dd, d);
-                    ratio_max(n, dd, n2, d2);
-                }
-                mn = n;
-                md = dd;
-            }
-            // lane i: the suffix starting at st = Lst - 1 - i, l = pt - st
-            const int32_t st = Lst - 1 - lane;
-            const int l = Lq + lane;
-            const bool act = st >= wstart && T * l < 10 * rwe;   // a prefix of the lanes (the loop's break)
-            int r = act ? dust_later(Q0, Q1, l) : 0;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const int y = __shfl_up(r, d);
-                if (lane >= d) r += y;
-            }
-            r += rL;
-            const int ki = st & 63;
-            const uint32_t si = (uint32_t)__shfl((int)sv, ki);
-            const bool has = act && ((oset >> ki) & 1ull);
-            const int sr = (int)(si & 0xFFF), sl = (int)((si >> 12) & 0xFF);
-            const bool pass = act && r * 10 > T * l;
-            int vn = 0, vd = 1;
-            if (has) { vn = sr; vd = sl; }
-            if (pass) ratio_max(vn, vd, r, l);
-            // exclusive max-scan of (vn, vd), seeded with the L-suffix's best
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const int n2 = __shfl_up(vn, d), d2 = __shfl_up(vd, d);
-                if (lane >= d) ratio_max(vn, vd, n2, d2);
-            }
-            int en = __shfl_up(vn, 1), ed = __shfl_up(vd, 1);
-            if (lane == 0) { en = 0; ed = 1; }
-            ratio_max(en, ed, mn, md);
-            if (has) ratio_max(en, ed, sr, sl);
-            const bool perfect = pass && r * ed >= en * l;
-            if (perfect) {
-                const int end = j + 1 - st;
-                int nr = r, nl = l;
-                if (has && !(r * sl > sr * l)) { nr = sr; nl = sl; }
-                const int ne = has ? max(end, (int)((si >> 20) & 0x1FF)) : end;
-                os[ki] = ((uint32_t)ne << 20) | ((uint32_t)nl << 12) | (uint32_t)nr;
-            }
-            // lane i's slot is (Lst - 1 - i) & 63: the ballot reversed, rotated by Lst
-            const uint64_t rv = __builtin_bitreverse64(__ballot(perfect));
-            const int sh = Lst & 63;
-            oset |= sh ? (rv << sh) | (rv >> (64 - sh)) : rv;
-            if (lane == o) {
-                set = oset;
-                prs = oprs;
-                pw = wstart;
-            }
-        };
+        // Every lane's events, owner by owner (wave-uniform call): the whole
+        // wave works on one event at a time, lane a on the suffix ending at j
+        // that starts a triplets back (st = pt - a). Its score is a prefix
+        // sum over the lanes of "the later copies of the triplet at st"; the
+        // best ratio it is compared with -- the perfect intervals inside the
+        // L-suffix, then every shorter suffix's slot and every shorter suffix
+        // that passes the level (a passing one that does not beat the running
+        // best leaves it unchanged) -- is an exclusive max-scan over the same
+        // lanes: align_oracle.c dust_run's loop over the longer suffixes,
+        // without its walk. The owner's slots sit in the lanes (lane k: slot
+        // k) while its events run, one load and one store per owner.
         int nev = 0;
-        // every lane's events (wave-uniform call): round e runs each lane's
-        // event e -- alone when short, by the whole wave one owner at a time
-        // when its suffix loop is long (low-complexity runs: poly-A tails)
+        const uint64_t *const evb = evs + (size_t)blockIdx.x * DEVCAP * 3 * DW;
         auto run_events = [&]() {
-            for (int e = 0;; e++) {
-                const bool pend = e < nev;
-                if (!__ballot(pend)) break;
-                uint64_t x = 0, Q0 = 0, Q1 = 0;
-                bool heavy = false;
-                if (pend) {
-                    x = ev[(size_t)(3 * e) * DW];
-                    Q0 = ev[(size_t)(3 * e + 1) * DW];
-                    Q1 = ev[(size_t)(3 * e + 2) * DW];
-                    const int Lq = (int)((x >> 9) & 63), rwe = (int)((x >> 15) & 0x7FF);
-                    const int32_t j = (int32_t)(x >> 26), wstart = max(j + 1 - W, 0), Lst = j - 1 - Lq;
-                    const int lbrk = (10 * rwe + T - 1) / T;   // the first l the loop breaks at
-                    heavy = min(Lst - wstart, lbrk - Lq) > RC_DUST_HEAVY;
+            for (uint64_t hm = __ballot(nev > 0); hm; hm &= hm - 1) {
+                const int o = __builtin_ctzll(hm);
+                const int n = __builtin_amdgcn_readlane(nev, o);
+                uint64_t xv = 0, q0v = 0, q1v = 0;   // lane e: the owner's event e
+                if (lane < n) {
+                    xv = evb[(size_t)(3 * lane) * DW + o];
+                    q0v = evb[(size_t)(3 * lane + 1) * DW + o];
+                    q1v = evb[(size_t)(3 * lane + 2) * DW + o];
                 }
-                if (pend && !heavy) light_event(x, Q0, Q1);
-                for (uint64_t hm = __ballot(pend && heavy); hm; hm &= hm - 1) {
-                    const int o = __builtin_ctzll(hm);
-                    coop_event(o, rl64(x, o), rl64(Q0, o), rl64(Q1, o));
+                const uint64_t oc0 = rl64(c0, o), oc1 = rl64(c1, o);
+                uint64_t oset = rl64(set, o), oprs = rl64(prs, o);
+                int opw = __builtin_amdgcn_readlane(pw, o);
+                uint32_t *const os = slot0 + o * DWIN_MAX;
+                uint32_t sv = ((oset >> lane) & 1ull) ? os[lane] : 0u;
+                for (int e = 0; e < n; e++) {
+                    const uint64_t x = rl64(xv, e), Q0 = rl64(q0v, e), Q1 = rl64(q1v, e);
+                    const int rel = (int)(x & 0x1FF), Lq = (int)((x >> 9) & 63), rwe = (int)((x >> 15) & 0x7FF);
+                    const int32_t j = (int32_t)(x >> 26), pt = j - 2, wstart = max(j + 1 - W, 0);
+                    const uint64_t r0 = oc0 + (uint64_t)rel - (uint64_t)j;   // the run's start
+                    // finalize: the owner's intervals that start before the
+                    // window (all of them on a new run)
+                    bool mine = (oset >> lane) & 1ull;
+                    if (mine) {
+                        const uint64_t a = (uint64_t)opw + (uint64_t)((lane - opw) & 63);
+                        if (r0 != oprs || a < (uint64_t)wstart) {
+                            if (oprs + a < oc1) dust_mark(mask, oprs + a, oprs + a + ((sv >> 20) & 0x1FFu));
+                            mine = false;
+                        }
+                    }
+                    oset = __ballot(mine);
+                    oprs = r0;
+                    opw = wstart;
+                    // lane a: the suffix starting at st = pt - a (l = a)
+                    const int span = pt - wstart;   // the window's last lane
+                    const bool valid = lane <= span;
+                    const int r = dpp_add_scan(valid ? dust_later(Q0, Q1, lane) : 0);
+                    const int ki = (pt - lane) & 63;
+                    const uint32_t si = (uint32_t)__shfl((int)sv, ki);
+                    const bool has = valid && ((oset >> ki) & 1ull);
+                    const bool act = valid && lane >= Lq && T * lane < 10 * rwe;   // the loop's prefix (its break)
+                    const bool pass = act && r * 10 > T * lane;
+                    uint32_t c = has ? (si & 0xFFFu) | (((si >> 12) & 0xFFu) << 16) : RID;
+                    if (pass) c = rmax(c, (uint32_t)r | ((uint32_t)lane << 16));
+                    if (lane >= Lq && !act) c = RID;
+                    const uint32_t ex = rmax(dpp_shr1(dpp_max_scan(c)), has ? (si & 0xFFFu) | (((si >> 12) & 0xFFu) << 16) : RID);
+                    const int en = (int)(ex & 0xFFFF), ed = (int)(ex >> 16);
+                    const bool perfect = pass && r * ed >= en * lane;
+                    uint32_t nv = 0;
+                    if (perfect) {
+                        const int sr = (int)(si & 0xFFF), sl = (int)((si >> 12) & 0xFF);
+                        const int end = j + 1 - (pt - lane);
+                        int nr = r, nl = lane;
+                        if (has && !(r * sl > sr * lane)) { nr = sr; nl = sl; }
+                        const int ne = has ? max(end, (int)((si >> 20) & 0x1FF)) : end;
+                        nv = ((uint32_t)ne << 20) | ((uint32_t)nl << 12) | (uint32_t)nr;
+                    }
+                    // back to the slot lanes: slot k came from lane (pt - k) & 63
+                    const uint64_t pb = __ballot(perfect);
+                    if (pb) {
+                        const int src = (pt - lane) & 63;
+                        const uint32_t t = (uint32_t)__shfl((int)nv, src);
+                        if ((pb >> src) & 1ull) sv = t;
+                        const uint64_t rv = __builtin_bitreverse64(pb);
+                        const int sh = (pt + 1) & 63;
+                        oset |= sh ? (rv << sh) | (rv >> (64 - sh)) : rv;
+                    }
+                }
+                if ((oset >> lane) & 1ull) os[lane] = sv;
+                if (lane == o) {
+                    set = oset;
+                    prs = oprs;
+                    pw = opw;
                 }
             }
             nev = 0;

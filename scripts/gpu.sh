@@ -21,6 +21,7 @@
 #   c5full[:CFG]     scripts/c5_full.py (default C5s)
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS (ARGS: commas become spaces)
 #   bin:NAME[:ARGS]  benchbin/NAME ARGS (a micro-benchmark built here, in-tree)
+#   pmcbin:NAME:ARGS the same under one rocprofv3 PMC pass (instruction mix and waits)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -67,6 +68,7 @@ for step in "$@"; do
            [ $rc -eq 0 ] || exit $rc ;;
     c5full) c=${a:-C5s}; run 1100 "$D/${c}_full.log" python -u scripts/c5_full.py --config "$c" --outputs /tmp/rc_c5_outputs --out "$D/${c}_full.json" || exit $? ;;
     bin) run 300 "$D/${a}_${b//,/_}.log" "benchbin/$a" ${b//,/ } || exit $? ;;
+    pmcbin) run 300 "$D/pmc_${a}.log" rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY --output-format csv -d "$D/pmc_$a" -o run -- "benchbin/$a" ${b//,/ } || exit $? ;;
     py) run 900 "$D/$(basename "$a" .py).log" python -u "$a" ${b//,/ } || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
