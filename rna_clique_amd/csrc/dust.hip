@@ -36,7 +36,11 @@
 namespace rcg {
 
 constexpr int DW = 64;          // lanes per block (one wave)
-constexpr int DCHUNK = 256;     // bases per lane
+#ifndef RC_DUST_CHUNK
+#define RC_DUST_CHUNK 1024
+#endif
+constexpr int DCHUNK = RC_DUST_CHUNK;   // bases per lane (a multiple of 64)
+static_assert(DCHUNK % 64 == 0 && DCHUNK + 64 < 4096, "an event's chunk offset has 12 bits");
 constexpr int DWIN_MAX = 64;    // longest DUST window the kernel supports
 constexpr int DEVCAP = 64;  // events a lane holds (phase B runs between scan blocks when one nears this)
 
@@ -208,8 +212,8 @@ __global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t begin, 
                 uint32_t sv = ((oset >> lane) & 1ull) ? os[lane] : 0u;
                 for (int e = 0; e < n; e++) {
                     const uint64_t x = rl64(xv, e), Q0 = rl64(q0v, e), Q1 = rl64(q1v, e);
-                    const int rel = (int)(x & 0x1FF), Lq = (int)((x >> 9) & 63), rwe = (int)((x >> 15) & 0x7FF);
-                    const int32_t j = (int32_t)(x >> 26), pt = j - 2, wstart = max(j + 1 - W, 0);
+                    const int rel = (int)(x & 0xFFF), Lq = (int)((x >> 12) & 63), rwe = (int)((x >> 18) & 0x7FF);
+                    const int32_t j = (int32_t)(x >> 29), pt = j - 2, wstart = max(j + 1 - W, 0);
                     const uint64_t r0 = oc0 + (uint64_t)rel - (uint64_t)j;   // the run's start
                     // finalize: the owner's intervals that start before the
                     // window (all of them on a new run)
@@ -352,7 +356,7 @@ __global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t begin, 
                     }
                     if (rw * 10 <= (pt - Lst + 1) * T) continue;
                     // rare: B tries the longer suffixes; event = j | rw | L | rel
-                    ev[(size_t)(3 * nev) * DW] = ((uint64_t)j << 26) | ((uint64_t)rw << 15) | ((uint64_t)(pt - Lst + 1) << 9) | rel;
+                    ev[(size_t)(3 * nev) * DW] = ((uint64_t)j << 29) | ((uint64_t)rw << 18) | ((uint64_t)(pt - Lst + 1) << 12) | rel;
                     ev[(size_t)(3 * nev + 1) * DW] = P0;
                     ev[(size_t)(3 * nev + 2) * DW] = P1;
                     nev++;

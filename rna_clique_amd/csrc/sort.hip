@@ -190,7 +190,7 @@ __global__ void tile_order_kernel(const uint32_t *scratch, int p, uint32_t *orde
 // koff[t] + o is window o of transcript t) with the sort's segment
 // histograms counted on the way, so the sort does not read the keys to count
 // them. Wave per transcript, grid-stride; per-block LDS tables.
-__global__ __launch_bounds__(256) void kmer_fill_hist_kernel(const TxInfo *__restrict__ tx, uint32_t n_tx,
+__global__ __launch_bounds__(1024) void kmer_fill_hist_kernel(const TxInfo *__restrict__ tx, uint32_t n_tx,
                                                              const uint64_t *__restrict__ F,
                                                              const uint64_t *__restrict__ out_off,
                                                              uint64_t *__restrict__ ent, int np, uint64_t segsize,
@@ -198,11 +198,11 @@ __global__ __launch_bounds__(256) void kmer_fill_hist_kernel(const TxInfo *__res
 {
     extern __shared__ uint32_t h[];
     const int tab = OS_SEG * RADIX;
-    for (int i = threadIdx.x; i < np * tab; i += 256) h[i] = 0;
+    for (int i = threadIdx.x; i < np * tab; i += blockDim.x) h[i] = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const uint32_t nwave = gridDim.x * 4u;
-    for (uint32_t t = blockIdx.x * 4u + (threadIdx.x >> 6); t < n_tx; t += nwave) {
+    const uint32_t wpb = blockDim.x >> 6, nwave = gridDim.x * wpb;
+    for (uint32_t t = blockIdx.x * wpb + (threadIdx.x >> 6); t < n_tx; t += nwave) {
         const TxInfo ti = tx[t];
         const int64_t nwin = (int64_t)ti.len - W16 + 1;
         const uint64_t base = out_off[t];
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(256) void kmer_fill_hist_kernel(const TxInfo *__res
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < np * tab; i += 256)
+    for (int i = threadIdx.x; i < np * tab; i += blockDim.x)
         if (h[i]) atomicAdd(&pass_tab(scratch, i / tab).H[i % tab], h[i]);
 }
 
@@ -496,8 +496,11 @@ void os_fill_hist(const TxInfo *tx, uint32_t n_tx, const uint64_t *F, const uint
     if (!n_tx || !n) return;
     const int np = 4;
     const uint64_t segsize = (n + OS_SEG - 1) / OS_SEG;
-    const dim3 g(std::min<uint32_t>((n_tx + 3) / 4, 256 * 8));
-    hipLaunchKernelGGL(kmer_fill_hist_kernel, g, dim3(256), (size_t)np * OS_SEG * RADIX * sizeof(uint32_t), st, tx,
+    // 16-wave blocks, two per CU (r05: 4.84-4.97 ms at C3 against 5.71 for
+    // 2048 four-wave blocks, whose 32 KB tables made a second, partial round
+    // of blocks and twice the closing atomics)
+    const dim3 g(std::min<uint32_t>((n_tx + 15) / 16, 512));
+    hipLaunchKernelGGL(kmer_fill_hist_kernel, g, dim3(1024), (size_t)np * OS_SEG * RADIX * sizeof(uint32_t), st, tx,
                        n_tx, F, koff, ent, np, segsize, scratch);
 }
 

@@ -22,10 +22,13 @@
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS (ARGS: commas become spaces)
 #   bin:NAME[:ARGS]  benchbin/NAME ARGS (a micro-benchmark built here, in-tree)
 #   pmcbin:NAME:ARGS the same under one rocprofv3 PMC pass (instruction mix and waits)
+#   env:VAR=VALUE    export VAR=VALUE for the later steps (A/B knobs); output
+#                    names of later bench/stats steps carry _VAR=VALUE
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 TAG=$1; shift
+ET=""
 D=gpurun_out/$TAG
 mkdir -p "$D"
 log() { echo "$*" >> "$D/commands.txt"; }
@@ -46,11 +49,12 @@ for step in "$@"; do
            else
              run 1100 "$D/gpu_tests.log" python -u -m pytest tests -m gpu -x -v --timeout 700 --timeout-method thread -p no:cacheprovider || exit $?
            fi ;;
-    bench) c=${a:-C3}; run 600 "$D/${c}_bench.json" python bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e || exit $? ;;
+    env) export "$a"; ET="${ET}_$a"; log "export $a" ;;
+    bench) c=${a:-C3}; run 600 "$D/${c}_bench${ET}.json" python bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e || exit $? ;;
     benchfull) run 900 "$D/bench_default.json" python bench.py || exit $? ;;
     e2e) c=${a:-C3}; run 600 "$D/${c}_e2e.json" python bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
     stats) c=${a:-C3}
-           run 600 "$D/${c}_stats.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$D/${c}_stats" -o run -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e || exit $? ;;
+           run 600 "$D/${c}_stats${ET}.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$D/${c}_stats${ET}" -o run -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e || exit $? ;;
     pmc) c=${a:-C3}; log "bash scripts/gpu_pmc.sh $c  (-> gpurun_out/pmc_$c)"; bash scripts/gpu_pmc.sh "$c" || exit $? ;;
     pmcx) IFS=';' read -ra groups <<< "$b"; i=0
           for grp in "${groups[@]}"; do
