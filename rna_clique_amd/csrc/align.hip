@@ -2526,49 +2526,74 @@ __global__ __launch_bounds__(256) void first_finish_kernel(ExtParams P)
         const Cand cd = P.cands[ci];
         // shared searches: each directed search of the candidate on its own --
         // its first seed's box (cand_box, or cand_box2 when the reverse
-        // search's first seed is another seed), its own seeds, its own cut
+        // search's first seed is another seed), its own seeds, its own cut.
+        // Both searches' containment tests share one pass over the seeds.
         const int ndir = P.share ? 2 : 1;
+        bool live[2] = {false, false};
+        int bqa[2] = {0, 0}, bqb[2] = {0, 0}, bsa[2] = {0, 0}, bsb[2] = {0, 0}, ex[2] = {-1, -1};
+        const int *fxd[2] = {nullptr, nullptr};
         for (int dir = 0; dir < ndir; dir++) {
-            DHsp *const hsp_out = dir ? P.cand_hsp_r : P.cand_hsp;
-            uint8_t *const nh_out = dir ? P.cand_nh_r : P.cand_nh;
-            uint32_t *const ovf_out = dir ? P.cand_ovf_r : P.cand_ovf;
             if (P.share && !((cd.dflags >> dir) & 1)) {   // this search found no seed here
-                nh_out[ci] = 0;
-                ovf_out[ci] = 0;
+                (dir ? P.cand_nh_r : P.cand_nh)[ci] = 0;
+                (dir ? P.cand_ovf_r : P.cand_ovf)[ci] = 0;
                 continue;
             }
             const bool second = dir == 1 && cd.e1 != SEED_NONE;
-            const int *fx = (second ? P.cand_box2 : P.cand_box) + ci * BOX_REC;
-            const uint32_t dbit = !P.share ? 0u : (dir ? SEED_R : SEED_F);
-            auto defer_dir = [&]() {
+            fxd[dir] = (second ? P.cand_box2 : P.cand_box) + ci * BOX_REC;
+            if (fxd[dir][FX_STATUS] < 0) {   // (shared searches) the row kernel gave it up
+                if (P.why) atomicAdd(&P.why[1], 1ull);
                 const unsigned long long di = atomicAdd(dir ? P.defer_r_count : P.defer_count, 1ull);
                 (dir ? P.defer_r : P.defer)[di] = (uint32_t)ci;
-            };
-            if (fx[FX_STATUS] < 0) {   // (shared searches) the row kernel gave it up
-                if (P.why) atomicAdd(&P.why[1], 1ull);
-                defer_dir();
                 continue;
             }
-            const uint32_t e = second ? cd.e1 : cd.e0;
-            const GSeed s0 = P.seeds[cd.seed_off + e];
+            ex[dir] = (int)(second ? cd.e1 : cd.e0);
+            const GSeed s0 = P.seeds[cd.seed_off + ex[dir]];
+            const int *fx = fxd[dir];
             const int x = (int)s0.x, y = (int)s0.y, len = (int)(s0.len & SEED_LEN);
+            bqa[dir] = x - fx[FX_L + 1];
+            bqb[dir] = x + len + fx[FX_R + 1];
+            bsa[dir] = y - fx[FX_L + 2];
+            bsb[dir] = y + len + fx[FX_R + 2];
+            live[dir] = true;
+        }
+        // the other seeds of each live search inside its box? (four seeds'
+        // loads in flight at a time)
+        bool in0 = live[0], in1 = live[1];
+        const GSeed *const sp = P.seeds + cd.seed_off;
+        const uint32_t ns = cand_seeds(cd);
+        for (uint32_t i0 = 0; i0 < ns && (in0 || in1); i0 += 4) {
+            GSeed s4[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) s4[k] = i0 + k < ns ? sp[i0 + k] : GSeed{0u, 0u, 0u};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int i = (int)(i0 + k);
+                if (i >= (int)ns) break;
+                const int sl = (int)(s4[k].len & SEED_LEN), sx = (int)s4[k].x, sy = (int)s4[k].y;
+                // without shared searches every seed is the one search's
+                const bool f = !P.share || (s4[k].len & SEED_F), r = P.share && (s4[k].len & SEED_R);
+                if (in0 && f && i != ex[0])
+                    in0 = bqa[0] <= sx && sx + sl <= bqb[0] && bsa[0] <= sy && sy + sl <= bsb[0];
+                if (in1 && r && i != ex[1])
+                    in1 = bqa[1] <= sx && sx + sl <= bqb[1] && bsa[1] <= sy && sy + sl <= bsb[1];
+            }
+        }
+        for (int dir = 0; dir < ndir; dir++) {
+            if (!live[dir]) continue;
+            DHsp *const hsp_out = dir ? P.cand_hsp_r : P.cand_hsp;
+            uint8_t *const nh_out = dir ? P.cand_nh_r : P.cand_nh;
+            uint32_t *const ovf_out = dir ? P.cand_ovf_r : P.cand_ovf;
+            if (!(dir ? in1 : in0)) {
+                if (P.why) atomicAdd(&P.why[2], 1ull);
+                const unsigned long long di = atomicAdd(dir ? P.defer_r_count : P.defer_count, 1ull);
+                (dir ? P.defer_r : P.defer)[di] = (uint32_t)ci;
+                continue;
+            }
+            const int *fx = fxd[dir];
+            const int len = (int)(P.seeds[cd.seed_off + ex[dir]].len & SEED_LEN);
             const int rsc = fx[FX_R], ri = fx[FX_R + 1], rj = fx[FX_R + 2], rd = fx[FX_R + 3], rgo = fx[FX_R + 4];
             const int lsc = fx[FX_L], lI = fx[FX_L + 1], lJ = fx[FX_L + 2], ld = fx[FX_L + 3], lgo = fx[FX_L + 4];
             const int lg = lgo & GMASK, lo2 = (lgo >> OBIT) & GMASK, rg = rgo & GMASK, ro = (rgo >> OBIT) & GMASK;
-            const int bqa = x - lI, bqb = x + len + ri, bsa = y - lJ, bsb = y + len + rj;
-            bool all_in = true;
-            for (uint32_t i = 0, ns = cand_seeds(cd); i < ns && all_in; i++) {
-                if (i == e) continue;
-                const GSeed s = P.seeds[cd.seed_off + i];
-                if (dbit && !(s.len & dbit)) continue;
-                const int sl = (int)(s.len & SEED_LEN);
-                all_in = bqa <= (int)s.x && (int)s.x + sl <= bqb && bsa <= (int)s.y && (int)s.y + sl <= bsb;
-            }
-            if (!all_in) {
-                if (P.why) atomicAdd(&P.why[2], 1ull);
-                defer_dir();
-                continue;
-            }
             const int bsc = lsc + 2 * len + rsc, bd = ld + rd, bg = lg + rg, bo = lo2 + ro;
             const int bni = len + (lI + lJ - 2 * ld + lg) / 2 + (ri + rj - 2 * rd + rg) / 2;
             const int thr_f = P.thr[(size_t)cd.ssam * (size_t)(P.max_len + 1) + (size_t)cd.Lq];
@@ -2580,9 +2605,10 @@ __global__ __launch_bounds__(256) void first_finish_kernel(ExtParams P)
                 h.q_tx = cd.q_gtx;
                 h.s_tx = cd.s_gtx;
                 if (!cd.strand) {
-                    h.qstart = bqa + 1; h.qend = bqb; h.sstart = bsa + 1; h.send = bsb;
+                    h.qstart = bqa[dir] + 1; h.qend = bqb[dir]; h.sstart = bsa[dir] + 1; h.send = bsb[dir];
                 } else {
-                    h.qstart = cd.Lq - bqb + 1; h.qend = cd.Lq - bqa; h.sstart = bsb; h.send = bsa + 1;
+                    h.qstart = cd.Lq - bqb[dir] + 1; h.qend = cd.Lq - bqa[dir];
+                    h.sstart = bsb[dir]; h.send = bsa[dir] + 1;
                 }
                 h.gaps = bg;
                 h.gapopen = bo;

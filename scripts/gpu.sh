@@ -49,7 +49,7 @@ for step in "$@"; do
            else
              run 1100 "$D/gpu_tests.log" python -u -m pytest tests -m gpu -x -v --timeout 700 --timeout-method thread -p no:cacheprovider || exit $?
            fi ;;
-    env) export "$a"; ET="${ET}_$a"; log "export $a" ;;
+    env) export "$a"; ET="${ET}_${a//\//_}"; log "export $a" ;;
     bench) c=${a:-C3}; run 600 "$D/${c}_bench${ET}.json" python bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e || exit $? ;;
     benchfull) run 900 "$D/bench_default.json" python bench.py || exit $? ;;
     e2e) c=${a:-C3}; run 600 "$D/${c}_e2e.json" python bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
