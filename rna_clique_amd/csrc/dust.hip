@@ -287,8 +287,10 @@ __global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t begin, 
         uint64_t P0 = 0, P1 = 0;   // bit planes of the last 64 bases, bit a = a bases back
         bool in_run = false, done = !have;
         int nb = 0, tri = 0, tri2 = 0, rw = 0, Lst = 0;
-        for (uint64_t k = 0;; k++) {
-            if (!done && c0 + 32 * k >= lim) done = true;
+        // chunk-relative limits (32-bit: a chunk scan is < 2^12 bases)
+        const uint32_t limr = (uint32_t)(lim - c0), c1r = (uint32_t)(c1 - c0);
+        for (uint32_t k = 0;; k++) {
+            if (!done && 32 * k >= limr) done = true;
             if (!__ballot(!done)) break;
             if (!done) {
                 const uint64_t wn = word(w0 + k + 1), an = aword(w0 + k + 1);
@@ -298,27 +300,25 @@ __global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t begin, 
                 const uint64_t tw = o < 32 ? (wpp >> (2 * o)) | (wp << (64 - 2 * o))
                                            : (o == 32 ? wp : (wp >> (2 * (o - 32))) | (wc << (64 - 2 * (o - 32))));
                 const uint32_t txb = (uint32_t)(tc >> (32 * (k & 1)));
-                for (int i = 0; i < 32; i++) {
-                    const uint64_t rel = 32 * k + (uint64_t)i;
-                    const uint64_t u = c0 + rel;
-                    if (u >= lim) {
-                        done = true;
-                        break;
-                    }
+                const uint32_t nval = min(32u, limr - 32 * k);   // the block's bases before the scan's reach
+                for (uint32_t i = 0; i < nval; i++) {
+                    const uint32_t rel = 32 * k + i;
                     const bool amb = AMB && ((ac >> (2 * i)) & 3u);
                     const int b = (int)((wc >> (2 * i)) & 3u);
-                    // the trailing cursor: the triplet that leaves the window starts at u - W
-                    if ((int64_t)rel - W + 2 >= 0) tri2 = ((tri2 << 2) | (int)((tw >> (2 * i)) & 3u)) & 63;
-                    if (in_run && (amb || ((txb >> i) & 1u))) in_run = false;   // ambiguous base or next transcript
-                    if (amb) {
-                        if (u >= c1) {
+                    // the trailing cursor: the triplet that leaves the window
+                    // starts at u - W (its first steps shift in bases from before
+                    // the chunk; they are out of it before a triplet leaves)
+                    tri2 = ((tri2 << 2) | (int)((tw >> (2 * i)) & 3u)) & 63;
+                    if (AMB && amb) {
+                        in_run = false;
+                        if (rel >= c1r) {
                             done = true;
                             break;
                         }
                         continue;
                     }
-                    if (!in_run) {
-                        if (u >= c1) {   // runs starting past the chunk are the next lane's
+                    if (!in_run || ((txb >> i) & 1u)) {   // a run starts: the chunk's first base or a transcript's
+                        if (rel >= c1r) {   // runs starting past the chunk are the next lane's
                             done = true;
                             break;
                         }
@@ -334,11 +334,14 @@ __global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t begin, 
                     const int32_t j = nb - 1;        // run offset of u
                     const int32_t pt = j - 2;        // start of the new triplet
                     const int32_t wstart = max(j + 1 - W, 0);
-                    if (j >= W) {   // the leaving triplet (start j - W): its partners are its other copies
-                        const int c2 = (int)C[tri2] - 1;
-                        C[tri2] = (uint8_t)c2;
-                        rw -= c2;
-                    }
+                    // the leaving triplet (start j - W, once j >= W; before
+                    // that a spare counter byte takes the update): its
+                    // partners are its other copies
+                    const bool leave = j >= W;
+                    const int ls = leave ? tri2 : 64;
+                    const int c2 = (int)C[ls] - 1;
+                    C[ls] = (uint8_t)c2;
+                    rw -= leave ? c2 : 0;
                     const int cw = (int)C[tri];   // the new triplet's copies in the window
                     C[tri] = (uint8_t)(cw + 1);
                     rw += cw;
@@ -354,13 +357,15 @@ __global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t begin, 
                         const int p = need ? pt - (int)__builtin_ctzll(m) : pt;
                         if (p >= Lst) Lst = p + 1;
                     }
-                    if (rw * 10 <= (pt - Lst + 1) * T) continue;
+                    // (24-bit multiplies: full rate; rw < 2^11, L < 64)
+                    if (__mul24(rw, 10) <= __mul24(pt - Lst + 1, T)) continue;
                     // rare: B tries the longer suffixes; event = j | rw | L | rel
                     ev[(size_t)(3 * nev) * DW] = ((uint64_t)j << 29) | ((uint64_t)rw << 18) | ((uint64_t)(pt - Lst + 1) << 12) | rel;
                     ev[(size_t)(3 * nev + 1) * DW] = P0;
                     ev[(size_t)(3 * nev + 2) * DW] = P1;
                     nev++;
                 }
+                if (nval < 32) done = true;   // the scan's reach
                 wpp = wp;
                 wp = wc;
                 wc = wn;
