@@ -2150,25 +2150,40 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 const GW qw = QA + (q0 >> 5), tw = dF + (s0 >> 5);
                 const GW qrw = QR + (rq0 >> 5), trw = dRC + (rs0 >> 5);
                 {
+                    // the first two words per lane of the four arrays in two
+                    // batches (forward with the first seed, then reverse), each
+                    // in flight together: the empty asm takes a batch whole, so
+                    // the scheduler cannot sink its loads behind the LDS writes
+                    // (r05_z: 2 round trips instead of 6, extension -0.5 ms at
+                    // C3; one batch of all eight spills 16 VGPRs: +0.5 ms)
                     const uint32_t e01 = (uint32_t)meta[RM_REC + RC_E01];
                     const GSeed g0 =
                         K->P.seeds[(uint32_t)meta[RM_REC + RC_SOFF] + (K->P.which ? e01 >> 16 : e01 & 0xFFFFu)];
                     const uint64_t a0 = rl < nwq ? qw[rl] : 0ull, a1 = rl + RW < nwq ? qw[rl + RW] : 0ull;
                     const uint64_t b0 = rl < nwt ? tw[rl] : 0ull, b1 = rl + RW < nwt ? tw[rl + RW] : 0ull;
+                    asm volatile("" ::"v"(a0), "v"(a1), "v"(b0), "v"(b1));
                     if (rl < nwq) stg[rl] = a0;
                     if (rl + RW < nwq) stg[rl + RW] = a1;
                     if (rl < nwt) stg[sw + rl] = b0;
                     if (rl + RW < nwt) stg[sw + rl + RW] = b1;
+                    const uint64_t c0 = rl < nwqr ? qrw[rl] : 0ull, c1 = rl + RW < nwqr ? qrw[rl + RW] : 0ull;
+                    const uint64_t d0 = rl < nwtr ? trw[rl] : 0ull, d1 = rl + RW < nwtr ? trw[rl + RW] : 0ull;
+                    asm volatile("" ::"v"(c0), "v"(c1), "v"(d0), "v"(d1));
+                    if (rl < nwqr) stg[2 * sw + rl] = c0;
+                    if (rl + RW < nwqr) stg[2 * sw + rl + RW] = c1;
+                    if (rl < nwtr) stg[3 * sw + rl] = d0;
+                    if (rl + RW < nwtr) stg[3 * sw + rl + RW] = d1;
                     if (rl == 0) {
                         meta[RM_X] = (int)g0.x;
                         meta[RM_Y] = (int)g0.y;
                         meta[RM_LEN] = (int)(g0.len & SEED_LEN);
                     }
                 }
+                // (transcripts of more than 2 RW words: the rest)
                 for (int w = rl + 2 * RW; w < nwq; w += RW) stg[w] = qw[w];
                 for (int w = rl + 2 * RW; w < nwt; w += RW) stg[sw + w] = tw[w];
-                for (int w = rl; w < nwqr; w += RW) stg[2 * sw + w] = qrw[w];
-                for (int w = rl; w < nwtr; w += RW) stg[3 * sw + w] = trw[w];
+                for (int w = rl + 2 * RW; w < nwqr; w += RW) stg[2 * sw + w] = qrw[w];
+                for (int w = rl + 2 * RW; w < nwtr; w += RW) stg[3 * sw + w] = trw[w];
                 if (AMB) {
                     GW dAF = (GW)K->db.AF, dARC = (GW)K->db.ARC;
                     asm volatile("" : "+s"(dAF), "+s"(dARC));
