@@ -2030,7 +2030,13 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
         } while (ballot(pend));
     };
 
+#ifdef RC_ROW_TIMING
+    unsigned long long t_ei = 0;   // extension starts (part of the transitions)
+#endif
     auto ext_init = [&](int done_act) {
+#ifdef RC_ROW_TIMING
+        const unsigned long long e0t = __builtin_readcyclecounter();
+#endif
         int r0 = 0;
         if constexpr (WIN) {
             win_begin(done_act == A_LDONE ? 1 : 0);
@@ -2067,10 +2073,13 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
             meta[RM_KOF] = 0;
         }
         act = (min(alen, blen) - r0 <= 0) ? done_act : done_act + (A_STEP_R - A_RDONE);
+#ifdef RC_ROW_TIMING
+        t_ei += __builtin_readcyclecounter() - e0t;
+#endif
     };
 
 #ifdef RC_ROW_TIMING
-    unsigned long long t_tr = 0, t_st = 0;
+    unsigned long long t_tr = 0, t_st = 0, t_fe = 0, t_sl = 0;   // transitions, steps; fetches and window slides (parts of the transitions)
 #endif
     for (;;) {
 #ifdef RC_ROW_TIMING
@@ -2079,6 +2088,9 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
         // ---------------- transitions ----------------
         while (act < A_DONE) {
             if (act == A_FETCH) {
+#ifdef RC_ROW_TIMING
+                const unsigned long long f0t = __builtin_readcyclecounter();
+#endif
                 if (lnx >= s_ncand) {
                     // no work left: the row's lanes go dead for good (the
                     // other row's steps shift this row's edge lanes in)
@@ -2265,7 +2277,13 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                     }
                 }
                 ext_init(A_RDONE);
+#ifdef RC_ROW_TIMING
+                t_fe += __builtin_readcyclecounter() - f0t;
+#endif
             } else if (act == A_SLIDE) {
+#ifdef RC_ROW_TIMING
+                const unsigned long long s0t = __builtin_readcyclecounter();
+#endif
                 // a live lane at the window's edge: centre the live diagonals
                 const uint32_t livem = rw_mask<RW>(ballot(R >= 0), row);
                 const int kof = meta[RM_KOF];
@@ -2327,6 +2345,9 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 act = meta[RM_PHASE] + (A_STEP_R - A_RDONE);
+#ifdef RC_ROW_TIMING
+                t_sl += __builtin_readcyclecounter() - s0t;
+#endif
             } else if (act == A_RDONE || act == A_LDONE) {
                 int ei, ed, ego, kb;   // the best record and its diagonal
                 if (bl == BL_PARKED) {
@@ -2512,6 +2533,9 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
     if (lane == 0 && counters) {
         atomicAdd(&counters[8], t_tr);
         atomicAdd(&counters[9], t_st);
+        atomicAdd(&counters[27], t_fe);   // (d_count[28], [29]: slots nothing else uses)
+        atomicAdd(&counters[28], t_sl);
+        atomicAdd(&counters[29], t_ei);
     }
 #endif
     unsigned long long *const ctr = row_args()->P.counters;

@@ -2067,7 +2067,12 @@ static int align_tile(rc_engine *e, int ti)
         HIPCHK(hipMemcpyAsync(&status, e->d_status.p, sizeof status, hipMemcpyDeviceToHost, e->st));
         CHK(wait_st(e));
         if (ctr[8] || ctr[9]) {   // built with RC_ROW_TIMING: wave cycles in transitions / steps
-            fprintf(stderr, "row kernel wave-cycles: transitions %.4g steps %.4g\n", (double)ctr[8], (double)ctr[9]);
+            unsigned long long tfs[3] = {0, 0, 0};   // fetches, window slides, extension starts (parts of the transitions)
+            HIPCHK(hipMemcpy(tfs, e->d_count.p + 28, sizeof tfs, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemset(e->d_count.p + 28, 0, sizeof tfs));
+            fprintf(stderr, "row kernel wave-cycles: transitions %.4g (fetches %.4g, window slides %.4g, extension "
+                            "starts %.4g) steps %.4g\n",
+                    (double)ctr[8], (double)tfs[0], (double)tfs[1], (double)tfs[2], (double)ctr[9]);
             unsigned long long pr[10];
             HIPCHK(hipMemcpy(pr, e->d_prof.p, sizeof pr, hipMemcpyDeviceToHost));
             fprintf(stderr, "seed kernel block-cycles: prologue %.4g words: usable %.4g lookup %.4g scan %.4g "
