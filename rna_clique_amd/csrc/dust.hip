@@ -237,6 +237,7 @@ __global__ __launch_bounds__(DW, RC_DUST_MINW) void dust_kernel(uint64_t begin, 
                     const bool has = valid && ((oset >> ki) & 1ull);
                     const bool act = valid && lane >= Lq && T * lane < 10 * rwe;   // the loop's prefix (its break)
                     const bool pass = act && r * 10 > T * lane;
+                    if (!__ballot(pass)) continue;   // no longer suffix reaches the level: nothing is perfect
                     uint32_t c = has ? (si & 0xFFFu) | (((si >> 12) & 0xFFu) << 16) : RID;
                     if (pass) c = rmax(c, (uint32_t)r | ((uint32_t)lane << 16));
                     if (lane >= Lq && !act) c = RID;
