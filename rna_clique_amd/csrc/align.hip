@@ -1446,7 +1446,7 @@ __global__ __launch_bounds__(EBLOCK, EXT_MIN_WAVES) void extend_kernel(Db db, Ex
 // copies of both transcripts staged next to the forward ones.
 
 #ifndef ROW_MIN_WAVES
-#define ROW_MIN_WAVES 7   // measured best at C3 (5-8 tried, r02)
+#define ROW_MIN_WAVES 8   // r05_zn/zo: 8 beats 7 (C3 rows 84.1 -> 82.7 ms, C4 459 -> 450) and 6 (87.5); r02/r04: 7 was best then
 #endif
 
 // max over the 16 lanes of each DPP row, in every lane of the row
@@ -2934,7 +2934,7 @@ static void launch_rows(bool amb, const Db &db, const ExtParams &P, hipStream_t 
 }
 
 // Staging slot (u64 words per staged array) the 32-lane row kernel can have
-// at ROW_MIN_WAVES waves per SIMD (7 blocks per CU in 160 KB of LDS); a longer
+// at ROW_MIN_WAVES waves per SIMD (as many 4-wave blocks per CU in 160 KB of LDS); a longer
 // transcript runs on the windowed instantiation.
 int row_slot_words_max(bool amb)
 {
