@@ -368,8 +368,14 @@ struct GroupParams {
 };
 
 // Parameters of the two reciprocal-best-hit passes.
+// an HSP as the RBH kernel's selection loops read it (hkey_kernel)
+struct HKey {
+    int32_t bits10;
+    uint32_t gene;   // the subject transcript's gene
+};
 struct RbhParams {
     const DHsp *hsp;
+    const HKey *hk;                      // parallel to hsp
     const uint32_t *grp_off, *grp_cnt;   // [grp_index(gene, T)], full gene range
     const uint32_t *tx_gene;
     const TxInfo *tx;

@@ -75,6 +75,7 @@ int row_slot_words_max(bool amb);
 void launch_group(const GroupParams &, int, hipStream_t);
 
 void launch_rbh(const RbhParams &, int, hipStream_t);
+void launch_hkey(const DHsp *h, uint64_t n, const uint32_t *tx_gene, HKey *out, hipStream_t st);
 void launch_rbh_place(const RbhParams &, hipStream_t);
 void launch_gather_rows(const DHsp *, const DRow *, uint64_t, DHsp *, hipStream_t);
 void launch_cc(const DEdge *, uint64_t, uint32_t, const int32_t *, int, int, uint32_t *, uint32_t *, uint32_t *,
@@ -403,6 +404,7 @@ struct rc_engine {
     DBuf<uint8_t> d_tmp;
     DBuf<int32_t> d_thr, d_bits10;
     DBuf<DHsp> d_hsp;
+    DBuf<HKey> d_hkey;   // RBH: (bit score, subject gene) per d_hsp entry
     DBuf<GSeed> d_seeds;
     DBuf<Cand> d_cands;
     DBuf<DHsp> d_cand_hsp, d_ovf;
@@ -2280,8 +2282,13 @@ static int do_rbh(rc_engine *e)
     CHK(e->d_cnt4.ensure(4 * (ni + 1)));
     CHK(e->d_off4.ensure(4 * (ni + 1)));
     HIPCHK(hipMemsetAsync(e->d_cnt4.p, 0, 4 * (ni + 1) * 4, e->st));
+    // the RBH selection loops' 8-byte view of the group table (bit score,
+    // subject gene): r05, rbh_kernel 6.5 -> see DESIGN §4
+    CHK(e->d_hkey.ensure(std::max<uint64_t>(e->n_hsps, 1)));   // (n_hsps: aligned or imported)
+    launch_hkey(e->d_hsp.p, e->n_hsps, e->d_tx_gene.p, e->d_hkey.p, e->st);
     RbhParams R{};
     R.hsp = e->d_hsp.p;
+    R.hk = e->d_hkey.p;
     R.grp_off = e->d_grp_off.p;
     R.grp_cnt = e->d_grp_cnt.p;
     R.n_genes = (uint32_t)e->gene_sample.size();
@@ -3101,7 +3108,7 @@ int rc_trim(rc_engine *e)
     e->d_sort_status.release(); e->d_bucket.release(); e->d_pos_tx.release(); e->d_sample_pos.release();
     e->d_txstart.release(); e->d_dmask.release(); e->d_dust_scratch.release(); e->d_dust_events.release();
     e->d_prof.release(); e->d_tmp.release(); e->d_seeds.release(); e->d_cands.release();
-    e->d_cand_hsp.release(); e->d_ovf.release(); e->d_cand_nh.release(); e->d_cand_box.release();
+    e->d_cand_hsp.release(); e->d_ovf.release(); e->d_cand_nh.release(); e->d_cand_box.release(); e->d_hkey.release();
     e->d_cand_box2.release(); e->d_cand_hsp_r.release(); e->d_cand_nh_r.release(); e->d_cand_ovf_r.release();
     e->d_defer_r.release(); e->d_list2.release(); e->d_wide0.release(); e->d_wide1.release(); e->d_resume.release();
     e->d_rows_tmp.release(); e->d_edges_tmp.release(); e->d_cand_ovf.release(); e->d_gc_off.release();

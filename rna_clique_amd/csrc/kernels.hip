@@ -203,8 +203,28 @@ __global__ __launch_bounds__(256) void bucket_fill_kernel(const uint64_t *__rest
 
 
 
+// the RBH kernel's view of the group table: each HSP's bit score and its
+// subject transcript's gene (8 bytes instead of the 56-byte record and a
+// transcript -> gene gather in every selection loop)
+__global__ void hkey_kernel(const DHsp *__restrict__ h, uint64_t n, const uint32_t *__restrict__ tx_gene,
+                            HKey *__restrict__ out)
+{
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        HKey k;
+        k.bits10 = h[i].bits10;
+        k.gene = tx_gene[h[i].s_tx];
+        out[i] = k;
+    }
+}
+void launch_hkey(const DHsp *h, uint64_t n, const uint32_t *tx_gene, HKey *out, hipStream_t st)
+{
+    if (!n) return;
+    const uint64_t g = std::min<uint64_t>((n + 255) / 256, 65536);
+    hipLaunchKernelGGL(hkey_kernel, dim3((unsigned)g), dim3(256), 0, st, h, n, tx_gene, out);
+}
+
 // threshold of highest_bitscores(n, keep="all") over one group's bitscores
-__device__ __forceinline__ int group_thr(const DHsp *h, uint32_t off, uint32_t cnt, int n)
+__device__ __forceinline__ int group_thr(const HKey *h, uint32_t off, uint32_t cnt, int n)
 {
     if (cnt == 0) return INT_MAX;
     if ((int)cnt <= n) {
@@ -229,7 +249,7 @@ __device__ __forceinline__ int group_thr(const DHsp *h, uint32_t off, uint32_t c
 
 // rank of element i among a group in (bits desc, index asc) order, restricted by pred
 template <typename Pred>
-__device__ __forceinline__ uint32_t desc_rank(const DHsp *h, uint32_t off, uint32_t cnt, uint32_t i, Pred pred)
+__device__ __forceinline__ uint32_t desc_rank(const HKey *h, uint32_t off, uint32_t cnt, uint32_t i, Pred pred)
 {
     const int bi = h[off + i].bits10;
     uint32_t r = 0;
@@ -273,23 +293,26 @@ __global__ void rbh_kernel(RbhParams P, int pass)
         const int N = P.N;
         const size_t fgi = grp_index(b, A, P.n_genes);
         const uint32_t foff = P.grp_off[fgi], fcnt = P.grp_cnt[fgi];
-        const DHsp *H = P.hsp;
+        // the groups' bit scores and subject genes, 8 bytes an HSP (hkey_kernel;
+        // the 56-byte records are read for the rows that make edges only)
+        const HKey *H = P.hk;
+        const DHsp *HF = P.hsp;
         const int fthr = group_thr(H, foff, fcnt, P.top_n);
         // per F_top row: R-existence of its pair
         uint32_t fsel = 0, rsel = 0, nrows = 0, nedges = 0;
         int M = INT_MIN;
         // pass over F_top rows: compute M and counts
         for (uint32_t i = 0; i < fcnt; i++) {
-            const DHsp &f = H[foff + i];
+            const HKey &f = H[foff + i];
             if (f.bits10 < fthr) continue;
-            const uint32_t a = P.tx_gene[f.s_tx];
+            const uint32_t a = f.gene;
             const size_t rgi = grp_index(a, B, P.n_genes);
             const uint32_t roff = P.grp_off[rgi], rcnt = P.grp_cnt[rgi];
             const int rthr = group_thr(H, roff, rcnt, P.top_n);
             bool inP = false;
             for (uint32_t j = 0; j < rcnt; j++) {
-                const DHsp &r = H[roff + j];
-                if (r.bits10 >= rthr && P.tx_gene[r.s_tx] == b) {
+                const HKey &r = H[roff + j];
+                if (r.bits10 >= rthr && r.gene == b) {
                     inP = true;
                     break;
                 }
@@ -300,16 +323,16 @@ __global__ void rbh_kernel(RbhParams P, int pass)
             // first F_top row of this pair?
             bool first = true;
             for (uint32_t i2 = 0; i2 < i; i2++) {
-                const DHsp &f2 = H[foff + i2];
-                if (f2.bits10 >= fthr && P.tx_gene[f2.s_tx] == a) {
+                const HKey &f2 = H[foff + i2];
+                if (f2.bits10 >= fthr && f2.gene == a) {
                     first = false;
                     break;
                 }
             }
             if (!first) continue;
             for (uint32_t j = 0; j < rcnt; j++) {
-                const DHsp &r = H[roff + j];
-                if (r.bits10 >= rthr && P.tx_gene[r.s_tx] == b) {
+                const HKey &r = H[roff + j];
+                if (r.bits10 >= rthr && r.gene == b) {
                     rsel++;
                     M = max(M, r.bits10);
                 }
@@ -336,9 +359,9 @@ __global__ void rbh_kernel(RbhParams P, int pass)
             bool found = false;
             uint32_t a = 0;
             for (uint32_t i = 0; i < fcnt; i++) {
-                const DHsp &f = H[foff + i];
+                const HKey &f = H[foff + i];
                 if (f.bits10 < fthr) continue;
-                const uint32_t ai = P.tx_gene[f.s_tx];
+                const uint32_t ai = f.gene;
                 if (have_prev && ai <= prev_a) continue;
                 if (!found || ai < a) a = ai, found = true;
             }
@@ -349,8 +372,8 @@ __global__ void rbh_kernel(RbhParams P, int pass)
             const uint32_t roff = P.grp_off[rgi], rcnt = P.grp_cnt[rgi];
             const int rthr = group_thr(H, roff, rcnt, P.top_n);
             auto r_sel = [&](uint32_t j) {
-                const DHsp &r = H[roff + j];
-                return r.bits10 >= rthr && P.tx_gene[r.s_tx] == b;
+                const HKey &r = H[roff + j];
+                return r.bits10 >= rthr && r.gene == b;
             };
             bool inP = false;
             for (uint32_t j = 0; j < rcnt; j++)
@@ -362,19 +385,19 @@ __global__ void rbh_kernel(RbhParams P, int pass)
             int en = 0, ed = 0, erows = 0;
             // F rows of this pair at M
             for (uint32_t i = 0; i < fcnt && !done; i++) {
-                const DHsp &f = H[foff + i];
-                if (f.bits10 < fthr || P.tx_gene[f.s_tx] != a || f.bits10 != M) continue;
+                const HKey &f = H[foff + i];
+                if (f.bits10 < fthr || f.gene != a || f.bits10 != M) continue;
                 if (pass) {
                     // label: rank among F_sel rows of b in F_top order + earlier genes
                     const uint32_t rk = desc_rank(H, foff, fcnt, i, [&](uint32_t j) {
-                        const DHsp &f2 = H[foff + j];
+                        const HKey &f2 = H[foff + j];
                         if (f2.bits10 < fthr) return false;
-                        const uint32_t a2 = P.tx_gene[f2.s_tx];
+                        const uint32_t a2 = f2.gene;
                         const size_t g2 = grp_index(a2, B, P.n_genes);
                         const uint32_t o2 = P.grp_off[g2], c2 = P.grp_cnt[g2];
                         const int t2 = group_thr(H, o2, c2, P.top_n);
                         for (uint32_t k2 = 0; k2 < c2; k2++)
-                            if (H[o2 + k2].bits10 >= t2 && P.tx_gene[H[o2 + k2].s_tx] == b) return true;
+                            if (H[o2 + k2].bits10 >= t2 && H[o2 + k2].gene == b) return true;
                         return false;
                     });
                     DRow row;
@@ -384,8 +407,8 @@ __global__ void rbh_kernel(RbhParams P, int pass)
                     row.pad = 0;
                     put_row(row);
                 }
-                en += f.nident;
-                ed += f.length - f.gaps;
+                en += HF[foff + i].nident;
+                ed += HF[foff + i].length - HF[foff + i].gaps;
                 erows++;
                 if (!P.keep_all) done = true;
             }
@@ -403,24 +426,24 @@ __global__ void rbh_kernel(RbhParams P, int pass)
             bool have_before = false;
             for (uint32_t j = 0; j < rcnt && !done; j++) {
                 if (!r_sel(j) || H[roff + j].bits10 != M) continue;
-                const DHsp &r = H[roff + j];
+                const HKey &r = H[roff + j];
                 if (pass) {
                     if (!have_before) {
                         have_before = true;
                         uint32_t afirst = 0xFFFFFFFFu;   // this pair's first F_top row
                         for (uint32_t i = 0; i < fcnt; i++)
-                            if (H[foff + i].bits10 >= fthr && P.tx_gene[H[foff + i].s_tx] == a &&
+                            if (H[foff + i].bits10 >= fthr && H[foff + i].gene == a &&
                                 (afirst == 0xFFFFFFFFu || precedes(i, afirst)))
                                 afirst = i;
                         for (uint32_t i = 0; i < fcnt; i++) {
-                            const DHsp &f = H[foff + i];
+                            const HKey &f = H[foff + i];
                             if (f.bits10 < fthr) continue;
-                            const uint32_t a2 = P.tx_gene[f.s_tx];
+                            const uint32_t a2 = f.gene;
                             if (a2 == a || precedes(afirst, i)) continue;
                             // is f the first F_top row of pair a2?
                             bool firstrow = true;
                             for (uint32_t i2 = 0; i2 < fcnt && firstrow; i2++)
-                                if (i2 != i && H[foff + i2].bits10 >= fthr && P.tx_gene[H[foff + i2].s_tx] == a2 &&
+                                if (i2 != i && H[foff + i2].bits10 >= fthr && H[foff + i2].gene == a2 &&
                                     precedes(i2, i))
                                     firstrow = false;
                             if (!firstrow) continue;
@@ -428,7 +451,7 @@ __global__ void rbh_kernel(RbhParams P, int pass)
                             const uint32_t o2 = P.grp_off[g2], c2 = P.grp_cnt[g2];
                             const int t2 = group_thr(H, o2, c2, P.top_n);
                             for (uint32_t k2 = 0; k2 < c2; k2++)
-                                if (H[o2 + k2].bits10 >= t2 && P.tx_gene[H[o2 + k2].s_tx] == b) before++;
+                                if (H[o2 + k2].bits10 >= t2 && H[o2 + k2].gene == b) before++;
                         }
                     }
                     const uint32_t rk = desc_rank(H, roff, rcnt, j, r_sel);
@@ -439,8 +462,8 @@ __global__ void rbh_kernel(RbhParams P, int pass)
                     row.pad = 0;
                     put_row(row);
                 }
-                en += r.nident;
-                ed += r.length - r.gaps;
+                en += HF[roff + j].nident;
+                ed += HF[roff + j].length - HF[roff + j].gaps;
                 erows++;
                 if (!P.keep_all) done = true;
             }
