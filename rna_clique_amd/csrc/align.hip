@@ -2740,8 +2740,11 @@ __device__ __forceinline__ uint64_t cand_slot(const GroupParams &P, uint64_t li)
     return (uint64_t)lo * P.cand_cap + (li - P.shard_prefix[lo]);
 }
 
-// pass 0: count mirrored HSPs per (gene of the subject tx, query sample);
-// pass 1: scatter them (order fixed later by mirror_sort_kernel)
+// pass 0: count mirrored HSPs per (gene of the subject tx, query sample),
+// one atomic per candidate (its HSPs share the group), whose return -- the
+// candidate's first slot in the group -- is kept per candidate; pass 1:
+// scatter them from there, no atomics (the order inside a group is fixed
+// later by mirror_sort_kernel)
 __global__ void mirror_scatter_kernel(GroupParams P, int pass)
 {
     for (uint64_t li = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; li < P.n_cand;
@@ -2750,23 +2753,26 @@ __global__ void mirror_scatter_kernel(GroupParams P, int pass)
         const uint32_t nh = P.cand_nh[ci];
         if (!nh) continue;
         const uint32_t ov = P.cand_ovf[ci];
+        uint64_t gi = 0, slot = 0;
+        uint32_t c = 0;
         for (uint32_t k = 0; k < nh; k++) {
             const DHsp &h = k ? P.ovf[ov + k - 1] : P.cand_hsp[ci];
             if (!(h.strand & HSP_REV)) continue;
             // the reverse search's query tx (its gene and isoform position) and subject tx
             const uint32_t rq = h.s_tx, rs = h.q_tx;
-            const uint64_t gi = grp_index(P.tx_gene[rq], P.tx[rs].sample, P.n_genes);
-            if (pass == 0) {
-                atomicAdd(&P.mcnt[gi], 1u);
-            } else {
-                const uint64_t slot = P.mbase + P.mscan[gi] + atomicAdd(&P.mcur[gi], 1u);
-                P.out[slot] = mirror_hsp(h);
-                // order: (isoform position, strand) then (subject tx, index)
-                P.mkey[2 * (slot - P.mbase)] = ((uint64_t)P.tx_pos[rq] << 1) | (uint64_t)(h.strand & 1);
-                P.mkey[2 * (slot - P.mbase) + 1] =
-                    ((uint64_t)rs << 8) | (uint64_t)((h.strand >> HSP_IDX_SHIFT) & 7);
+            if (c == 0) {
+                gi = grp_index(P.tx_gene[rq], P.tx[rs].sample, P.n_genes);
+                if (pass == 1) slot = P.mbase + P.mscan[gi] + P.mcur[li];
             }
+            c++;
+            if (pass == 0) continue;
+            P.out[slot] = mirror_hsp(h);
+            // order: (isoform position, strand) then (subject tx, index)
+            P.mkey[2 * (slot - P.mbase)] = ((uint64_t)P.tx_pos[rq] << 1) | (uint64_t)(h.strand & 1);
+            P.mkey[2 * (slot - P.mbase) + 1] = ((uint64_t)rs << 8) | (uint64_t)((h.strand >> HSP_IDX_SHIFT) & 7);
+            slot++;
         }
+        if (pass == 0 && c) P.mcur[li] = atomicAdd(&P.mcnt[gi], c);
     }
 }
 

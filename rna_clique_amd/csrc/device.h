@@ -359,7 +359,7 @@ struct GroupParams {
     const TxInfo *tx;
     uint32_t *mcnt;               // [gene * N + T]
     const uint64_t *mscan;        // exclusive scan of mcnt
-    uint32_t *mcur;               // scatter cursors [gene * N + T]
+    uint32_t *mcur;               // per candidate (linear index): its first slot in its mirrored group (pass 0 -> pass 1)
     uint64_t mbase;               // first output slot of the mirrored region
     uint64_t *mkey;               // order keys of the mirrored region (parallel to out)
     uint64_t *mbig;               // mirrored groups too large for one thread's sort (mirror_sort_big_kernel)

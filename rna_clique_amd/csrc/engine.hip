@@ -2157,12 +2157,11 @@ static int align_tile(rc_engine *e, int ti)
     }
     if (mirror) {
         CHK(e->d_mcnt.ensure(ngrp + 1));
-        CHK(e->d_mcur.ensure(ngrp));
+        CHK(e->d_mcur.ensure(std::max<uint64_t>(n_cand, 1)));   // per candidate: its slots' start in its group
         CHK(e->d_mscan.ensure(ngrp + 1));
         G.mcnt = e->d_mcnt.p;
         G.mcur = e->d_mcur.p;
         HIPCHK(hipMemsetAsync(e->d_mcnt.p, 0, (ngrp + 1) * 4, e->st));
-        HIPCHK(hipMemsetAsync(e->d_mcur.p, 0, ngrp * 4, e->st));
         launch_group(G, 2, e->st);   // mirrored groups (spec 5b)
         CHK(exscan(e->d_mcnt.p, e->d_mscan.p, ngrp + 1));
         HIPCHK(hipMemcpyAsync(&nm, e->d_mscan.p + ngrp, 8, hipMemcpyDeviceToHost, e->st));
