@@ -39,6 +39,15 @@ static_assert((SEED_CAP & (SEED_CAP - 1)) == 0, "RC_SEED_CAP must be a power of 
 #define RC_HBATCH 4
 #endif
 constexpr int HBATCH = RC_HBATCH;                  // hits per lane per batch of the seed kernel
+// The reverse pass (REV) keeps no seeds in LDS and finds few hits (the
+// near-mask index is small): its own instantiation, without the seed and
+// per-sample arrays and with fewer hits per lane, runs more workgroups per CU.
+#ifndef RC_SEED_REV_WAVES
+#define RC_SEED_REV_WAVES 7
+#endif
+#ifndef RC_REV_HBATCH
+#define RC_REV_HBATCH 2
+#endif
 #ifndef RC_PASS_SAMPLES
 #define RC_PASS_SAMPLES 256
 #endif
@@ -142,9 +151,13 @@ __device__ __forceinline__ bool word_usable(const Db &db, uint64_t qs, int Lq, i
 // ISOG (with BIG = false): one workgroup per gene of P.iso_list -- the genes
 // with more than ISO_LDS isoforms, whose isoform tables are read from HBM; the
 // plain launch leaves them to it (so its own code has no such path).
-template <bool AMB, bool BIG, bool ISOG>
-__global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Index ix, SeedParams P)
+template <bool AMB, bool BIG, bool ISOG, bool REV>
+__global__ __launch_bounds__(SBLOCK, REV ? RC_SEED_REV_WAVES : RC_SEED_WAVES) void seed_kernel(Db db, Index ix,
+                                                                                          SeedParams P)
 {
+    static_assert(!(REV && BIG), "the reverse pass has no global-memory passes");
+    constexpr int HB = REV ? RC_REV_HBATCH : HBATCH;   // hits per lane per batch
+    constexpr bool LSEEDS = !BIG && !REV;             // the pass's seeds in LDS
     const uint64_t big_e = BIG ? P.big_list[blockIdx.x] : 0ull;
     const uint32_t g = BIG ? P.gene_begin + (uint32_t)(big_e >> 16)
                            : (ISOG ? P.iso_list[blockIdx.x] : P.gene_begin + blockIdx.x);
@@ -152,23 +165,23 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
     const int tid = threadIdx.x;
 
     using SegIdx = typename std::conditional<BIG, uint32_t, uint16_t>::type;
-    __shared__ LSeed seeds_lds[BIG ? 1 : SEED_CAP];
-    __shared__ SegIdx seg_lds[BIG ? 1 : SEED_CAP + 1];
-    __shared__ __attribute__((aligned(16))) uint8_t segT_lds[BIG ? 4 : SEED_CAP];
-    const uint32_t cap = BIG ? P.big_cap : (uint32_t)SEED_CAP;
+    __shared__ LSeed seeds_lds[LSEEDS ? SEED_CAP : 1];
+    __shared__ SegIdx seg_lds[LSEEDS ? SEED_CAP + 1 : 1];
+    __shared__ __attribute__((aligned(16))) uint8_t segT_lds[LSEEDS ? SEED_CAP : 4];
+    const uint32_t cap = BIG ? P.big_cap : (REV ? 0u : (uint32_t)SEED_CAP);
     LSeed *const seeds = BIG ? P.big_seeds + (size_t)blockIdx.x * cap : seeds_lds;
     SegIdx *const seg_begin = BIG ? reinterpret_cast<SegIdx *>(P.big_seg + (size_t)blockIdx.x * (cap + 1)) : seg_lds;
     uint8_t *const seg_T = BIG ? P.big_segT + (size_t)blockIdx.x * cap : segT_lds;
     __shared__ uint32_t it_lo[SBLOCK], it_cnt[SBLOCK], it_pre[SBLOCK + 1], it_info[SBLOCK];
     __shared__ uint32_t it_key[SBLOCK];
     __shared__ uint32_t it_d[SBLOCK];   // D(p): distance to the previous usable query word (spec 2)
-    __shared__ uint32_t hq_pos[SBLOCK / 64][64 * HBATCH];   // per-wave queue of hits for the full test
-    __shared__ uint8_t hq_k[SBLOCK / 64][64 * HBATCH];
+    __shared__ uint32_t hq_pos[SBLOCK / 64][64 * HB];   // per-wave queue of hits for the full test
+    __shared__ uint8_t hq_k[SBLOCK / 64][64 * HB];
     __shared__ uint64_t it_qlw[SBLOCK], it_qlm[AMB ? SBLOCK : 1];
     __shared__ uint64_t iso_start[ISO_LDS];
     __shared__ uint32_t iso_len[ISO_LDS], iso_gtx[ISO_LDS], iso_pre[ISO_LDS + 1];
     __shared__ uint16_t it_iso[SBLOCK];   // isoform of each word item (it_info: p | strand << 24)
-    __shared__ uint32_t tcnt[PASS_SAMPLES], tpre[PASS_SAMPLES + 1];   // by subject sample - T0
+    __shared__ uint32_t tcnt[REV ? 1 : PASS_SAMPLES], tpre[REV ? 1 : PASS_SAMPLES + 1];   // by subject sample - T0
     __shared__ uint32_t wsum[SBLOCK / 64];
     __shared__ uint32_t sh_nseed, sh_flags, sh_rs0, sh_rs1;
     __shared__ unsigned long long sh_sbase, sh_cbase, sh_lbase;
@@ -396,17 +409,17 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
             const int lane = tid & 63, wid = tid >> 6;
             uint32_t *wqp = hq_pos[wid];
             uint8_t *wqk = hq_k[wid];
-            for (uint32_t hb0 = 0; hb0 < nh; hb0 += SBLOCK * HBATCH) {
-                // pass A: HBATCH hits per lane with their loads in flight
+            for (uint32_t hb0 = 0; hb0 < nh; hb0 += SBLOCK * HB) {
+                // pass A: HB hits per lane with their loads in flight
                 // together; drop other keys, other samples and hits the
                 // sequence pre-test proves non-canonical (the s bases before
                 // them equal and unambiguous, no transcript start in
                 // (pos - s, pos]: the full test below would reject them)
-                uint32_t hk[HBATCH];
-                uint64_t hev[HBATCH], hsw[HBATCH], hsm[HBATCH], hbw[HBATCH];
-                bool live[HBATCH];
+                uint32_t hk[HB];
+                uint64_t hev[HB], hsw[HB], hsm[HB], hbw[HB];
+                bool live[HB];
 #pragma unroll
-                for (int j = 0; j < HBATCH; j++) {
+                for (int j = 0; j < HB; j++) {
                     const uint32_t h = hb0 + (uint32_t)j * SBLOCK + (uint32_t)tid;
                     live[j] = h < nh;
                     hk[j] = live[j] ? (uint32_t)run_of(it_pre, h) : 0u;
@@ -422,18 +435,18 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                 // hit binary-searches its previous word's list there; hits whose
                 // previous list is not wholly in this chunk take the sequence
                 // pre-test.
-                constexpr uint32_t HCHUNK = SBLOCK * HBATCH;
+                constexpr uint32_t HCHUNK = SBLOCK * HB;
                 uint32_t *chk = &hq_pos[0][0];
                 if (lpre) {
                     __syncthreads();   // the previous chunk's queue is consumed
 #pragma unroll
-                    for (int j = 0; j < HBATCH; j++)
+                    for (int j = 0; j < HB; j++)
                         if (live[j]) chk[(uint32_t)j * SBLOCK + (uint32_t)tid] = (uint32_t)hev[j];
                     __syncthreads();
                 }
                 SEED_TICK(5);
 #pragma unroll
-                for (int j = 0; j < HBATCH; j++) {
+                for (int j = 0; j < HB; j++) {
                     const uint32_t pos = (uint32_t)hev[j];
                     live[j] = live[j] && (uint32_t)(hev[j] >> 32) == it_key[hk[j]] && pos >= pb0 && pos < pb1 &&
                               (pos < qpb0 || pos >= qpb1);
@@ -472,7 +485,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                 if (lpre) __syncthreads();   // every wave is done with chk before the queue reuses it
                 uint32_t qn = 0;
 #pragma unroll
-                for (int j = 0; j < HBATCH; j++) {
+                for (int j = 0; j < HB; j++) {
                     if (live[j] && (((hsw[j] | hsm[j]) >> (64 - 2 * stride)) == 0) && ((hbw[j] >> (64 - stride)) == 0))
                         live[j] = false;
                     const uint64_t m = __ballot(live[j]);
@@ -544,7 +557,7 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
                     }
                     const int len = l + W16 + r;
                     if (len < P.word) continue;
-                    if (P.rev) {
+                    if (REV) {
                         // the reverse pass: only runs the forward pass cannot see
                         // go on -- no usable aligned word of the subject (the
                         // forward query, oriented by the strand) inside -- as
@@ -603,7 +616,15 @@ __global__ __launch_bounds__(SBLOCK, RC_SEED_WAVES) void seed_kernel(Db db, Inde
             }
             __syncthreads();
         }
-        if (P.rev) break;   // the reverse pass keeps no seeds of its own
+        if (REV) {   // the reverse pass keeps no seeds of its own: on to the next subject samples
+            T0 = T1;
+            T1 = min(Tr, T0 + PASS_SAMPLES);
+            if (T0 < Tr) {
+                pass_mask(T0);
+                __syncthreads();
+            }
+            continue;
+        }
         if (sh_flags & 1u) {   // too many seeds: fewer subject samples per pass
             if (T1 - T0 == 1) {
                 // one subject sample alone overflows: the global-memory pass
@@ -2865,20 +2886,22 @@ __global__ __launch_bounds__(256) void mirror_sort_big_kernel(GroupParams P)
 // launchers
 // ------------------------------------------------------------------------
 
+template <bool AMB, bool REV>
+static void launch_seed_t(const Db &db, const Index &ix, const SeedParams &P, uint32_t n, hipStream_t st)
+{
+    hipLaunchKernelGGL((seed_kernel<AMB, false, false, REV>), dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
+    if (P.iso_n)   // the run's genes with more than ISO_LDS isoforms
+        hipLaunchKernelGGL((seed_kernel<AMB, false, true, REV>), dim3(P.iso_n), dim3(SBLOCK), 0, st, db, ix, P);
+}
+
 void launch_seed(bool amb, const Db &db, const Index &ix, const SeedParams &P, hipStream_t st)
 {
     const uint32_t n = P.gene_end - P.gene_begin;
     if (n == 0) return;
-    if (amb)
-        hipLaunchKernelGGL((seed_kernel<true, false, false>), dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
+    if (P.rev)
+        (amb ? launch_seed_t<true, true> : launch_seed_t<false, true>)(db, ix, P, n, st);
     else
-        hipLaunchKernelGGL((seed_kernel<false, false, false>), dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
-    if (P.iso_n) {   // the run's genes with more than ISO_LDS isoforms
-        if (amb)
-            hipLaunchKernelGGL((seed_kernel<true, false, true>), dim3(P.iso_n), dim3(SBLOCK), 0, st, db, ix, P);
-        else
-            hipLaunchKernelGGL((seed_kernel<false, false, true>), dim3(P.iso_n), dim3(SBLOCK), 0, st, db, ix, P);
-    }
+        (amb ? launch_seed_t<true, false> : launch_seed_t<false, false>)(db, ix, P, n, st);
 }
 
 // the global-memory passes of the (gene, sample) entries P.big_list[0, n)
@@ -2886,9 +2909,9 @@ void launch_seed_big(bool amb, const Db &db, const Index &ix, const SeedParams &
 {
     if (n == 0) return;
     if (amb)
-        hipLaunchKernelGGL((seed_kernel<true, true, false>), dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
+        hipLaunchKernelGGL((seed_kernel<true, true, false, false>), dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
     else
-        hipLaunchKernelGGL((seed_kernel<false, true, false>), dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
+        hipLaunchKernelGGL((seed_kernel<false, true, false, false>), dim3(n), dim3(SBLOCK), 0, st, db, ix, P);
 }
 
 void launch_extend(bool amb, const Db &db, const ExtParams &P, hipStream_t st)

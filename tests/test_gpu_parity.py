@@ -560,6 +560,37 @@ def test_more_than_256_samples(native):
     eng.close()
 
 
+def test_reverse_pass_beyond_256_subjects(native):
+    """The reverse pass (shared searches with DUST: reverse-search runs no
+    forward word finds, from poly-A context) over more than 256 subject
+    samples: queries past sample 256 take a second 256-sample pass (round 5
+    and earlier stopped after the first). Samples 0-255 and 256-299 are two
+    unrelated corpora (no run of 28 matching bases between them), the second
+    with poly-A tails, so the reverse-only seeds of the whole run are exactly
+    those of the two corpora run alone; every pair among samples 256-299 and
+    pairs across the blocks bit-exact against the oracle."""
+    import dataclasses
+    import itertools
+    from oracle.parity import check_pairs
+    from rna_clique_amd.simulate import simulate
+    low, _ = simulate(256, 8, seed=62, mutation_rate=0.003, p_revcomp=0.3)
+    high, _ = simulate(44, 8, seed=63, mutation_rate=0.003, polya=(0.6, 10, 60), p_revcomp=0.3)
+    high = [dataclasses.replace(s, name="H" + s.name) for s in high]
+    samples = low + high
+    counts = []
+    for part in (low, high, samples):
+        eng = _run_sim(part)
+        counts.append(eng.timings()["reverse_seeds"])
+        if part is not samples:
+            eng.close()
+    assert counts[1] > 0 and counts[2] == counts[0] + counts[1], counts
+    picks = list(itertools.combinations(range(256, 300), 2))
+    picks += [(a, b) for a in range(0, 256, 17) for b in (256, 271, 299)]
+    msgs = check_pairs(eng, samples, picks)
+    assert not msgs, "\n".join(msgs[:10])
+    eng.close()
+
+
 def test_gene_with_4200_isoforms(native):
     """A gene with 4200 transcripts (more than round 3's 4095: the 12-bit
     isoform field of the seed key; the field now takes what the longest
