@@ -2592,6 +2592,12 @@ __global__ __launch_bounds__(256) void first_finish_kernel(ExtParams P)
         bool live[2] = {false, false};
         int bqa[2] = {0, 0}, bqb[2] = {0, 0}, bsa[2] = {0, 0}, bsb[2] = {0, 0}, ex[2] = {-1, -1};
         const int *fxd[2] = {nullptr, nullptr};
+        // each live search's HSP fields from its box, computed (and the bit
+        // score and cut loads issued) before the pass over the seeds, so that
+        // they are not round trips of their own after it
+        int bsc[2] = {0, 0}, bd[2] = {0, 0}, bg[2] = {0, 0}, bo[2] = {0, 0}, bni[2] = {0, 0}, b10[2] = {0, 0};
+        const int thr_f = P.thr[(size_t)cd.ssam * (size_t)(P.max_len + 1) + (size_t)cd.Lq];
+        const int thr_r = P.thr[(size_t)cd.qsam * (size_t)(P.max_len + 1) + (size_t)cd.Lt];
         for (int dir = 0; dir < ndir; dir++) {
             if (P.share && !((cd.dflags >> dir) & 1)) {   // this search found no seed here
                 (dir ? P.cand_nh_r : P.cand_nh)[ci] = 0;
@@ -2615,6 +2621,15 @@ __global__ __launch_bounds__(256) void first_finish_kernel(ExtParams P)
             bsa[dir] = y - fx[FX_L + 2];
             bsb[dir] = y + len + fx[FX_R + 2];
             live[dir] = true;
+            const int rsc = fx[FX_R], ri = fx[FX_R + 1], rj = fx[FX_R + 2], rd = fx[FX_R + 3], rgo = fx[FX_R + 4];
+            const int lsc = fx[FX_L], lI = fx[FX_L + 1], lJ = fx[FX_L + 2], ld = fx[FX_L + 3], lgo = fx[FX_L + 4];
+            const int lg = lgo & GMASK, lo2 = (lgo >> OBIT) & GMASK, rg = rgo & GMASK, ro = (rgo >> OBIT) & GMASK;
+            bsc[dir] = lsc + 2 * len + rsc;
+            bd[dir] = ld + rd;
+            bg[dir] = lg + rg;
+            bo[dir] = lo2 + ro;
+            bni[dir] = len + (lI + lJ - 2 * ld + lg) / 2 + (ri + rj - 2 * rd + rg) / 2;
+            b10[dir] = P.bits10[bsc[dir]];
         }
         // the other seeds of each live search inside its box? (four seeds'
         // loads in flight at a time)
@@ -2649,17 +2664,8 @@ __global__ __launch_bounds__(256) void first_finish_kernel(ExtParams P)
                 (dir ? P.defer_r : P.defer)[di] = (uint32_t)ci;
                 continue;
             }
-            const int *fx = fxd[dir];
-            const int len = (int)(P.seeds[cd.seed_off + ex[dir]].len & SEED_LEN);
-            const int rsc = fx[FX_R], ri = fx[FX_R + 1], rj = fx[FX_R + 2], rd = fx[FX_R + 3], rgo = fx[FX_R + 4];
-            const int lsc = fx[FX_L], lI = fx[FX_L + 1], lJ = fx[FX_L + 2], ld = fx[FX_L + 3], lgo = fx[FX_L + 4];
-            const int lg = lgo & GMASK, lo2 = (lgo >> OBIT) & GMASK, rg = rgo & GMASK, ro = (rgo >> OBIT) & GMASK;
-            const int bsc = lsc + 2 * len + rsc, bd = ld + rd, bg = lg + rg, bo = lo2 + ro;
-            const int bni = len + (lI + lJ - 2 * ld + lg) / 2 + (ri + rj - 2 * rd + rg) / 2;
-            const int thr_f = P.thr[(size_t)cd.ssam * (size_t)(P.max_len + 1) + (size_t)cd.Lq];
-            const int thr_r = P.thr[(size_t)cd.qsam * (size_t)(P.max_len + 1) + (size_t)cd.Lt];
-            const bool pf = (!P.share || dir == 0) && bsc >= thr_f;
-            const bool pr = (P.sym || (P.share && dir == 1)) && bsc >= thr_r;
+            const bool pf = (!P.share || dir == 0) && bsc[dir] >= thr_f;
+            const bool pr = (P.sym || (P.share && dir == 1)) && bsc[dir] >= thr_r;
             if (pf || pr) {
                 DHsp h;
                 h.q_tx = cd.q_gtx;
@@ -2670,13 +2676,13 @@ __global__ __launch_bounds__(256) void first_finish_kernel(ExtParams P)
                     h.qstart = cd.Lq - bqb[dir] + 1; h.qend = cd.Lq - bqa[dir];
                     h.sstart = bsb[dir]; h.send = bsa[dir] + 1;
                 }
-                h.gaps = bg;
-                h.gapopen = bo;
-                h.mismatch = bd - bg;
-                h.nident = bni;
-                h.length = bni + bd;
-                h.score_half = bsc;
-                h.bits10 = P.bits10[bsc];
+                h.gaps = bg[dir];
+                h.gapopen = bo[dir];
+                h.mismatch = bd[dir] - bg[dir];
+                h.nident = bni[dir];
+                h.length = bni[dir] + bd[dir];
+                h.score_half = bsc[dir];
+                h.bits10 = b10[dir];
                 h.strand = cd.strand | (pf ? HSP_FWD : 0) | (pr ? HSP_REV : 0);
                 hsp_out[ci] = h;
             }
