@@ -35,10 +35,13 @@ constexpr int SBLOCK = 256;
 #endif
 constexpr int SEED_CAP = RC_SEED_CAP;   // seeds of one pass in LDS (a power of two: the bitonic sort pads to one)
 static_assert((SEED_CAP & (SEED_CAP - 1)) == 0, "RC_SEED_CAP must be a power of two");
+// Hits per lane per batch of the forward pass (their loads in flight
+// together; r05 at C3: 3 / 4 / 6 / 7 -> 59.1 / 58.3 / 56.6 / 71.4 ms, 7 no
+// longer fits 5 workgroups' LDS; C3v 86.3 -> 84.6 ms at 6)
 #ifndef RC_HBATCH
-#define RC_HBATCH 4
+#define RC_HBATCH 6
 #endif
-constexpr int HBATCH = RC_HBATCH;                  // hits per lane per batch of the seed kernel
+constexpr int HBATCH = RC_HBATCH;
 // The reverse pass (REV) keeps no seeds in LDS and finds few hits (the
 // near-mask index is small): its own instantiation, without the seed and
 // per-sample arrays and with fewer hits per lane, runs more workgroups per CU.
