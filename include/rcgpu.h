@@ -287,7 +287,9 @@ int rc_dust_mask(rc_engine *eng, int32_t s, uint8_t *buf, uint64_t cap, uint64_t
  * own; out == NULL queries n_words. `on_device`: out is a device pointer.
  * Results of an earlier rc_align / rc_finish stay valid (they do not depend
  * on the loaded tile's tables); rc_dust_mask then reads this pass's tile and
- * fails with RC_E_STATE when the pass used a tile of its own.
+ * fails with RC_E_STATE when the pass used a tile of its own, or -- a pass
+ * over the loaded tile itself -- for a sample the pass did not list (its mask
+ * was cleared; the next rc_align / rc_run masks every sample again).
  * rc_set_dust_masks: masks for these samples (replacing any given before;
  * n = 0 clears them): rc_align copies them into its tiles instead of running
  * DUST on those samples. They must come from engines with the same DUST

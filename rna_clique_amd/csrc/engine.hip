@@ -340,6 +340,9 @@ struct rc_engine {
     // DUST masks given by rc_set_dust_masks (computed once per sample across
     // shards): word offset of each sample's mask in d_dust_imp, ~0 = not given
     std::vector<uint64_t> dust_imp_off;
+    // after an rc_dust_masks pass over the loaded tile itself: which samples'
+    // masks it recomputed (the others were cleared); empty = every tile sample
+    std::vector<char> dmask_only;
     // the b chunk (split tiles) whose index and DUST masks the device holds
     // from this run's previous tile (-1: none)
     int idx_bchunk = -1;
@@ -1653,6 +1656,7 @@ static int align_tile(rc_engine *e, int ti)
     // of any other tile -- except those given by rc_set_dust_masks, whose
     // masks are copied in (samples start at 256-base boundaries: whole words)
     std::vector<int> dust_here;
+    e->dmask_only.clear();   // every sample of this tile gets its mask
     if (dust) {
         const size_t mw = (total >> 6) + 4;
         CHK(e->d_dmask.ensure(mw));
@@ -2819,6 +2823,8 @@ int rc_dust_mask(rc_engine *e, int32_t s, uint8_t *buf, uint64_t cap, uint64_t *
     const auto &ts = e->tiles[e->tile_loaded].samples;
     if (std::find(ts.begin(), ts.end(), s) == ts.end())
         return fail(RC_E_STATE, "the sample is not in the last alignment pass (tile)");
+    if (!e->dmask_only.empty() && !e->dmask_only[s])
+        return fail(RC_E_STATE, "the last rc_dust_masks pass did not mask this sample");
     CHK(set_device(e));
     const uint64_t b0 = e->tile_pos[s];
     const uint64_t w0 = b0 >> 6, w1 = (b0 + S.nbases + 63) >> 6;
@@ -2945,6 +2951,10 @@ int rc_dust_masks(rc_engine *e, const int32_t *samples, int32_t n, uint64_t *out
             e->tile_loaded = -1;
         }
     }
+    if (own) {   // the loaded tile's masks now hold the listed samples only
+        e->dmask_only.assign(N, 0);
+        for (int s : ss) e->dmask_only[s] = 1;
+    }
     // bits past each sample's last base cleared (its last word)
     uint64_t o = 0;
     for (int32_t i = 0; rc == RC_OK && dust && i < n; i++) {
@@ -3054,6 +3064,20 @@ int rc_import_edge_parts(rc_engine *e, const void *buf, const uint64_t *counts, 
             }
         }
     }
+    if (on_device) {
+        // the same range check on the device, over the caller's blocks before
+        // anything of the engine's is replaced: a malformed all-gather must
+        // not reach the union-find kernels, and a refused import leaves the
+        // engine's own edges in place
+        unsigned int bad = 0;
+        HIPCHK(hipMemsetAsync(e->d_status.p + 2, 0, sizeof(unsigned int), e->st));
+        for (int32_t r = 0; r < parts; r++)
+            if (counts[r]) launch_edge_check(src + (uint64_t)r * stride, counts[r], ng, np, e->d_status.p + 2, e->st);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(&bad, e->d_status.p + 2, sizeof bad, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipStreamSynchronize(e->st));
+        if (bad) return fail(RC_E_ARG, "edge record out of range");
+    }
     // the local edges are replaced: their buffer goes before the new one is
     // allocated (a sharded rank's peak holds the gathered records once)
     if (e->d_edges.cap < n) e->d_edges.release();
@@ -3067,22 +3091,7 @@ int rc_import_edge_parts(rc_engine *e, const void *buf, const uint64_t *counts, 
     }
     e->n_edges = n;
     e->n_local_edges = 0;   // the local edges are gone
-    if (on_device) {
-        // the same range check on the device: a malformed all-gather must not
-        // reach the union-find kernels
-        unsigned int bad = 0;
-        HIPCHK(hipMemsetAsync(e->d_status.p + 2, 0, sizeof(unsigned int), e->st));
-        launch_edge_check(e->d_edges.p, n, ng, np, e->d_status.p + 2, e->st);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(&bad, e->d_status.p + 2, sizeof bad, hipMemcpyDeviceToHost, e->st));
-        HIPCHK(hipStreamSynchronize(e->st));
-        if (bad) {
-            e->n_edges = 0;
-            return fail(RC_E_ARG, "edge record out of range");
-        }
-    } else {
-        HIPCHK(hipStreamSynchronize(e->st));   // (the caller's host buffer is not retained)
-    }
+    HIPCHK(hipStreamSynchronize(e->st));   // (the caller's host buffer is not retained)
     return do_graph(e);
 }
 

@@ -144,44 +144,55 @@ def exchange_edges(eng, process_group=None, trim=None):
     """All-gather the shards' graph edges and run the graph phase on them.
     The engine must have run align() and finish().
 
-    RCCL path: the counts go first; each rank's records are exported straight
-    into its own slot of one padded receive buffer (W x the largest count),
-    gathered in place, and the engine imports that buffer as it is
-    (rc_import_edge_parts: no compacting copy). `trim`: free the engine's
-    alignment working set first (rc_trim) -- None = only when the receive
-    buffer and the imported records would not fit in free device memory
-    (C5: 17 GB + 16 GB beside a ~146 GB alignment working set)."""
+    The counts go first; each rank's records are exported straight into its
+    own slot of one padded receive buffer (W x the largest count), gathered in
+    place, and the engine imports that buffer as it is (rc_import_edge_parts:
+    no compacting copy). RCCL: a device buffer, device-to-device throughout;
+    gloo: the same buffer in host memory (the CPU tests run this exact
+    sequence: slot aliasing, padding, unequal counts). `trim`: free the
+    engine's alignment working set first (rc_trim) -- None = only when the
+    receive buffer, the imported records and the graph writer's sort buffers
+    would not fit in free device memory (C5: 17 GB + 16 GB beside a ~146 GB
+    alignment working set)."""
     import torch
     import torch.distributed as dist
     rs = eng.edge_record_size()
     on_gpu = dist.get_backend(process_group) != "gloo" and torch.cuda.is_available()
-    if not on_gpu:
-        local = torch.from_numpy(eng.export_edges())
-        allt, total = all_gather_records(local, rs, process_group)
-        eng.import_edges(allt.numpy())
-        return
+    dev = "cuda" if on_gpu else "cpu"
     W, R = world(process_group)
     n = eng.local_edge_count()
-    c = torch.tensor([n], dtype=torch.int64, device="cuda")
+    c = torch.tensor([n], dtype=torch.int64, device=dev)
     cs = [torch.zeros_like(c) for _ in range(W)]
     dist.all_gather(cs, c, group=process_group)
     counts = [int(x.item()) for x in cs]
     mx = max(counts)
-    if trim is None:
+    if on_gpu and trim is None:
         free, _ = torch.cuda.mem_get_info()
-        trim = (W * mx + sum(counts)) * rs > 0.9 * free
-    if trim:
+        trim = exchange_device_bytes(counts, rs) > 0.9 * free
+    if on_gpu and trim:
         eng.trim()
-    recv = torch.empty(max(W * mx * rs, 1), dtype=torch.uint8, device="cuda")
+    recv = torch.empty(max(W * mx * rs, 1), dtype=torch.uint8, device=dev)
     if mx:
         mine = recv[R * mx * rs:(R + 1) * mx * rs]
-        eng.export_edges(mine)             # device-to-device, engine stream synced
+        eng.export_edges(mine)             # into this rank's slot (device-to-device on GPUs)
         dist.all_gather_into_tensor(recv[:W * mx * rs], mine, group=process_group)
-        torch.cuda.current_stream().synchronize()   # the engine runs on its own stream
+        if on_gpu:
+            torch.cuda.current_stream().synchronize()   # the engine runs on its own stream
     eng.import_edge_parts(recv, counts, mx)
     del recv
-    if mx * W * rs >= (1 << 30):
+    if on_gpu and mx * W * rs >= (1 << 30):
         torch.cuda.empty_cache()   # the engine allocates outside torch's pool
+
+
+def exchange_device_bytes(counts, record_size):
+    """Device bytes the edge exchange and the graph phase after it add on top
+    of an engine's alignment working set: the imported copy of every record,
+    plus the larger of the padded receive buffer (W x the largest count; freed
+    after the import) and what rc_write_graph then allocates for the device
+    sort of the records (16 B of keys and indices per record, a sorted record
+    copy, and the radix sort's scratch, about its key bytes)."""
+    W, mx, tot = len(counts), max(counts) if counts else 0, sum(counts)
+    return tot * record_size + max(W * mx * record_size, tot * (16 + record_size + 8))
 
 
 def dust_owners(sample_bases, shard_count):

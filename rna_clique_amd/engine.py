@@ -139,8 +139,9 @@ class Engine:
         return int(nat.lib().rc_edge_record_size())
 
     def export_edges(self, out=None):
-        """This shard's graph edges as opaque records: into `out` (a CUDA
-        uint8 tensor, written device-to-device) or a new host uint8 array."""
+        """This shard's graph edges as opaque records: into `out` (a uint8
+        tensor: CUDA, written device-to-device, or CPU) or a new host uint8
+        array."""
         L = nat.lib()
         n = ctypes.c_uint64()
         nat.check(L.rc_export_edges(self._h, None, 0, ctypes.byref(n), 0))
@@ -150,7 +151,7 @@ class Engine:
                 raise ValueError("edge buffer too small")
             if n.value:
                 nat.check(L.rc_export_edges(self._h, ctypes.c_void_p(out.data_ptr()), n.value,
-                                            ctypes.byref(n), 1))
+                                            ctypes.byref(n), 1 if out.is_cuda else 0))
             return n.value
         buf = np.zeros(n.value * rs, dtype=np.uint8)
         if n.value:
@@ -182,6 +183,8 @@ class Engine:
         records -- e.g. an all-gather's padded receive buffer as it is."""
         L = nat.lib()
         c = np.ascontiguousarray(counts, dtype=np.uint64)
+        if not isinstance(buf, np.ndarray) and not buf.is_cuda:
+            buf = buf.numpy()
         if isinstance(buf, np.ndarray):
             buf = np.ascontiguousarray(buf, dtype=np.uint8)
             ptr, dev = buf.ctypes.data_as(ctypes.c_void_p), 0

@@ -12,7 +12,30 @@ import torch.multiprocessing as mp
 REC = 20   # sizeof(DEdge)
 
 
-class FakeShardEngine:
+class SlotExchange:
+    """Engine.export_edges(out) into this rank's slot of the padded receive
+    buffer (a CPU tensor under gloo) and Engine.import_edge_parts over that
+    buffer as it is (blocks of counts[r] records at stride `stride`): the
+    exchange's exact sequence, in-place all-gather and padding included."""
+
+    def export_edges(self, out=None):
+        rec = self._records()
+        if out is None:
+            return rec.copy()
+        assert out.numel() >= rec.size
+        out.numpy()[:rec.size] = rec
+        return rec.size // self.edge_record_size()
+
+    def import_edge_parts(self, buf, counts, stride):
+        rs = self.edge_record_size()
+        b = buf.numpy() if hasattr(buf, "numpy") else np.asarray(buf)
+        assert b.size >= len(counts) * stride * rs
+        self.parts = list(counts)
+        self.import_edges(np.concatenate([b[r * stride * rs:(r * stride + c) * rs] for r, c in enumerate(counts)]
+                                         + [np.zeros(0, np.uint8)]))
+
+
+class FakeShardEngine(SlotExchange):
     """The part of Engine the exchange touches; records are 20-byte blobs."""
 
     def __init__(self, rank, n):
@@ -28,9 +51,8 @@ class FakeShardEngine:
     def local_edge_count(self):
         return len(self.local) // REC
 
-    def export_edges(self, out=None):
-        assert out is None
-        return self.local.copy()
+    def _records(self):
+        return self.local
 
     def import_edges(self, buf, n=None):
         self.imported = np.asarray(buf).copy()
@@ -59,7 +81,7 @@ def _worker(rank, world, port, sizes, q):
         assert distributed.world() == (world, rank)
         eng = FakeShardEngine(rank, sizes[rank])
         distributed.sharded_run(eng)
-        q.put((rank, eng.calls, eng.imported.tobytes()))
+        q.put((rank, eng.calls, eng.imported.tobytes(), eng.parts))
     finally:
         dist.destroy_process_group()
 
@@ -134,8 +156,11 @@ def test_gloo_dust_exchange_world2(bases):
         assert got[r][1] == made_all and got[r][2] == want
 
 
-@pytest.mark.parametrize("sizes", [(3, 5), (0, 4), (0, 0)])
+@pytest.mark.parametrize("sizes", [(3, 5), (7, 2), (0, 4), (0, 0)])
 def test_gloo_edge_exchange_world2(sizes):
+    """Unequal counts: each rank's records go into its slot of one padded
+    buffer, gathered in place, imported as blocks at the largest count's
+    stride."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -144,8 +169,9 @@ def test_gloo_edge_exchange_world2(sizes):
         p.start()
     got = {}
     for _ in procs:
-        r, calls, blob = q.get(timeout=120)
+        r, calls, blob, parts = q.get(timeout=120)
         got[r] = (calls, blob)
+        assert parts == list(sizes)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -195,7 +221,7 @@ def test_c5_fits_hbm_per_rank():
     assert max(fp) < 0.65 * one
 
 
-class OracleShardEngine:
+class OracleShardEngine(SlotExchange):
     """The engine's sharded surface computed on the CPU oracles, so that the
     N > 1 host path runs on real alignments: its pairs from plan_pairs, DUST
     masks made by their owners and exchanged (each rank checks what it
@@ -255,8 +281,7 @@ class OracleShardEngine:
     def local_edge_count(self):
         return len(self.edges)
 
-    def export_edges(self, out=None):
-        assert out is None
+    def _records(self):
         rec = np.array([e + (0,) for e in self.edges], dtype=np.int32).reshape(-1, 5)
         return rec.view(np.uint8).reshape(-1)
 
