@@ -275,7 +275,8 @@ def e2e_wall_clock(samples, genes, rank, world, dist, ref):
         dist.barrier()
     if rank == 0:
         shutil.rmtree(root, ignore_errors=True)
-    return {"wall_clock_s": round(dt, 3), "matrix_h5_bytes": size, "matrix_equal_to_steps": same,
+    return {"wall_clock_s": round(dt, 3), "to_matrix_h5_s": round(last_timings.get("to_matrix_s", dt), 3),
+            "matrix_h5_bytes": size, "matrix_equal_to_steps": same,
             "od2_tables": n_tables, "graph_pkl_mb": graph_mb, "fasta_write_s": round(t_w, 1),
             "phases_s": {k: round(v, 3) for k, v in last_timings.items()},
             "what": "transcripts FASTA on disk -> top-gene selection -> GPU path -> od2/*.h5 gene matches "

@@ -5,6 +5,7 @@
 // coordinates, pandas index labels, sorted-label matrix order).
 #include "../../include/rcgpu.h"
 #include "device.h"
+#include "graph_pickle.h"
 
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
@@ -56,6 +57,8 @@ void launch_tx_masked(const TxInfo *, uint32_t, const uint64_t *, uint8_t *, hip
 void launch_edge_check(const DEdge *, uint64_t, uint32_t, uint64_t, unsigned int *, hipStream_t);
 void launch_edge_key(const DEdge *, uint64_t, const uint32_t *, uint32_t *, uint32_t *, hipStream_t);
 void launch_edge_gather(const DEdge *, const uint32_t *, uint64_t, DEdge *, hipStream_t);
+void launch_edge_uv(const DEdge *, const uint32_t *, const uint32_t *, uint64_t, uint32_t *, uint32_t *, uint64_t *,
+                    hipStream_t);
 void launch_tile_tables(const TileSeg *, uint32_t, uint32_t, const uint64_t *, const uint64_t *, TxInfo *, TxInfo *,
                         uint32_t *, TxInfo *, uint64_t *, uint32_t, uint64_t, uint64_t *, IsoRec *, uint64_t,
                         const uint64_t *, PosTx *, uint64_t, hipStream_t);
@@ -3183,29 +3186,46 @@ int rc_shard_pairs(rc_engine *e, int64_t *first, int64_t *last)
 // sharded run's after rc_import_edges) are stably sorted on the device by
 // their pair's combinations rank and copied to the host; tbeg[k] is the first
 // record of the k-th non-empty pair.
-static int sorted_edge_tables(rc_engine *e, std::vector<DEdge> &rec, std::vector<uint64_t> &tbeg)
+// graph.pkl's tables from the edge records: sorted on the device into every
+// pair's table in combinations order (stable: record order inside a pair),
+// then handed to the writer as node-slot pairs -- a record's genes are global
+// gene indices, sample-major, so sample s's nodes are the slots
+// [gene_base[s], gene_base[s + 1]) -- with the tables' row ranges. One
+// record per edge (the RBH kernel aggregates an edge's rows into it), so the
+// writer skips its edge deduplication.
+static int edge_slots(rc_engine *e, GraphSlots &G)
 {
     if (!e->finished) return fail(RC_E_STATE, "no results yet");
     CHK(set_device(e));
     const uint64_t n = e->n_edges;
     const int N = (int)e->samples.size();
     if (n > 0xFFFFFFFFull) return fail(RC_E_LIMIT, "more than 2^32 graph edges");
-    std::vector<uint32_t> comb(e->pair_a.size());
-    for (size_t p = 0; p < comb.size(); p++) {
+    const size_t ncomb = e->pair_a.size();
+    std::vector<uint32_t> comb(ncomb);
+    for (size_t p = 0; p < ncomb; p++) {
         const uint64_t a = (uint64_t)e->pair_a[p], b = (uint64_t)e->pair_b[p];
         comb[p] = (uint32_t)(a * (2 * (uint64_t)N - a - 1) / 2 + (b - a - 1));
     }
-    rec.resize(n);
-    tbeg.clear();
+    G = GraphSlots();
+    G.ns = N;
+    G.base.assign((size_t)N + 1, 0);
+    for (int32_t s : e->gene_sample) G.base[(size_t)s + 1]++;
+    for (int s = 0; s < N; s++) G.base[s + 1] += G.base[s];
+    G.slot_gene = e->gene_id.data();
+    G.unique = true;
+    G.rows = n;
+    std::vector<uint64_t> first(ncomb, ~0ull);
     if (n) {
         DBuf<uint32_t> dcomb, k0, k1, v0, v1;
-        DBuf<DEdge> out;
-        CHK(dcomb.ensure(comb.size()));
+        DBuf<uint64_t> dfirst;
+        CHK(dcomb.ensure(ncomb));
+        CHK(dfirst.ensure(std::max<size_t>(ncomb, 1)));
         CHK(k0.ensure(n));
         CHK(k1.ensure(n));
         CHK(v0.ensure(n));
         CHK(v1.ensure(n));
-        HIPCHK(hipMemcpyAsync(dcomb.p, comb.data(), comb.size() * 4, hipMemcpyHostToDevice, e->st));
+        HIPCHK(hipMemcpyAsync(dcomb.p, comb.data(), ncomb * 4, hipMemcpyHostToDevice, e->st));
+        HIPCHK(hipMemsetAsync(dfirst.p, 0xFF, ncomb * 8, e->st));
         launch_edge_key(e->d_edges.p, n, dcomb.p, k0.p, v0.p, e->st);
         HIPCHK(hipGetLastError());
         size_t tmp = 0;
@@ -3214,62 +3234,52 @@ static int sorted_edge_tables(rc_engine *e, std::vector<DEdge> &rec, std::vector
         HIPCHK(rocprim::radix_sort_pairs(e->d_tmp.p, tmp, k0.p, k1.p, v0.p, v1.p, (size_t)n, 0u, 32u, e->st));
         uint32_t last = 0;
         HIPCHK(hipMemcpyAsync(&last, k1.p + n - 1, 4, hipMemcpyDeviceToHost, e->st));
-        k0.release();
-        v0.release();
-        CHK(out.ensure(n));
-        launch_edge_gather(e->d_edges.p, v1.p, n, out.p, e->st);
+        // the (a, b) arrays reuse the sort's input buffers
+        launch_edge_uv(e->d_edges.p, v1.p, k1.p, n, k0.p, v0.p, dfirst.p, e->st);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(rec.data(), out.p, n * sizeof(DEdge), hipMemcpyDeviceToHost, e->st));
+        G.U = Raw<uint32_t>(n);
+        G.V = Raw<uint32_t>(n);
+        HIPCHK(hipMemcpyAsync(G.U.data(), k0.p, n * 4, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipMemcpyAsync(G.V.data(), v0.p, n * 4, hipMemcpyDeviceToHost, e->st));
+        if (ncomb) HIPCHK(hipMemcpyAsync(first.data(), dfirst.p, ncomb * 8, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipStreamSynchronize(e->st));
         if (last == ~0u)
             return fail(RC_E_STATE, "an imported graph with isolated nodes or rows outside it: no graph.pkl from edges");
     }
-    for (uint64_t i = 0; i < n; i++)
-        if (i == 0 || rec[i].pair != rec[i - 1].pair) tbeg.push_back(i);
-    tbeg.push_back(n);
+    // the tables: combinations with records, in order (a table ends where the
+    // next one starts)
+    uint64_t end = n;
+    std::vector<GraphSlots::Tab> rev;
+    for (size_t c = ncomb; c-- > 0;) {
+        if (first[c] == ~0ull) continue;
+        const uint64_t o = first[c];
+        rev.push_back(GraphSlots::Tab{e->gene_sample[G.U[o]], e->gene_sample[G.V[o]], o, end - o});
+        end = o;
+    }
+    G.tabs.assign(rev.rbegin(), rev.rend());
     return RC_OK;
 }
 
-// the pickle of sorted_edge_tables' output (gene arrays filled on `threads`
-// host threads); RC_OK or a code (message set)
-static int write_graph_from_edges(const rc_engine *e, const std::vector<DEdge> &rec, const std::vector<uint64_t> &tbeg,
-                                  const char *path, int threads)
+static int write_graph_slots(const rc_engine *e, GraphSlots &G, const char *path)
 {
-    rc_gpickle *g = nullptr;
-    if (rc_graph_pickle_begin(&g) != RC_OK) return fail(RC_E_NOMEM, "graph pickle");
-    std::unique_ptr<rc_gpickle, void (*)(rc_gpickle *)> hold(g, rc_graph_pickle_free);
-    const size_t nt = tbeg.empty() ? 0 : tbeg.size() - 1;
-    std::vector<int64_t *> sgp(nt), qgp(nt);
-    for (size_t t = 0; t < nt; t++) {
-        const DEdge &r0 = rec[tbeg[t]];
-        if (graph_pickle_table(g, e->gene_sample[r0.a], e->gene_sample[r0.b], tbeg[t + 1] - tbeg[t], &sgp[t], &qgp[t]) !=
-            RC_OK)
-            return RC_E_LIMIT;
-    }
-    std::atomic<size_t> next{0};
-    auto fill = [&]() {
-        for (size_t t; (t = next.fetch_add(1)) < nt;)
-            for (uint64_t i = tbeg[t]; i < tbeg[t + 1]; i++) {
-                sgp[t][i - tbeg[t]] = e->gene_id[rec[i].a];
-                qgp[t][i - tbeg[t]] = e->gene_id[rec[i].b];
-            }
-    };
-    std::vector<std::thread> th;
-    for (int k = 1; k < std::max(1, threads); k++) th.emplace_back(fill);
-    fill();
-    for (auto &x : th) x.join();
     std::vector<const char *> names;
     for (const SampleRec &s : e->samples) names.push_back(s.label.c_str());
-    return rc_graph_pickle_write(g, path, (int32_t)names.size(), names.data());
+    return graph_pickle_write_slots(G, path, (int32_t)names.size(), names.data());
 }
 
 extern "C" int rc_write_graph(rc_engine *e, const char *path, int32_t threads)
 {
     if (!e || !path) return fail(RC_E_ARG, "null argument");
-    std::vector<DEdge> rec;
-    std::vector<uint64_t> tbeg;
-    CHK(sorted_edge_tables(e, rec, tbeg));
-    return write_graph_from_edges(e, rec, tbeg, path, std::max(1, std::min(64, (int)threads)));
+    const char *otv = getenv("RC_OUT_TIMING");
+    const bool otime = otv && atoi(otv);
+    const auto t0 = std::chrono::steady_clock::now();
+    (void)threads;   // (the writer sizes its own pool)
+    GraphSlots G;
+    CHK(edge_slots(e, G));
+    if (otime)
+        fprintf(stderr, "rc_write_graph: edge records sorted and fetched %.3f s\n",
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+    return write_graph_slots(e, G, path);
 }
 
 // The outputs a run writes next to matrix.h5: the od2 gene matches tables of
@@ -3316,15 +3326,14 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
     // graph.pkl over every pair in combinations order comes from the edge
     // records (sorted on the device first), written on its own thread beside
     // the tables; other pair lists (and imported graphs) take the rows
-    std::vector<DEdge> grec;
-    std::vector<uint64_t> gbeg;
+    GraphSlots gslots;
     bool edge_graph = false;
     if (graph_path) {
         const int N = (int)e->samples.size();
         bool all = (int64_t)n_pairs == (int64_t)N * (N - 1) / 2;
         for (int a = 0, k = 0; all && a < N; a++)
             for (int b = a + 1; all && b < N; b++, k++) all = s1[k] == a && s2[k] == b;
-        edge_graph = all && sorted_edge_tables(e, grec, gbeg) == RC_OK;
+        edge_graph = all && edge_slots(e, gslots) == RC_OK;
     }
     auto worker = [&]() {
         std::vector<rc_row> buf;
@@ -3419,7 +3428,7 @@ int rc_write_outputs(rc_engine *e, int32_t n_pairs, const int32_t *s1, const int
     slabs.cap = (size_t)(2 * nt + 8);
     auto edge_grapher = [&]() {
         const long long w0 = now_ns();
-        const int rc = write_graph_from_edges(e, grec, gbeg, graph_path, 8);
+        const int rc = write_graph_slots(e, gslots, graph_path);
         if (rc != RC_OK) set_err(rc);
         t_gwrite += now_ns() - w0;
     };

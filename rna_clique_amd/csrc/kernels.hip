@@ -1064,6 +1064,27 @@ __global__ void edge_gather_kernel(const DEdge *edges, const uint32_t *idx, uint
         out[i] = edges[idx[i]];
 }
 
+// the sorted records as the graph.pkl writer takes them: node pairs (a, b)
+// in two arrays, and the first record of each combination (table) -- keys
+// sorted, so a key's first record is where it differs from its predecessor
+__global__ void edge_uv_kernel(const DEdge *edges, const uint32_t *idx, const uint32_t *key, uint64_t n, uint32_t *u,
+                               uint32_t *v, uint64_t *first)
+{
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const DEdge d = edges[idx[i]];
+        u[i] = d.a;
+        v[i] = d.b;
+        const uint32_t k = key[i];
+        if (k != ~0u && (i == 0 || key[i - 1] != k)) first[k] = i;
+    }
+}
+
+void launch_edge_uv(const DEdge *edges, const uint32_t *idx, const uint32_t *key, uint64_t n, uint32_t *u, uint32_t *v,
+                    uint64_t *first, hipStream_t st)
+{
+    if (n) hipLaunchKernelGGL(edge_uv_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, edges, idx, key, n, u, v, first);
+}
+
 void launch_edge_key(const DEdge *edges, uint64_t n, const uint32_t *comb_of_pair, uint32_t *key, uint32_t *idx,
                      hipStream_t st)
 {

@@ -121,6 +121,13 @@ def rna_clique(
     sim = SampleSimilarity.from_engine(eng, store_dfs=store_dfs)
     from . import distributed
     writer = distributed.world(process_group)[1] == 0
+    # matrix.h5 as soon as the distances exist: it does not wait for the
+    # tables or graph.pkl (the reference writes graph.pkl first,
+    # filtering_step.py:157-159 then rna_clique.py:175-177; the outputs are
+    # independent)
+    if writer and output_matrix is not None:
+        write_matrix(sim.get_dissimilarity_df(), output_matrix)
+    t3 = time.perf_counter()
     graph_done = False
     if out_dir_2 is not None and table_format != "none":
         # every rank writes the tables of the pairs it owns (all of them on one
@@ -132,19 +139,17 @@ def rna_clique(
         write_pair_tables(eng, [s.path for s in samples], out_dir_2, pts.__getitem__, ext, max(1, jobs),
                           graph_path=gpath)
         graph_done = gpath is not None
-    t3 = time.perf_counter()
+    t4 = time.perf_counter()
     if writer and output_graph is not None and not graph_done:
         sim.write_graph(output_graph)
-    t4 = time.perf_counter()
-    if writer and output_matrix is not None:
-        write_matrix(sim.get_dissimilarity_df(), output_matrix)
     last_timings.clear()
-    last_timings.update(select_s=t1 - t0, engine_s=t2 - t1, tables_s=t3 - t2, graph_s=t4 - t3,
-                        matrix_s=time.perf_counter() - t4)
+    last_timings.update(select_s=t1 - t0, engine_s=t2 - t1, matrix_s=t3 - t2, tables_s=t4 - t3,
+                        graph_s=time.perf_counter() - t4, to_matrix_s=t3 - t0)
     return sim, pts
 
 
 # wall-clock phases of the last rna_clique() call in this process (seconds):
 # top-gene selection with the inputs' upload beside it, engine (GPU path),
-# od2 tables, graph.pkl, matrix.h5
+# matrix.h5, od2 tables (+ graph.pkl on one GPU), graph.pkl (sharded runs);
+# to_matrix_s: from the call to matrix.h5 on disk
 last_timings: dict = {}

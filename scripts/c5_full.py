@@ -14,7 +14,7 @@ filtered_distance.py:30-39, rna_clique.py:171-177).
 Checks (any failure: exit 1):
 * every rank's owned pairs are its plan's; per rank, two pairs (its first
   and the middle one) bit-exact against the C oracle (both directed searches,
-  the pair's table and unfiltered sums; oracle/parity.compare_pair), the
+  the pair's table and unfiltered sums; oracle/parity.compare_pair_fast), the
   oracle running on the host beside the next ranks' GPU work;
 * the graph engine's unfiltered sums of every pair equal the owning rank's
   own (a pair's table depends on nothing else);
@@ -92,7 +92,7 @@ def main():
     from rna_clique_amd.engine import Engine
     from rna_clique_amd.simulate import CONFIGS, simulate
     from oracle.align import OracleDB
-    from oracle.parity import capture_pairs, compare_pair, oracle_threads
+    from oracle.parity import capture_pairs, compare_pair_fast as compare_pair, oracle_threads
     from treecheck import nj_splits, robinson_foulds, tree_splits
 
     S = args.shards

@@ -9,7 +9,8 @@
 * C2 (8 x 10 000): full oracle check (every directed search on the oracle's
   thread pool).
 * C3 (32 x 50 000) at full size, plain and with isoforms, indels, minus-strand
-  genes, recent paralogs and poly-A tails: the oracle on 12 sampled pairs
+  genes, recent paralogs and poly-A tails: the oracle on 20 sampled pairs
+  covering every sample
   (bit exact: HSPs, tables, unfiltered sums), size-independent properties of the
   whole run (symmetric hollow matrix, determinism, filtered <= unfiltered
   sums), and the NJ tree of all 32 samples.
@@ -130,23 +131,26 @@ def _c3_properties(eng, samples, tree, pairs, name="C3"):
     return st
 
 
-def covering_pairs(n, fixed, k=8, seed=2024):
-    """The fixed pairs plus k pairs of a seeded random matching of the n
-    samples: 2k more samples in an oracle-checked pair, at random tree
-    distances (the oracle's Python post-processing costs ~10 s per full-size
-    pair, so the suite keeps to k = 8)."""
+def covering_pairs(n, fixed, k=None, seed=2024):
+    """The fixed pairs plus k pairs (default n // 2: every sample) of a seeded
+    random matching of the n samples, at random tree distances. (Through
+    round 5 the oracle's per-pair Python post-processing took ~10 s and kept
+    k at 8; the vectorised table check, oracle/post_fast.py, takes well under
+    a second, so every sample is now in a checked pair.)"""
+    k = n // 2 if k is None else k
     perm = np.random.default_rng(seed).permutation(n)
     extra = [tuple(sorted((int(perm[2 * i]), int(perm[2 * i + 1])))) for i in range(min(k, n // 2))]
     return list(fixed) + sorted(set(extra) - set(fixed))
 
 
 C3_PAIRS = covering_pairs(32, [(0, 1), (5, 17), (12, 31), (30, 31)])
+assert len(C3_PAIRS) >= 20 and len({x for p in C3_PAIRS for x in p}) == 32
 
 
 @pytest.mark.heartbeat(300)
 def test_config_C3_full_size(native):
-    """C3 at full size (32 x 50 000, ~1.6 Gbp): 12 sampled pairs bit-exact vs
-    the oracle, whole-run properties, NJ tree."""
+    """C3 at full size (32 x 50 000, ~1.6 Gbp): 20 sampled pairs (every
+    sample) bit-exact vs the oracle, whole-run properties, NJ tree."""
     from rna_clique_amd.simulate import CONFIGS, simulate
     samples, tree = simulate(**CONFIGS["C3"])
     eng = _engine_run(samples)
@@ -171,13 +175,15 @@ def test_config_C3_correctness_variant(native):
 
 @pytest.mark.heartbeat(400)
 def test_config_C4_full_size(native):
-    """C4 (64 x 50 000, ~3.3 Gbp, 2016 pairs on one GPU): 12 sampled pairs
-    bit-exact vs the oracle, whole-run properties and the NJ tree of all 64
-    samples (BASELINE configs[3])."""
+    """C4 (64 x 50 000, ~3.3 Gbp, 2016 pairs on one GPU): 36 sampled pairs
+    (every sample) bit-exact vs the oracle, whole-run properties and the NJ
+    tree of all 64 samples (BASELINE configs[3])."""
     from rna_clique_amd.simulate import CONFIGS, simulate
     samples, tree = simulate(**CONFIGS["C4"])
     eng = _engine_run(samples)
-    st = _c3_properties(eng, samples, tree, covering_pairs(64, [(0, 1), (7, 40), (33, 63), (62, 63)]), name="C4")
+    pairs = covering_pairs(64, [(0, 1), (7, 40), (33, 63), (62, 63)])
+    assert len(pairs) >= 36 and len({x for p in pairs for x in p}) == 64
+    st = _c3_properties(eng, samples, tree, pairs, name="C4")
     # the 64-taxon tree is deeper: a few hundred genes miss an edge between
     # distant samples and their components are not ideal cliques
     assert st["components"] == 50000 and st["ideal_components"] > 49000

@@ -10,7 +10,7 @@
 * C5 (128 x 100 000, 200 bp - 5 kb, BASELINE configs[4]): the rank of 8 with
   the largest modelled HBM footprint alone on the GPU with only its ~60 of 128
   samples generated and resident, cut into alignment tiles: whole-shard
-  properties, determinism, two owned pairs bit-exact vs the oracle, and the
+  properties, determinism, four owned pairs bit-exact vs the oracle, and the
   measured HBM use against distributed.hbm_footprint's model.
 """
 import json
@@ -274,8 +274,9 @@ def test_C5_one_rank_shard(native):
                          "hbm_model_gb": model[R] / 1e9, "timings": tm, "stats": st})
     # the model is what planning relies on: the engine's own peak within 20 %
     assert 0.8 * model[R] < peak < 1.2 * model[R]
-    # two owned pairs against the oracle (both directed searches, table, sums)
-    picks = [own[0], own[len(own) // 2]]
+    # four owned pairs against the oracle (both directed searches, table,
+    # sums), spread over the rank's rectangle
+    picks = [own[0], own[len(own) // 4], own[len(own) // 2], own[(3 * len(own)) // 4]]
     with _heartbeat(f"C5: oracle on pairs {picks}"):
         msgs = check_pairs(eng, samples, picks)
     assert not msgs, "\n".join(msgs[:10])

@@ -106,3 +106,82 @@ def test_reference_quirks_recorded():
     noideal = [f for f in FIX if f["expected"].get("matrix", 1) is None
                and "matrix" in f["expected"]["errors"]]
     assert noideal
+
+
+# --- the vectorised restatement (oracle/post_fast.py) used for large pairs
+
+FAST_COLS = {"label": "label", "length": "length", "mismatch": "mismatch", "gapopen": "gapopen",
+             "qstart": "qstart", "qend": "qend", "sstart": "sstart", "send": "send", "bitscore": "bits",
+             "gaps": "gaps", "nident": "nident", "qgene": "qgene", "qiso": "qiso", "sgene": "sgene",
+             "siso": "siso", "reverse": "reverse"}
+
+
+def _fast_rows(t):
+    import numpy as np
+    n = len(t["label"])
+    out = []
+    for i in range(n):
+        r = {c: t[f][i].item() for c, f in FAST_COLS.items()}
+        r["sstrand"] = "minus" if t["strand"][i] else "plus"
+        r["reverse"] = bool(r["reverse"])
+        out.append(r)
+    return out
+
+
+@pytest.mark.parametrize("fx", FIX, ids=[f"s{f['seed']}-n{f['top_matches']}-{f['keep_all']}" for f in FIX])
+def test_fast_match_table_matches_reference(fx):
+    """post_fast.match_table gives the reference's own gene matches tables
+    (labels, row order and every column) on the golden fixtures."""
+    import itertools
+    from oracle import post_fast as pf
+    exp = fx["expected"]
+    if any(k != "matrix" for k in exp["errors"]):
+        pytest.skip("reference raised: " + ", ".join(exp["errors"].values()))
+    hits = {}
+    for k, rows in fx["hits"].items():
+        q, s = k.split("|")
+        hits[(q, s)] = [dict(zip(HC, r)) for r in rows]
+    cmp_cols = ["label"] + [c for c in COLS[1:] if c in FAST_COLS or c == "sstrand"]
+    for t1, t2 in itertools.combinations(fx["samples"], 2):
+        fwd = pf.rows_from_dicts(hits.get((t2, t1), []), po.default_parse_id)
+        rev = pf.rows_from_dicts(hits.get((t1, t2), []), po.default_parse_id)
+        got = _fast_rows(pf.match_table(fwd, rev, fx["top_matches"], fx["keep_all"]))
+        want = [dict(zip(COLS, r)) for r in exp["tables"][f"{t1}|{t2}"]]
+        assert [[r[c] for c in cmp_cols] for r in got] == [[r[c] for c in cmp_cols] for r in want], (t1, t2)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_fast_match_table_equals_plain_restatement(seed):
+    """Randomised tie-heavy searches (few genes and isoforms, few distinct bit
+    scores, empty searches): post_fast.match_table == post_oracle.match_table
+    for top_matches 1-3 and keep_all both ways."""
+    import numpy as np
+    from oracle import post_fast as pf
+    rng = np.random.default_rng(seed)
+
+    def search(n, gq, gs):
+        out = []
+        for _ in range(n):
+            out.append({"qseqid": f"x_cov_1.0_g{rng.integers(0, gq)}_i{rng.integers(1, 3)}",
+                        "sseqid": f"y_cov_2.5_g{rng.integers(0, gs)}_i{rng.integers(1, 3)}",
+                        "pident": 0.0, "length": int(rng.integers(30, 900)), "mismatch": int(rng.integers(0, 9)),
+                        "gapopen": int(rng.integers(0, 3)), "qstart": int(rng.integers(1, 50)),
+                        "qend": int(rng.integers(50, 900)), "sstart": int(rng.integers(1, 900)),
+                        "send": int(rng.integers(1, 900)), "evalue": 0.0,
+                        "bitscore": float(rng.choice([100.0, 250.5, 250.5, 400.0, 401.5])),
+                        "gaps": int(rng.integers(0, 4)), "nident": int(rng.integers(20, 800)),
+                        "sstrand": "minus" if rng.random() < 0.3 else "plus"})
+        return out
+
+    for trial in range(6):
+        nf, nr = [0 if rng.random() < 0.1 else int(rng.integers(1, 400)) for _ in range(2)]
+        gq, gs = int(rng.integers(2, 40)), int(rng.integers(2, 40))
+        fwd, rev = search(nf, gq, gs), search(nr, gs, gq)
+        for top in (1, 2, 3):
+            for keep_all in (True, False):
+                want = po.match_table(po.parse_hits(fwd, po.default_parse_id), po.parse_hits(rev, po.default_parse_id),
+                                      top, keep_all)
+                got = _fast_rows(pf.match_table(pf.rows_from_dicts(fwd, po.default_parse_id),
+                                                pf.rows_from_dicts(rev, po.default_parse_id), top, keep_all))
+                keys = list(FAST_COLS) + ["sstrand"]
+                assert [[r[k] for k in keys] for r in got] == [[r[k] for k in keys] for r in want], (trial, top)
