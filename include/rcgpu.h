@@ -150,8 +150,6 @@ typedef struct rc_timing {
     double load_ms;           /* host wall time loading alignment tiles (tile tables, working copy) */
     double align_wall_ms;     /* host wall time of rc_align (every tile, kernels and host work) */
     double host_wait_ms;      /* host wall time blocked on the engine's stream inside rc_align */
-    double ext_row16_over;    /* first-seed extensions that outgrew a 16-lane row (14 diagonals) and went on
-                                 on 32-lane rows from their saved state (r06) */
 } rc_timing;
 
 void rc_default_opts(rc_opts *opts);

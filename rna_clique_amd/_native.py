@@ -88,7 +88,7 @@ class RcTiming(ctypes.Structure):
         "ext_calls", "ext_fullband", "ext_deferred", "big_passes", "tiles", "dust_ms",
         "band_bound", "maxhsp_bound", "ext_second", "near_index", "reverse_seeds", "ext_slides", "ext_wide", "dev_bytes",
         "dev_peak_bytes", "defer_length", "defer_gaveup", "defer_outside", "index_reused",
-        "ext_retries", "load_ms", "align_wall_ms", "host_wait_ms", "ext_row16_over")]
+        "ext_retries", "load_ms", "align_wall_ms", "host_wait_ms")]
 
 
 assert HSP_DTYPE.itemsize == ctypes.sizeof(RcHsp)

@@ -1677,20 +1677,14 @@ __device__ __forceinline__ int slide_fwd(uint32_t pa, uint32_t pb, int maxn, uin
     }
     int n = x ? (int)(__builtin_ctzll(x) >> 1) : 32;
 #if RC_SLIDE_UNIFORM
-    // the loop is wave-uniform (lane masks in scalar registers): lanes whose
-    // run ended stop advancing and re-read their last window. Per round only
-    // "did the whole window match": a lane that stops on a mismatch keeps
-    // that window's difference, and its matching prefix is counted once
-    // after the loop (r06: 23 -> 14 VALU per round). Round r reads the window
-    // at n = 32 + 32 r (dword offset o = 8 r); a lane goes on while
-    // 32 + 32 r < maxn, i.e. o < 8 ceil((maxn - 32) / 32).
-    const bool go0 = n == 32 && maxn > 32;
-    uint64_t gom = __builtin_amdgcn_ballot_w64(go0);
-    if (gom) {
+    // the loop is wave-uniform (a ballot per round): lanes whose run ended
+    // keep their count and stop advancing; no exec-mask bookkeeping per round
+    // (the dword addresses follow n: a stopped lane re-reads its last window)
+    bool go = n == 32 && maxn > 32;
+    if (__builtin_amdgcn_ballot_w64(go)) {
         const uint32_t a0 = ((pa + 32u) >> 2) & ~3u, b0 = ((pb + 32u) >> 2) & ~3u;
-        const uint32_t olim = 8u * (uint32_t)((maxn - 1) >> 5);   // (maxn > 32 on going lanes)
-        uint32_t o = 0, xlo = 0, xhi = 0;
         do {
+            const uint32_t o = ((uint32_t)(n - 32) >> 2) & ~7u;
             uint64_t wa, wb;
             lds_pair_at(a0 + o, b0 + o, pa, pb, wa, wb);
             x = wa ^ wb;
@@ -1698,16 +1692,10 @@ __device__ __forceinline__ int slide_fwd(uint32_t pa, uint32_t pb, int maxn, uin
                 lds_pair_at(a0 + o + moff / 4u, b0 + o + moff / 4u, pa, pb, wa, wb);
                 x |= wa | wb;
             }
-            const uint64_t mfull = __builtin_amdgcn_ballot_w64(x == 0ull);
-            const uint64_t mstop = gom & ~mfull, madv = gom & mfull;
-            xlo = (uint32_t)lane_sel(mstop, (int)(uint32_t)x, (int)xlo);
-            xhi = (uint32_t)lane_sel(mstop, (int)(uint32_t)(x >> 32), (int)xhi);
-            o = (uint32_t)lane_sel(madv, (int)(o + 8u), (int)o);
-            gom = madv & __builtin_amdgcn_ballot_w64(o < olim);
-        } while (gom);
-        const uint64_t xs = ((uint64_t)xhi << 32) | xlo;
-        const int k = xs ? (int)(__builtin_ctzll(xs) >> 1) : 0;
-        if (go0) n = 32 + 4 * (int)o + k;
+            const int k = x ? (int)(__builtin_ctzll(x) >> 1) : 32;
+            n = go ? n + k : n;
+            go = go && k == 32 && n < maxn;
+        } while (__builtin_amdgcn_ballot_w64(go));
     }
 #else
     if (n == 32 && maxn > 32) {
@@ -1850,7 +1838,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
     RowWin *const rows_win = reinterpret_cast<RowWin *>(rcnt + 8);   // (WIN only)
     {
         const RowArgsK K = row_args();
-        if (threadIdx.x < 7 && threadIdx.x != 4) rcnt[threadIdx.x] = 0;   // [5]: 6 x row steps, [6]: 16-lane overflows
+        if (threadIdx.x < 4 || threadIdx.x == 5) rcnt[threadIdx.x] = 0;   // [5]: 6 x row steps
         for (int i = threadIdx.x; i <= NSHARD; i += EBLOCK) sprefix[i] = K->P.shard_prefix[i];
         // list mode: the candidates are P.list[0, *P.list_n) (a previous row
         // kernel's deferrals), else the linear index space over the shards
@@ -2116,12 +2104,13 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
 
 #ifdef RC_ROW_TIMING
     unsigned long long t_tr = 0, t_st = 0, t_fe = 0, t_sl = 0;   // transitions, steps; fetches and window slides (parts of the transitions)
-    // what 16-lane rows could take: a row's steps until its candidate's live
-    // span first exceeds 14 diagonals (a 16-lane window's limit), and the
-    // candidates that never do
+    // what 16-lane rows could take (r06, profiles/r06_row16): a row's steps
+    // until its candidate's live span first outgrows a 16-lane window (14
+    // diagonals, simulated with its own centring), the candidates that never
+    // do, and that window's slides
     unsigned long long n16 = 0, c16 = 0, sl16 = 0;
     bool ov16 = false, had = false;
-    int w16 = 0;   // the 16-lane window's centre diagonal (simulated)
+    int w16 = 0;
 #endif
     for (;;) {
 #ifdef RC_ROW_TIMING
@@ -2275,19 +2264,13 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                     const uint32_t t = pa; pa = pb; pb = t;
                     const int u = alen; alen = blen; blen = u;
                 }
-                if constexpr (RW == 64 || (RW == 32 && SAVE)) {
-                    // an extension a narrower pass saved when it outgrew its
-                    // window (32 -> 64 lanes; r06: 16 -> 32): continue it
-                    // from the saved state. This window is centred on the
-                    // saved one as far as the band lets it (|kof| <= 31 -
-                    // RW/2), so it holds every saved diagonal; diagonals
-                    // outside the saved window were never reached.
-                    if (K->P.resume_in && K->P.list && lidx < K->P.res_in_cap) {
-                        const int *rec = K->P.resume_in + (size_t)lidx * RES_REC;
-                        const int srw = K->P.res_in_rw;
+                if constexpr (RW == 64) {
+                    // a 32-lane extension that outgrew its window: continue it
+                    // from the saved state (the diagonals outside the window
+                    // were never reached, so the full band's state is it)
+                    if (K->P.resume && K->P.list && lidx < K->P.res_cap) {
+                        const int *rec = K->P.resume + (size_t)lidx * RES_REC;
                         const int phase = rec[RES_PHASE], kof = rec[RES_KOF];
-                        constexpr int KMAX = RW >= 64 ? 0 : 31 - RW / 2;
-                        const int kn = max(-KMAX, min(KMAX, kof));
                         if (phase == A_LDONE) {
                             if (rl < 5) meta[RM_RSC + rl] = rec[RES_RSC + rl];
                             // left extension: forward from reversed position L - x
@@ -2305,53 +2288,27 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                         if (rl == 0) atomicAdd(&rcnt[5], (uint32_t)(d6 - rec[RES_D6]));
                         d6 = rec[RES_D6];
                         best = rec[RES_BEST];
-                        const int kb = rec[RES_PK];   // the best record's diagonal
-                        const int w = rl - RC0 + kn - kof + srw / 2;   // this diagonal's lane in the saved window
-                        const bool inw = w >= 0 && w < srw;
+                        const int kb = rec[RES_PK];
+                        bl = kb + RC0;
+                        const int w = rl - RC0 - kof + 16;   // this diagonal's lane in the saved window
+                        const bool inw = w >= 0 && w < 32;
                         R = inw ? rec[RES_R + (inw ? w : 0)] : -1;
                         goe = inw ? rec[RES_G + (inw ? w : 0)] : 0;
-                        const int lb = kb - kn + RC0;
-                        if (lb >= 0 && lb < RW) {
-                            bl = lb;
-                            if (rl == bl) {
-                                wi = rec[RES_PWI];
-                                wg = rec[RES_PWG];
-                                wd = rec[RES_PWD];
-                            }
-                        } else {
-                            // outside this window: parked, as a slide parks it
-                            bl = BL_PARKED;
-                            if (rl == 0) {
-                                meta[RM_PWI] = rec[RES_PWI];
-                                meta[RM_PWG] = rec[RES_PWG];
-                                meta[RM_PWD] = rec[RES_PWD];
-                                meta[RM_PK] = kb;
-                            }
+                        if (rl == bl) {
+                            wi = rec[RES_PWI];
+                            wg = rec[RES_PWG];
+                            wd = rec[RES_PWD];
                         }
-                        if constexpr (WIN) {
-                            win_begin(phase == A_LDONE ? 1 : 0);
-                            pbk -= (uint32_t)kn;
-                            win_lane(k + kn);
-                        } else {
-                            pbk = pb - (uint32_t)(k + kn);
-                        }
-                        blk = blen + k + kn;
+                        if constexpr (WIN) win_begin(phase == A_LDONE ? 1 : 0); else pbk = pb - (uint32_t)k;
+                        blk = blen + k;
                         mnk = max(min(alen, blk), 0);
-                        nkd = -(k + kn + d6);
+                        nkd = -(k + d6);
                         if (rl == 0) {
                             atomicAdd(&rcnt[0], 1u);
                             meta[RM_PHASE] = phase;
-                            meta[RM_KOF] = kn;
+                            meta[RM_KOF] = 0;
                         }
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                        __builtin_amdgcn_wave_barrier();
                         act = phase + (A_STEP_R - A_RDONE);
-                        // a live lane on this window's edge (the saved window
-                        // sat at the band's edge): the slide logic decides
-                        // before any step (edge lanes are dead when steps start)
-                        if constexpr (RW < 64) {
-                            if (rw_mask<RW>(ballot(R >= 0), row) & (1u | (1u << (RW - 1)))) act = A_SLIDE;
-                        }
                         continue;
                     }
                 }
@@ -2372,7 +2329,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                 const int s = kn - kof;
                 if (s == 0 || lmin - s < 1 || lmax - s > RW - 2) {
                     act = A_ABORT;   // wider than the window, or at the band's edge
-                    if constexpr (SAVE && RW < 64) {
+                    if constexpr (SAVE && RW == 32) {
                         // what the 64-lane pass needs to continue it (A_ABORT
                         // saves it with the frontier): the best record parked
                         // as a slide parks it, the step count, the best score
@@ -2482,7 +2439,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
             } else {   // A_ABORT: the sub-band overflowed
                 const uint64_t ci = (uint64_t)(uint32_t)meta[RM_CLO] | ((uint64_t)(uint32_t)meta[RM_CHI] << 32);
                 const unsigned long long wi2 = defer(ci, true);
-                if constexpr (SAVE && RW < 64) {
+                if constexpr (SAVE && RW == 32) {
                     // the wide pass continues from here: the window's frontier
                     // and the header A_SLIDE left in the bookkeeping
                     if (wi2 != ~0ull) {
@@ -2499,7 +2456,7 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
                         }
                     }
                 }
-                if (rl == 0) atomicAdd(&rcnt[RW == 16 ? 6 : 2], 1u);   // (16-lane overflows apart: they continue on 32 lanes)
+                if (rl == 0) atomicAdd(&rcnt[2], 1u);
                 act = A_FETCH;
             }
         }
@@ -2649,7 +2606,6 @@ __global__ __launch_bounds__(EBLOCK, MINW) void extend_rows_kernel(RowArgs)
     __syncthreads();
     if (threadIdx.x < 4 && ctr) atomicAdd(&ctr[1 + threadIdx.x], (unsigned long long)rcnt[threadIdx.x]);   // [4]: slides
     if (threadIdx.x == 5 && ctr) atomicAdd(&ctr[0], (unsigned long long)(rcnt[5] / 6u));
-    if (threadIdx.x == 6 && ctr && rcnt[6]) atomicAdd(&ctr[38], (unsigned long long)rcnt[6]);
 }
 
 // The candidates' first-seed extensions -> box; the other seeds of the
@@ -3037,18 +2993,10 @@ static unsigned resident_blocks(K kernel, size_t lds)
 
 // A row-kernel launch: the windowed instantiation when the staging slot is
 // shorter than the longest transcript (P.win), one resident round of blocks.
-// 16-lane rows (four candidates per wave) stage twice the rows per block:
-// fewer waves per SIMD keep a C3 transcript in the staging slot
-#ifndef ROW16_MIN_WAVES
-#define ROW16_MIN_WAVES 6
-#endif
-template <int RWV>
-constexpr int row_min_waves() { return RWV == 16 ? ROW16_MIN_WAVES : ROW_MIN_WAVES; }
-
 template <bool A, int RWV, bool SV, bool WV>
 static void launch_rows_t(const Db &db, const ExtParams &P, hipStream_t st)
 {
-    auto kern = extend_rows_kernel<A, RWV, row_min_waves<RWV>(), SV, WV>;
+    auto kern = extend_rows_kernel<A, RWV, ROW_MIN_WAVES, SV, WV>;
     const size_t lds = row_lds_bytes(RWV, A ? 8 : 4, P.dsw, WV);
     hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, lds)), dim3(EBLOCK), lds, st, RowArgs{db, P});
 }
@@ -3065,11 +3013,11 @@ static void launch_rows(bool amb, const Db &db, const ExtParams &P, hipStream_t 
 // Staging slot (u64 words per staged array) the 32-lane row kernel can have
 // at ROW_MIN_WAVES waves per SIMD (as many 4-wave blocks per CU in 160 KB of LDS); a longer
 // transcript runs on the windowed instantiation.
-int row_slot_words_max(bool amb, int rw)
+int row_slot_words_max(bool amb)
 {
-    const int na = amb ? 8 : 4, rows = EBLOCK / rw;
-    const size_t per_block = (size_t)(160 * 1024) / (size_t)(rw == 16 ? ROW16_MIN_WAVES : ROW_MIN_WAVES);
-    const size_t fixed = row_lds_bytes(rw, na, 0, true);
+    const int na = amb ? 8 : 4, rows = EBLOCK / 32;
+    const size_t per_block = (size_t)(160 * 1024) / (size_t)ROW_MIN_WAVES;
+    const size_t fixed = row_lds_bytes(32, na, 0, true);
     return (int)((per_block - fixed) / ((size_t)rows * na * 8));
 }
 
@@ -3147,60 +3095,33 @@ void launch_extend_rows(bool amb, const Db &db, const ExtParams &P, int row_widt
         // 64-lane pass is not redone: C3v 806 vs 875 ms per step.
         const char *wv = getenv("RC_WIDE");
         const bool widep = !(wv && atoi(wv) == 0) && P.wide0;
-        // a directed-search pass of first seeds over B's candidates (B.list:
-        // e1 over list2, else e0 over all): 32-lane rows, their overflows on
-        // 64-lane rows -- r06 (P.row16): 16-lane rows first, their overflows
-        // continued on 32-lane rows (list wide16), theirs on 64-lane rows.
-        // Each narrower pass saves the state of what outgrew its window
-        // (resume16: 16-lane states; resume: 32-lane states), so the wider
-        // pass continues it instead of starting over.
-        auto chain = [&](ExtParams B, uint32_t *wide, unsigned long long *wide_n, unsigned long long *work_w,
-                         uint32_t *w16, unsigned long long *w16_n, unsigned long long *work16) {
-            B.wide = widep ? wide : nullptr;
-            B.wide_n = wide_n;
-            B.resume = widep ? P.resume : nullptr;
-            B.resume_in = nullptr;
-            if (widep && P.row16) {
-                ExtParams X = B;
-                X.wide = w16;
-                X.wide_n = w16_n;
-                X.resume = P.resume16;
-                X.res_cap = P.res16_cap;
-                X.dsw = P.dsw16;
-                X.win = P.win16;
-                launch_rows<16, true>(amb, db, X, st);
-                // the 32-lane pass over the 16-lane pass's overflows
-                B.list = w16;
-                B.list_n = w16_n;
-                B.work = work16;
-                B.resume_in = P.resume16;
-                B.res_in_cap = P.res16_cap;
-                B.res_in_rw = 16;
-            }
-            // (the resuming 32-lane pass is the saving instantiation: the plain
-            // one carries no resume code -- its registers cost the step loop)
-            if (B.resume || B.resume_in) launch_rows<32, true>(amb, db, B, st); else launch_rows<32>(amb, db, B, st);
-            if (widep) {
-                ExtParams V = B;
-                V.list = wide;
-                V.list_n = wide_n;
-                V.work = work_w;
-                V.wide = nullptr;
-                V.wide_n = nullptr;
-                V.resume_in = B.resume;
-                V.res_in_cap = B.resume ? P.res_cap : 0u;
-                V.res_in_rw = 32;
-                launch_rows<64>(amb, db, V, st);
-            }
+        auto wide_pass = [&](const ExtParams &B, uint32_t *lst, unsigned long long *lst_n, unsigned long long *wk) {
+            ExtParams V = B;
+            V.list = lst;
+            V.list_n = lst_n;
+            V.work = wk;
+            V.wide = nullptr;
+            V.wide_n = nullptr;
+            launch_rows<64>(amb, db, V, st);
         };
         W.which = 0;
-        chain(W, P.wide0, P.wide0_n, P.work_w0, P.wide16_0, P.wide16_0_n, P.work16_0);
+        W.wide = widep ? P.wide0 : nullptr;
+        W.wide_n = P.wide0_n;
+        W.resume = widep ? P.resume : nullptr;
+        auto rows_pass = [&](const ExtParams &B) {
+            if (B.resume) launch_rows<32, true>(amb, db, B, st); else launch_rows<32>(amb, db, B, st);
+        };
+        rows_pass(W);
+        if (widep) wide_pass(W, P.wide0, P.wide0_n, P.work_w0);
         ExtParams W2 = W;
         W2.which = 1;
         W2.list = P.list2;
         W2.list_n = P.list2_n;
         W2.work = P.work3;
-        chain(W2, P.wide1, P.wide1_n, P.work_w1, P.wide16_1, P.wide16_1_n, P.work16_1);
+        W2.wide = widep ? P.wide1 : nullptr;
+        W2.wide_n = P.wide1_n;
+        rows_pass(W2);
+        if (widep) wide_pass(W2, P.wide1, P.wide1_n, P.work_w1);
         W.list = nullptr;
         W.list_n = nullptr;
         hipLaunchKernelGGL(first_finish_kernel, dim3((unsigned)g), dim3(256), 0, st, W);

@@ -318,22 +318,6 @@ struct ExtParams {
     // 64-lane pass continues it instead of starting over (RES_REC ints each)
     int32_t *resume;
     uint32_t res_cap;
-    // the saved states a pass continues (list mode: the entry of its list
-    // index, the first res_in_cap entries), saved by rows of res_in_rw lanes:
-    // the 64-lane pass continues the 32-lane pass's, and (r06) the 32-lane
-    // pass after a 16-lane first pass continues that one's
-    const int32_t *resume_in;
-    uint32_t res_in_cap;
-    int32_t res_in_rw;
-    // r06: 16-lane first passes (4 candidates per wave) in front of each
-    // 32-lane pass: their overflows go to wide16 (with states in resume16),
-    // which the 32-lane pass then takes as its list
-    int32_t row16;
-    int32_t dsw16, win16;
-    int32_t *resume16;
-    uint32_t res16_cap;
-    uint32_t *wide16_0, *wide16_1;
-    unsigned long long *wide16_0_n, *wide16_1_n, *work16_0, *work16_1;
     // why searches leave the row kernels: [0] a transcript past the staging
     // slot (row kernel), [1] a directed search whose first seed the row
     // kernels gave up on, [2] one with a seed outside its first HSP's box

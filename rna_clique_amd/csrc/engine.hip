@@ -74,7 +74,7 @@ uint64_t dust_event_words(uint32_t);
 void launch_extend(bool, const Db &, const ExtParams &, hipStream_t);
 void launch_extend_rows(bool, const Db &, const ExtParams &, int, hipStream_t, bool);
 void launch_extend_retry(bool, const Db &, const ExtParams &, hipStream_t);
-int row_slot_words_max(bool amb, int rw);
+int row_slot_words_max(bool amb);
 void launch_group(const GroupParams &, int, hipStream_t);
 
 void launch_rbh(const RbhParams &, int, hipStream_t);
@@ -392,7 +392,6 @@ struct rc_engine {
     DBuf<int32_t> d_trange, d_rtrange;   // [N][2] subject-sample range of each query sample (tmask / rtmask)
     uint64_t rseed_cap = 0, n_rseeds = 0;
     uint32_t res_cap = 0;
-    bool row16 = false;
     // fraction of the last run's candidates whose first-seed extension
     // outgrew the 32-lane window (selects the saving row kernel, RC_RESUME)
     double ovf_frac = 0.0;
@@ -422,9 +421,6 @@ struct rc_engine {
     DBuf<uint8_t> d_cand_nh_r;
     DBuf<uint32_t> d_cand_ovf_r, d_defer_r, d_list2, d_wide0, d_wide1;
     DBuf<int32_t> d_resume;   // saved 32-lane extension states for the 64-lane pass (RES_REC ints each)
-    DBuf<int32_t> d_resume16;   // saved 16-lane extension states for the 32-lane pass (r06)
-    DBuf<uint32_t> d_wide16_0, d_wide16_1;
-    uint32_t res16_cap = 0;
     bool share = false;
     DBuf<DRow> d_rows_tmp;
     DBuf<DEdge> d_edges_tmp;
@@ -1771,7 +1767,7 @@ static int align_tile(rc_engine *e, int ti)
     ixm.bits = e->mindex_bits;
     // --- seeds ---
     std::vector<unsigned long long> shard_cnt(2 * NSHARD);
-    CHK(e->d_count.ensure(40));
+    CHK(e->d_count.ensure(34));
     unsigned long long *big_n = e->d_count.p + 12, *big_retry_n = e->d_count.p + 13;
     uint64_t n_big = 0;
     HIPCHK(hipEventRecord(e->ev[3], e->st));
@@ -1943,23 +1939,6 @@ static int align_tile(rc_engine *e, int ti)
             if (!(rv && atoi(rv) == 1) && e->ovf_frac <= 0.02) e->res_cap = 0;   // not needed: no buffer
             if (e->res_cap) CHK(e->d_resume.ensure((size_t)e->res_cap * RES_REC));
         }
-        // 16-lane first passes (r06, RC_ROW16=1; off by default: C3 275 vs
-        // 214 ms per step): when the transcripts fit their staging
-        // slot whole. About 40 % of C3's candidates outgrow 14 diagonals and
-        // continue on 32-lane rows from their saved state: room for 16 M of
-        // them (5 GB); later ones start over there.
-        {
-            const char *r16 = getenv("RC_ROW16");
-            const int need = ((e->max_len + 31) >> 5) + 4;
-            e->row16 = r16 && atoi(r16) == 1 && need <= row_slot_words_max(e->has_amb, 16) &&
-                       !(getenv("RC_WIDE") && atoi(getenv("RC_WIDE")) == 0);
-            if (e->row16) {
-                e->res16_cap = (uint32_t)std::min<uint64_t>(n_cand, 16u << 20);
-                CHK(e->d_resume16.ensure((size_t)e->res16_cap * RES_REC));
-                CHK(e->d_wide16_0.ensure(std::max<uint64_t>(n_cand, 1)));
-                CHK(e->d_wide16_1.ensure(std::max<uint64_t>(n_cand, 1)));
-            }
-        }
     }
     CHK(e->d_defer.ensure(std::max<uint64_t>(n_cand, 1)));
     CHK(e->d_defer2.ensure(std::max<uint64_t>(n_cand, 1)));
@@ -1971,7 +1950,6 @@ static int align_tile(rc_engine *e, int ti)
             HIPCHK(hipMemsetAsync(e->d_count.p + 14, 0, 2 * sizeof(unsigned long long), e->st));
             HIPCHK(hipMemsetAsync(e->d_count.p + 17, 0, 2 * sizeof(unsigned long long), e->st));
             HIPCHK(hipMemsetAsync(e->d_count.p + 20, 0, 7 * sizeof(unsigned long long), e->st));
-            HIPCHK(hipMemsetAsync(e->d_count.p + 34, 0, 6 * sizeof(unsigned long long), e->st));
         } else {
             // a retry redoes extend_kernel only: its overflow count restarts,
             // every other counter and list stands
@@ -2003,7 +1981,7 @@ static int align_tile(rc_engine *e, int ti)
             // windows of that slot (the windowed instantiation). RC_WIN_WORDS
             // forces windows of that many words (tests: many refills).
             const int need = ((e->max_len + 31) >> 5) + 4;
-            const int smax = row_slot_words_max(e->has_amb, 32);
+            const int smax = row_slot_words_max(e->has_amb);
             const char *wwv = getenv("RC_WIN_WORDS");
             const int forced = wwv ? std::max(4, atoi(wwv)) : 0;
             X.win = forced ? 1 : (need > smax ? 1 : 0);
@@ -2043,19 +2021,6 @@ static int align_tile(rc_engine *e, int ti)
         }
         X.work_w0 = e->d_count.p + 22;
         X.work_w1 = e->d_count.p + 23;
-        X.row16 = e->share && e->row16 ? 1 : 0;
-        if (X.row16) {
-            X.dsw16 = ((e->max_len + 31) >> 5) + 4;
-            X.win16 = 0;
-            X.resume16 = e->d_resume16.p;
-            X.res16_cap = e->res16_cap;
-            X.wide16_0 = e->d_wide16_0.p;
-            X.wide16_1 = e->d_wide16_1.p;
-            X.wide16_0_n = e->d_count.p + 34;
-            X.wide16_1_n = e->d_count.p + 35;
-            X.work16_0 = e->d_count.p + 36;
-            X.work16_1 = e->d_count.p + 37;
-        }
         X.why = e->d_count.p + 24;   // [24, 27): deferral causes
         {
             const char *cv = getenv("RC_ROW_CHUNK");
@@ -2117,13 +2082,13 @@ static int align_tile(rc_engine *e, int ti)
             fprintf(stderr, "row kernel wave-cycles: transitions %.4g (fetches %.4g, window slides %.4g, extension "
                             "starts %.4g) steps %.4g\n",
                     (double)ctr[8], (double)tfs[0], (double)tfs[1], (double)tfs[2], (double)ctr[9]);
-            unsigned long long r16[3] = {0, 0, 0};   // 32-lane rows: steps / candidates within 14 diagonals, 16-lane slides
+            // 32-lane rows: steps and candidates within a 16-lane window, its slides (profiles/r06_row16)
+            unsigned long long r16[3] = {0, 0, 0};
             HIPCHK(hipMemcpy(&r16[0], e->d_count.p + 27, 8, hipMemcpyDeviceToHost));
             HIPCHK(hipMemcpy(&r16[1], e->d_count.p + 31, 8, hipMemcpyDeviceToHost));
             HIPCHK(hipMemcpy(&r16[2], e->d_count.p + 32, 8, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemset(e->d_count.p + 32, 0, 8));
             HIPCHK(hipMemset(e->d_count.p + 27, 0, 8));
-            HIPCHK(hipMemset(e->d_count.p + 31, 0, 8));
+            HIPCHK(hipMemset(e->d_count.p + 31, 0, 16));
             fprintf(stderr, "row steps before a live span over 14 diagonals %.4g of %.4g; candidates never over 14: "
                             "%.4g of %.4g; 16-lane window slides %.4g\n", (double)r16[0], (double)ctr[0],
                     (double)r16[1], (double)ctr[2], (double)r16[2]);
@@ -2135,9 +2100,6 @@ static int align_tile(rc_engine *e, int ti)
                     (double)pr[5], (double)pr[6], (double)pr[7], (double)pr[3], (double)pr[4]);
         }
         if (!(status & 1u)) {
-            unsigned long long o16 = 0;
-            HIPCHK(hipMemcpy(&o16, e->d_count.p + 39, sizeof o16, hipMemcpyDeviceToHost));
-            e->tm.ext_row16_over += (double)o16;
             e->tm.ext_steps += (double)ctr[0];
             e->tm.ext_calls += (double)ctr[1];
             // candidates the one-wave kernel took (the 64-lane pass's list, or the row kernel's)
@@ -3170,7 +3132,6 @@ int rc_trim(rc_engine *e)
     e->d_cand_hsp.release(); e->d_ovf.release(); e->d_cand_nh.release(); e->d_cand_box.release(); e->d_hkey.release();
     e->d_cand_box2.release(); e->d_cand_hsp_r.release(); e->d_cand_nh_r.release(); e->d_cand_ovf_r.release();
     e->d_defer_r.release(); e->d_list2.release(); e->d_wide0.release(); e->d_wide1.release(); e->d_resume.release();
-    e->d_resume16.release(); e->d_wide16_0.release(); e->d_wide16_1.release();
     e->d_rows_tmp.release(); e->d_edges_tmp.release(); e->d_cand_ovf.release(); e->d_gc_off.release();
     e->d_gc_cnt.release(); e->d_gcount.release(); e->d_defer.release(); e->d_defer2.release(); e->d_gscan.release();
     e->d_mscan.release(); e->d_mkey.release(); e->d_tmask.release(); e->d_mbig.release(); e->d_mcnt.release();
