@@ -1690,8 +1690,16 @@ static int align_tile(rc_engine *e, int ti)
         return RC_OK;
     };
     const char *dev = getenv("RC_DUST_EARLY");
-    const bool dust_early = !(dev && atoi(dev) == 0);
-    if (dust && dust_early) CHK(start_dust());
+    const int dmode = dev ? atoi(dev) : 1;   // 1: beside the fill (default), 0: after the sort's table kernels, 2: before the index
+    const bool dust_early = dmode != 0;
+    if (dust && dmode == 2) {
+        // DUST alone on the engine's stream, then the index build alone
+        HIPCHK(hipEventRecord(e->evd[0], e->st));
+        CHK(dust_samples(e, dust_here, e->st));
+        HIPCHK(hipEventRecord(e->evd[1], e->st));
+    } else if (dust && dust_early) {
+        CHK(start_dust());
+    }
     if (reuse) {
         if (dust && !dust_early) CHK(start_dust());
         e->tm.index_reused += 1.0;
