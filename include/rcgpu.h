@@ -150,6 +150,10 @@ typedef struct rc_timing {
     double load_ms;           /* host wall time loading alignment tiles (tile tables, working copy) */
     double align_wall_ms;     /* host wall time of rc_align (every tile, kernels and host work) */
     double host_wait_ms;      /* host wall time blocked on the engine's stream inside rc_align */
+    double later_seeds;       /* later seeds of deferred searches extended on the row kernels (the
+                                 later-seed rounds, one seed per search per round) */
+    double later_whole;       /* deferred searches extend_kernel ran whole (a row kernel gave a seed up,
+                                 or past the rounds' capacity, RC_LATER_CAP) */
 } rc_timing;
 
 void rc_default_opts(rc_opts *opts);
@@ -157,6 +161,9 @@ void rc_default_opts(rc_opts *opts);
 int rc_create(const rc_opts *opts, rc_engine **eng);
 int rc_destroy(rc_engine *eng);
 const char *rc_last_error(void);
+/* Reset the process's device-memory peak (rc_timing.dev_peak_bytes) to what
+ * its engines hold now, so that the next engine's own peak can be read. */
+void rc_dev_peak_reset(void);
 
 /* Add one sample: `seq` holds all transcripts concatenated (ASCII; A/C/G/T
  * any case, anything else is an ambiguous base), tx_offsets[n_tx + 1] their

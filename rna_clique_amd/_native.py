@@ -88,7 +88,7 @@ class RcTiming(ctypes.Structure):
         "ext_calls", "ext_fullband", "ext_deferred", "big_passes", "tiles", "dust_ms",
         "band_bound", "maxhsp_bound", "ext_second", "near_index", "reverse_seeds", "ext_slides", "ext_wide", "dev_bytes",
         "dev_peak_bytes", "defer_length", "defer_gaveup", "defer_outside", "index_reused",
-        "ext_retries", "load_ms", "align_wall_ms", "host_wait_ms")]
+        "ext_retries", "load_ms", "align_wall_ms", "host_wait_ms", "later_seeds", "later_whole")]
 
 
 assert HSP_DTYPE.itemsize == ctypes.sizeof(RcHsp)
@@ -102,6 +102,7 @@ SIGNATURES = {
     "rc_create": (ctypes.c_int, [P(RcOpts), P(VP)]),
     "rc_destroy": (ctypes.c_int, [VP]),
     "rc_last_error": (ctypes.c_char_p, []),
+    "rc_dev_peak_reset": (None, []),
     "rc_add_sample": (ctypes.c_int, [VP, ctypes.c_char_p, ctypes.c_char_p,
                                      P(ctypes.c_uint64), P(ctypes.c_int32),
                                      P(ctypes.c_int32), ctypes.c_uint32,

@@ -2734,6 +2734,288 @@ __global__ __launch_bounds__(256) void first_finish_kernel(ExtParams P)
     }
 }
 
+// HSP box of a seed (x, y, len) from its row-kernel results (cand_box
+// record): what process_search builds from extend_seed's two results
+__device__ __forceinline__ void box_from_fx(const int *fx, int x, int y, int len, int *b)
+{
+    constexpr int OBIT = 13, GMASK = 8191;
+    const int rsc = fx[FX_R], ri = fx[FX_R + 1], rj = fx[FX_R + 2], rd = fx[FX_R + 3], rgo = fx[FX_R + 4];
+    const int lsc = fx[FX_L], lI = fx[FX_L + 1], lJ = fx[FX_L + 2], ld = fx[FX_L + 3], lgo = fx[FX_L + 4];
+    const int lg = lgo & GMASK, lo = (lgo >> OBIT) & GMASK, rg = rgo & GMASK, ro = (rgo >> OBIT) & GMASK;
+    b[LB_QA] = x - lI;
+    b[LB_QB] = x + len + ri;
+    b[LB_SA] = y - lJ;
+    b[LB_SB] = y + len + rj;
+    b[LB_SC] = lsc + 2 * len + rsc;
+    b[LB_D] = ld + rd;
+    b[LB_G] = lg + rg;
+    b[LB_O] = lo + ro;
+    b[LB_NI] = len + (lI + lJ - 2 * ld + lg) / 2 + (ri + rj - 2 * rd + rg) / 2;
+}
+
+// A search the later-seed rounds cannot take: extend_kernel runs it whole
+// (from its first seed's HSP, P.reuse_first)
+__device__ __forceinline__ void later_full(const LaterParams &L, int dir, uint64_t ci)
+{
+    const unsigned long long i = atomicAdd(&L.full_n[dir], 1ull);
+    (dir ? L.full1 : L.full0)[i] = (uint32_t)ci;
+    if (L.counters) atomicAdd(&L.counters[1], 1ull);
+}
+
+// One round of the later-seed rounds, one thread per active search: take the
+// result of the seed the previous round extended (round 0: the first seed's,
+// from cand_box / cand_box2) as the search's next HSP, then pick the next seed
+// as process_search does -- the first in the search's order outside every box
+// so far -- and list it for the row kernels as a candidate record whose e0 is
+// that seed. A search with no such seed is finished; one at MAX_HSP HSPs with
+// such a seed is finished and MAX_HSP-bound (spec 3).
+__device__ __forceinline__ bool later_step(const ExtParams &P, const LaterParams &L, uint64_t s, uint32_t &bi_out)
+{
+    const int dir = s >= L.n0 ? 1 : 0;
+    const uint64_t ci = dir ? L.defer1[s - L.n0] : L.defer0[s];
+    if (s >= L.n_cap) {   // (round 0 only: past the states' capacity)
+        later_full(L, dir, ci);
+        return false;
+    }
+    int *const st = L.state + s * LATER_REC;
+    const Cand cd = P.cands[ci];
+    const GSeed *const sd = P.seeds + cd.seed_off;
+    int nh;
+    if (L.round == 0) {
+        const bool second = dir == 1 && cd.e1 != SEED_NONE;
+        const int *fx = (second ? P.cand_box2 : P.cand_box) + ci * BOX_REC;
+        st[LS_CAPPED] = 0;
+        st[LS_PEND] = -1;
+        if (fx[FX_STATUS] < 0) {   // the row kernels gave its first seed up
+            st[LS_STATE] = LATER_FULL;
+            later_full(L, dir, ci);
+            return false;
+        }
+        const GSeed g = sd[second ? cd.e1 : cd.e0];
+        box_from_fx(fx, (int)g.x, (int)g.y, (int)(g.len & SEED_LEN), st + LS_BOX);
+        nh = 1;
+    } else {
+        nh = st[LS_STATE];
+        const int w = st[LS_PEND];
+        const int *fx = L.box_in + (size_t)w * BOX_REC;
+        if (fx[FX_STATUS] < 0) {   // the row kernels gave this seed up
+            st[LS_STATE] = LATER_FULL;
+            later_full(L, dir, ci);
+            return false;
+        }
+        const GSeed g = sd[L.vc_in[w].e0];
+        box_from_fx(fx, (int)g.x, (int)g.y, (int)(g.len & SEED_LEN), st + LS_BOX + nh * LB_N);
+        nh++;
+    }
+    // the next seed: the search's own seeds, in its order, outside every box
+    // (the boxes in registers; an unused one is empty)
+    int qa[MAX_HSP], qb[MAX_HSP], sa[MAX_HSP], sb[MAX_HSP];
+#pragma unroll
+    for (int h = 0; h < MAX_HSP; h++) {
+        const int *b = st + LS_BOX + h * LB_N;
+        const bool u = h < nh;
+        qa[h] = u ? b[LB_QA] : INT_MAX;
+        qb[h] = u ? b[LB_QB] : INT_MIN;
+        sa[h] = u ? b[LB_SA] : INT_MAX;
+        sb[h] = u ? b[LB_SB] : INT_MIN;
+    }
+    const uint32_t dbit = dir ? SEED_R : SEED_F;
+    const uint32_t ns = cand_seeds(cd);
+    unsigned long long bk = ~0ull;
+    uint32_t bi = 0;
+    for (uint32_t i = 0; i < ns; i++) {
+        const GSeed g = sd[i];
+        if (!(g.len & dbit)) continue;
+        const int x = (int)g.x, y = (int)g.y, len = (int)(g.len & SEED_LEN);
+        bool in = false;
+#pragma unroll
+        for (int h = 0; h < MAX_HSP; h++)
+            in = in || (qa[h] <= x && x + len <= qb[h] && sa[h] <= y && y + len <= sb[h]);
+        if (in) continue;
+        const unsigned long long key =
+            !dir ? ((unsigned long long)g.x << 32) | g.y
+                 : (cd.strand ? ((unsigned long long)(uint32_t)~(g.y + (uint32_t)len) << 32) |
+                                    (uint32_t)~(g.x + (uint32_t)len)
+                              : ((unsigned long long)g.y << 32) | g.x);
+        if (key < bk) {
+            bk = key;
+            bi = i;
+        }
+    }
+    st[LS_STATE] = nh;
+    if (bk == ~0ull) return false;   // every seed inside a box: finished
+    if (nh >= MAX_HSP) {             // MAX_HSP binds
+        st[LS_CAPPED] = 1;
+        return false;
+    }
+    if (bi >= SEED_NONE) {           // past the record's 16-bit seed field
+        st[LS_STATE] = LATER_FULL;
+        later_full(L, dir, ci);
+        return false;
+    }
+    bi_out = bi;   // (its record goes out once the wave has its work slots)
+    return true;
+}
+
+__global__ __launch_bounds__(256) void later_round_kernel(ExtParams P, LaterParams L)
+{
+    const uint64_t n = L.round == 0 ? L.n_search : (uint64_t)*L.act_in_n;
+    const int lane = threadIdx.x & 63;
+    // whole waves iterate together (the work slots are allocated per wave)
+    for (uint64_t b0 = blockIdx.x * (uint64_t)blockDim.x; b0 < n; b0 += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t li = b0 + threadIdx.x;
+        uint64_t s = 0;
+        uint32_t bi = 0;
+        bool emit = false;
+        if (li < n) {
+            s = L.round == 0 ? li : (uint64_t)L.act_in[li];
+            emit = later_step(P, L, s, bi);
+        }
+        const uint64_t m = __ballot(emit);
+        if (!m) continue;
+        const int cnt = __popcll(m);
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        unsigned long long wb = 0, ab = 0;
+        if (lane == leader) {
+            wb = atomicAdd(L.work_n, (unsigned long long)cnt);
+            ab = atomicAdd(L.act_out_n, (unsigned long long)cnt);
+        }
+        wb = (unsigned long long)__shfl((long long)wb, leader);
+        ab = (unsigned long long)__shfl((long long)ab, leader);
+        if (emit) {
+            const int rk = __popcll(m & ((1ull << lane) - 1ull));
+            const uint64_t w = wb + rk;
+            const int dir = s >= L.n0 ? 1 : 0;
+            const uint64_t ci = dir ? L.defer1[s - L.n0] : L.defer0[s];
+            Cand v = P.cands[ci];
+            v.e0 = (uint16_t)bi;
+            v.e1 = SEED_NONE;
+            L.vc[w] = v;
+            L.list[w] = (uint32_t)w;
+            L.state[s * LATER_REC + LS_PEND] = (int)w;
+            L.act_out[ab + rk] = (uint32_t)s;
+        }
+    }
+}
+
+// The searches the rounds finished, one thread each: extend_kernel's end of a
+// search -- purge of HSPs with a common end point, by (score desc, index
+// asc), then the direction's e-value cut -- and its records: the first in
+// cand_hsp (_r), the others in the overflow buffer (one atomic per wave).
+__global__ __launch_bounds__(256) void later_finish_kernel(ExtParams P, LaterParams L)
+{
+    const uint64_t n = L.n_search < L.n_cap ? L.n_search : L.n_cap;
+    const int lane = threadIdx.x & 63;
+    for (uint64_t b0 = blockIdx.x * (uint64_t)blockDim.x; b0 < n; b0 += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t s = b0 + threadIdx.x;
+        const int *const st = L.state + s * LATER_REC;
+        const int nh = s < n ? st[LS_STATE] : -1;
+        const bool live = nh >= 0;
+        const int dir = s >= L.n0 ? 1 : 0;
+        uint64_t ci = 0;
+        Cand cd{};
+        int qa[MAX_HSP], qb[MAX_HSP], sa[MAX_HSP], sb[MAX_HSP], sc[MAX_HSP];
+        uint32_t outm = 0, pfm = 0, prm = 0;
+        bool capped = false;
+        if (live) {
+            ci = dir ? L.defer1[s - L.n0] : L.defer0[s];
+            cd = P.cands[ci];
+            capped = st[LS_CAPPED] != 0;
+#pragma unroll
+            for (int h = 0; h < MAX_HSP; h++) {
+                const int *b = st + LS_BOX + h * LB_N;
+                const bool u = h < nh;
+                qa[h] = u ? b[LB_QA] : 0;
+                qb[h] = u ? b[LB_QB] : 0;
+                sa[h] = u ? b[LB_SA] : 0;
+                sb[h] = u ? b[LB_SB] : 0;
+                sc[h] = u ? b[LB_SC] : INT_MIN;
+            }
+            // purge: in (score desc, index asc) order, an HSP sharing its start
+            // or its end point with one kept before it goes
+            uint32_t kept = 0, done = 0;
+            for (int rr = 0; rr < nh; rr++) {
+                int i = -1, bs = INT_MIN;
+#pragma unroll
+                for (int h = 0; h < MAX_HSP; h++)
+                    if (h < nh && !((done >> h) & 1u) && (i < 0 || sc[h] > bs)) {
+                        i = h;
+                        bs = sc[h];
+                    }
+                done |= 1u << i;
+                bool conflict = false;
+#pragma unroll
+                for (int h = 0; h < MAX_HSP; h++)
+                    conflict = conflict || (((kept >> h) & 1u) && ((qa[h] == qa[i] && sa[h] == sa[i]) ||
+                                                                   (qb[h] == qb[i] && sb[h] == sb[i])));
+                if (!conflict) kept |= 1u << i;
+            }
+            const int thr_f = P.thr[(size_t)cd.ssam * (size_t)(P.max_len + 1) + (size_t)cd.Lq];
+            const int thr_r = P.thr[(size_t)cd.qsam * (size_t)(P.max_len + 1) + (size_t)cd.Lt];
+#pragma unroll
+            for (int h = 0; h < MAX_HSP; h++) {
+                const bool pf = (!P.share || !dir) && sc[h] >= thr_f;
+                const bool pr = (P.sym || (P.share && dir)) && sc[h] >= thr_r;
+                if (((kept >> h) & 1u) && (pf || pr)) {
+                    outm |= 1u << h;
+                    pfm |= (pf ? 1u : 0u) << h;
+                    prm |= (pr ? 1u : 0u) << h;
+                }
+            }
+        }
+        // overflow slots of HSPs 2.. of the wave's searches: one atomic
+        const int nout = __popc(outm);
+        const uint32_t need = nout > 1 ? (uint32_t)(nout - 1) : 0u;
+        uint32_t incl = need;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = (uint32_t)__shfl_up((int)incl, o);
+            if (lane >= o) incl += v;
+        }
+        const uint32_t tot = (uint32_t)__shfl((int)incl, 63);
+        unsigned long long wb = 0;
+        if (lane == 63 && tot) {
+            wb = atomicAdd(P.ovf_count, (unsigned long long)tot);
+            if (wb + tot > P.ovf_cap) atomicOr(P.status, 1u);
+        }
+        wb = (unsigned long long)__shfl((long long)wb, 63);
+        if (P.counters) {
+            const uint64_t cm = __ballot(capped);
+            if (lane == 0 && cm) atomicAdd(&P.counters[10], (unsigned long long)__popcll(cm));
+        }
+        if (!live) continue;
+        const uint32_t obase = need ? (uint32_t)(wb + incl - need) : 0u;
+        DHsp *const hsp_out = dir ? P.cand_hsp_r : P.cand_hsp;
+        int rk = 0;
+        for (int h = 0; h < nh; h++) {
+            if (!((outm >> h) & 1u)) continue;
+            const int *b = st + LS_BOX + h * LB_N;
+            DHsp o;
+            o.q_tx = cd.q_gtx;
+            o.s_tx = cd.s_gtx;
+            if (!cd.strand) {
+                o.qstart = b[LB_QA] + 1; o.qend = b[LB_QB]; o.sstart = b[LB_SA] + 1; o.send = b[LB_SB];
+            } else {
+                o.qstart = cd.Lq - b[LB_QB] + 1; o.qend = cd.Lq - b[LB_QA]; o.sstart = b[LB_SB]; o.send = b[LB_SA] + 1;
+            }
+            const int bd = b[LB_D], bg = b[LB_G], bni = b[LB_NI];
+            o.gaps = bg;
+            o.gapopen = b[LB_O];
+            o.mismatch = bd - bg;
+            o.nident = bni;
+            o.length = bni + (bd - bg) + bg;
+            o.score_half = b[LB_SC];
+            o.bits10 = P.bits10[b[LB_SC]];
+            o.strand = cd.strand | (((pfm >> h) & 1u) ? HSP_FWD : 0) | (((prm >> h) & 1u) ? HSP_REV : 0) |
+                       (h << HSP_IDX_SHIFT);
+            if (rk == 0) hsp_out[ci] = o;
+            else if ((uint64_t)obase + (rk - 1) < P.ovf_cap) P.ovf[obase + rk - 1] = o;
+            rk++;
+        }
+        (dir ? P.cand_nh_r : P.cand_nh)[ci] = (uint8_t)nout;
+        (dir ? P.cand_ovf_r : P.cand_ovf)[ci] = obase;
+    }
+}
+
 // ------------------------------------------------------------------------
 // (gene, sample) groups
 // ------------------------------------------------------------------------
@@ -3064,6 +3346,83 @@ void launch_extend_retry(bool amb, const Db &db, const ExtParams &P, hipStream_t
         W.defer_count = P.defer2_count;
     }
     extend_lists(amb, db, W, st);
+}
+
+// Later-seed rounds over the searches first_finish_kernel deferred (shared
+// searches; after launch_extend_rows with lists = false): MAX_HSP rounds of
+// later_round_kernel, with the row kernels (32-lane, then the 64-lane pass
+// over what outgrew the sliding sub-band) over each round's seeds between
+// them. Every count stays on the device: an empty round is a few idle
+// launches. cnt: LATER_CNT zeroed counters per round; the work buffers
+// (vc, list, box) and the active lists alternate between rounds.
+void launch_later_rounds(bool amb, const Db &db, const ExtParams &P, const LaterParams &L0, Cand *const vc[2],
+                         uint32_t *const list[2], int32_t *const box[2], uint32_t *const act[2],
+                         unsigned long long *cnt, hipStream_t st)
+{
+    if (!L0.n_search) return;
+    const char *wv = getenv("RC_WIDE");
+    const bool widep = !(wv && atoi(wv) == 0) && P.wide0;
+    // later seeds nearly all outgrow the 32-lane window (C3v: 15.3 M of 15.3 M,
+    // profiles/r06_later): straight to 64-lane rows (RC_LATER_ROWS=32: the
+    // 32-lane pass first)
+    const char *rv = getenv("RC_LATER_ROWS");
+    const bool rows64 = !(rv && atoi(rv) == 32);
+    uint64_t g = (L0.n_search + 255) / 256;
+    if (g > 8192) g = 8192;
+    for (int r = 0; r < MAX_HSP; r++) {
+        unsigned long long *c = cnt + (size_t)r * LATER_CNT;
+        LaterParams L = L0;
+        L.round = r;
+        L.vc = vc[r & 1];
+        L.list = list[r & 1];
+        L.vc_in = vc[(r + 1) & 1];
+        L.box_in = box[(r + 1) & 1];
+        L.act_out = act[r & 1];
+        L.act_out_n = c + 1;
+        L.act_in = act[(r + 1) & 1];
+        L.act_in_n = r ? cnt + (size_t)(r - 1) * LATER_CNT + 1 : nullptr;
+        L.work_n = c;
+        hipLaunchKernelGGL(later_round_kernel, dim3((unsigned)g), dim3(256), 0, st, P, L);
+        if (r == MAX_HSP - 1) break;   // (every search has MAX_HSP boxes or none to add)
+        ExtParams B = P;
+        B.which = 0;
+        B.cands = vc[r & 1];
+        B.cand_box = box[r & 1];
+        B.list = list[r & 1];
+        B.list_n = c;
+        B.work = c + 2;
+        if (rows64) {   // RC_LATER_ROWS=64: straight to the spec's whole band
+            B.wide = nullptr;
+            B.wide_n = nullptr;
+            B.resume = nullptr;
+            launch_rows<64>(amb, db, B, st);
+            continue;
+        }
+        B.wide = widep ? P.wide0 : nullptr;
+        B.wide_n = c + 3;
+        B.resume = widep ? P.resume : nullptr;
+        if (B.resume) launch_rows<32, true>(amb, db, B, st); else launch_rows<32>(amb, db, B, st);
+        if (widep) {
+            ExtParams V = B;
+            V.list = P.wide0;
+            V.list_n = c + 3;
+            V.work = c + 4;
+            V.wide = nullptr;
+            V.wide_n = nullptr;
+            launch_rows<64>(amb, db, V, st);
+        }
+    }
+}
+
+// The searches the later-seed rounds finished: purge, cuts, records (again
+// after an HSP overflow-buffer retry: the search states stand)
+void launch_later_finish(const ExtParams &P, const LaterParams &L, hipStream_t st)
+{
+    const uint64_t n = std::min(L.n_search, L.n_cap);
+    if (!n) return;
+    uint64_t g = (n + 255) / 256;
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(later_finish_kernel, dim3((unsigned)g), dim3(256), 0, st, P, L);
 }
 
 // lists = false: up to first_finish_kernel only (the caller sizes the HSP

@@ -324,7 +324,44 @@ struct ExtParams {
     // (first_finish_kernel)
     unsigned long long *why;
 };
-constexpr int RES_REC = 80;   // phase, kof, d6, best, best record (i, gap, d6, diagonal), right results, R[32], goe[32]
+constexpr int RES_REC = 80;
+
+// Later-seed rounds: a deferred directed search (a seed outside its first
+// HSP's box) extends its next seed -- the first in its order outside every box
+// so far, the sequential rule of spec 3 -- on the 64-lane row kernel, one seed
+// per search per round, instead of on one wave of extend_kernel; a finished
+// search is purged, cut and written by later_finish_kernel. Search state:
+// [0] LS_STATE (below), [1] the pending work item, [2] MAX_HSP bound,
+// then MAX_HSP boxes of LB_N ints.
+enum { LS_STATE = 0, LS_PEND = 1, LS_CAPPED = 2, LS_BOX = 4 };
+enum { LB_QA, LB_QB, LB_SA, LB_SB, LB_SC, LB_D, LB_G, LB_O, LB_NI, LB_N };
+constexpr int LATER_REC = LS_BOX + MAX_HSP * LB_N;
+// LS_STATE: >= 0 finished with that many HSPs; LATER_ACTIVE in a round;
+// LATER_FULL: extend_kernel runs the search whole (a row kernel gave a seed
+// up, or a seed index past the record's 16 bits)
+constexpr int LATER_ACTIVE = -1, LATER_FULL = -2;
+// device counters per round: work items, searches still active, the 32-lane
+// pass's work counter, its wide list, the 64-lane pass's work counter
+constexpr int LATER_CNT = 8;
+struct LaterParams {
+    int32_t *state;                       // [n_cap][LATER_REC]
+    uint64_t n_search, n0;                // searches; the first n0 are forward ones (defer0), then defer1
+    uint64_t n_cap;                       // searches with a state (the rest run whole)
+    const uint32_t *defer0, *defer1;      // first_finish_kernel's defer lists (candidate slots)
+    uint32_t *full0, *full1;              // the searches extend_kernel runs whole, per direction
+    unsigned long long *full_n;           // [2]
+    int32_t round;                        // 0: start from the first seed's box
+    Cand *vc;                             // the round's work: candidate records whose e0 is the seed to extend
+    uint32_t *list;                       // their indices (the row kernels' list mode)
+    const Cand *vc_in;                    // the previous round's work (the buffers alternate)
+    const int32_t *box_in;                // the row kernels' results for it (BOX_REC each)
+    const uint32_t *act_in;               // searches still active (rounds > 0)
+    const unsigned long long *act_in_n;
+    uint32_t *act_out;
+    unsigned long long *act_out_n;
+    unsigned long long *work_n;           // work items of the round
+    unsigned long long *counters;         // [0] (unused), [1] searches run whole
+};   // phase, kof, d6, best, best record (i, gap, d6, diagonal), right results, R[32], goe[32]
 
 // DHsp.strand carries, besides the strand (bit 0), the direction flags of a
 // freshly extended HSP (bit 1: passes the query->subject e-value cut, bit 2:

@@ -74,6 +74,9 @@ uint64_t dust_event_words(uint32_t);
 void launch_extend(bool, const Db &, const ExtParams &, hipStream_t);
 void launch_extend_rows(bool, const Db &, const ExtParams &, int, hipStream_t, bool);
 void launch_extend_retry(bool, const Db &, const ExtParams &, hipStream_t);
+void launch_later_rounds(bool, const Db &, const ExtParams &, const LaterParams &, Cand *const[2], uint32_t *const[2],
+                         int32_t *const[2], uint32_t *const[2], unsigned long long *, hipStream_t);
+void launch_later_finish(const ExtParams &, const LaterParams &, hipStream_t);
 int row_slot_words_max(bool amb);
 void launch_group(const GroupParams &, int, hipStream_t);
 
@@ -421,6 +424,12 @@ struct rc_engine {
     DBuf<uint8_t> d_cand_nh_r;
     DBuf<uint32_t> d_cand_ovf_r, d_defer_r, d_list2, d_wide0, d_wide1;
     DBuf<int32_t> d_resume;   // saved 32-lane extension states for the 64-lane pass (RES_REC ints each)
+    // later-seed rounds (shared searches): search states, the rounds' work
+    // (alternating), active lists, counters
+    DBuf<int32_t> d_later, d_lbox0, d_lbox1;
+    DBuf<Cand> d_lvc0, d_lvc1;
+    DBuf<uint32_t> d_llist0, d_llist1, d_lact0, d_lact1, d_lfull0, d_lfull1;
+    DBuf<unsigned long long> d_lcnt;
     bool share = false;
     DBuf<DRow> d_rows_tmp;
     DBuf<DEdge> d_edges_tmp;
@@ -515,6 +524,8 @@ void rc_default_opts(rc_opts *o)
 }
 
 const char *rc_last_error(void) { return g_err.c_str(); }
+
+void rc_dev_peak_reset(void) { g_dev_peak.store(g_dev_bytes.load()); }
 
 uint64_t rc_edge_record_size(void) { return sizeof(DEdge); }
 
@@ -1950,6 +1961,11 @@ static int align_tile(rc_engine *e, int ti)
     }
     CHK(e->d_defer.ensure(std::max<uint64_t>(n_cand, 1)));
     CHK(e->d_defer2.ensure(std::max<uint64_t>(n_cand, 1)));
+    // later-seed rounds: their parameters once they ran (a retry finishes
+    // the searches again from the states, and extend_kernel takes the lists
+    // of the searches they left whole instead of first_finish_kernel's)
+    bool later_on = false;
+    LaterParams lat{};
     for (int attempt = 0;; attempt++) {
         if (attempt == 4) return fail(RC_E_NOMEM, "HSP overflow buffer kept overflowing");
         CHK(e->d_ovf.ensure(e->ovf_cap));
@@ -2061,8 +2077,64 @@ static int align_tile(rc_engine *e, int ti)
                 X.ovf = e->d_ovf.p;
                 X.ovf_cap = e->ovf_cap;
             }
+            // later-seed rounds: the deferred searches' later seeds on the row
+            // kernels (RC_LATER=0: extend_kernel runs them whole); searches
+            // past RC_LATER_CAP (default 24 M, 12 GB of state and work) run whole
+            const char *lv = getenv("RC_LATER");
+            const uint64_t nsrch = dn[0] + dn[1];
+            if (e->share && X.reuse_first && !(lv && atoi(lv) == 0) && nsrch) {
+                const char *cv = getenv("RC_LATER_CAP");
+                const uint64_t cap = cv ? (uint64_t)std::max(atoll(cv), 1ll) : (24ull << 20);
+                const uint64_t n = std::min(nsrch, cap);
+                CHK(e->d_later.ensure(n * LATER_REC));
+                CHK(e->d_lbox0.ensure(n * BOX_REC));
+                CHK(e->d_lbox1.ensure(n * BOX_REC));
+                CHK(e->d_lvc0.ensure(n));
+                CHK(e->d_lvc1.ensure(n));
+                CHK(e->d_llist0.ensure(n));
+                CHK(e->d_llist1.ensure(n));
+                CHK(e->d_lact0.ensure(n));
+                CHK(e->d_lact1.ensure(n));
+                CHK(e->d_lfull0.ensure(std::max<uint64_t>(dn[0], 1)));
+                CHK(e->d_lfull1.ensure(std::max<uint64_t>(dn[1], 1)));
+                const size_t nc = (size_t)MAX_HSP * LATER_CNT + 4;
+                CHK(e->d_lcnt.ensure(nc));
+                HIPCHK(hipMemsetAsync(e->d_lcnt.p, 0, nc * sizeof(unsigned long long), e->st));
+                lat = LaterParams{};
+                lat.state = e->d_later.p;
+                lat.n_search = nsrch;
+                lat.n0 = dn[0];
+                lat.n_cap = n;
+                lat.defer0 = X.defer;
+                lat.defer1 = X.defer_r;
+                lat.full0 = e->d_lfull0.p;
+                lat.full1 = e->d_lfull1.p;
+                lat.counters = e->d_lcnt.p + (size_t)MAX_HSP * LATER_CNT;
+                lat.full_n = lat.counters + 2;
+                Cand *const vc[2] = {e->d_lvc0.p, e->d_lvc1.p};
+                uint32_t *const ls[2] = {e->d_llist0.p, e->d_llist1.p};
+                int32_t *const bx[2] = {e->d_lbox0.p, e->d_lbox1.p};
+                uint32_t *const ac[2] = {e->d_lact0.p, e->d_lact1.p};
+                launch_later_rounds(e->has_amb, db, X, lat, vc, ls, bx, ac, e->d_lcnt.p, e->st);
+                HIPCHK(hipGetLastError());
+                later_on = true;
+            }
+            if (later_on) {
+                launch_later_finish(X, lat, e->st);
+                X.defer = lat.full0;
+                X.defer_count = lat.full_n;
+                X.defer_r = lat.full1;
+                X.defer_r_count = lat.full_n + 1;
+            }
             launch_extend_retry(e->has_amb, db, X, e->st);
         } else {
+            if (later_on) {
+                launch_later_finish(X, lat, e->st);
+                X.defer = lat.full0;
+                X.defer_count = lat.full_n;
+                X.defer_r = lat.full1;
+                X.defer_r_count = lat.full_n + 1;
+            }
             X.counters = nullptr;   // (the first attempt counted this work)
             launch_extend_retry(e->has_amb, db, X, e->st);
             e->tm.ext_retries += 1.0;
@@ -2123,6 +2195,13 @@ static int align_tile(rc_engine *e, int ti)
             e->tm.defer_length += (double)why[0];
             e->tm.defer_gaveup += (double)why[1];
             e->tm.defer_outside += (double)why[2];
+            if (later_on) {   // later-seed rounds: seeds extended on the row kernels, searches run whole
+                std::vector<unsigned long long> lc((size_t)MAX_HSP * LATER_CNT + 4);
+                HIPCHK(hipMemcpy(lc.data(), e->d_lcnt.p, lc.size() * sizeof(unsigned long long),
+                                 hipMemcpyDeviceToHost));
+                for (int r = 0; r < MAX_HSP; r++) e->tm.later_seeds += (double)lc[(size_t)r * LATER_CNT];
+                e->tm.later_whole += (double)lc[(size_t)MAX_HSP * LATER_CNT + 1];
+            }
             break;
         }
         e->ovf_cap = std::max<uint64_t>(e->ovf_cap, ovn * 5 / 4 + 1024);
@@ -3140,6 +3219,9 @@ int rc_trim(rc_engine *e)
     e->d_cand_hsp.release(); e->d_ovf.release(); e->d_cand_nh.release(); e->d_cand_box.release(); e->d_hkey.release();
     e->d_cand_box2.release(); e->d_cand_hsp_r.release(); e->d_cand_nh_r.release(); e->d_cand_ovf_r.release();
     e->d_defer_r.release(); e->d_list2.release(); e->d_wide0.release(); e->d_wide1.release(); e->d_resume.release();
+    e->d_later.release(); e->d_lbox0.release(); e->d_lbox1.release(); e->d_lvc0.release(); e->d_lvc1.release();
+    e->d_llist0.release(); e->d_llist1.release(); e->d_lact0.release(); e->d_lact1.release(); e->d_lcnt.release();
+    e->d_lfull0.release(); e->d_lfull1.release();
     e->d_rows_tmp.release(); e->d_edges_tmp.release(); e->d_cand_ovf.release(); e->d_gc_off.release();
     e->d_gc_cnt.release(); e->d_gcount.release(); e->d_defer.release(); e->d_defer2.release(); e->d_gscan.release();
     e->d_mscan.release(); e->d_mkey.release(); e->d_tmask.release(); e->d_mbig.release(); e->d_mcnt.release();

@@ -67,17 +67,53 @@ def needed_samples(sample_bases, shard_count, rank):
     return out
 
 
+def _tiles(pairs, sample_bases, tile_bases):
+    """The alignment tiles of a rank's pairs, as the engine plans them
+    (engine.hip plan_tiles): one tile when its samples fit `tile_bases`, else
+    every (a chunk, b chunk) with pairs, chunks of at most half the cap."""
+    U = sorted({s for p in pairs for s in p})
+    if sum(sample_bases[s] for s in U) <= tile_bases:
+        return [pairs]
+
+    def chunks(R):
+        out, acc = [[]], 0
+        for s in R:
+            if out[-1] and acc + sample_bases[s] > tile_bases // 2:
+                out.append([])
+                acc = 0
+            out[-1].append(s)
+            acc += sample_bases[s]
+        return out
+    CA = chunks(sorted({a for a, _ in pairs}))
+    CB = chunks(sorted({b for _, b in pairs}))
+    ia = {s: i for i, c in enumerate(CA) for s in c}
+    ib = {s: j for j, c in enumerate(CB) for s in c}
+    tiles = {}
+    for a, b in pairs:
+        tiles.setdefault((ia[a], ib[b]), []).append((a, b))
+    return list(tiles.values())
+
+
+# device bytes per candidate slot of a tile: the record (48), both directed
+# searches' first-seed results (2 x 48), HSP slots (2 x 56), counts and
+# overflow offsets, defer / wide lists, ~10 seeds of 12 B; capacities grow by
+# 1.25x (calibrated on the engines' measured peaks, r06: C3 59.9 GB, C4
+# 177.2 GB, a C5 rank 139.6 GB)
+CAND_BYTES = 525
+
+
 def hbm_footprint(sample_bases, sample_genes, shard_count, tile_bases=(1 << 32) - (1 << 24),
                   hsps_per_gene=1.0):
     """Modelled device bytes of every rank (a planning aid: bench and tests
     check that a configuration fits 288 GB per GPU before running it; the
     engine reports what it actually holds, rc_timing.dev_peak_bytes). Per rank:
     * its samples' bases, resident (1 B/base; the array grows by 1.25x);
-    * the largest alignment tile's working set: the 16-mer index and its sort
-      buffer (16 B/base), the tile's gathered copy (1), packed forward + reverse
+    * the largest alignment tile's working set (`_tiles`: the engine's tile
+      plan): the tile's gathered copy (1 B/base), packed forward + reverse
       complement (0.5), transcript-start and DUST bit arrays (0.25), the
-      near-mask index (0.5), seeds and candidates (~3), plus the 2^28-bucket
-      table (1 GiB);
+      near-mask index (0.5); the 16-mer index and its sort buffer over the
+      tile's subject samples only (16 B/base); its candidates (one per gene of
+      each pair, CAND_BYTES each); the 2^28-bucket table (1 GiB);
     * its HSP store (56 B per HSP, both directed searches of every pair; the
       store grows by 1.5x) and table rows (16 B each);
     * the (gene, sample) group tables over all genes x samples (24 B: offset,
@@ -93,8 +129,12 @@ def hbm_footprint(sample_bases, sample_genes, shard_count, tile_bases=(1 << 32) 
         pairs = order[int(first[r]):int(first[r + 1])]
         samples = {s for p in pairs for s in p}
         resident = sum(sample_bases[s] for s in samples)
-        tile = min(resident, tile_bases)
-        work = tile * (16 + 1 + 0.5 + 0.25 + 0.5 + 3) + (1 << 30)
+        work = 0
+        for tp in _tiles(pairs, sample_bases, tile_bases):
+            tile = sum(sample_bases[s] for s in {s for p in tp for s in p})
+            subj = sum(sample_bases[s] for s in {b for _, b in tp})
+            cands = sum(min(sample_genes[a], sample_genes[b]) for a, b in tp)
+            work = max(work, tile * (1 + 0.5 + 0.25 + 0.5) + subj * 16 + cands * CAND_BYTES + (1 << 30))
         nh = sum(sample_genes[a] + sample_genes[b] for a, b in pairs) * hsps_per_gene
         items = sum(sample_genes[b] for a, b in pairs)
         groups = genes * n * 24

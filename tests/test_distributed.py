@@ -207,9 +207,9 @@ def test_c5_fits_hbm_per_rank():
     ~33 Gbp) on 8 GPUs: every rank's modelled HBM footprint (resident samples,
     one tile's working set, its HSP store, the group table) is within the
     288 GB of an MI355X, and within it with room to spare at the configuration's
-    mean transcript length. (The model is calibrated on the engine's own
-    device-memory peak of rank 2 at C5, tests/test_gpu_scale.py: 202 GB
-    measured device-wide in r03.)"""
+    mean transcript length. (The model is calibrated on the engines' own
+    device-memory peaks, r06: C3 59.9 GB, C4 177.2 GB, and the C5 rank of
+    tests/test_gpu_scale.py 139.6 GB, which that test checks within 20 %.)"""
     from rna_clique_amd import distributed
     n, genes, mean_len = 128, 100_000, 2600
     bases = [genes * mean_len] * n

@@ -241,6 +241,7 @@ def test_C5_one_rank_shard(native):
         samples, need, (order, first) = shard_samples("C5", S, R)
     assert len(need) < len(samples) and all((samples[i].seq is None) == (i not in need) for i in range(128))
     free0, _ = torch.cuda.mem_get_info(0)
+    native.rc_dev_peak_reset()   # this engine's own peak, not an earlier test's
     eng = Engine(device=0, shard_rank=R, shard_count=S)
     for i, s in enumerate(samples):
         eng.add_sample(s.name, s.seq if i in need else None, s.tx_offsets, s.gene, s.iso)
