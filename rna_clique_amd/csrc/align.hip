@@ -2781,6 +2781,7 @@ __device__ __forceinline__ bool later_step(const ExtParams &P, const LaterParams
     const Cand cd = P.cands[ci];
     const GSeed *const sd = P.seeds + cd.seed_off;
     int nh;
+    uint32_t last;   // the seed extended last
     if (L.round == 0) {
         const bool second = dir == 1 && cd.e1 != SEED_NONE;
         const int *fx = (second ? P.cand_box2 : P.cand_box) + ci * BOX_REC;
@@ -2791,7 +2792,8 @@ __device__ __forceinline__ bool later_step(const ExtParams &P, const LaterParams
             later_full(L, dir, ci);
             return false;
         }
-        const GSeed g = sd[second ? cd.e1 : cd.e0];
+        last = second ? cd.e1 : cd.e0;
+        const GSeed g = sd[last];
         box_from_fx(fx, (int)g.x, (int)g.y, (int)(g.len & SEED_LEN), st + LS_BOX);
         nh = 1;
     } else {
@@ -2803,7 +2805,8 @@ __device__ __forceinline__ bool later_step(const ExtParams &P, const LaterParams
             later_full(L, dir, ci);
             return false;
         }
-        const GSeed g = sd[L.vc_in[w].e0];
+        last = L.vc_in[w].e0;
+        const GSeed g = sd[last];
         box_from_fx(fx, (int)g.x, (int)g.y, (int)(g.len & SEED_LEN), st + LS_BOX + nh * LB_N);
         nh++;
     }
@@ -2823,7 +2826,10 @@ __device__ __forceinline__ bool later_step(const ExtParams &P, const LaterParams
     const uint32_t ns = cand_seeds(cd);
     unsigned long long bk = ~0ull;
     uint32_t bi = 0;
-    for (uint32_t i = 0; i < ns; i++) {
+    // the forward search's order is the seeds' (x, y) order: the seeds before
+    // the last one extended were inside a box when it was picked, and boxes
+    // only grow, so they still are (the reverse order is another permutation)
+    for (uint32_t i = dir ? 0u : last + 1u; i < ns; i++) {
         const GSeed g = sd[i];
         if (!(g.len & dbit)) continue;
         const int x = (int)g.x, y = (int)g.y, len = (int)(g.len & SEED_LEN);
