@@ -89,6 +89,7 @@ def main():
     import numpy as np
     from concurrent.futures import ThreadPoolExecutor
     from rna_clique_amd import distributed
+    from rna_clique_amd import _native
     from rna_clique_amd.engine import Engine
     from rna_clique_amd.simulate import CONFIGS, simulate
     from oracle.align import OracleDB
@@ -121,6 +122,7 @@ def main():
             t0 = time.perf_counter()
             samples = simulate(only=sorted(need), **cfg)[0] if whole is None else whole
             t_gen = time.perf_counter() - t0
+        _native.lib().rc_dev_peak_reset()   # each rank's own engine peak (ranks run one after another)
         eng = Engine(device=0, shard_rank=r, shard_count=S)
         for i, s in enumerate(samples):
             eng.add_sample(s.name, s.seq if i in need else None, s.tx_offsets, s.gene, s.iso)
@@ -189,6 +191,7 @@ def main():
     with Heartbeat(f"graph phase: {sum(x['edges'] for x in ranks)} edges of {S} ranks"):
         allrec = np.concatenate(parts)
         del parts
+        _native.lib().rc_dev_peak_reset()
         g = Engine(device=0, shard_rank=0, shard_count=S)
         for s in meta:
             g.add_sample(s.name, None, s.tx_offsets, s.gene, s.iso)
