@@ -295,6 +295,38 @@ def test_windowed_staging_exact(native, monkeypatch, words, share, amb):
     assert summary["hsps"] > 0 and tm["defer_length"] == 0 and (tm["ext_wide"] > 0 or not share)
 
 
+@pytest.mark.parametrize("later,rows,cap,words", [("1", "64", None, None), ("1", "32", None, None),
+                                                   ("1", "64", "7", None), ("0", None, None, None),
+                                                   ("1", "64", None, "6")])
+def test_later_seed_rounds_exact(native, monkeypatch, later, rows, cap, words):
+    """Searches with a seed outside their first HSP's box (indels): the
+    later-seed rounds (each round extends every such search's next seed on
+    the row kernels; a finishing kernel purges and cuts) give every HSP, table
+    and distance of the oracle -- with later seeds on 64-lane rows (default)
+    or 32-lane rows first, with a state capacity of 7 searches (the rest run
+    whole on extend_kernel), with the rounds off, and with windowed staging."""
+    monkeypatch.setenv("RC_LATER", later)
+    if rows:
+        monkeypatch.setenv("RC_LATER_ROWS", rows)
+    if cap:
+        monkeypatch.setenv("RC_LATER_CAP", cap)
+    if words:
+        monkeypatch.setenv("RC_WIN_WORDS", words)
+    from rna_clique_amd.simulate import simulate
+    samples, _ = simulate(4, 100, seed=29, p_iso2=0.2, indel_rate=0.012, p_revcomp=0.5, polya=(0.3, 10, 40),
+                          len_loc=600, len_n=2000, len_p=0.5)
+    eng = _run_sim(samples)
+    msgs, summary = full_check(eng, samples)
+    assert not msgs, "\n".join(msgs[:10])
+    tm = eng.timings()
+    assert summary["hsps"] > 0 and tm["defer_outside"] > 0
+    if later == "1":
+        assert tm["later_seeds"] > 0
+        assert (tm["later_whole"] > 0) == (cap is not None)
+    else:
+        assert tm["later_seeds"] == 0
+
+
 @pytest.mark.parametrize("top_matches,keep_all,two_pass", [(1, True, False), (1, False, False), (2, True, False),
                                                             (2, True, True), (1, False, True)])
 def test_simulated_parity_options(native, monkeypatch, top_matches, keep_all, two_pass):
