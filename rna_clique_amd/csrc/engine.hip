@@ -49,9 +49,8 @@ uint64_t os_scratch_words(uint64_t n);
 bool os_sort_keys(uint64_t *keys, uint64_t *alt, uint64_t n, int bb, uint32_t *scratch, uint64_t *status,
                   uint32_t &epoch, hipStream_t st, const std::function<void()> &after_prep, bool counted,
                   const TxInfo *gen_tx, const uint64_t *gen_koff, const uint64_t *gen_F, uint32_t gen_ntx,
-                  uint32_t *gen_tile, uint32_t *bucket, int bucket_bits, uint32_t *seams);
+                  uint32_t *gen_tile);
 uint64_t os_gen_tile_words(uint64_t n);
-uint64_t os_seam_words(uint64_t n);
 void os_fill_hist(const TxInfo *tx, uint32_t n_tx, const uint64_t *F, const uint64_t *koff, uint64_t *ent,
                   uint64_t n, uint32_t *scratch, hipStream_t st);
 void launch_tx_masked(const TxInfo *, uint32_t, const uint64_t *, uint8_t *, hipStream_t);
@@ -402,7 +401,7 @@ struct rc_engine {
     DBuf<uint64_t> d_ent, d_ent2;   // (k-mer << 32 | position), unsorted / sorted
     // the index sort's scratch (sort.hip): digit histograms + tile counters,
     // the look-back table (zeroed when allocated; tagged by pass epoch)
-    DBuf<uint32_t> d_sort_scratch, d_gen_tile, d_seams;
+    DBuf<uint32_t> d_sort_scratch, d_gen_tile;
     DBuf<uint64_t> d_sort_status;
     uint32_t sort_epoch = 0;
     DBuf<uint32_t> d_bucket;
@@ -1193,17 +1192,6 @@ static int sort_index(rc_engine *e, DBuf<uint64_t> &ent, DBuf<uint64_t> &ent2, u
 {
     static const bool lib = getenv("RC_SORT") && !strcmp(getenv("RC_SORT"), "rocprim");
     bool prepped = false;   // after_prep runs exactly once, also for an empty index
-    const char *ibv = getenv("RC_INDEX_BITS_MAX");
-    const int bmax = ibv ? std::max(16, std::min(30, atoi(ibv))) : 28;
-    int bits = 16;
-    while (bits < bmax && (1ull << bits) < (npos << extra)) bits++;
-    bits_out = bits;
-    CHK(bucket.ensure((1ull << bits) + 1));
-    // the sort's last pass fills the bucket table on its way out (it has each
-    // key's predecessor in LDS) instead of a kernel re-reading the sorted
-    // entries (RC_BUCKET_FUSE=0: that kernel)
-    static const bool fuse_off = getenv("RC_BUCKET_FUSE") && atoi(getenv("RC_BUCKET_FUSE")) == 0;
-    bool fused = false;
     if (lib) {   // A/B only: rocPRIM's onesweep
         // (rocPRIM sorts up to 2^20 items with a merge sort that did not keep
         // the input order for a partial bit range: there, all 64 bits -- the
@@ -1227,16 +1215,13 @@ static int sort_index(rc_engine *e, DBuf<uint64_t> &ent, DBuf<uint64_t> &ent2, u
         }
         int prc = RC_OK;
         if (gen) CHK(e->d_gen_tile.ensure(os_gen_tile_words(npos)));
-        fused = !fuse_off && (64u - bb) > 8u;   // (one pass: no earlier pass to order the keys)
-        if (fused) CHK(e->d_seams.ensure(os_seam_words(npos)));
         const bool in_alt = os_sort_keys(ent.p, ent2.p, npos, (int)bb, e->d_sort_scratch.p, e->d_sort_status.p,
                                          e->sort_epoch, e->st, [&]() {
                                              prepped = true;
                                              if (after_prep) prc = after_prep();
                                          }, counted, gen ? gen->tx : nullptr, gen ? gen->koff : nullptr,
                                          gen ? gen->F : nullptr, gen ? gen->n_tx : 0u,
-                                         gen ? e->d_gen_tile.p : nullptr, fused ? bucket.p : nullptr, bits,
-                                         fused ? e->d_seams.p : nullptr);
+                                         gen ? e->d_gen_tile.p : nullptr);
         CHK(prc);
         HIPCHK(hipGetLastError());
         if (!in_alt) {
@@ -1245,7 +1230,13 @@ static int sort_index(rc_engine *e, DBuf<uint64_t> &ent, DBuf<uint64_t> &ent2, u
         }
     }
     if (!prepped && after_prep) CHK(after_prep());
-    if (!fused) launch_bucket_fill(ent2.p, npos, bits, bucket.p, e->st);
+    const char *ibv = getenv("RC_INDEX_BITS_MAX");
+    const int bmax = ibv ? std::max(16, std::min(30, atoi(ibv))) : 28;
+    int bits = 16;
+    while (bits < bmax && (1ull << bits) < (npos << extra)) bits++;
+    bits_out = bits;
+    CHK(bucket.ensure((1ull << bits) + 1));
+    launch_bucket_fill(ent2.p, npos, bits, bucket.p, e->st);
     return RC_OK;
 }
 
@@ -3221,7 +3212,7 @@ int rc_trim(rc_engine *e)
     e->d_tile_masked.release(); e->d_ment.release(); e->d_ment2.release(); e->d_mbucket.release();
     e->d_rseeds.release(); e->d_rseed_gene.release(); e->d_rs_key.release(); e->d_rs_idx.release();
     e->d_rs_range.release(); e->d_rctr.release(); e->d_rtmask.release(); e->d_trange.release(); e->d_rtrange.release();
-    e->d_ent.release(); e->d_ent2.release(); e->d_sort_scratch.release(); e->d_gen_tile.release(); e->d_seams.release();
+    e->d_ent.release(); e->d_ent2.release(); e->d_sort_scratch.release(); e->d_gen_tile.release();
     e->d_sort_status.release(); e->d_bucket.release(); e->d_pos_tx.release(); e->d_sample_pos.release();
     e->d_txstart.release(); e->d_dmask.release(); e->d_dust_scratch.release(); e->d_dust_events.release();
     e->d_prof.release(); e->d_tmp.release(); e->d_seeds.release(); e->d_cands.release();

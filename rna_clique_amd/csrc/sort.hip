@@ -279,23 +279,13 @@ __device__ unsigned long long os_stats[4];   // look-back loads, not-ready polls
 // waves 0-3 then walk the look-back (one digit per thread) while waves 4-7
 // rank their keys, and rank theirs after it; the keys go to LDS in digit
 // order and out in runs.
-// BKT (the last pass): the index's bucket table on the way out -- bucket[x] =
-// the first output slot whose key's top bits are >= x -- from each key and
-// its predecessor in LDS; the first key of each of the tile's digit runs has
-// its predecessor in another tile, so its slot goes to seams[tile][digit]
-// for bucket_seam_kernel.
-struct BucketOut {
-    uint32_t *bucket;
-    uint32_t *seams;   // [tiles][RADIX]: output slot of each digit run's first key, ~0 if empty
-    int sh;            // 64 - bits
-};
-template <bool GEN, bool BKT>
+template <bool GEN>
 __global__ __launch_bounds__(OS_BLOCK, OS_MINB * OS_WAVES / 4) void onesweep_kernel(const uint64_t *__restrict__ in,
                                                                      uint64_t *__restrict__ out, int shift,
                                                                      const uint32_t *scratch, int p,
                                                                      const uint32_t *__restrict__ order,
                                                                      gu64 *status, uint32_t epoch, uint32_t *tile_ctr,
-                                                                     uint64_t n_all, KeyGen G, BucketOut B)
+                                                                     uint64_t n_all, KeyGen G)
 {
     static_assert(OS_BLOCK >= RADIX && OS_TILE <= 65536 && OS_ITEMS % 2 == 0, "one look-back thread per digit; 16-bit ranks");
     __shared__ uint64_t s_keys[OS_TILE];
@@ -476,49 +466,12 @@ __global__ __launch_bounds__(OS_BLOCK, OS_MINB * OS_WAVES / 4) void onesweep_ker
     }
     __syncthreads();
     const uint32_t cnt = (uint32_t)(n - t0);
-    if constexpr (BKT) {
-        if (tid < RADIX)
-            B.seams[(uint64_t)tile * RADIX + tid] = s_cnt[tid] ? (uint32_t)(s_goff[tid] + s_start[tid]) : ~0u;
-    }
 #pragma unroll 4
     for (uint32_t s = tid; s < cnt; s += OS_BLOCK) {
         const uint64_t key = s_keys[s];
-        const uint32_t d = (uint32_t)(key >> shift) & 255u;
-        const uint64_t gi = s_goff[d] + s;
+        const uint64_t gi = s_goff[(uint32_t)(key >> shift) & 255u] + s;
         if (gi < n_all) out[gi] = key;   // always, unless the counts were inconsistent
-        if constexpr (BKT) {
-            if (s != s_start[d] && gi < n_all) {
-                const uint64_t lo = (s_keys[s - 1] >> B.sh) + 1, hi = key >> B.sh;
-                for (uint64_t x = lo; x <= hi; x++) B.bucket[x] = (uint32_t)gi;
-            }
-        }
     }
-}
-
-// The bucket slots the last pass left to the digit runs' seams: slot gi's
-// range from its predecessor's top bits (exclusive) to its own; the extra
-// thread closes the table (slots past the last key = n).
-__global__ void bucket_seam_kernel(const uint64_t *__restrict__ out, uint64_t n, const uint32_t *__restrict__ seams,
-                                   const uint32_t *scratch, int p, int sh, uint32_t *__restrict__ bucket)
-{
-    // the last pass's tiles (ids 0 .. its tile count) wrote every seam entry
-    const uint64_t nseam = (uint64_t)pass_tab(const_cast<uint32_t *>(scratch), p).tbase[OS_SEG] * RADIX;
-    const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (j > nseam) return;
-    uint64_t lo, hi;
-    uint32_t v;
-    if (j == nseam) {
-        lo = n ? (out[n - 1] >> sh) + 1 : 0;
-        hi = 1ull << (64 - sh);
-        v = (uint32_t)n;
-    } else {
-        const uint32_t gi = seams[j];
-        if (gi == ~0u || gi >= n) return;
-        lo = gi ? (out[gi - 1] >> sh) + 1 : 0;
-        hi = out[gi] >> sh;
-        v = gi;
-    }
-    for (uint64_t x = lo; x <= hi; x++) bucket[x] = v;
 }
 
 // Sort keys[0, n) stably on bits [bb, 64) by ping-pong passes between keys
@@ -556,15 +509,10 @@ void os_fill_hist(const TxInfo *tx, uint32_t n_tx, const uint64_t *F, const uint
 // (keys need not hold them); gen_tile: scratch of os_gen_tile_words(n) u32.
 uint64_t os_gen_tile_words(uint64_t n) { return (n + OS_TILE - 1) / OS_TILE + OS_SEG; }
 
-// bucket (optional): the bucket table of the sorted keys' top `bucket_bits`
-// bits (bucket_fill_kernel's table) filled by the last pass and
-// bucket_seam_kernel, seams: os_seam_words(n) u32 of scratch.
-uint64_t os_seam_words(uint64_t n) { return ((n + OS_TILE - 1) / OS_TILE + OS_SEG) * (uint64_t)RADIX; }
-
 bool os_sort_keys(uint64_t *keys, uint64_t *alt, uint64_t n, int bb, uint32_t *scratch, uint64_t *status,
                   uint32_t &epoch, hipStream_t st, const std::function<void()> &after_prep, bool counted,
                   const TxInfo *gen_tx, const uint64_t *gen_koff, const uint64_t *gen_F, uint32_t gen_ntx,
-                  uint32_t *gen_tile, uint32_t *bucket, int bucket_bits, uint32_t *seams)
+                  uint32_t *gen_tile)
 {
     const int np = (64 - bb + 7) / 8;
     if (n == 0) return false;
@@ -582,8 +530,6 @@ bool os_sort_keys(uint64_t *keys, uint64_t *alt, uint64_t n, int bb, uint32_t *s
     uint64_t *src = keys, *dst = alt;
     const bool gen = counted && gen_koff && bb == 32;
     KeyGen G{gen_tx, gen_koff, gen_F, gen_ntx, gen_tile};
-    const bool bkt = bucket && seams && np > 1 && bucket_bits > 0 && bucket_bits <= 32;
-    const BucketOut B{bucket, seams, 64 - bucket_bits};
     for (int p = 0; p < np; p++) {
         hipLaunchKernelGGL(tile_order_kernel, dim3((tmax + 255) / 256), dim3(256), 0, st, scratch, p, order, tmax);
         if (p == 0 && gen)
@@ -591,21 +537,12 @@ bool os_sort_keys(uint64_t *keys, uint64_t *alt, uint64_t n, int bb, uint32_t *s
         if (p == 0 && after_prep) after_prep();
         ++epoch;
         if (p == 0 && gen)
-            hipLaunchKernelGGL((onesweep_kernel<true, false>), dim3(grid), dim3(OS_BLOCK), 0, st, src, dst, bb + 8 * p,
-                               scratch, p, order, (gu64 *)status, epoch, ctr + p, n, G, B);
-        else if (p == np - 1 && bkt)
-            hipLaunchKernelGGL((onesweep_kernel<false, true>), dim3(grid), dim3(OS_BLOCK), 0, st, src, dst, bb + 8 * p,
-                               scratch, p, order, (gu64 *)status, epoch, ctr + p, n, G, B);
+            hipLaunchKernelGGL(onesweep_kernel<true>, dim3(grid), dim3(OS_BLOCK), 0, st, src, dst, bb + 8 * p, scratch,
+                               p, order, (gu64 *)status, epoch, ctr + p, n, G);
         else
-            hipLaunchKernelGGL((onesweep_kernel<false, false>), dim3(grid), dim3(OS_BLOCK), 0, st, src, dst,
-                               bb + 8 * p, scratch, p, order, (gu64 *)status, epoch, ctr + p, n, G, B);
+            hipLaunchKernelGGL(onesweep_kernel<false>, dim3(grid), dim3(OS_BLOCK), 0, st, src, dst, bb + 8 * p,
+                               scratch, p, order, (gu64 *)status, epoch, ctr + p, n, G);
         std::swap(src, dst);
-    }
-    if (bkt) {
-        // (a grid for tmax tiles; the kernel reads the pass's own tile count)
-        const uint64_t nmax = (uint64_t)tmax * RADIX + 1;
-        hipLaunchKernelGGL(bucket_seam_kernel, dim3((unsigned)((nmax + 255) / 256)), dim3(256), 0, st, src, n, seams,
-                           scratch, np - 1, 64 - bucket_bits, bucket);
     }
     return src == alt;
 }

@@ -108,8 +108,7 @@ int main(int argc, char **argv)
             CK(hipMemcpyAsync(a, src, c.n * 8, hipMemcpyDeviceToDevice, st));
             CK(hipGetLastError());
             CK(hipEventRecord(e0, st));
-            in_alt = os_sort_keys(a, b, c.n, c.bb, scratch, status, epoch, st, nullptr, false, nullptr, nullptr, nullptr, 0, nullptr,
-                                  nullptr, 0, nullptr);
+            in_alt = os_sort_keys(a, b, c.n, c.bb, scratch, status, epoch, st, nullptr, false, nullptr, nullptr, nullptr, 0, nullptr);
             CK(hipEventRecord(e1, st));
             CK(hipEventSynchronize(e1));
             float ms;
