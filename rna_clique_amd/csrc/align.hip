@@ -1,15 +1,22 @@
-// Seed-and-extend (the BLAST+ replacement), three kernels:
+// Seed-and-extend (the BLAST+ replacement):
 //
-//   seed_kernel    one workgroup per query gene: 16-mer lookups at stride
-//                  W-15 on both strands of every isoform, canonical maximal
-//                  exact runs >= W (seeds), sorted per candidate
-//                  (query tx, strand, subject tx); candidates grouped by
-//                  subject sample.
-//   extend_kernel  one wave per candidate: query and subject staged in LDS,
-//                  greedy X-drop extension with one diagonal per lane,
-//                  containment skip, common-endpoint purge, e-value cut.
-//   group_*        per (query gene, subject sample): HSPs made contiguous
-//                  in candidate order (the order the oracle emits).
+//   seed_kernel          one workgroup per query gene: 16-mer lookups at
+//                        stride W-15 on both strands of every isoform,
+//                        canonical maximal exact runs >= W (seeds), sorted per
+//                        candidate (query tx, strand, subject tx); candidates
+//                        grouped by subject sample.
+//   extend_rows_kernel   each candidate's first seed on a sliding 32-lane
+//                        sub-band row (two rows per wave), greedy X-drop; the
+//                        64-lane instantiation continues what outgrew it.
+//   first_finish_kernel  one thread per candidate: a search whose seeds all
+//                        lie in the first seed's box is done (cuts, record).
+//   later_round_kernel   the other searches, one seed per round: the next
+//   later_finish_kernel  seed outside every box goes to the 64-lane rows;
+//                        then purge and cuts, one thread per search.
+//   extend_kernel        one wave per search (the full band, seeds by
+//                        selection, purge, cuts): what the rounds cannot take.
+//   group_* / mirror_*   per (query gene, subject sample): HSPs made
+//                        contiguous in candidate order (the oracle's order).
 //
 // Semantics: oracle/align_oracle.c ("RC-megablast v1"), bit for bit.
 #include "device.h"
