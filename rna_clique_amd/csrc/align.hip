@@ -3125,7 +3125,7 @@ __global__ void mirror_scatter_kernel(GroupParams P, int pass)
             // the reverse search's query tx (its gene and isoform position) and subject tx
             const uint32_t rq = h.s_tx, rs = h.q_tx;
             if (c == 0) {
-                gi = grp_index(P.tx_gene[rq], P.tx[rs].sample, P.n_genes);
+                gi = (uint64_t)(P.tx[rs].sample - P.ms0) * P.mgw + (P.tx_gene[rq] - P.mg0);   // (the tile's window)
                 if (pass == 1) slot = P.mbase + P.mscan[gi] + P.mcur[li];
             }
             c++;
@@ -3147,14 +3147,16 @@ __global__ void mirror_scatter_kernel(GroupParams P, int pass)
 constexpr uint32_t MSORT_SMALL = 32;
 __global__ void mirror_sort_kernel(GroupParams P)
 {
-    const uint64_t n = (uint64_t)P.n_genes * (uint64_t)P.N;
+    const uint64_t n = (uint64_t)P.mgw * (uint64_t)P.msn;
     for (uint64_t gi = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; gi < n;
          gi += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t c = P.mcnt[gi];
         if (!c) continue;
         const uint64_t b = P.mscan[gi];
-        P.grp_off[gi] = (uint32_t)(P.mbase + b);
-        P.grp_cnt[gi] = c;
+        // the window's (sample, gene) in the whole group table
+        const uint64_t gg = grp_index(P.mg0 + (uint32_t)(gi % P.mgw), P.ms0 + (int)(gi / P.mgw), P.n_genes);
+        P.grp_off[gg] = (uint32_t)(P.mbase + b);
+        P.grp_cnt[gg] = c;
         if (c > MSORT_SMALL) {
             const unsigned long long k = atomicAdd(P.mbig_n, 1ull);
             P.mbig[k] = gi;   // capacity: nm / (MSORT_SMALL + 1) + 1 entries
@@ -3531,7 +3533,7 @@ void launch_group(const GroupParams &P, int pass, hipStream_t st)
     // 0 direct count, 1 direct write, 2 mirror count, 3 mirror scatter, 4 mirror sort
     uint64_t n = (uint64_t)(P.gene_end - P.gene_begin) * (uint64_t)P.N;
     if (pass == 2 || pass == 3) n = P.n_cand;
-    if (pass == 4) n = (uint64_t)P.n_genes * (uint64_t)P.N;
+    if (pass == 4) n = (uint64_t)P.mgw * (uint64_t)P.msn;
     if (!n) return;
     uint64_t g = (n + 255) / 256;
     if (g > 65536) g = 65536;

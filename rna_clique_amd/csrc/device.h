@@ -394,7 +394,13 @@ struct GroupParams {
     uint64_t n_cand, cand_cap;
     const uint32_t *tx_gene, *tx_pos;   // gene of a transcript, its position in the gene
     const TxInfo *tx;
-    uint32_t *mcnt;               // [gene * N + T]
+    // mirrored groups of the tile: the genes [mg0, mg0 + mgw) of its subject
+    // samples (the reverse searches' queries) x its query samples [ms0,
+    // ms0 + msn), counted in that window rather than over every gene and
+    // sample (a C5 rank's tile: 3 M groups instead of 820 M)
+    uint32_t mg0, mgw;
+    int32_t ms0, msn;
+    uint32_t *mcnt;               // [(T - ms0) * mgw + gene - mg0]
     const uint64_t *mscan;        // exclusive scan of mcnt
     uint32_t *mcur;               // per candidate (linear index): its first slot in its mirrored group (pass 0 -> pass 1)
     uint64_t mbase;               // first output slot of the mirrored region

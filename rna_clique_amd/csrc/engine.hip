@@ -1652,7 +1652,6 @@ static int align_tile(rc_engine *e, int ti)
     const int N = (int)e->samples.size();
     const uint64_t total = e->tile_total;
     const uint32_t n_genes = (uint32_t)e->gene_sample.size();
-    const size_t ngrp = (size_t)n_genes * N;
     CHK(pack_tile(e));
     const bool dust = e->o.dust_level > 0;
     // a split tile of the b chunk the previous tile had: its 16-mer index
@@ -2260,15 +2259,31 @@ static int align_tile(rc_engine *e, int ti)
         G.cand_ovf = e->d_cand_ovf_r.p;
     }
     if (mirror) {
-        CHK(e->d_mcnt.ensure(ngrp + 1));
+        // the window of the tile's mirrored groups: every HSP is between a
+        // query transcript of a pair's a (lower sample) and a subject
+        // transcript of its b, so its mirrored group is (gene of b, sample a)
+        int a_lo = N, a_hi = 0, b_lo = N, b_hi = 0;
+        for (const auto &pr : TT.pairs) {
+            a_lo = std::min(a_lo, pr.first);
+            a_hi = std::max(a_hi, pr.first + 1);
+            b_lo = std::min(b_lo, pr.second);
+            b_hi = std::max(b_hi, pr.second + 1);
+        }
+        if (a_hi <= a_lo || b_hi <= b_lo) a_lo = a_hi = b_lo = b_hi = 0;
+        G.ms0 = a_lo;
+        G.msn = a_hi - a_lo;
+        G.mg0 = e->sample_gene_begin[b_lo];
+        G.mgw = e->sample_gene_begin[b_hi] - e->sample_gene_begin[b_lo];
+        const size_t nwin = (size_t)G.mgw * (size_t)G.msn;
+        CHK(e->d_mcnt.ensure(nwin + 1));
         CHK(e->d_mcur.ensure(std::max<uint64_t>(n_cand, 1)));   // per candidate: its slots' start in its group
-        CHK(e->d_mscan.ensure(ngrp + 1));
+        CHK(e->d_mscan.ensure(nwin + 1));
         G.mcnt = e->d_mcnt.p;
         G.mcur = e->d_mcur.p;
-        HIPCHK(hipMemsetAsync(e->d_mcnt.p, 0, (ngrp + 1) * 4, e->st));
+        HIPCHK(hipMemsetAsync(e->d_mcnt.p, 0, (nwin + 1) * 4, e->st));
         launch_group(G, 2, e->st);   // mirrored groups (spec 5b)
-        CHK(exscan(e->d_mcnt.p, e->d_mscan.p, ngrp + 1));
-        HIPCHK(hipMemcpyAsync(&nm, e->d_mscan.p + ngrp, 8, hipMemcpyDeviceToHost, e->st));
+        CHK(exscan(e->d_mcnt.p, e->d_mscan.p, nwin + 1));
+        HIPCHK(hipMemcpyAsync(&nm, e->d_mscan.p + nwin, 8, hipMemcpyDeviceToHost, e->st));
     }
     CHK(wait_st(e));
     uint64_t ndt = 0;

@@ -98,7 +98,7 @@ def _tiles(pairs, sample_bases, tile_bases):
 # searches' first-seed results (2 x 48), HSP slots (2 x 56), counts and
 # overflow offsets, defer / wide lists, ~10 seeds of 12 B; capacities grow by
 # 1.25x (calibrated on the engines' measured peaks, r06: C3 59.9 GB, C4
-# 177.2 GB, a C5 rank 139.6 GB)
+# 177.2 GB, a C5 rank 120.0 GB)
 CAND_BYTES = 525
 
 
@@ -116,8 +116,8 @@ def hbm_footprint(sample_bases, sample_genes, shard_count, tile_bases=(1 << 32) 
       each pair, CAND_BYTES each); the 2^28-bucket table (1 GiB);
     * its HSP store (56 B per HSP, both directed searches of every pair; the
       store grows by 1.5x) and table rows (16 B each);
-    * the (gene, sample) group tables over all genes x samples (24 B: offset,
-      count, mirror count, cursor, mirror scan);
+    * the (gene, sample) group table over all genes x samples (8 B: offset,
+      count); each tile's group counts and scans are part of its working set;
     * per (pair, gene) RBH item 100 B (row and edge slots, counts, offsets)
       and the edge records (20 B) of all ranks after the exchange."""
     import math
@@ -134,10 +134,15 @@ def hbm_footprint(sample_bases, sample_genes, shard_count, tile_bases=(1 << 32) 
             tile = sum(sample_bases[s] for s in {s for p in tp for s in p})
             subj = sum(sample_bases[s] for s in {b for _, b in tp})
             cands = sum(min(sample_genes[a], sample_genes[b]) for a, b in tp)
-            work = max(work, tile * (1 + 0.5 + 0.25 + 0.5) + subj * 16 + cands * CAND_BYTES + (1 << 30))
+            # the tile's group counts and scans (12 B each): direct groups of
+            # its query genes x every sample, mirrored ones of its subject
+            # genes x its query samples
+            A, B = {a for a, _ in tp}, {b for _, b in tp}
+            gcount = 12 * (sum(sample_genes[a] for a in A) * n + sum(sample_genes[b] for b in B) * len(A))
+            work = max(work, tile * (1 + 0.5 + 0.25 + 0.5) + subj * 16 + cands * CAND_BYTES + gcount + (1 << 30))
         nh = sum(sample_genes[a] + sample_genes[b] for a, b in pairs) * hsps_per_gene
         items = sum(sample_genes[b] for a, b in pairs)
-        groups = genes * n * 24
+        groups = genes * n * 8
         edges = sum(min(sample_genes[a], sample_genes[b]) for a, b in order) * 20
         out.append(int(1.25 * resident + work + nh * (56 * 1.5 + 16) + items * 100 + groups + edges
                        + math.comb(n, 2) * 64))

@@ -209,7 +209,7 @@ def test_c5_fits_hbm_per_rank():
     288 GB of an MI355X, and within it with room to spare at the configuration's
     mean transcript length. (The model is calibrated on the engines' own
     device-memory peaks, r06: C3 59.9 GB, C4 177.2 GB, and the C5 rank of
-    tests/test_gpu_scale.py 139.6 GB, which that test checks within 20 %.)"""
+    tests/test_gpu_scale.py 120.0 GB, which that test checks within 20 %.)"""
     from rna_clique_amd import distributed
     n, genes, mean_len = 128, 100_000, 2600
     bases = [genes * mean_len] * n
