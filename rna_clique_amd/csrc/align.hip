@@ -3298,13 +3298,8 @@ static void launch_rows_t(const Db &db, const ExtParams &P, hipStream_t st)
     hipLaunchKernelGGL(kern, dim3(resident_blocks(kern, lds)), dim3(EBLOCK), lds, st, RowArgs{db, P});
 }
 template <int RWV, bool SV = false>
-static void launch_rows(bool amb, const Db &db, const ExtParams &P0, hipStream_t st)
+static void launch_rows(bool amb, const Db &db, const ExtParams &P, hipStream_t st)
 {
-    ExtParams P = P0;
-    if (RWV == 64 && P.dsw64 > 0) {   // 64-lane rows: half the rows per block, twice the slot in the same LDS
-        P.dsw = P.dsw64;
-        P.win = P.win64;
-    }
     if (amb) {
         if (P.win) launch_rows_t<true, RWV, SV, true>(db, P, st); else launch_rows_t<true, RWV, SV, false>(db, P, st);
     } else {
@@ -3312,15 +3307,14 @@ static void launch_rows(bool amb, const Db &db, const ExtParams &P0, hipStream_t
     }
 }
 
-// Staging slot (u64 words per staged array) the rw-lane row kernel can have
+// Staging slot (u64 words per staged array) the 32-lane row kernel can have
 // at ROW_MIN_WAVES waves per SIMD (as many 4-wave blocks per CU in 160 KB of LDS); a longer
-// transcript runs on the windowed instantiation. 64-lane rows have half the
-// rows per block, so about twice the slot.
-int row_slot_words_max(bool amb, int rw)
+// transcript runs on the windowed instantiation.
+int row_slot_words_max(bool amb)
 {
-    const int na = amb ? 8 : 4, rows = EBLOCK / rw;
+    const int na = amb ? 8 : 4, rows = EBLOCK / 32;
     const size_t per_block = (size_t)(160 * 1024) / (size_t)ROW_MIN_WAVES;
-    const size_t fixed = row_lds_bytes(rw, na, 0, true);
+    const size_t fixed = row_lds_bytes(32, na, 0, true);
     return (int)((per_block - fixed) / ((size_t)rows * na * 8));
 }
 

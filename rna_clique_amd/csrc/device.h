@@ -280,7 +280,6 @@ struct ExtParams {
     // shorter than the longest transcript, the windowed instantiation runs
     int32_t dsw;
     int32_t win;
-    int32_t dsw64, win64;         // the 64-lane passes' slot and windowing (0: the 32-lane ones)
     int32_t *cand_box;            // row kernel: status + right/left results of each candidate's first seed
     int32_t chunk;                // row kernel: candidates per work grab (0: static round robin)
     unsigned long long *work;     // row kernel: work counter

@@ -77,7 +77,7 @@ void launch_extend_retry(bool, const Db &, const ExtParams &, hipStream_t);
 void launch_later_rounds(bool, const Db &, const ExtParams &, const LaterParams &, Cand *const[2], uint32_t *const[2],
                          int32_t *const[2], uint32_t *const[2], unsigned long long *, hipStream_t);
 void launch_later_finish(const ExtParams &, const LaterParams &, hipStream_t);
-int row_slot_words_max(bool amb, int rw);
+int row_slot_words_max(bool amb);
 void launch_group(const GroupParams &, int, hipStream_t);
 
 void launch_rbh(const RbhParams &, int, hipStream_t);
@@ -2004,20 +2004,11 @@ static int align_tile(rc_engine *e, int ti)
             // windows of that slot (the windowed instantiation). RC_WIN_WORDS
             // forces windows of that many words (tests: many refills).
             const int need = ((e->max_len + 31) >> 5) + 4;
-            const int smax = row_slot_words_max(e->has_amb, 32);
+            const int smax = row_slot_words_max(e->has_amb);
             const char *wwv = getenv("RC_WIN_WORDS");
             const int forced = wwv ? std::max(4, atoi(wwv)) : 0;
             X.win = forced ? 1 : (need > smax ? 1 : 0);
             X.dsw = forced ? std::min(forced, smax) : std::min(need, smax);
-            // the 64-lane passes (wide first seeds, later seeds) stage in their
-            // own, larger slot: whole transcripts up to twice as long, or
-            // windows twice as wide (RC_SLOT64=0: the 32-lane slot)
-            const char *s64 = getenv("RC_SLOT64");
-            if (!(s64 && atoi(s64) == 0)) {
-                const int smax64 = row_slot_words_max(e->has_amb, 64);
-                X.win64 = forced ? 1 : (need > smax64 ? 1 : 0);
-                X.dsw64 = forced ? std::min(forced, smax64) : std::min(need, smax64);
-            }
         }
         X.defer = e->d_defer.p;
         X.defer_count = e->d_count.p + 6;
