@@ -62,7 +62,7 @@ for step in "$@"; do
             run 300 "$D/pmcx_${a}_p$i.log" rocprofv3 --kernel-trace --pmc ${grp//,/ } --output-format csv -d "$D/pmcx_$a/p$i" -o run -- python3 bench.py --config "$a" --steps 1 --warmup 0 --no-cpu-baseline --no-e2e || exit $?
           done ;;
     counters) run 120 "$D/counters.txt" rocprofv3 -L || exit $? ;;
-    shard) run 900 "$D/${a}_shard${b//\//of}.json" python -u bench.py --shard "$b" --config "$a" --steps 1 --warmup 1 || exit $? ;;
+    shard) run 900 "$D/${a}_shard${b//\//of}${ET}.json" python -u bench.py --shard "$b" --config "$a" --steps 1 --warmup 1 || exit $? ;;
     shardprof) P="$D/${a}_shardprof${b//\//of}"
            run 900 "$P.log" rocprofv3 --kernel-trace --hip-trace --stats --output-format csv -d "$P" -o run -- python3 -u bench.py --shard "$b" --config "$a" --steps 1 --warmup 1 || exit $?
            T=$(python3 -c "import json,sys; print(int([json.loads(l) for l in open('$P.log') if l.startswith('{\"metric')][-1]['phases_ms']['tiles']))")
