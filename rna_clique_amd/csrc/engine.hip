@@ -550,19 +550,8 @@ int rc_create(const rc_opts *opts, rc_engine **out)
     if (opts->device < 0 || opts->device >= ndev) return fail(RC_E_ARG, "bad device ordinal");
     rc_engine *e = new rc_engine();
     e->o = *opts;
-    // the engine's stream at the highest priority, the side stream (DUST
-    // beside the index build) at the lowest: the sort's one-block table
-    // kernels get a slot ahead of DUST's waves (RC_STREAM_PRIO=0: both default)
-    int prio_lo = 0, prio_hi = 0;
-    const char *pv = getenv("RC_STREAM_PRIO");
-    if (!(pv && atoi(pv) == 0) && hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) {
-        (void)hipGetLastError();
-        prio_lo = prio_hi = 0;
-    }
-    if (pv && atoi(pv) == 0) prio_lo = prio_hi = 0;
-    if (hipSetDevice(e->o.device) != hipSuccess ||
-        hipStreamCreateWithPriority(&e->st, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&e->st2, hipStreamNonBlocking, prio_lo) != hipSuccess) {
+    if (hipSetDevice(e->o.device) != hipSuccess || hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->st2, hipStreamNonBlocking) != hipSuccess) {
         delete e;
         return fail(RC_E_HIP, "stream creation failed");
     }
